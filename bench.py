@@ -1,0 +1,339 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident GB/s reduced (float32 MPI_SUM) per GPU and % of the HBM3E roofline.
+
+Workload (BASELINE.json configs[1]): persistent Allreduce, float32 MPI_SUM, 16 MiB per rank,
+EXT_MPI_COPYIN '6;1 -R R' (copy-in method 6), device-resident synthetic buffers.
+
+  N = 1  (python bench.py): 8 node ranks whose send/recv buffers all live in the one GPU's HBM
+         (the reference's XPMEM / IPC-mapped node, ext_mpi_xpmem.c:68-133), one fused
+         copy-in + copy-out fold launch per step. Buffer sets are rotated so the working set
+         between re-uses (1 GiB) exceeds the 256 MiB Infinity Cache.
+  N > 1  (torchrun, one rank per GPU): each GPU holds one rank's 16 MiB; reduce-scatter and
+         allgather legs over RCCL/xGMI, the fold on the owner GPU.
+
+A step is one full Allreduce. value = bytes folded by all ranks (R x 16 MiB per step at N = 1,
+N x 16 MiB at N > 1) / wall time of K steps (max over ranks), inputs already in HBM.
+The roofline object prices the fold kernel: algorithmic bytes per launch (R reads + D writes
+per owner chunk) / its average launch time from HIP events on the
+stream it runs on. cpu_baseline times the oracle's threaded restatement of the reference's
+CPU path (oracle/ref_cpu_threads.c) on this host, rank 0 at N = 1 only.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+MIB = 1 << 20
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--size-mib", type=float, default=16.0, help="message bytes per rank")
+    ap.add_argument("--ranks", type=int, default=8, help="node ranks resident in one GPU (N = 1)")
+    ap.add_argument("--dtype", default="float", choices=["float", "double", "int", "long"])
+    ap.add_argument("--copyin", default=None, help="EXT_MPI_COPYIN (default '6;1 -R R')")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the 256 MiB and host-buffer points")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU baseline sample")
+    return ap.parse_args()
+
+
+def dtype_info(name):
+    import torch
+    import ext_mpi_collectives_amd as emac
+    return {"float": (torch.float32, emac.FLOAT, "f32", 4), "double": (torch.float64, emac.DOUBLE, "f64", 8),
+            "int": (torch.int32, emac.INT, "i32", 4), "long": (torch.int64, emac.LONG, "i64", 8)}[name]
+
+
+def fill(t, seed):
+    import torch
+    g = torch.Generator(device=t.device)
+    g.manual_seed(seed)
+    if t.dtype.is_floating_point:
+        t.uniform_(-1.0, 1.0, generator=g)
+    else:
+        t.random_(-(1 << 20), (1 << 20), generator=g)
+
+
+def traffic_from_profiles(tag):
+    """HBM bytes per launch measured by rocprofv3 PMC (profiles/traffic_<tag>.json), or None."""
+    path = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
+    if os.path.exists(path):
+        try:
+            return json.load(open(path)).get("hbm_bytes_per_launch")
+        except (ValueError, OSError):
+            return None
+    return None
+
+
+def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * MIB, host=False):
+    """Time `steps` node-form Allreduces (R ranks in this GPU). Returns dict of timings."""
+    import torch
+    import ext_mpi_collectives_amd as emac
+    tsize = torch.empty((), dtype=tdtype).element_size()
+    set_bytes = 2 * R * count * tsize
+    nsets = 1 if host else max(2, math.ceil(min_set_bytes / max(1, set_bytes)))
+    stream = torch.cuda.Stream()
+    sets, handles = [], []
+    for s in range(nsets):
+        if host:
+            sends = [torch.empty(count, dtype=tdtype).pin_memory() for _ in range(R)]
+            recvs = [torch.empty(count, dtype=tdtype).pin_memory() for _ in range(R)]
+            for r, t in enumerate(sends):
+                t.copy_(torch.rand(count, dtype=torch.float64).mul_(2).sub_(1).to(tdtype))
+        else:
+            sends = [torch.empty(count, dtype=tdtype, device="cuda") for _ in range(R)]
+            recvs = [torch.empty(count, dtype=tdtype, device="cuda") for _ in range(R)]
+            for r, t in enumerate(sends):
+                fill(t, 0x5EED0000 + 97 * s + r)
+        h = emac.node_allreduce_init([t.data_ptr() for t in sends], [t.data_ptr() for t in recvs], count, code, copyin)
+        emac.set_stream(h, stream.cuda_stream)
+        sets.append((sends, recvs))
+        handles.append(h)
+    torch.cuda.synchronize()
+    for k in range(warmup):
+        emac.start(handles[k % nsets])
+    stream.synchronize()
+    # sanity: set 0 against a float64 sum (parity proper is tests/test_gpu_parity.py)
+    emac.start(handles[0])
+    stream.synchronize()
+    sends, recvs = sets[0]
+    ref = torch.stack([t.to("cuda", torch.float64) for t in sends]).sum(0)
+    got = recvs[0].to("cuda", torch.float64)
+    tol = 1e-5 * R if tdtype.is_floating_point else 0.0
+    checked = bool(torch.allclose(got, ref, rtol=0, atol=tol)) and all(
+        torch.equal(recvs[0], recvs[r]) for r in range(1, R))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        emac.start(handles[k % nsets])
+    e1.record(stream)
+    stream.synchronize()
+    t1 = time.perf_counter()
+    for h in handles:
+        emac.done(h)
+    del sets
+    return {"wall_s": t1 - t0, "event_ms": e0.elapsed_time(e1), "nsets": nsets, "checked": checked,
+            "set_bytes": set_bytes}
+
+
+def stream_copy_peak():
+    """Measured device copy rate (read + write bytes / s) of a 2 GiB buffer, for context."""
+    import torch
+    n = (1 << 31) // 4
+    a = torch.empty(n, dtype=torch.float32, device="cuda")
+    b = torch.empty_like(a)
+    a.fill_(1.0)
+    for _ in range(3):
+        b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbps = 10 * 2 * a.numel() * 4 / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return gbps
+
+
+def cpu_baseline(R, count, np_dtype, copyin, seconds):
+    """The oracle's threaded CPU restatement of the reference path on a bounded sample."""
+    from oracle import oracle
+    rng = np.random.default_rng(0x5EED0000)
+    sends = [(rng.random(count) * 2 - 1).astype(np_dtype) for _ in range(R)]
+    recvs = [np.empty_like(s) for s in sends]
+    iters, t = 1, 0.0
+    budget_left = seconds
+    # tests/benchmark.c:92-157: double the iteration count until a run takes >= 2 s
+    while True:
+        t = oracle.cpu_allreduce_threads(sends, recvs, copyin, iters)
+        budget_left -= t
+        if t >= 2.0 or budget_left < 2.5 * t:
+            break
+        iters *= 2
+    return {"value": round(iters * R * count * np.dtype(np_dtype).itemsize / t / 1e9, 3), "unit": "GB/s",
+            "cores": R, "kind": "port",
+            "sample": f"{iters} Allreduce(s) of {R} ranks x {count * np.dtype(np_dtype).itemsize // MIB} MiB "
+                      f"'{copyin}' in {t:.2f} s: R pthreads replaying each rank's SMEMCPY/SREDUCE program "
+                      f"(gcc -O3 restatement of ext_mpi_native_exec.c:207-234) with spin barriers; "
+                      f"host nproc={os.cpu_count()}"}
+
+
+def single_gpu(args):
+    import torch
+    import ext_mpi_collectives_amd as emac
+    tdtype, code, dname, tsize = dtype_info(args.dtype)
+    R = args.ranks
+    count = int(args.size_mib * MIB) // tsize
+    S = count * tsize
+    copyin = args.copyin or f"6;1 -{R} {R}"
+    emac.lib()
+    main = node_run(R, count, tdtype, code, copyin, args.steps, args.warmup)
+    kernel_s = main["event_ms"] * 1e-3 / args.steps
+    bytes_reduced_per_step = R * S
+    algo_bytes = 2 * R * S  # R buckets x (R leaf reads + R fan-out writes) x chunk S/R
+    achieved = algo_bytes / kernel_s / 1e9
+    out = {
+        "metric": "device-resident GB/s reduced (float32 MPI_SUM) per GPU; % HBM3E roofline",
+        "value": round(bytes_reduced_per_step * args.steps / main["wall_s"] / 1e9, 2),
+        "unit": "GB/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(main["wall_s"] * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": dname,
+        "data": f"synthetic: uniform [-1,1) per rank (seeded), device-resident, {main['nsets']} rotated buffer sets "
+                f"({main['nsets'] * main['set_bytes'] // MIB} MiB > 256 MiB Infinity Cache)",
+        "config": {"workload": f"persistent Allreduce {args.dtype} MPI_SUM, {S // MIB} MiB per rank, {R} node ranks "
+                               f"resident in one MI355X (BASELINE configs[1]), EXT_MPI_COPYIN '{copyin}', fused "
+                               f"reduce_copyin + reduce_copyout fold",
+                   "ranks": R, "message_bytes_per_rank": S, "copyin": copyin, "layout": "node-in-one-HBM",
+                   "checked_vs_fp64_sum": main["checked"]},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "traffic": traffic_from_profiles(f"node_r{R}_{S // MIB}mib_{args.dtype}"),
+                     "kernel": "fold_kernel", "algorithmic_bytes_per_launch": algo_bytes,
+                     "avg_launch_us": round(kernel_s * 1e6, 2)},
+    }
+    if not args.no_extras:
+        extras = {}
+        try:
+            extras["stream_copy_gbps"] = round(stream_copy_peak(), 1)
+            out["roofline"]["frac_of_measured_copy"] = round(achieved / extras["stream_copy_gbps"], 4)
+        except RuntimeError as e:
+            log("stream copy peak failed:", e)
+        big = (256 * MIB) // tsize
+        r256 = node_run(R, big, tdtype, code, copyin, max(4, args.steps // 5), 2)
+        k256 = r256["event_ms"] * 1e-3 / max(4, args.steps // 5)
+        extras["point_256MiB"] = {
+            "gbps_reduced": round(R * big * tsize / k256 / 1e9, 1),
+            "achieved_gbps": round(2 * R * big * tsize / k256 / 1e9, 1),
+            "frac_of_peak": round(2 * R * big * tsize / k256 / 1e9 / HBM_PEAK_GBPS, 4),
+            "read_gbps": round(R * big * tsize / k256 / 1e9, 1),
+            "avg_launch_us": round(k256 * 1e6, 1), "checked": r256["checked"]}
+        hst = node_run(R, count, tdtype, code, copyin, 5, 1, host=True)
+        extras["host_buffers_pcie_inclusive"] = {
+            "gbps_reduced": round(R * S * 5 / hst["wall_s"] / 1e9, 2),
+            "ms_per_step": round(hst["wall_s"] * 1e3 / 5, 3), "checked": hst["checked"],
+            "note": "pinned host send/recv buffers: H2D + fold + D2H on one stream"}
+        out["extras"] = extras
+    if not args.no_cpu_baseline:
+        np_dtype = {"float": np.float32, "double": np.float64, "int": np.int32, "long": np.int64}[args.dtype]
+        out["cpu_baseline"] = cpu_baseline(R, count, np_dtype, copyin, args.cpu_seconds)
+    print(json.dumps(out), flush=True)
+
+
+def multi_gpu(args):
+    import torch
+    import torch.distributed as dist
+    import ext_mpi_collectives_amd as emac
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    torch.cuda.set_device(local)
+    dist.init_process_group("gloo")
+    tdtype, code, dname, tsize = dtype_info(args.dtype)
+    count = int(args.size_mib * MIB) // tsize
+    S = count * tsize
+    copyin = args.copyin or f"6;1 -{world} {world}"
+    uid = [emac.get_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    comm = emac.comm_init(rank, world, uid[0], local)
+    send = torch.empty(count, dtype=tdtype, device="cuda")
+    recv = torch.empty(count, dtype=tdtype, device="cuda")
+    fill(send, 0x5EED0000 + rank)
+    h = emac.allreduce_init(send.data_ptr(), recv.data_ptr(), count, code, comm, copyin)
+    stream = torch.cuda.Stream()
+    emac.set_stream(h, stream.cuda_stream)
+    for _ in range(args.warmup):
+        emac.start(h)
+    stream.synchronize()
+    # sanity against torch's own sum of the gathered inputs (parity proper: tests/)
+    allin = [torch.empty_like(send).cpu() for _ in range(world)]
+    dist.all_gather(allin, send.cpu())
+    ref = torch.stack([t.double() for t in allin]).sum(0).to("cuda")
+    checked = torch.tensor([int(torch.allclose(recv.double(), ref, rtol=0, atol=1e-5 * world))])
+    dist.all_reduce(checked, op=dist.ReduceOp.MIN)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        emac.start(h)
+    stream.synchronize()
+    dist.barrier()
+    t1 = time.perf_counter()
+    el = torch.tensor([t1 - t0], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    # the fold kernel alone, on each GPU, inside the N-GPU job (staging holds real slices)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    dist.barrier()
+    e0.record(stream)
+    for _ in range(args.steps):
+        emac.start_legs(h, emac.LEG_FOLD)
+    e1.record(stream)
+    stream.synchronize()
+    fold_s = torch.tensor([e0.elapsed_time(e1) * 1e-3 / args.steps], dtype=torch.float64)
+    dist.all_reduce(fold_s, op=dist.ReduceOp.MAX)
+    emac.done(h)
+    emac.comm_free(comm)
+    if rank == 0:
+        wall = el.item()
+        kf = fold_s.item()
+        chunk = S / world
+        algo = (world + 1) * chunk  # R leaf reads + 1 write of the owned chunk
+        achieved = algo / kf / 1e9
+        out = {
+            "metric": "device-resident GB/s reduced (float32 MPI_SUM) per GPU; % HBM3E roofline",
+            "value": round(world * S * args.steps / wall / 1e9, 2),
+            "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(wall * 1e3 / args.steps, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": dname,
+            "data": "synthetic: uniform [-1,1) per rank (seeded), device-resident",
+            "config": {"workload": f"persistent Allreduce {args.dtype} MPI_SUM, {S // MIB} MiB per rank, one rank per "
+                                   f"GPU, EXT_MPI_COPYIN '{copyin}': reduce-scatter + allgather legs over RCCL/xGMI, "
+                                   f"fold on the owner GPU",
+                       "ranks": world, "message_bytes_per_rank": S, "copyin": copyin, "layout": "rank-per-gpu",
+                       "checked_vs_fp64_sum": bool(checked.item())},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None, "kernel": "fold_kernel",
+                         "algorithmic_bytes_per_launch": int(algo), "avg_launch_us": round(kf * 1e6, 2)},
+            "extras": {"fold_gbps_reduced_per_gpu": round(S / kf / 1e9, 1),
+                       "end_to_end_algbw_gbps_per_gpu": round(S * args.steps / wall / 1e9, 2)},
+        }
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        multi_gpu(args)
+    else:
+        single_gpu(args)
+
+
+if __name__ == "__main__":
+    main()

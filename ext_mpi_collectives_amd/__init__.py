@@ -1,0 +1,189 @@
+"""MI355X-native bucket-reduction path of ext_mpi_collectives (persistent MPI_SUM Allreduce).
+
+The product is the C library ``libext_mpi_amd.so`` (host C engine + gfx950 HIP kernels, built
+from ``csrc/``) and its PMPI layer ``libext_mpi_collectives.so``. This module is a thin ctypes
+front-end for tests and benchmarks; it mirrors the reference's native API
+(``EXT_MPI_Allreduce_init / EXT_MPI_Start / EXT_MPI_Test / EXT_MPI_Wait / EXT_MPI_Done``,
+include/mpi/ext_mpi.h:69-89) with integer handles and plain pointers. Buffers are passed as
+raw device/host addresses (e.g. ``tensor.data_ptr()``); nothing here computes on the CPU.
+
+There is no fallback: if the native library is missing, importing :func:`lib` raises.
+"""
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libext_mpi_amd.so")
+MPI_LIB_PATH = os.path.join(HERE, "libext_mpi_collectives.so")
+
+DOUBLE, LONG, FLOAT, INT = 0, 1, 2, 3
+SUM = 0
+UNIQUE_ID_BYTES = 128
+MAX_RANKS = 16
+ERRORS = {-1: "ERROR_MALLOC", -2: "ERROR_SHMEM", -3: "ERROR_ARG", -4: "ERROR_UNSUPPORTED",
+          -5: "ERROR_DEVICE", -6: "ERROR_TRANSPORT"}
+
+_TORCH_DTYPE_CODES = {"torch.float32": FLOAT, "torch.float64": DOUBLE, "torch.int32": INT,
+                      "torch.int64": LONG}
+_NUMPY_DTYPE_CODES = {"float32": FLOAT, "float64": DOUBLE, "int32": INT, "int64": LONG}
+
+
+class ExtMpiError(RuntimeError):
+    def __init__(self, what, code):
+        super().__init__(f"{what} failed: {ERRORS.get(code, code)} ({code})")
+        self.code = code
+
+
+def build(with_mpi=True):
+    """Compile the native libraries in-tree (hipcc --offload-arch=gfx950)."""
+    targets = ["all"] if with_mpi else [os.path.join("..", "libext_mpi_amd.so")]
+    subprocess.run(["make", "-s", "-j8", "-C", os.path.join(HERE, "csrc")] + targets, check=True)
+
+
+_lib = None
+
+
+def lib():
+    """The loaded native library. Raises if it has not been built (no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: run ext_mpi_collectives_amd.build() "
+                              "(the HIP path has no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        c_int, c_long, c_void_p = ctypes.c_int, ctypes.c_long, ctypes.c_void_p
+        P = ctypes.POINTER
+        L.ext_mpi_amd_node_allreduce_init.argtypes = [c_int, P(c_void_p), P(c_void_p), c_long, c_int, c_int,
+                                                      ctypes.c_char_p, P(c_int)]
+        L.ext_mpi_amd_get_unique_id.argtypes = [c_void_p]
+        L.ext_mpi_amd_comm_init.argtypes = [c_int, c_int, c_void_p, c_int, P(c_int)]
+        L.ext_mpi_amd_comm_free.argtypes = [c_int]
+        L.ext_mpi_amd_allreduce_init.argtypes = [c_void_p, c_void_p, c_long, c_int, c_int, c_int,
+                                                 ctypes.c_char_p, P(c_int)]
+        for name in ("start", "test", "wait", "done"):
+            getattr(L, "ext_mpi_amd_" + name).argtypes = [c_int]
+            getattr(L, "ext_mpi_amd_" + name).restype = c_int
+        L.ext_mpi_amd_set_stream.argtypes = [c_int, c_void_p]
+        L.ext_mpi_amd_start_legs.argtypes = [c_int, c_int]
+        L.ext_mpi_amd_stream.argtypes = [c_int]
+        L.ext_mpi_amd_stream.restype = c_void_p
+        L.ext_mpi_amd_plan_describe.argtypes = [c_int, c_long, c_int, ctypes.c_char_p, c_int, P(c_long),
+                                                P(c_long), c_int, P(c_int), P(c_int), P(ctypes.c_ubyte),
+                                                P(ctypes.c_ubyte), P(c_int)]
+        L.ext_mpi_amd_version.restype = ctypes.c_char_p
+        _lib = L
+    return _lib
+
+
+def dtype_code(dt):
+    """Map a torch/numpy dtype (or its name) to the library's element type code."""
+    key = str(dt)
+    if key in _TORCH_DTYPE_CODES:
+        return _TORCH_DTYPE_CODES[key]
+    if key in _NUMPY_DTYPE_CODES:
+        return _NUMPY_DTYPE_CODES[key]
+    raise ValueError(f"unsupported element type {dt} (float, double, int, long only)")
+
+
+def _check(what, rc):
+    if rc < 0:
+        raise ExtMpiError(what, rc)
+    return rc
+
+
+def _enc(copyin):
+    return copyin.encode() if copyin else None
+
+
+def node_allreduce_init(sendptrs, recvptrs, count, dtype, copyin=None, op=SUM):
+    """Persistent Allreduce over len(sendptrs) node ranks whose buffers all live in this
+    process (device or host addresses). Returns an integer handle."""
+    n = len(sendptrs)
+    s = (ctypes.c_void_p * n)(*sendptrs)
+    r = (ctypes.c_void_p * n)(*recvptrs)
+    h = ctypes.c_int(-1)
+    _check("ext_mpi_amd_node_allreduce_init",
+           lib().ext_mpi_amd_node_allreduce_init(n, s, r, count, dtype, op, _enc(copyin), ctypes.byref(h)))
+    return h.value
+
+
+def get_unique_id():
+    buf = ctypes.create_string_buffer(UNIQUE_ID_BYTES)
+    _check("ext_mpi_amd_get_unique_id", lib().ext_mpi_amd_get_unique_id(buf))
+    return buf.raw
+
+
+def comm_init(rank, size, unique_id, device=-1):
+    c = ctypes.c_int(-1)
+    buf = ctypes.create_string_buffer(bytes(unique_id), UNIQUE_ID_BYTES)
+    _check("ext_mpi_amd_comm_init", lib().ext_mpi_amd_comm_init(rank, size, buf, device, ctypes.byref(c)))
+    return c.value
+
+
+def comm_free(comm):
+    _check("ext_mpi_amd_comm_free", lib().ext_mpi_amd_comm_free(comm))
+
+
+def allreduce_init(sendptr, recvptr, count, dtype, comm, copyin=None, op=SUM):
+    """Persistent Allreduce of this rank's buffer over a communicator (one rank per GPU)."""
+    h = ctypes.c_int(-1)
+    _check("ext_mpi_amd_allreduce_init",
+           lib().ext_mpi_amd_allreduce_init(sendptr, recvptr, count, dtype, op, comm, _enc(copyin), ctypes.byref(h)))
+    return h.value
+
+
+def start(h):
+    return _check("ext_mpi_amd_start", lib().ext_mpi_amd_start(h))
+
+
+def test(h):
+    return _check("ext_mpi_amd_test", lib().ext_mpi_amd_test(h))
+
+
+def wait(h):
+    return _check("ext_mpi_amd_wait", lib().ext_mpi_amd_wait(h))
+
+
+def done(h):
+    return _check("ext_mpi_amd_done", lib().ext_mpi_amd_done(h))
+
+
+LEG_STAGE, LEG_REDUCE_SCATTER, LEG_FOLD, LEG_ALLGATHER, LEG_ALL = 1, 2, 4, 8, 15
+
+
+def start_legs(h, legs):
+    return _check("ext_mpi_amd_start_legs", lib().ext_mpi_amd_start_legs(h, legs))
+
+
+def set_stream(h, stream_ptr):
+    return _check("ext_mpi_amd_set_stream", lib().ext_mpi_amd_set_stream(h, stream_ptr))
+
+
+def stream(h):
+    """hipStream_t (as int) the handle's work runs on."""
+    return lib().ext_mpi_amd_stream(h)
+
+
+def plan_describe(nranks, count, dtype, copyin, pos, max_pieces=4096):
+    """Fold schedule of owner position ``pos`` (no GPU needed).
+
+    Returns dict(owner, pieces=[(off, len)], leaves=[node ranks in fold order],
+    first=[...], close=[...], nlev)."""
+    off = (ctypes.c_long * max_pieces)()
+    ln = (ctypes.c_long * max_pieces)()
+    owner = ctypes.c_int()
+    leaves = (ctypes.c_int * MAX_RANKS)()
+    first = (ctypes.c_ubyte * MAX_RANKS)()
+    close = (ctypes.c_ubyte * MAX_RANKS)()
+    nlev = ctypes.c_int()
+    n = _check("ext_mpi_amd_plan_describe",
+               lib().ext_mpi_amd_plan_describe(nranks, count, dtype, _enc(copyin), pos, off, ln, max_pieces,
+                                                ctypes.byref(owner), leaves, first, close, ctypes.byref(nlev)))
+    return {"owner": owner.value, "pieces": [(off[i], ln[i]) for i in range(min(n, max_pieces))],
+            "leaves": list(leaves[:nranks]), "first": list(first[:nranks]), "close": list(close[:nranks]),
+            "nlev": nlev.value}
+
+
+def version():
+    return lib().ext_mpi_amd_version().decode()

@@ -1,0 +1,530 @@
+/*
+ * engine.c -- persistent-Allreduce handles of the MI355X bucket-reduction path (host C).
+ *
+ * Mirrors the reference's handle life cycle (src/mpi/ext_mpi_native.c: init :657-1113 with
+ * init_epilogue :389-655, Start :215-230, Test/Wait :232-267, Done :269-387) without its
+ * text-IR pipeline: at init the planner (plan.c) fixes every owner chunk's fold tree, the
+ * device-side bucket descriptors are written once (the analogue of byte_code.c:987-992's
+ * descriptor H2D copy), buffers are mapped once; Start only enqueues work on the handle's
+ * stream; Wait synchronises that stream.
+ *
+ * Two execution forms:
+ *  NODE: all R node ranks' buffers live in this process (one device). One fold launch per
+ *        Start performs copy-in (reduce-scatter) AND copy-out (allgather fan-out): every
+ *        bucket reads its R leaves once and stores the result into all R receive buffers.
+ *  COMM: one rank per GPU. The reduce-scatter leg moves each rank's slice of every owner
+ *        chunk to the owner with grouped RCCL send/recv (one all-to-all round over the
+ *        fully connected xGMI links instead of log R recursive-halving rounds, each of
+ *        which would be bound by ONE 153 GB/s link); the owner folds the R slices in the
+ *        reference's order (bit-exact); the allgather leg pushes the owned chunk to every
+ *        peer, again as one grouped round. RCCL's own reductions are never used: their
+ *        summation order differs from the reference's.
+ * Host (non-device) buffers are supported in both forms by staging through device mirrors
+ * (H2D before, D2H after, on the same stream); the buffers are page-locked once at init,
+ * as the reference maps its XPMEM peers once (src/mpi/ext_mpi_xpmem.c:68-133).
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include "ext_mpi_amd.h"
+#include "gpu.h"
+#include "plan.h"
+
+#define MAX_HANDLES 4096
+#define MAX_COMMS 64
+
+enum { KIND_NODE = 1, KIND_COMM = 2 };
+
+typedef struct {
+  int used;
+  int rank, size, device;
+  ncclComm_t nccl;
+} emac_comm;
+
+typedef struct {
+  int kind;
+  emac_plan plan;
+  int device;
+  void *stream;
+  emac_bucket *d_buckets;
+  int nb;
+  long ntiles;
+  int nsrc;
+  size_t bytes; /* message bytes per rank */
+  int nbuf;     /* ranks with buffers in this process */
+  void *user_send[EMAC_MAX_RANKS], *user_recv[EMAC_MAX_RANKS];
+  void *dsend[EMAC_MAX_RANKS], *drecv[EMAC_MAX_RANKS];
+  unsigned char send_mirror[EMAC_MAX_RANKS], recv_mirror[EMAC_MAX_RANKS];
+  unsigned char send_reg[EMAC_MAX_RANKS], recv_reg[EMAC_MAX_RANKS];
+  /* COMM form */
+  int comm;
+  int me, me_pos;
+  void *staging;
+  long *stage_off;    /* per piece: byte offset of the piece's slot block */
+  long *stage_stride; /* per piece: bytes between peer slots (16-byte multiple) */
+  long *stage_mis;    /* per piece: 16-byte phase shared with the send buffer's chunk */
+  int started;
+  int own_stream; /* 0 once the caller supplied the stream (ext_mpi_amd_set_stream) */
+} emac_handle;
+
+static emac_handle *handles[MAX_HANDLES];
+static long stage_slot(const emac_handle *h, int pc, int q);
+static emac_comm comms[MAX_COMMS];
+
+static int new_handle_slot(void) {
+  int i;
+  for (i = 0; i < MAX_HANDLES; i++)
+    if (!handles[i]) return i;
+  return -1;
+}
+
+static void release(emac_handle *h) {
+  int r;
+  if (!h) return;
+  if (h->stream) {
+    emac_gpu_stream_sync(h->stream);
+    if (h->own_stream) emac_gpu_stream_destroy(h->stream);
+  }
+  emac_gpu_free(h->d_buckets);
+  emac_gpu_free(h->staging);
+  for (r = 0; r < h->nbuf; r++) {
+    int same = h->dsend[r] == h->drecv[r];
+    if (h->send_mirror[r]) emac_gpu_free(h->dsend[r]);
+    if (h->recv_mirror[r] && !(same && h->send_mirror[r])) emac_gpu_free(h->drecv[r]);
+    if (h->send_reg[r]) emac_gpu_host_unregister(h->user_send[r]);
+    if (h->recv_reg[r]) emac_gpu_host_unregister(h->user_recv[r]);
+  }
+  free(h->stage_off);
+  free(h->stage_stride);
+  free(h->stage_mis);
+  emac_plan_free(&h->plan);
+  free(h);
+}
+
+/* Device view of rank r's buffers: user device pointers are used in place; host buffers get
+   a device mirror (in place stays in place) and are page-locked for async DMA. */
+static int map_buffers(emac_handle *h, int r, const void *send, void *recv) {
+  int rc;
+  h->user_send[r] = (void *)send;
+  h->user_recv[r] = recv;
+  if (emac_gpu_is_device_pointer(recv)) {
+    h->drecv[r] = recv;
+  } else {
+    if ((rc = emac_gpu_malloc(&h->drecv[r], h->bytes))) return rc;
+    h->recv_mirror[r] = 1;
+    h->recv_reg[r] = emac_gpu_host_register(recv, h->bytes) == 0;
+  }
+  if (send == recv) {
+    h->dsend[r] = h->drecv[r];
+  } else if (emac_gpu_is_device_pointer(send)) {
+    h->dsend[r] = (void *)send;
+  } else {
+    if ((rc = emac_gpu_malloc(&h->dsend[r], h->bytes))) return rc;
+    h->send_mirror[r] = 1;
+    h->send_reg[r] = emac_gpu_host_register((void *)send, h->bytes) == 0;
+  }
+  return 0;
+}
+
+/* head / vector / tail split of one bucket: vectors need every pointer 16-byte aligned at
+   the same element; if the pointers disagree the whole bucket takes the element path. */
+static void split_alignment(emac_bucket *b, int nsrc, long off, long len, int tsize) {
+  long head = 0;
+  int i, ok = 1;
+  unsigned long mis = (unsigned long)((const char *)b->src[0] + off * tsize) & 15ul;
+  if (mis % (unsigned long)tsize == 0) head = (long)((16ul - mis) & 15ul) / tsize;
+  else ok = 0;
+  if (head > len) head = len;
+  for (i = 0; ok && i < nsrc; i++)
+    if (((unsigned long)((const char *)b->src[i] + (off + head) * tsize) & 15ul) != 0) ok = 0;
+  for (i = 0; ok && i < b->ndst; i++)
+    if (((unsigned long)((char *)b->dst[i] + (off + head) * tsize) & 15ul) != 0) ok = 0;
+  for (i = 0; i < nsrc; i++) b->src[i] = (const char *)b->src[i] + off * tsize;
+  for (i = 0; i < b->ndst; i++) b->dst[i] = (char *)b->dst[i] + off * tsize;
+  if (!ok) {
+    b->scalar = 1;
+    b->head = b->tail = 0;
+    b->nvec = len;
+    return;
+  }
+  b->scalar = 0;
+  b->head = head;
+  b->nvec = (len - head) * tsize / 16;
+  b->tail = len - head - b->nvec * (16 / tsize);
+}
+
+static int upload_buckets(emac_handle *h, emac_bucket *b, int nb) {
+  long tv = emac_gpu_tile_vectors(h->plan.dtype, h->nsrc), tiles = 0;
+  int i, rc;
+  for (i = 0; i < nb; i++) {
+    long n = b[i].scalar ? b[i].nvec : b[i].nvec;
+    long t = (n + tv - 1) / tv;
+    if (!b[i].scalar && t == 0 && b[i].head + b[i].tail > 0) t = 1;
+    if (t == 0) t = 1;
+    b[i].tile0 = tiles;
+    tiles += t;
+  }
+  h->nb = nb;
+  h->ntiles = tiles;
+  if (!nb) return 0;
+  if ((rc = emac_gpu_malloc((void **)&h->d_buckets, sizeof(emac_bucket) * (size_t)nb))) return rc;
+  return emac_gpu_memcpy(h->d_buckets, b, sizeof(emac_bucket) * (size_t)nb);
+}
+
+static int parse_cfg(const char *copyin, int nranks, emac_copyin *cfg) {
+  if (!copyin || !*copyin) {
+    emac_default_copyin(nranks, cfg);
+    return 0;
+  }
+  return emac_parse_copyin(copyin, cfg);
+}
+
+static int finish_init(emac_handle *h, int *handle) {
+  int slot = new_handle_slot();
+  h->own_stream = 1;
+  if (slot < 0) return EMAC_ERR_MALLOC;
+  handles[slot] = h;
+  *handle = slot;
+  return 0;
+}
+
+int ext_mpi_amd_node_allreduce_init(int nranks, const void *const *sendbufs, void *const *recvbufs, long count,
+                                    int dtype, int op, const char *copyin, int *handle) {
+  emac_handle *h;
+  emac_copyin cfg;
+  emac_bucket *b = NULL;
+  int rc, r, pc, c, t, nb = 0;
+  if (!handle || !sendbufs || !recvbufs || nranks < 1 || nranks > EMAC_MAX_RANKS || count < 0)
+    return EMAC_ERR_ARG;
+  *handle = -1;
+  if ((rc = parse_cfg(copyin, nranks, &cfg))) return rc;
+  if (emac_gpu_device_count() <= 0) return EMAC_ERR_DEVICE;
+  h = (emac_handle *)calloc(1, sizeof(emac_handle));
+  if (!h) return EMAC_ERR_MALLOC;
+  h->kind = KIND_NODE;
+  if ((rc = emac_plan_build(&h->plan, nranks, count, dtype, op, &cfg))) goto fail;
+  emac_gpu_get_device(&h->device);
+  h->bytes = (size_t)count * (size_t)h->plan.tsize;
+  h->nbuf = nranks;
+  h->nsrc = nranks;
+  for (r = 0; r < nranks; r++)
+    if ((rc = map_buffers(h, r, sendbufs[r], recvbufs[r]))) goto fail;
+  b = (emac_bucket *)calloc((size_t)h->plan.npieces * nranks, sizeof(emac_bucket));
+  if (!b) {
+    rc = EMAC_ERR_MALLOC;
+    goto fail;
+  }
+  for (pc = 0; pc < h->plan.npieces; pc++) {
+    for (c = 0; c < nranks; c++) {
+      long off = h->plan.chunk_off[(size_t)pc * nranks + c], len = h->plan.chunk_len[(size_t)pc * nranks + c];
+      emac_bucket *bk = &b[nb];
+      if (len <= 0) continue;
+      for (t = 0; t < nranks; t++) bk->src[t] = h->dsend[h->plan.leaf_rank[c][t]];
+      for (r = 0; r < nranks; r++) bk->dst[r] = h->drecv[r];
+      bk->ndst = nranks;
+      split_alignment(bk, nranks, off, len, h->plan.tsize);
+      nb++;
+    }
+  }
+  if ((rc = upload_buckets(h, b, nb))) goto fail;
+  free(b);
+  b = NULL;
+  if ((rc = emac_gpu_stream_create(&h->stream))) goto fail;
+  if ((rc = finish_init(h, handle))) goto fail;
+  return 0;
+fail:
+  free(b);
+  release(h);
+  return rc;
+}
+
+/* ------------------------------ COMM form (RCCL) ------------------------------ */
+
+int ext_mpi_amd_get_unique_id(void *id) {
+  ncclUniqueId u;
+  if (!id) return EMAC_ERR_ARG;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return EMAC_ERR_TRANSPORT;
+  memcpy(id, &u, sizeof(u));
+  return 0;
+}
+
+int ext_mpi_amd_comm_init(int rank, int size, const void *id, int device, int *comm) {
+  ncclUniqueId u;
+  int i;
+  if (!id || !comm || size < 1 || size > EMAC_MAX_RANKS || rank < 0 || rank >= size) return EMAC_ERR_ARG;
+  if (emac_gpu_device_count() <= 0) return EMAC_ERR_DEVICE;
+  for (i = 0; i < MAX_COMMS && comms[i].used; i++);
+  if (i == MAX_COMMS) return EMAC_ERR_MALLOC;
+  if (device >= 0 && emac_gpu_set_device(device)) return EMAC_ERR_DEVICE;
+  emac_gpu_get_device(&comms[i].device);
+  memcpy(&u, id, sizeof(u));
+  if (ncclCommInitRank(&comms[i].nccl, size, u, rank) != ncclSuccess) return EMAC_ERR_TRANSPORT;
+  comms[i].used = 1;
+  comms[i].rank = rank;
+  comms[i].size = size;
+  *comm = i;
+  return 0;
+}
+
+int ext_mpi_amd_comm_free(int comm) {
+  if (comm < 0 || comm >= MAX_COMMS || !comms[comm].used) return EMAC_ERR_ARG;
+  ncclCommDestroy(comms[comm].nccl);
+  comms[comm].used = 0;
+  return 0;
+}
+
+int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, int dtype, int op, int comm,
+                               const char *copyin, int *handle) {
+  emac_handle *h;
+  emac_comm *cm;
+  emac_copyin cfg;
+  emac_bucket *b = NULL;
+  int rc, pc, t, R, nb = 0;
+  long stage_total = 0;
+  if (!handle || comm < 0 || comm >= MAX_COMMS || !comms[comm].used || count < 0) return EMAC_ERR_ARG;
+  *handle = -1;
+  cm = &comms[comm];
+  R = cm->size;
+  if ((rc = parse_cfg(copyin, R, &cfg))) return rc;
+  if (emac_gpu_set_device(cm->device)) return EMAC_ERR_DEVICE;
+  h = (emac_handle *)calloc(1, sizeof(emac_handle));
+  if (!h) return EMAC_ERR_MALLOC;
+  h->kind = KIND_COMM;
+  h->comm = comm;
+  h->device = cm->device;
+  if ((rc = emac_plan_build(&h->plan, R, count, dtype, op, &cfg))) goto fail;
+  h->me = cm->rank;
+  h->me_pos = h->plan.rank_pos[h->me];
+  h->bytes = (size_t)count * (size_t)h->plan.tsize;
+  h->nbuf = 1;
+  h->nsrc = R;
+  if ((rc = map_buffers(h, 0, sendbuf, recvbuf))) goto fail;
+  h->stage_off = (long *)calloc((size_t)h->plan.npieces, sizeof(long));
+  h->stage_stride = (long *)calloc((size_t)h->plan.npieces, sizeof(long));
+  h->stage_mis = (long *)calloc((size_t)h->plan.npieces, sizeof(long));
+  b = (emac_bucket *)calloc((size_t)h->plan.npieces, sizeof(emac_bucket));
+  if (!h->stage_off || !h->stage_stride || !h->stage_mis || !b) {
+    rc = EMAC_ERR_MALLOC;
+    goto fail;
+  }
+  /* peer slots of a piece start at the same 16-byte phase as the chunk in the send buffer,
+     so the fold keeps its dwordx4 path */
+  for (pc = 0; pc < h->plan.npieces; pc++) {
+    long off = h->plan.chunk_off[(size_t)pc * R + h->me_pos], len = h->plan.chunk_len[(size_t)pc * R + h->me_pos];
+    h->stage_mis[pc] = (long)(((unsigned long)h->dsend[0] + (unsigned long)(off * h->plan.tsize)) & 15ul);
+    h->stage_stride[pc] = ((len * h->plan.tsize + 15) / 16) * 16 + 16;
+    h->stage_off[pc] = stage_total;
+    stage_total += (long)(R - 1) * h->stage_stride[pc];
+  }
+  if ((rc = emac_gpu_malloc(&h->staging, (size_t)stage_total))) goto fail;
+  for (pc = 0; pc < h->plan.npieces; pc++) {
+    long off = h->plan.chunk_off[(size_t)pc * R + h->me_pos], len = h->plan.chunk_len[(size_t)pc * R + h->me_pos];
+    emac_bucket *bk = &b[nb];
+    if (len <= 0) continue;
+    for (t = 0; t < R; t++) {
+      int q = h->plan.leaf_rank[h->me_pos][t];
+      if (q == h->me) {
+        bk->src[t] = h->dsend[0];
+      } else {
+        /* shifted back by the chunk offset: split_alignment adds it to every pointer */
+        bk->src[t] = (const char *)h->staging + stage_slot(h, pc, q) - off * h->plan.tsize;
+      }
+    }
+    bk->dst[0] = h->drecv[0];
+    bk->ndst = 1;
+    split_alignment(bk, R, off, len, h->plan.tsize);
+    nb++;
+  }
+  if ((rc = upload_buckets(h, b, nb))) goto fail;
+  free(b);
+  b = NULL;
+  if ((rc = emac_gpu_stream_create(&h->stream))) goto fail;
+  if ((rc = finish_init(h, handle))) goto fail;
+  return 0;
+fail:
+  free(b);
+  release(h);
+  return rc;
+}
+
+/* byte offset, inside the staging buffer, of peer q's slice of this rank's chunk of piece pc */
+static long stage_slot(const emac_handle *h, int pc, int q) {
+  int R = h->plan.nranks;
+  long slot = (q - h->me - 1 + R) % R;
+  return h->stage_off[pc] + slot * h->stage_stride[pc] + h->stage_mis[pc];
+}
+
+/* reduce-scatter leg: every rank sends its slice of each owner chunk to the owner */
+static int exchange_reduce_scatter(emac_handle *h) {
+  emac_comm *cm = &comms[h->comm];
+  hipStream_t s = (hipStream_t)h->stream;
+  int R = cm->size, pc, q;
+  long tsize = h->plan.tsize;
+  if (ncclGroupStart() != ncclSuccess) return EMAC_ERR_TRANSPORT;
+  for (pc = 0; pc < h->plan.npieces; pc++) {
+    long mylen = h->plan.chunk_len[(size_t)pc * R + h->me_pos];
+    for (q = 0; q < R; q++) {
+      long qoff, qlen;
+      if (q == h->me) continue;
+      qoff = h->plan.chunk_off[(size_t)pc * R + h->plan.rank_pos[q]];
+      qlen = h->plan.chunk_len[(size_t)pc * R + h->plan.rank_pos[q]];
+      if (qlen > 0 &&
+          ncclSend((const char *)h->dsend[0] + qoff * tsize, (size_t)(qlen * tsize), ncclInt8, q, cm->nccl, s) !=
+              ncclSuccess)
+        goto err;
+      if (mylen > 0) {
+        char *dst = (char *)h->staging + stage_slot(h, pc, q);
+        if (ncclRecv(dst, (size_t)(mylen * tsize), ncclInt8, q, cm->nccl, s) != ncclSuccess) goto err;
+      }
+    }
+  }
+  return ncclGroupEnd() == ncclSuccess ? 0 : EMAC_ERR_TRANSPORT;
+err:
+  ncclGroupEnd();
+  return EMAC_ERR_TRANSPORT;
+}
+
+/* allgather leg: the owned (folded) chunk goes to every peer's receive buffer */
+static int exchange_allgather(emac_handle *h) {
+  emac_comm *cm = &comms[h->comm];
+  hipStream_t s = (hipStream_t)h->stream;
+  int R = cm->size, pc, q;
+  long tsize = h->plan.tsize;
+  if (ncclGroupStart() != ncclSuccess) return EMAC_ERR_TRANSPORT;
+  for (pc = 0; pc < h->plan.npieces; pc++) {
+    long myoff = h->plan.chunk_off[(size_t)pc * R + h->me_pos], mylen = h->plan.chunk_len[(size_t)pc * R + h->me_pos];
+    for (q = 0; q < R; q++) {
+      long qoff, qlen;
+      if (q == h->me) continue;
+      qoff = h->plan.chunk_off[(size_t)pc * R + h->plan.rank_pos[q]];
+      qlen = h->plan.chunk_len[(size_t)pc * R + h->plan.rank_pos[q]];
+      if (mylen > 0 &&
+          ncclSend((const char *)h->drecv[0] + myoff * tsize, (size_t)(mylen * tsize), ncclInt8, q, cm->nccl, s) !=
+              ncclSuccess)
+        goto err;
+      if (qlen > 0 &&
+          ncclRecv((char *)h->drecv[0] + qoff * tsize, (size_t)(qlen * tsize), ncclInt8, q, cm->nccl, s) != ncclSuccess)
+        goto err;
+    }
+  }
+  return ncclGroupEnd() == ncclSuccess ? 0 : EMAC_ERR_TRANSPORT;
+err:
+  ncclGroupEnd();
+  return EMAC_ERR_TRANSPORT;
+}
+
+static int stage_in(emac_handle *h) {
+  int r, rc;
+  for (r = 0; r < h->nbuf; r++) {
+    void *src = h->send_mirror[r] ? h->user_send[r] : (h->recv_mirror[r] && h->dsend[r] == h->drecv[r] ? h->user_recv[r] : NULL);
+    if (src && (rc = emac_gpu_memcpy_async(h->dsend[r], src, h->bytes, h->stream))) return rc;
+  }
+  return 0;
+}
+
+static int stage_out(emac_handle *h) {
+  int r, rc;
+  for (r = 0; r < h->nbuf; r++)
+    if (h->recv_mirror[r] && (rc = emac_gpu_memcpy_async(h->user_recv[r], h->drecv[r], h->bytes, h->stream)))
+      return rc;
+  return 0;
+}
+
+static emac_handle *get(int handle) {
+  if (handle < 0 || handle >= MAX_HANDLES) return NULL;
+  return handles[handle];
+}
+
+int ext_mpi_amd_start_legs(int handle, int legs) {
+  emac_handle *h = get(handle);
+  int rc, multi;
+  if (!h) return EMAC_ERR_ARG;
+  multi = h->kind == KIND_COMM && h->plan.nranks > 1;
+  if (emac_gpu_set_device(h->device)) return EMAC_ERR_DEVICE;
+  if ((legs & EXT_MPI_AMD_LEG_STAGE) && (rc = stage_in(h))) return rc;
+  if ((legs & EXT_MPI_AMD_LEG_REDUCE_SCATTER) && multi && (rc = exchange_reduce_scatter(h))) return rc;
+  if ((legs & EXT_MPI_AMD_LEG_FOLD) &&
+      (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, &h->plan.codes, h->d_buckets, h->nb, h->ntiles,
+                          h->stream)))
+    return rc;
+  if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && multi && (rc = exchange_allgather(h))) return rc;
+  if ((legs & EXT_MPI_AMD_LEG_STAGE) && (rc = stage_out(h))) return rc;
+  h->started = 1;
+  return 0;
+}
+
+int ext_mpi_amd_start(int handle) { return ext_mpi_amd_start_legs(handle, EXT_MPI_AMD_LEG_ALL); }
+
+int ext_mpi_amd_set_stream(int handle, void *stream) {
+  emac_handle *h = get(handle);
+  if (!h || !stream) return EMAC_ERR_ARG;
+  emac_gpu_stream_sync(h->stream);
+  if (h->own_stream) emac_gpu_stream_destroy(h->stream);
+  h->stream = stream;
+  h->own_stream = 0;
+  return 0;
+}
+
+int ext_mpi_amd_test(int handle) {
+  emac_handle *h = get(handle);
+  int rc;
+  if (!h) return EMAC_ERR_ARG;
+  if (!h->started) return 1;
+  rc = emac_gpu_stream_query(h->stream);
+  if (rc == 1) h->started = 0;
+  return rc;
+}
+
+int ext_mpi_amd_wait(int handle) {
+  emac_handle *h = get(handle);
+  int rc;
+  if (!h) return EMAC_ERR_ARG;
+  rc = emac_gpu_stream_sync(h->stream);
+  h->started = 0;
+  return rc;
+}
+
+int ext_mpi_amd_done(int handle) {
+  emac_handle *h = get(handle);
+  if (!h) return EMAC_ERR_ARG;
+  handles[handle] = NULL;
+  release(h);
+  return 0;
+}
+
+void *ext_mpi_amd_stream(int handle) {
+  emac_handle *h = get(handle);
+  return h ? h->stream : NULL;
+}
+
+int ext_mpi_amd_plan_describe(int nranks, long count, int dtype, const char *copyin, int pos, long *piece_off,
+                              long *piece_len, int max_pieces, int *owner_rank, int *leaf_ranks,
+                              unsigned char *first, unsigned char *close, int *nlev) {
+  emac_plan p;
+  emac_copyin cfg;
+  int rc, pc, t, n;
+  if (nranks < 1 || nranks > EMAC_MAX_RANKS || pos < 0 || pos >= nranks) return EMAC_ERR_ARG;
+  if ((rc = parse_cfg(copyin, nranks, &cfg))) return rc;
+  if ((rc = emac_plan_build(&p, nranks, count, dtype, EMAC_SUM, &cfg))) return rc;
+  n = p.npieces < max_pieces ? p.npieces : max_pieces;
+  for (pc = 0; pc < n; pc++) {
+    piece_off[pc] = p.chunk_off[(size_t)pc * nranks + pos];
+    piece_len[pc] = p.chunk_len[(size_t)pc * nranks + pos];
+  }
+  *owner_rank = p.pos_rank[pos];
+  for (t = 0; t < p.codes.nleaf; t++) {
+    leaf_ranks[t] = p.leaf_rank[pos][t];
+    first[t] = p.codes.first[t];
+    close[t] = p.codes.close[t];
+  }
+  *nlev = p.codes.nlev;
+  rc = p.npieces;
+  emac_plan_free(&p);
+  return rc;
+}
+
+const char *ext_mpi_amd_version(void) { return "ext_mpi_collectives_amd 0.1 (gfx950)"; }

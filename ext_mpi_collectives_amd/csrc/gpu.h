@@ -1,0 +1,62 @@
+/*
+ * gpu.h -- internal C ABI between the host C engine and the HIP code (fold.hip).
+ *
+ * Replaces the reference's device C-ABI include/gpu/gpu_core.h:11-22 (ext_mpi_gpu_malloc,
+ * _free, _memcpy_hd/_dh, _is_device_pointer, _synchronize, _copy_reduce). Differences that
+ * matter on MI355X: sizes are size_t (the reference's int caps buffers at 2 GiB, far below
+ * 288 GB of HBM3E), every operation is stream-ordered instead of device-synchronous, and
+ * the fold takes per-chunk bucket descriptors instead of a per-element descriptor walk.
+ */
+#ifndef EMAC_GPU_H_
+#define EMAC_GPU_H_
+
+#include <stddef.h>
+#include "plan.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* One owner chunk of a launch: `nsrc` leaves (plan leaf order) folded element-wise and the
+   result stored to `ndst` destinations. Element e of the chunk is at src[t] + e (elements). */
+typedef struct {
+  const void *src[EMAC_MAX_RANKS];
+  void *dst[EMAC_MAX_RANKS];
+  long head;   /* leading elements before the first 16-byte aligned vector (scalar path) */
+  long nvec;   /* 16-byte vectors after the head (or, if scalar, all elements) */
+  long tail;   /* trailing elements after the vectors (scalar path) */
+  long tile0;  /* first tile index of this bucket inside the launch */
+  int ndst;
+  int scalar;  /* 1: pointers disagree on 16-byte alignment -> element-granular path */
+} emac_bucket;
+
+#define EMAC_BLOCK 256
+
+int emac_gpu_device_count(void);
+int emac_gpu_get_device(int *dev);
+int emac_gpu_set_device(int dev);
+int emac_gpu_malloc(void **p, size_t bytes);
+int emac_gpu_free(void *p);
+int emac_gpu_memcpy(void *dst, const void *src, size_t bytes); /* synchronous, any direction */
+int emac_gpu_memcpy_async(void *dst, const void *src, size_t bytes, void *stream);
+int emac_gpu_memset_async(void *dst, int v, size_t bytes, void *stream);
+int emac_gpu_is_device_pointer(const void *p);
+int emac_gpu_host_register(void *p, size_t bytes);
+int emac_gpu_host_unregister(void *p);
+int emac_gpu_stream_create(void **stream);
+int emac_gpu_stream_destroy(void *stream);
+int emac_gpu_stream_sync(void *stream);
+int emac_gpu_stream_query(void *stream); /* 1 idle, 0 busy, <0 error */
+int emac_gpu_device_sync(void);
+
+/* vectors (16 B) one tile covers for an nsrc-leaf fold of dtype */
+long emac_gpu_tile_vectors(int dtype, int nsrc);
+
+/* Launch the fold over nb device-resident buckets (ntiles tiles in total) on `stream`. */
+int emac_gpu_fold(int dtype, int op, int nsrc, const emac_codes *codes, const emac_bucket *d_buckets,
+                  int nb, long ntiles, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

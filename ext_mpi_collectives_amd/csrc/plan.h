@@ -1,0 +1,86 @@
+/*
+ * plan.h -- schedule planner of the MI355X bucket-reduction path (host C, no HIP).
+ *
+ * The reference compiles EXT_MPI_COPYIN into a text IR of SMEMCPY/SREDUCE lines
+ * (src/core/reduce_copyin.c:674-842), assembles it into bytecode (src/core/byte_code.c) and
+ * interprets it line by line. This planner computes the same arithmetic directly:
+ *
+ *   - the chunk partition of the message (reduce_copyin.c:396-427),
+ *   - the permuted rank order of radix chains (reduce_copyin.c:375-394),
+ *   - for every owner chunk, the exact fold tree its elements are summed in: the left fold
+ *     of each recursive-halving step (own partial first, partners by ascending substep) nested
+ *     step over step (reduce_copyin.c:687-744), flattened to a leaf order plus per-leaf
+ *     level codes that a register-resident kernel replays without any intermediate buffer.
+ *
+ * Because every leaf is read exactly once and the tree is evaluated in registers, a whole
+ * multi-step reduce-scatter (and the allgather fan-out) becomes ONE pass over HBM while the
+ * per-element operation order, and therefore every float/double bit, stays the reference's.
+ */
+#ifndef EMAC_PLAN_H_
+#define EMAC_PLAN_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EMAC_MAX_RANKS 16  /* ranks of one node fold (sources and fan-out destinations) */
+#define EMAC_MAX_LEVELS 8  /* radices in one leg */
+#define EMAC_MAX_PIECES 65536
+
+/* element types: same codes as include/ext_mpi_amd.h */
+enum { EMAC_DOUBLE = 0, EMAC_LONG = 1, EMAC_FLOAT = 2, EMAC_INT = 3 };
+enum { EMAC_SUM = 0, EMAC_MIN = 1, EMAC_MAX = 2 };
+
+/* error codes (the first two follow include/core/constants.h:67-69 of the reference) */
+enum {
+  EMAC_OK = 0,
+  EMAC_ERR_MALLOC = -1,
+  EMAC_ERR_SHMEM = -2,
+  EMAC_ERR_ARG = -3,
+  EMAC_ERR_UNSUPPORTED = -4,
+  EMAC_ERR_DEVICE = -5,
+  EMAC_ERR_TRANSPORT = -6
+};
+
+typedef struct {
+  int method;                  /* 6 (recursive); 9 is accepted as its shm-staged alias */
+  int split;                   /* factors[0]: k>0 equal pieces, -k fixed k-element fractions */
+  int nrs, rs[EMAC_MAX_LEVELS]; /* reduce-scatter radices, in application order */
+  int nag, ag[EMAC_MAX_LEVELS]; /* allgather radices (0 of them = direct push) */
+} emac_copyin;
+
+int emac_parse_copyin(const char *s, emac_copyin *out);
+void emac_default_copyin(int nranks, emac_copyin *out); /* "6;1 -R R" */
+int emac_validate_copyin(const emac_copyin *c, int nranks);
+int emac_type_size(int dtype);
+
+/* per-leaf replay codes of a fold tree (shared by every chunk of a plan) */
+typedef struct {
+  unsigned char first[EMAC_MAX_RANKS]; /* bit l: leaf t opens a fresh level-l accumulator */
+  unsigned char close[EMAC_MAX_RANKS]; /* levels completed right after leaf t */
+  int nlev;
+  int nleaf;
+} emac_codes;
+
+typedef struct {
+  int nranks;
+  int dtype, tsize, op;
+  long count;                             /* elements */
+  emac_copyin cfg;
+  int pos_rank[EMAC_MAX_RANKS];           /* position -> node rank */
+  int rank_pos[EMAC_MAX_RANKS];           /* node rank -> position */
+  int npieces;
+  long *chunk_off;                        /* [piece * nranks + position], elements */
+  long *chunk_len;
+  int leaf_rank[EMAC_MAX_RANKS][EMAC_MAX_RANKS]; /* [owner position][leaf t] = node rank */
+  emac_codes codes;
+} emac_plan;
+
+/* Build the plan of an nranks-rank Allreduce of `count` elements. 0 or an EMAC_ERR_* code. */
+int emac_plan_build(emac_plan *p, int nranks, long count, int dtype, int op, const emac_copyin *cfg);
+void emac_plan_free(emac_plan *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,104 @@
+/*
+ * ext_mpi_amd.h -- MPI-free C ABI of the MI355X bucket-reduction path
+ * (libext_mpi_amd.so, ext_mpi_collectives_amd/).
+ *
+ * Plain C: pointers, sizes and int handles only. Every entry point mirrors a reference entry
+ * point (paths relative to the eth-cscs/ext_mpi_collectives checkout):
+ *
+ *   ext_mpi_amd_allreduce_init   <- EXT_MPI_Allreduce_init      include/mpi/ext_mpi.h:75-77,
+ *                                   src/mpi/ext_mpi.c:974-979 -> ext_mpi_allreduce_init_general
+ *                                   :626-729 (one rank per GPU; legs over RCCL on xGMI)
+ *   ext_mpi_amd_node_allreduce_init <- the same persistent Allreduce with every node rank's
+ *                                   buffers mapped into one process: the reference maps peers
+ *                                   with XPMEM (src/mpi/ext_mpi_xpmem.c:68-133) or CUDA IPC
+ *                                   (src/gpu/cuda_shmem.c:218-299) and executes copy-in
+ *                                   method 6 on them; here all ranks live in one GPU's HBM
+ *   ext_mpi_amd_start            <- EXT_MPI_Start  ext_mpi.h:86, ext_mpi.c:1011-1017
+ *   ext_mpi_amd_test             <- EXT_MPI_Test   ext_mpi.h:87, ext_mpi.c:1019-1025
+ *   ext_mpi_amd_wait             <- EXT_MPI_Wait   ext_mpi.h:88, ext_mpi.c:1027-1033
+ *   ext_mpi_amd_done             <- EXT_MPI_Done   ext_mpi.h:89, ext_mpi.c:1035-1041
+ *   ext_mpi_amd_get_unique_id /
+ *   ext_mpi_amd_comm_init / _free <- the node communicator set-up of EXT_MPI_Init_native
+ *                                   (src/mpi/ext_mpi_native.c:1895-1911), which the MPI layer
+ *                                   (libext_mpi_collectives.so) bootstraps with PMPI_Bcast
+ *   ext_mpi_amd_plan_describe    <- the text IR the reference's pipe-stage tests print
+ *                                   (tests/test_*.c): the fold schedule, for inspection/tests
+ *
+ * Return codes: 0 success; EXT_MPI_AMD_ERROR_MALLOC (-1) and EXT_MPI_AMD_ERROR_SHMEM (-2) as
+ * ERROR_MALLOC / ERROR_SHMEM in include/core/constants.h:67-69; the others are new. Unlike
+ * the reference (which exit()s on GPU errors, src/gpu/cuda_core.cu:14-48), errors are
+ * returned, never fatal.
+ *
+ * Configuration: `copyin` is an EXT_MPI_COPYIN string ("6;1 -8 8", "6;1 -2 -2 -2 2 2 2",
+ * "6;-64 -8 8", "9;..." as alias of 6); NULL means "6;1 -R R" (the reference requires the
+ * variable, README "Installation"). Threading: MPI_THREAD_SERIALIZED, like the reference.
+ */
+#ifndef EXT_MPI_AMD_H_
+#define EXT_MPI_AMD_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* element types (reference opcode order: OPCODE_REDUCE_SUM_DOUBLE, _LONG_INT, _FLOAT, _INT) */
+#define EXT_MPI_AMD_DOUBLE 0
+#define EXT_MPI_AMD_LONG 1
+#define EXT_MPI_AMD_FLOAT 2
+#define EXT_MPI_AMD_INT 3
+/* operations (only SUM is on the hot path) */
+#define EXT_MPI_AMD_SUM 0
+
+#define EXT_MPI_AMD_SUCCESS 0
+#define EXT_MPI_AMD_ERROR_MALLOC (-1)
+#define EXT_MPI_AMD_ERROR_SHMEM (-2)
+#define EXT_MPI_AMD_ERROR_ARG (-3)
+#define EXT_MPI_AMD_ERROR_UNSUPPORTED (-4)
+#define EXT_MPI_AMD_ERROR_DEVICE (-5)
+#define EXT_MPI_AMD_ERROR_TRANSPORT (-6)
+
+#define EXT_MPI_AMD_UNIQUE_ID_BYTES 128
+#define EXT_MPI_AMD_MAX_RANKS 16
+
+/* ---- persistent Allreduce, every node rank's buffers in this process (one device) ---- */
+int ext_mpi_amd_node_allreduce_init(int nranks, const void *const *sendbufs, void *const *recvbufs, long count,
+                                    int dtype, int op, const char *copyin, int *handle);
+
+/* ---- node communicator: one rank per GPU, reduce-scatter / allgather legs over RCCL ---- */
+int ext_mpi_amd_get_unique_id(void *id /* EXT_MPI_AMD_UNIQUE_ID_BYTES */);
+int ext_mpi_amd_comm_init(int rank, int size, const void *id, int device, int *comm);
+int ext_mpi_amd_comm_free(int comm);
+int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, int dtype, int op, int comm,
+                               const char *copyin, int *handle);
+
+/* ---- execution (stream-ordered on the handle's own HIP stream) ---- */
+int ext_mpi_amd_start(int handle);
+int ext_mpi_amd_test(int handle); /* 1 complete, 0 in flight, <0 error */
+int ext_mpi_amd_wait(int handle);
+int ext_mpi_amd_done(int handle);
+void *ext_mpi_amd_stream(int handle); /* hipStream_t the handle runs on */
+/* Run later Starts on a caller-owned hipStream_t (e.g. to serialise several handles). */
+int ext_mpi_amd_set_stream(int handle, void *hip_stream);
+/* Start a subset of the legs (benchmarking / profiling): the reference interleaves them in one
+   byte-code stream (src/mpi/ext_mpi_native_exec.c:345-587); here they are separable. */
+#define EXT_MPI_AMD_LEG_STAGE 1          /* H2D / D2H of host buffers */
+#define EXT_MPI_AMD_LEG_REDUCE_SCATTER 2 /* COMM form: slice exchange (reduce_copyin transport) */
+#define EXT_MPI_AMD_LEG_FOLD 4           /* the bucket fold kernel (+ node fan-out) */
+#define EXT_MPI_AMD_LEG_ALLGATHER 8      /* COMM form: owned chunk to every peer (reduce_copyout) */
+#define EXT_MPI_AMD_LEG_ALL 15
+int ext_mpi_amd_start_legs(int handle, int legs);
+
+/* ---- introspection (no GPU needed) ----
+ * Fold schedule of owner position `pos` of an nranks-rank plan: element range of each piece
+ * and the node ranks of the leaves in fold order; level codes per leaf. Returns the number of
+ * pieces written (<= max_pieces) or an error code. leaf_ranks needs nranks ints; first/close
+ * need nranks bytes each. owner_rank receives the node rank owning position `pos`. */
+int ext_mpi_amd_plan_describe(int nranks, long count, int dtype, const char *copyin, int pos, long *piece_off,
+                              long *piece_len, int max_pieces, int *owner_rank, int *leaf_ranks,
+                              unsigned char *first, unsigned char *close, int *nlev);
+
+const char *ext_mpi_amd_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,96 @@
+/*
+ * ref_emulate.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Single-process emulator of an R-rank, single-node ext_mpi Allreduce (copy-in method 6):
+ * every rank's copy-in and copy-out program (ref_schedule.c) is executed against host
+ * buffers, phase by phase. A phase ends at a SET_NODE_BARRIER line; the reference orders
+ * each step after its partners' previous step with pairwise spin flags
+ * (ext_mpi_native_exec.c:21-84, :513-528), which a global lock-step reproduces for a
+ * race-free schedule. Rank-relative buffer indices resolve as ext_mpi_xpmem.c:114-130:
+ * index j of rank r is the buffer of node rank (r + j) mod R.
+ */
+#include <stdlib.h>
+#include <string.h>
+#include "ref_oracle.h"
+
+#define MAX_FACTORS 64
+
+typedef struct {
+  ref_op *ops;
+  int n;
+  int pc;
+} rank_prog;
+
+static int build_programs(int R, long count, int dtype, const char *copyin, int in_place,
+                          rank_prog *progs) {
+  int method, factors[MAX_FACTORS], nf, r, cap;
+  long bytes = count * (long)ref_type_size(dtype);
+  nf = ref_parse_copyin(copyin, &method, factors, MAX_FACTORS);
+  if (nf < 1) return -1;
+  cap = 8 * R * (R + 8) * (factors[0] > 0 ? factors[0] : 1) + 256;
+  if (method != 6 && method != 9) return -1; /* 9 = the same generator on shm staging */
+  for (r = 0; r < R; r++) {
+    int n1, n2;
+    progs[r].ops = (ref_op *)malloc(sizeof(ref_op) * (size_t)cap * 2);
+    progs[r].pc = 0;
+    n1 = ref_schedule(R, r, bytes, dtype, factors, nf, in_place, 1, progs[r].ops, cap);
+    if (n1 < 0) return -1;
+    progs[r].ops[n1].op = REF_OP_PHASE; /* copy-in and copy-out are separate stages */
+    n2 = ref_schedule(R, r, bytes, dtype, factors, nf, in_place, 2, progs[r].ops + n1 + 1, cap);
+    if (n2 < 0) return -1;
+    progs[r].n = n1 + 1 + n2;
+  }
+  return 0;
+}
+
+static void exec_op(int R, int r, const ref_op *o, int dtype, void *const *send, void *const *recv) {
+  char *dst = (char *)(o->dbuf == REF_BUF_RECV ? recv : send)[(r + o->drel) % R] + o->doff;
+  const char *src = (const char *)(o->sbuf == REF_BUF_RECV ? recv : send)[(r + o->srel) % R] + o->soff;
+  if (o->op == REF_OP_COPY) {
+    if (dst != src) memmove(dst, src, (size_t)o->bytes);
+  } else if (o->op == REF_OP_SUM) {
+    ref_reduction(dtype, dst, src, o->bytes / ref_type_size(dtype));
+  }
+}
+
+int ref_emulate(int R, long count, int dtype, const char *copyin, int in_place,
+                void *const *sendbufs, void *const *recvbufs) {
+  rank_prog *progs;
+  void *const *send = in_place ? recvbufs : sendbufs;
+  int r, active, rc = 0;
+  if (R < 1 || count < 0 || ref_type_size(dtype) <= 0) return -1;
+  if (R == 1) { /* a one-rank allreduce is a copy */
+    if (!in_place) memcpy(recvbufs[0], sendbufs[0], (size_t)(count * ref_type_size(dtype)));
+    return 0;
+  }
+  progs = (rank_prog *)calloc((size_t)R, sizeof(rank_prog));
+  if (build_programs(R, count, dtype, copyin, in_place, progs)) {
+    rc = -1;
+    goto done;
+  }
+  do {
+    active = 0;
+    for (r = 0; r < R; r++) {
+      rank_prog *p = &progs[r];
+      while (p->pc < p->n && p->ops[p->pc].op != REF_OP_PHASE) exec_op(R, r, &p->ops[p->pc++], dtype, send, recvbufs);
+      if (p->pc < p->n) p->pc++; /* step over the phase marker */
+      if (p->pc < p->n) active = 1;
+    }
+  } while (active);
+done:
+  for (r = 0; r < R; r++) free(progs[r].ops);
+  free(progs);
+  return rc;
+}
+
+/* debug_persistent.c:491-497 (host pattern, add = 73) and :426-432 (device pattern, add = 0) */
+void ref_kat_fill(void *buf, long count, int tsize, int world_rank, long add) {
+  long i, words = (count * tsize) / (long)sizeof(long int);
+  for (i = 0; i < words; i++) ((long int *)buf)[i] = world_rank * count + i + add;
+  if ((count * tsize) % (long)sizeof(long int)) ((int *)buf)[count - 1] = (int)(world_rank * count + count - 1);
+}
+
+/* exported for the threaded baseline */
+int ref_build_programs_(int R, long count, int dtype, const char *copyin, int in_place, void *progs_out) {
+  return build_programs(R, count, dtype, copyin, in_place, (rank_prog *)progs_out);
+}

@@ -1,0 +1,52 @@
+"""The product planner (ext_mpi_collectives_amd/csrc/plan.c, via ext_mpi_amd_plan_describe)
+against the oracle: replaying the described fold trees on the CPU must reproduce the
+oracle's emulation of the reference schedule bit for bit. No GPU needed."""
+import numpy as np
+import pytest
+
+import ext_mpi_collectives_amd as emac
+from helpers import ORACLE_CODE, replay_plan, xorshift_inputs
+
+CONFIGS = [
+    (2, "6;1 -2 2"), (2, "6;1 -2"), (2, "6;3 -2 2"), (2, "6;-5 -2 2"),
+    (3, "6;1 -3 3"),
+    (4, "6;1 -4 4"), (4, "6;1 -2 -2 2 2"), (4, "6;2 -2 -2 4"), (4, "6;-7 -4 4"), (4, "6;1 -2 -2"),
+    (6, "6;1 -6 6"), (6, "6;1 -2 -3 3 2"), (6, "6;1 -3 -2 2 3"),
+    (8, "6;1 -8 8"), (8, "6;1 -2 -2 -2 2 2 2"), (8, "6;1 -4 -2 2 4"), (8, "6;1 -2 -4 4 2"),
+    (8, "6;-64 -8 8"), (8, "6;3 -8 8"), (8, "9;1 -8 8"),
+    (12, "6;1 -2 -2 -3 3 2 2"), (16, "6;1 -16 16"), (16, "6;1 -2 -2 -2 -2 2 2 2 2"), (16, "6;1 -4 -4 4 4"),
+]
+CODES = [emac.FLOAT, emac.DOUBLE, emac.INT, emac.LONG]
+
+
+@pytest.mark.parametrize("R,copyin", CONFIGS)
+@pytest.mark.parametrize("code", CODES)
+def test_plan_replay_equals_oracle(oracle, R, copyin, code):
+    for count in (0, 1, 7, 1000, 4099):
+        sends = xorshift_inputs(R, count, code)
+        want = oracle.allreduce(sends, copyin)
+        got = replay_plan(sends, code, copyin)
+        for w in want:
+            assert np.array_equal(w.view(np.uint8), got.view(np.uint8)), (R, copyin, code, count)
+
+
+def test_default_copyin_is_linear():
+    d = emac.plan_describe(8, 800, emac.FLOAT, None, 3)
+    assert d["leaves"] == [3, 0, 1, 2, 4, 5, 6, 7]
+    assert d["pieces"] == [(300, 100)] and d["nlev"] == 1
+
+
+def test_chain_leaf_order():
+    # "6;1 -2 -2 -2 2 2 2", owner position 0 (node rank 0): ((s0+s1)+(s2+s3))+((s4+s5)+(s6+s7))
+    # in node ranks, per the captured schedule of golden/schedules_survey.json
+    d = emac.plan_describe(8, 16384, emac.FLOAT, "6;1 -2 -2 -2 2 2 2", 0)
+    assert d["leaves"] == [0, 1, 2, 3, 4, 5, 6, 7]
+    assert d["nlev"] == 3
+    d5 = emac.plan_describe(8, 16384, emac.FLOAT, "6;1 -2 -2 -2 2 2 2", 5)
+    assert d5["owner"] == 5 and d5["pieces"] == [(10240, 2048)]
+
+
+@pytest.mark.parametrize("bad", ["6;1 -3 3", "6;1 -2 -2 2", "5;1 -4 4", "6;1 4 -4", "6;1 -4 1 4", "garbage", "6;"])
+def test_invalid_copyin_rejected(bad):
+    with pytest.raises(emac.ExtMpiError):
+        emac.plan_describe(4, 100, emac.FLOAT, bad, 0)
