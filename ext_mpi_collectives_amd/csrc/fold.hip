@@ -18,6 +18,7 @@
 // keep IEEE round-to-nearest with denormals (no fast-math, no FTZ flags at build time).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "gpu.h"
 
@@ -295,5 +296,79 @@ int emac_gpu_stream_query(void *stream) {
   return EMAC_ERR_DEVICE;
 }
 int emac_gpu_device_sync(void) { return ok(hipDeviceSynchronize()); }
+
+}  // extern "C"
+
+// ---- exported device C ABI (include/ext_mpi_amd_gpu.h; reference include/gpu/gpu_core.h) ----
+extern "C" {
+
+int ext_mpi_amd_gpu_malloc(void **p, size_t bytes) { return emac_gpu_malloc(p, bytes); }
+int ext_mpi_amd_gpu_free(void *p) { return emac_gpu_free(p); }
+int ext_mpi_amd_gpu_memcpy_hd(void *dst, const void *src, size_t bytes) {
+  return bytes ? ok(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice)) : 0;
+}
+int ext_mpi_amd_gpu_memcpy_dh(void *dst, const void *src, size_t bytes) {
+  return bytes ? ok(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost)) : 0;
+}
+int ext_mpi_amd_gpu_is_device_pointer(const void *p) { return emac_gpu_is_device_pointer(p); }
+int ext_mpi_amd_gpu_synchronize(void) { return emac_gpu_device_sync(); }
+int ext_mpi_amd_gpu_device_count(void) { return emac_gpu_device_count(); }
+int ext_mpi_amd_gpu_device_of(const void *p) {
+  hipPointerAttribute_t a;
+  if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  return (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) ? a.device : -1;
+}
+
+// One owner chunk as a one-bucket launch (stream-ordered; the descriptor is staged through a
+// small device scratch owned by the call and released after the launch completes).
+int ext_mpi_amd_gpu_copy_reduce(int dtype, int op, int nsrc, const void *const *srcs, int ndst, void *const *dsts,
+                                long count, void *hip_stream) {
+  emac_bucket b;
+  emac_codes codes;
+  emac_bucket *d = nullptr;
+  int tsize = emac_type_size(dtype), rc, i;
+  if (tsize < 0 || nsrc < 1 || nsrc > EMAC_MAX_RANKS || ndst < 0 || ndst > EMAC_MAX_RANKS || count < 0)
+    return EMAC_ERR_ARG;
+  if (!count) return 0;
+  memset(&b, 0, sizeof(b));
+  memset(&codes, 0, sizeof(codes));
+  codes.nlev = 1;
+  codes.nleaf = nsrc;
+  codes.first[0] = 1;
+  codes.close[nsrc - 1] = 1;
+  for (i = 0; i < nsrc; i++) b.src[i] = srcs[i];
+  for (i = 0; i < ndst; i++) b.dst[i] = dsts[i];
+  b.ndst = ndst;
+  {
+    // same head/vector/tail split as the engine (all pointers must share the 16-byte phase)
+    unsigned long mis = (unsigned long)b.src[0] & 15ul;
+    long head = (mis % (unsigned long)tsize == 0) ? (long)((16ul - mis) & 15ul) / tsize : -1;
+    bool vec = head >= 0;
+    if (vec && head > count) head = count;
+    for (i = 0; vec && i < nsrc; i++) vec = (((unsigned long)b.src[i] + head * tsize) & 15ul) == 0;
+    for (i = 0; vec && i < ndst; i++) vec = (((unsigned long)b.dst[i] + head * tsize) & 15ul) == 0;
+    if (vec) {
+      b.head = head;
+      b.nvec = (count - head) * tsize / 16;
+      b.tail = count - head - b.nvec * (16 / tsize);
+    } else {
+      b.scalar = 1;
+      b.nvec = count;
+    }
+  }
+  long tv = emac_gpu_tile_vectors(dtype, nsrc);
+  long ntiles = (b.nvec + tv - 1) / tv;
+  if (ntiles == 0) ntiles = 1;
+  hipStream_t s = static_cast<hipStream_t>(hip_stream);
+  if (hipMallocAsync((void **)&d, sizeof(b), s) != hipSuccess) return EMAC_ERR_MALLOC;
+  if ((rc = ok(hipMemcpyAsync(d, &b, sizeof(b), hipMemcpyHostToDevice, s)))) return rc;
+  rc = emac_gpu_fold(dtype, op, nsrc, &codes, d, 1, ntiles, hip_stream);
+  (void)hipFreeAsync(d, s);
+  if (!rc) rc = ok(hipStreamSynchronize(s));  // the host descriptor lives on this stack frame
+  return rc;
+}
 
 }  // extern "C"

@@ -1,0 +1,464 @@
+/*
+ * mpi_interface.c -- libext_mpi_collectives.so: the reference's PMPI drop-in surface for the
+ * persistent Allreduce, on top of the MPI-free engine (libext_mpi_amd.so).
+ *
+ * Reference surface restated (src/mpi/ext_mpi_interface.c):
+ *   MPI_Init / MPI_Init_thread / MPI_Finalize    :71-183  (thread level capped at SERIALIZED)
+ *   MPI_Allreduce_init                           :185-192 (inert placeholder request from
+ *                                                          Recv_init + request->handle map)
+ *   MPI_Start(all), MPI_Wait(all|any|some),
+ *   MPI_Test(all|any|some), MPI_Request_free     :248-426 (requests not owned -> PMPI_*)
+ * and the native API EXT_MPI_Init / _Allreduce_init / _Start / _Test / _Wait / _Done /
+ * _Finalize (src/mpi/ext_mpi.c:974-1061, include/mpi/ext_mpi.h:69-89).
+ *
+ * Configuration as the reference reads it (ext_mpi.c:43-187; rank 0 reads the environment and
+ * broadcasts): EXT_MPI_COPYIN, EXT_MPI_VERBOSE, EXT_MPI_DEBUG (default 1: the known-answer
+ * self-test of debug_persistent.c:393-568 runs inside every Allreduce_init),
+ * EXT_MPI_NUM_SOCKETS_PER_NODE / EXT_MPI_NUM_TASKS_PER_SOCKET (one socket supported). MPI_Info
+ * key "ext_mpi_copyin" overrides nothing the environment sets (num_ports_factors.c:25-36:
+ * env > info > default).
+ *
+ * Transport: one RCCL communicator per MPI communicator, cached as an MPI attribute and
+ * destroyed with it; bootstrapped with PMPI_Bcast of the unique id. The communicator must lie
+ * within one node (the reference's inter-node legs are out of this path's scope).
+ */
+#include <mpi.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "ext_mpi.h"
+#include "ext_mpi_amd.h"
+#include "ext_mpi_amd_gpu.h"
+#include "ext_mpi_interface.h"
+
+/* ------------------------------------------------------------------ configuration */
+
+static char cfg_copyin[1024];
+static int cfg_has_copyin = 0;
+static int cfg_verbose = 0;
+static int cfg_debug = 1;
+static int cfg_num_sockets = -1;
+static int initialised = 0;
+static int comm_keyval = MPI_KEYVAL_INVALID;
+
+static int env_int(const char *name, int *out) {
+  const char *c = getenv(name);
+  int v;
+  if (c && sscanf(c, "%d", &v) == 1) {
+    *out = v;
+    return 1;
+  }
+  return 0;
+}
+
+static void read_env(void) {
+  int rank, len = 0;
+  PMPI_Comm_rank(MPI_COMM_WORLD, &rank);
+  if (rank == 0) {
+    const char *c = getenv("EXT_MPI_COPYIN");
+    cfg_verbose = getenv("EXT_MPI_VERBOSE") != NULL;
+    env_int("EXT_MPI_DEBUG", &cfg_debug);
+    env_int("EXT_MPI_NUM_SOCKETS_PER_NODE", &cfg_num_sockets);
+    if (c) {
+      strncpy(cfg_copyin, c, sizeof(cfg_copyin) - 1);
+      len = (int)strlen(cfg_copyin) + 1;
+    }
+  }
+  PMPI_Bcast(&cfg_verbose, 1, MPI_INT, 0, MPI_COMM_WORLD);
+  PMPI_Bcast(&cfg_debug, 1, MPI_INT, 0, MPI_COMM_WORLD);
+  PMPI_Bcast(&cfg_num_sockets, 1, MPI_INT, 0, MPI_COMM_WORLD);
+  PMPI_Bcast(&len, 1, MPI_INT, 0, MPI_COMM_WORLD);
+  if (len > 0) PMPI_Bcast(cfg_copyin, len, MPI_CHAR, 0, MPI_COMM_WORLD);
+  cfg_has_copyin = len > 0;
+}
+
+/* ------------------------------------------- request -> handle map (hash_table.c:8-58) */
+
+typedef struct {
+  MPI_Request req;
+  int handle;
+  int used;
+} req_slot;
+
+static req_slot *rmap = NULL;
+static int rmap_cap = 0, rmap_n = 0;
+
+static unsigned long req_hash(const MPI_Request *r) {
+  const unsigned char *p = (const unsigned char *)r;
+  unsigned long h = 1469598103934665603ul;
+  size_t i;
+  for (i = 0; i < sizeof(MPI_Request); i++) h = (h ^ p[i]) * 1099511628211ul;
+  return h;
+}
+
+static int rmap_find(const MPI_Request *r) {
+  unsigned long i;
+  int k;
+  if (!rmap_cap) return -1;
+  for (k = 0, i = req_hash(r) % (unsigned long)rmap_cap; k < rmap_cap; k++, i = (i + 1) % (unsigned long)rmap_cap) {
+    if (!rmap[i].used) return -1;
+    if (rmap[i].used == 1 && !memcmp(&rmap[i].req, r, sizeof(MPI_Request))) return (int)i;
+  }
+  return -1;
+}
+
+static int rmap_insert(const MPI_Request *r, int handle);
+
+static void rmap_grow(void) {
+  req_slot *old = rmap;
+  int i, oldcap = rmap_cap;
+  rmap_cap = oldcap ? oldcap * 2 : 256;
+  rmap = (req_slot *)calloc((size_t)rmap_cap, sizeof(req_slot));
+  rmap_n = 0;
+  for (i = 0; i < oldcap; i++)
+    if (old[i].used == 1) rmap_insert(&old[i].req, old[i].handle);
+  free(old);
+}
+
+static int rmap_insert(const MPI_Request *r, int handle) {
+  unsigned long i;
+  if (2 * (rmap_n + 1) > rmap_cap) rmap_grow();
+  for (i = req_hash(r) % (unsigned long)rmap_cap; rmap[i].used == 1; i = (i + 1) % (unsigned long)rmap_cap);
+  rmap[i].req = *r;
+  rmap[i].handle = handle;
+  rmap[i].used = 1;
+  rmap_n++;
+  return 0;
+}
+
+static void rmap_delete(int slot) {
+  rmap[slot].used = 2; /* tombstone keeps probe chains intact */
+  rmap_n--;
+}
+
+static int request_handle(const MPI_Request *r) {
+  int s = rmap_find(r);
+  return s < 0 ? -1 : rmap[s].handle;
+}
+
+/* ----------------------------------------------- communicator -> RCCL communicator */
+
+typedef struct {
+  int ext_comm;
+} comm_attr;
+
+static int comm_attr_delete(MPI_Comm comm, int keyval, void *attr, void *extra) {
+  comm_attr *a = (comm_attr *)attr;
+  (void)comm;
+  (void)keyval;
+  (void)extra;
+  if (a) {
+    ext_mpi_amd_comm_free(a->ext_comm);
+    free(a);
+  }
+  return MPI_SUCCESS;
+}
+
+static int node_comm(MPI_Comm comm, const void *devbuf, int *ext_comm) {
+  comm_attr *a;
+  int flag, size, rank, nsize, nrank, device, ndev, rc;
+  MPI_Comm node;
+  unsigned char id[EXT_MPI_AMD_UNIQUE_ID_BYTES];
+  if (comm_keyval == MPI_KEYVAL_INVALID) return EXT_MPI_AMD_ERROR_ARG;
+  PMPI_Comm_get_attr(comm, comm_keyval, &a, &flag);
+  if (flag && a) {
+    *ext_comm = a->ext_comm;
+    return 0;
+  }
+  PMPI_Comm_size(comm, &size);
+  PMPI_Comm_rank(comm, &rank);
+  PMPI_Comm_split_type(comm, MPI_COMM_TYPE_SHARED, rank, MPI_INFO_NULL, &node);
+  PMPI_Comm_size(node, &nsize);
+  PMPI_Comm_rank(node, &nrank);
+  PMPI_Comm_free(&node);
+  flag = nsize == size;
+  PMPI_Allreduce(MPI_IN_PLACE, &flag, 1, MPI_INT, MPI_MIN, comm);
+  if (!flag) return EXT_MPI_AMD_ERROR_UNSUPPORTED; /* inter-node legs: out of scope */
+  ndev = ext_mpi_amd_gpu_device_count();
+  device = ext_mpi_amd_gpu_device_of(devbuf);
+  if (device < 0) device = ndev > 0 ? nrank % ndev : -1;
+  if (rank == 0 && (rc = ext_mpi_amd_get_unique_id(id))) memset(id, 0, sizeof(id));
+  PMPI_Bcast(id, EXT_MPI_AMD_UNIQUE_ID_BYTES, MPI_BYTE, 0, comm);
+  rc = ndev > 0 ? ext_mpi_amd_comm_init(rank, size, id, device, ext_comm) : EXT_MPI_AMD_ERROR_DEVICE;
+  flag = rc == 0;
+  PMPI_Allreduce(MPI_IN_PLACE, &flag, 1, MPI_INT, MPI_MIN, comm);
+  if (!flag) {
+    if (rc == 0) ext_mpi_amd_comm_free(*ext_comm);
+    return rc ? rc : EXT_MPI_AMD_ERROR_TRANSPORT;
+  }
+  a = (comm_attr *)malloc(sizeof(comm_attr));
+  a->ext_comm = *ext_comm;
+  PMPI_Comm_set_attr(comm, comm_keyval, a);
+  return 0;
+}
+
+/* ------------------------------------------------ datatype / op (ext_mpi_native.h:77-140) */
+
+static int map_type(MPI_Datatype t) {
+  if (t == MPI_FLOAT || t == MPI_REAL || t == MPI_REAL4) return EXT_MPI_AMD_FLOAT;
+  if (t == MPI_DOUBLE || t == MPI_DOUBLE_PRECISION || t == MPI_REAL8) return EXT_MPI_AMD_DOUBLE;
+  if (t == MPI_INT || t == MPI_INTEGER || t == MPI_INTEGER4) return EXT_MPI_AMD_INT;
+  if (t == MPI_LONG || t == MPI_INTEGER8) return EXT_MPI_AMD_LONG;
+  return -1;
+}
+
+/* ------------------------------------------- known-answer self-test (debug_persistent.c) */
+
+static void kat_fill(void *buf, long count, int tsize, int world_rank, long add) {
+  long i, words = (count * tsize) / (long)sizeof(long);
+  for (i = 0; i < words; i++) ((long *)buf)[i] = world_rank * count + i + add;
+  if ((count * tsize) % (long)sizeof(long)) ((int *)buf)[count - 1] = (int)(world_rank * count + count - 1);
+}
+
+/* debug_persistent.c:393-568: the same schedule on an integer view of the same byte size,
+   checked word for word against PMPI_Allreduce. Host pattern +73, device pattern +0. */
+static int known_answer_test(void *recvbuf, int in_place, int count, int tsize, MPI_Comm comm, int ext_comm,
+                             const char *copyin) {
+  int world_rank, on_dev = ext_mpi_amd_gpu_is_device_pointer(recvbuf), rc = 0, bad = 0, h = -1;
+  int itype = tsize == 8 ? EXT_MPI_AMD_LONG : EXT_MPI_AMD_INT;
+  size_t bytes = (size_t)count * (size_t)tsize;
+  void *hs = malloc(bytes ? bytes : 1), *hr = malloc(bytes ? bytes : 1), *ref = malloc(bytes ? bytes : 1);
+  void *ds = NULL, *dr = NULL;
+  long i;
+  PMPI_Comm_rank(MPI_COMM_WORLD, &world_rank);
+  kat_fill(hs, count, tsize, world_rank, on_dev ? 0 : 73);
+  PMPI_Allreduce(hs, ref, count, tsize == 8 ? MPI_LONG : MPI_INT, MPI_SUM, comm);
+  if (on_dev) {
+    if ((rc = ext_mpi_amd_gpu_malloc(&dr, bytes))) goto out;
+    if (!in_place && (rc = ext_mpi_amd_gpu_malloc(&ds, bytes))) goto out;
+    if ((rc = ext_mpi_amd_gpu_memcpy_hd(in_place ? dr : ds, hs, bytes))) goto out;
+    rc = ext_mpi_amd_allreduce_init(in_place ? dr : ds, dr, count, itype, EXT_MPI_AMD_SUM, ext_comm, copyin, &h);
+  } else {
+    if (in_place) memcpy(hr, hs, bytes);
+    rc = ext_mpi_amd_allreduce_init(in_place ? hr : hs, hr, count, itype, EXT_MPI_AMD_SUM, ext_comm, copyin, &h);
+  }
+  if (!rc) rc = ext_mpi_amd_start(h);
+  if (!rc) rc = ext_mpi_amd_wait(h);
+  if (h >= 0) ext_mpi_amd_done(h);
+  if (!rc && on_dev) rc = ext_mpi_amd_gpu_memcpy_dh(hr, dr, bytes);
+  if (!rc) {
+    if (tsize == 8) {
+      for (i = 0; i < count; i++) bad |= ((long *)hr)[i] != ((long *)ref)[i];
+    } else {
+      for (i = 0; i < count; i++) bad |= ((int *)hr)[i] != ((int *)ref)[i];
+    }
+  }
+out:
+  ext_mpi_amd_gpu_free(ds);
+  ext_mpi_amd_gpu_free(dr);
+  free(hs);
+  free(hr);
+  free(ref);
+  if (!rc && bad) {
+    printf("logical error in EXT_MPI_Allreduce %d\n", world_rank); /* debug_persistent.c:542-545 */
+    rc = EXT_MPI_AMD_ERROR_ARG;
+  }
+  return rc;
+}
+
+/* ------------------------------------------------------------------- native API */
+
+int EXT_MPI_Init(void) {
+  if (initialised) return 0;
+  read_env();
+  PMPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, comm_attr_delete, &comm_keyval, NULL);
+  initialised = 1;
+  return 0;
+}
+
+int EXT_MPI_Initialized(int *flag) {
+  *flag = initialised;
+  return 0;
+}
+
+int EXT_MPI_Finalize(void) {
+  if (!initialised) return 0;
+  initialised = 0;
+  return 0; /* the RCCL communicators go with their MPI communicators' attributes */
+}
+
+int EXT_MPI_Allreduce_init(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+                           MPI_Comm comm, MPI_Info info, int *handle) {
+  int dtype = map_type(datatype), ext_comm, rc, flag = 0, rank, tsize;
+  const char *copyin = NULL;
+  char info_copyin[1024];
+  *handle = -1;
+  if (!initialised) EXT_MPI_Init();
+  if (dtype < 0 || op != MPI_SUM || count < 0) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
+  if (sendbuf == MPI_IN_PLACE) sendbuf = recvbuf; /* ext_mpi.c:651-653 */
+  if (cfg_num_sockets > 1) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
+  if (cfg_has_copyin) {
+    copyin = cfg_copyin;
+  } else if (info != MPI_INFO_NULL) {
+    PMPI_Info_get(info, "ext_mpi_copyin", (int)sizeof(info_copyin) - 1, info_copyin, &flag);
+    if (flag) copyin = info_copyin;
+  }
+  if ((rc = node_comm(comm, recvbuf, &ext_comm))) return rc;
+  PMPI_Type_size(datatype, &tsize);
+  if (cfg_debug && (rc = known_answer_test(recvbuf, sendbuf == recvbuf, count, tsize, comm, ext_comm, copyin)))
+    return rc;
+  rc = ext_mpi_amd_allreduce_init(sendbuf, recvbuf, count, dtype, EXT_MPI_AMD_SUM, ext_comm, copyin, handle);
+  if (cfg_verbose) {
+    PMPI_Comm_rank(comm, &rank);
+    if (rank == 0) printf("# EXT_MPI allreduce parameters copyin %s\n", copyin ? copyin : "(default 6;1 -R R)");
+  }
+  return rc;
+}
+
+int EXT_MPI_Start(int handle) { return handle >= 0 ? ext_mpi_amd_start(handle) : -1; }
+int EXT_MPI_Test(int handle) { return handle >= 0 ? ext_mpi_amd_test(handle) : -1; }
+int EXT_MPI_Wait(int handle) { return handle >= 0 ? ext_mpi_amd_wait(handle) : -1; }
+int EXT_MPI_Done(int handle) { return handle >= 0 ? ext_mpi_amd_done(handle) : -1; }
+
+/* ------------------------------------------------------------------- PMPI hooks */
+
+int MPI_Init(int *argc, char ***argv) {
+  int ret = PMPI_Init(argc, argv);
+  EXT_MPI_Init();
+  return ret;
+}
+
+int MPI_Init_thread(int *argc, char ***argv, int required, int *provided) {
+  int ret = PMPI_Init_thread(argc, argv, required, provided);
+  EXT_MPI_Init();
+  if (!(*provided == MPI_THREAD_SINGLE || *provided == MPI_THREAD_FUNNELED || *provided == MPI_THREAD_SERIALIZED))
+    *provided = MPI_THREAD_SERIALIZED;
+  return ret;
+}
+
+int MPI_Finalize(void) {
+  EXT_MPI_Finalize();
+  free(rmap);
+  rmap = NULL;
+  rmap_cap = rmap_n = 0;
+  return PMPI_Finalize();
+}
+
+int MPI_Allreduce_init(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op, MPI_Comm comm,
+                       MPI_Info info, MPI_Request *request) {
+  int handle, ret;
+  /* an inert persistent request that only names the operation (ext_mpi_interface.c:187) */
+  PMPI_Recv_init(NULL, 0, datatype, MPI_PROC_NULL, 0, comm, request);
+  ret = EXT_MPI_Allreduce_init(sendbuf, recvbuf, count, datatype, op, comm, info, &handle);
+  if (!ret) rmap_insert(request, handle);
+  return ret;
+}
+
+int MPI_Request_free(MPI_Request *request) {
+  int s = rmap_find(request);
+  if (s >= 0) {
+    EXT_MPI_Done(rmap[s].handle);
+    rmap_delete(s);
+  }
+  return PMPI_Request_free(request);
+}
+
+int MPI_Start(MPI_Request *request) {
+  int h = request_handle(request);
+  if (h >= 0) return EXT_MPI_Start(h) < 0 ? MPI_ERR_OTHER : MPI_SUCCESS;
+  return PMPI_Start(request);
+}
+
+int MPI_Startall(int count, MPI_Request array_of_requests[]) {
+  int i, ret;
+  for (i = 0; i < count; i++) {
+    ret = MPI_Start(&array_of_requests[i]);
+    if (ret != MPI_SUCCESS) return ret;
+  }
+  return MPI_SUCCESS;
+}
+
+int MPI_Wait(MPI_Request *request, MPI_Status *status) {
+  int h = request_handle(request);
+  if (h >= 0) return EXT_MPI_Wait(h) < 0 ? MPI_ERR_OTHER : MPI_SUCCESS;
+  return PMPI_Wait(request, status);
+}
+
+int MPI_Test(MPI_Request *request, int *flag, MPI_Status *status) {
+  int h = request_handle(request);
+  if (h >= 0) {
+    int r = EXT_MPI_Test(h);
+    if (r < 0) return MPI_ERR_OTHER;
+    *flag = r;
+    return MPI_SUCCESS;
+  }
+  return PMPI_Test(request, flag, status);
+}
+
+static int owns_any(int count, MPI_Request reqs[]) {
+  int i;
+  for (i = 0; i < count; i++)
+    if (request_handle(&reqs[i]) >= 0) return 1;
+  return 0;
+}
+
+int MPI_Waitall(int count, MPI_Request array_of_requests[], MPI_Status array_of_statuses[]) {
+  int i, ret;
+  if (!owns_any(count, array_of_requests)) return PMPI_Waitall(count, array_of_requests, array_of_statuses);
+  for (i = 0; i < count; i++) {
+    ret = MPI_Wait(&array_of_requests[i],
+                   array_of_statuses == MPI_STATUSES_IGNORE ? MPI_STATUS_IGNORE : &array_of_statuses[i]);
+    if (ret != MPI_SUCCESS) return ret;
+  }
+  return MPI_SUCCESS;
+}
+
+int MPI_Testall(int count, MPI_Request array_of_requests[], int *flag, MPI_Status array_of_statuses[]) {
+  int i, ret, f;
+  if (!owns_any(count, array_of_requests)) return PMPI_Testall(count, array_of_requests, flag, array_of_statuses);
+  *flag = 1;
+  for (i = 0; i < count; i++) {
+    ret = MPI_Test(&array_of_requests[i], &f,
+                   array_of_statuses == MPI_STATUSES_IGNORE ? MPI_STATUS_IGNORE : &array_of_statuses[i]);
+    if (ret != MPI_SUCCESS) return ret;
+    if (!f) *flag = 0;
+  }
+  return MPI_SUCCESS;
+}
+
+int MPI_Testany(int count, MPI_Request array_of_requests[], int *indx, int *flag, MPI_Status *status) {
+  int i, ret, f;
+  if (!owns_any(count, array_of_requests)) return PMPI_Testany(count, array_of_requests, indx, flag, status);
+  *flag = 0;
+  for (i = 0; i < count; i++) {
+    ret = MPI_Test(&array_of_requests[i], &f, status);
+    if (ret != MPI_SUCCESS) return ret;
+    if (f) {
+      *flag = 1;
+      *indx = i;
+      return MPI_SUCCESS;
+    }
+  }
+  return MPI_SUCCESS;
+}
+
+int MPI_Waitany(int count, MPI_Request array_of_requests[], int *indx, MPI_Status *status) {
+  int flag = 0, ret;
+  if (!owns_any(count, array_of_requests)) return PMPI_Waitany(count, array_of_requests, indx, status);
+  while (!flag) {
+    ret = MPI_Testany(count, array_of_requests, indx, &flag, status);
+    if (ret != MPI_SUCCESS) return ret;
+  }
+  return MPI_SUCCESS;
+}
+
+int MPI_Waitsome(int incount, MPI_Request array_of_requests[], int *outcount, int array_of_indices[],
+                 MPI_Status array_of_statuses[]) {
+  if (!owns_any(incount, array_of_requests))
+    return PMPI_Waitsome(incount, array_of_requests, outcount, array_of_indices, array_of_statuses);
+  *outcount = 1;
+  return MPI_Waitany(incount, array_of_requests, &array_of_indices[0],
+                     array_of_statuses == MPI_STATUSES_IGNORE ? MPI_STATUS_IGNORE : &array_of_statuses[0]);
+}
+
+int MPI_Testsome(int incount, MPI_Request array_of_requests[], int *outcount, int array_of_indices[],
+                 MPI_Status array_of_statuses[]) {
+  int flag = 0, ret;
+  if (!owns_any(incount, array_of_requests))
+    return PMPI_Testsome(incount, array_of_requests, outcount, array_of_indices, array_of_statuses);
+  ret = MPI_Testany(incount, array_of_requests, &array_of_indices[0], &flag,
+                    array_of_statuses == MPI_STATUSES_IGNORE ? MPI_STATUS_IGNORE : &array_of_statuses[0]);
+  *outcount = flag ? 1 : 0;
+  return ret;
+}

@@ -1,0 +1,91 @@
+/* Drop-in check of libext_mpi_collectives.so, written like an application of the reference
+ * (tests/benchmark.c shape): only MPI calls plus the MPI-4 prototype from ext_mpi_interface.h.
+ * argv: count dtype(f|d|i|l) mem(dev|host) [inplace]. Prints "RESULT ok" / "RESULT no-device"
+ * / "RESULT fail ...". Integer inputs are checked exactly against PMPI_Allreduce; float inputs
+ * are integer-valued (exact in any order) so the same comparison applies. */
+#include <mpi.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "ext_mpi_amd_gpu.h"
+#include "ext_mpi_interface.h"
+
+int main(int argc, char **argv) {
+  int rank, size, count = argc > 1 ? atoi(argv[1]) : 1000, rc, i, bad = 0, flag;
+  char t = argc > 2 ? argv[2][0] : 'f';
+  int dev = argc > 3 ? !strcmp(argv[3], "dev") : 1, inplace = argc > 4 && !strcmp(argv[4], "inplace");
+  MPI_Datatype dt = t == 'd' ? MPI_DOUBLE : t == 'i' ? MPI_INT : t == 'l' ? MPI_LONG : MPI_FLOAT;
+  int ts = (t == 'd' || t == 'l') ? 8 : 4;
+  size_t bytes = (size_t)count * ts;
+  void *hs, *hr, *ref, *s = NULL, *r = NULL;
+  MPI_Request req, p2p[2];
+  MPI_Init(&argc, &argv);
+  MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+  MPI_Comm_size(MPI_COMM_WORLD, &size);
+  hs = malloc(bytes);
+  hr = malloc(bytes);
+  ref = malloc(bytes);
+  for (i = 0; i < count; i++) {
+    long v = (long)(rank + 1) * (i % 1000) - 7 * rank;
+    if (t == 'f') ((float *)hs)[i] = (float)v;
+    else if (t == 'd') ((double *)hs)[i] = (double)v;
+    else if (t == 'i') ((int *)hs)[i] = (int)v;
+    else ((long *)hs)[i] = v;
+  }
+  PMPI_Allreduce(hs, ref, count, dt, MPI_SUM, MPI_COMM_WORLD);
+  /* requests we do not own fall through to PMPI (ext_mpi_interface.c:257-265) */
+  {
+    int a = rank, b = -1, peer = (rank + 1) % size, from = (rank + size - 1) % size;
+    MPI_Send_init(&a, 1, MPI_INT, peer, 5, MPI_COMM_WORLD, &p2p[0]);
+    MPI_Recv_init(&b, 1, MPI_INT, from, 5, MPI_COMM_WORLD, &p2p[1]);
+    MPI_Startall(2, p2p);
+    MPI_Waitall(2, p2p, MPI_STATUSES_IGNORE);
+    MPI_Request_free(&p2p[0]);
+    MPI_Request_free(&p2p[1]);
+    if (b != from) bad |= 1;
+  }
+  if (ext_mpi_amd_gpu_device_count() <= 0) {
+    rc = MPI_Allreduce_init(hs, hr, count, dt, MPI_SUM, MPI_COMM_WORLD, MPI_INFO_NULL, &req);
+    if (rank == 0) printf("RESULT %s rc=%d\n", (rc == -5 && !bad) ? "no-device" : "fail", rc);
+    MPI_Finalize();
+    return 0;
+  }
+  if (dev) {
+    ext_mpi_amd_gpu_malloc(&r, bytes);
+    if (!inplace) ext_mpi_amd_gpu_malloc(&s, bytes);
+    ext_mpi_amd_gpu_memcpy_hd(inplace ? r : s, hs, bytes);
+  } else {
+    r = hr;
+    s = hs;
+    if (inplace) memcpy(hr, hs, bytes);
+  }
+  rc = MPI_Allreduce_init(inplace ? MPI_IN_PLACE : s, r, count, dt, MPI_SUM, MPI_COMM_WORLD, MPI_INFO_NULL, &req);
+  if (rc) {
+    printf("RESULT fail init rc=%d\n", rc);
+    MPI_Abort(MPI_COMM_WORLD, 1);
+  }
+  for (int it = 0; it < 3; it++) {
+    if (inplace) { /* the persistent buffer is reused: refill it each round */
+      if (dev) ext_mpi_amd_gpu_memcpy_hd(r, hs, bytes);
+      else memcpy(hr, hs, bytes);
+    }
+    MPI_Start(&req);
+    if (it == 1) {
+      do { MPI_Test(&req, &flag, MPI_STATUS_IGNORE); } while (!flag);
+    } else {
+      MPI_Wait(&req, MPI_STATUS_IGNORE);
+    }
+    if (dev) ext_mpi_amd_gpu_memcpy_dh(hr, r, bytes);
+    if (memcmp(hr, ref, bytes)) bad |= 2;
+  }
+  MPI_Request_free(&req);
+  MPI_Allreduce(MPI_IN_PLACE, &bad, 1, MPI_INT, MPI_BOR, MPI_COMM_WORLD);
+  if (rank == 0) printf("RESULT %s (size=%d count=%d type=%c mem=%s%s)\n", bad ? "fail" : "ok", size, count, t,
+                        dev ? "dev" : "host", inplace ? " inplace" : "");
+  if (dev) {
+    ext_mpi_amd_gpu_free(r);
+    ext_mpi_amd_gpu_free(s);
+  }
+  MPI_Finalize();
+  return 0;
+}

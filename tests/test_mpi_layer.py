@@ -1,0 +1,58 @@
+"""The drop-in PMPI layer (libext_mpi_collectives.so) driven by a plain MPI C program.
+
+CPU (here): the library links, requests it does not own fall through to PMPI, and without a
+GPU MPI_Allreduce_init fails loudly (ERROR_DEVICE) instead of reducing on the CPU.
+GPU box: one rank (RCCL communicator of size 1) with device and host buffers, in place, with
+the reference's known-answer self-test enabled (EXT_MPI_DEBUG=1, the reference default)."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+import ext_mpi_collectives_amd as emac
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MPI_HOME = "/opt/conda"
+SRC = os.path.join(ROOT, "tests", "mpi", "mpi_allreduce_check.c")
+
+
+def _build(tmp_path):
+    if not os.path.exists(os.path.join(MPI_HOME, "include", "mpi.h")) or not os.path.exists(emac.MPI_LIB_PATH):
+        pytest.skip("MPI headers or the MPI layer are not available")
+    exe = str(tmp_path / "mpi_allreduce_check")
+    libdir = os.path.dirname(emac.MPI_LIB_PATH)
+    # link order: the interception library before libmpi so its strong MPI_* symbols win
+    subprocess.run(["gcc", "-O2", SRC, "-o", exe, "-I" + os.path.join(ROOT, "include"),
+                    "-I" + os.path.join(MPI_HOME, "include"), "-L" + libdir, "-lext_mpi_collectives",
+                    "-lext_mpi_amd", os.path.join(MPI_HOME, "lib", "libmpi.so"),
+                    # resolve ROCm's libstdc++ needs against the system library, not conda's older one
+                    "-Wl,-rpath-link,/lib/x86_64-linux-gnu",
+                    "-Wl,-rpath," + libdir, "-Wl,-rpath," + os.path.join(MPI_HOME, "lib")], check=True)
+    return exe
+
+
+def _run(exe, n, args, env=None, timeout=240):
+    e = dict(os.environ, **(env or {}))
+    p = subprocess.run([os.path.join(MPI_HOME, "bin", "mpiexec"), "-n", str(n), exe] + [str(a) for a in args],
+                       capture_output=True, text=True, timeout=timeout, env=e)
+    out = p.stdout + p.stderr
+    return [l for l in out.splitlines() if l.startswith("RESULT")], out
+
+
+def test_mpi_layer_without_gpu(tmp_path):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by the gpu test")
+    exe = _build(tmp_path)
+    res, out = _run(exe, 2, [1000, "f", "host"])
+    assert res and res[0].startswith("RESULT no-device"), out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [[100003, "f", "dev"], [4099, "d", "dev", "inplace"], [100000, "i", "host"],
+                                  [777, "l", "host", "inplace"], [0, "f", "dev"]])
+def test_mpi_layer_single_rank_gpu(tmp_path, args):
+    exe = _build(tmp_path)
+    res, out = _run(exe, 1, args, env={"EXT_MPI_DEBUG": "1"})
+    assert res and res[0].startswith("RESULT ok"), out
