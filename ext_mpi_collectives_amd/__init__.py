@@ -29,6 +29,19 @@ _TORCH_DTYPE_CODES = {"torch.float32": FLOAT, "torch.float64": DOUBLE, "torch.in
 _NUMPY_DTYPE_CODES = {"float32": FLOAT, "float64": DOUBLE, "int32": INT, "int64": LONG}
 
 
+class P2P(ctypes.Structure):
+    _fields_ = [("leg", ctypes.c_int), ("peer", ctypes.c_int), ("is_send", ctypes.c_int), ("buf", ctypes.c_int),
+                ("offset", ctypes.c_long), ("bytes", ctypes.c_long)]
+
+
+class FoldDesc(ctypes.Structure):
+    _fields_ = [("piece", ctypes.c_int), ("offset", ctypes.c_long), ("count", ctypes.c_long),
+                ("buf", ctypes.c_int * MAX_RANKS), ("leaf_offset", ctypes.c_long * MAX_RANKS)]
+
+
+BUF_SEND, BUF_RECV, BUF_STAGE = 0, 1, 2
+
+
 class ExtMpiError(RuntimeError):
     def __init__(self, what, code):
         super().__init__(f"{what} failed: {ERRORS.get(code, code)} ({code})")
@@ -71,6 +84,8 @@ def lib():
         L.ext_mpi_amd_plan_describe.argtypes = [c_int, c_long, c_int, ctypes.c_char_p, c_int, P(c_long),
                                                 P(c_long), c_int, P(c_int), P(c_int), P(ctypes.c_ubyte),
                                                 P(ctypes.c_ubyte), P(c_int)]
+        L.ext_mpi_amd_comm_program.argtypes = [c_int, c_int, c_long, c_int, ctypes.c_char_p, c_long,
+                                               P(P2P), c_int, P(c_int), P(FoldDesc), c_int, P(c_int), P(c_long)]
         L.ext_mpi_amd_version.restype = ctypes.c_char_p
         _lib = L
     return _lib
@@ -183,6 +198,22 @@ def plan_describe(nranks, count, dtype, copyin, pos, max_pieces=4096):
     return {"owner": owner.value, "pieces": [(off[i], ln[i]) for i in range(min(n, max_pieces))],
             "leaves": list(leaves[:nranks]), "first": list(first[:nranks]), "close": list(close[:nranks]),
             "nlev": nlev.value}
+
+
+def comm_program(nranks, rank, count, dtype, copyin=None, send_phase=0, max_ops=65536, max_folds=4096):
+    """What Start executes for node rank ``rank`` in the COMM form (no GPU needed).
+
+    Returns (ops, folds, staging_bytes): ops = [(leg, peer, is_send, buf, offset, bytes)],
+    folds = [(offset, count, [(buf, leaf_offset)] in fold order)]."""
+    ops = (P2P * max_ops)()
+    folds = (FoldDesc * max_folds)()
+    nops, nf, stage = ctypes.c_int(), ctypes.c_int(), ctypes.c_long()
+    _check("ext_mpi_amd_comm_program",
+           lib().ext_mpi_amd_comm_program(nranks, rank, count, dtype, _enc(copyin), send_phase, ops, max_ops,
+                                          ctypes.byref(nops), folds, max_folds, ctypes.byref(nf), ctypes.byref(stage)))
+    o = [(x.leg, x.peer, x.is_send, x.buf, x.offset, x.bytes) for x in ops[:nops.value]]
+    f = [(x.offset, x.count, [(x.buf[t], x.leaf_offset[t]) for t in range(nranks)]) for x in folds[:nf.value]]
+    return o, f, stage.value
 
 
 def version():

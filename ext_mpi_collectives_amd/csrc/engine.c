@@ -64,15 +64,13 @@ typedef struct {
   int comm;
   int me, me_pos;
   void *staging;
-  long *stage_off;    /* per piece: byte offset of the piece's slot block */
-  long *stage_stride; /* per piece: bytes between peer slots (16-byte multiple) */
-  long *stage_mis;    /* per piece: 16-byte phase shared with the send buffer's chunk */
+  emac_p2p *ops; /* reduce-scatter and allgather point-to-point program (plan.c) */
+  int nops;
   int started;
   int own_stream; /* 0 once the caller supplied the stream (ext_mpi_amd_set_stream) */
 } emac_handle;
 
 static emac_handle *handles[MAX_HANDLES];
-static long stage_slot(const emac_handle *h, int pc, int q);
 static emac_comm comms[MAX_COMMS];
 
 static int new_handle_slot(void) {
@@ -98,9 +96,7 @@ static void release(emac_handle *h) {
     if (h->send_reg[r]) emac_gpu_host_unregister(h->user_send[r]);
     if (h->recv_reg[r]) emac_gpu_host_unregister(h->user_recv[r]);
   }
-  free(h->stage_off);
-  free(h->stage_stride);
-  free(h->stage_mis);
+  free(h->ops);
   emac_plan_free(&h->plan);
   free(h);
 }
@@ -283,7 +279,7 @@ int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, i
   emac_comm *cm;
   emac_copyin cfg;
   emac_bucket *b = NULL;
-  int rc, pc, t, R, nb = 0;
+  int rc, t, R, nb = 0;
   long stage_total = 0;
   if (!handle || comm < 0 || comm >= MAX_COMMS || !comms[comm].used || count < 0) return EMAC_ERR_ARG;
   *handle = -1;
@@ -303,41 +299,31 @@ int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, i
   h->nbuf = 1;
   h->nsrc = R;
   if ((rc = map_buffers(h, 0, sendbuf, recvbuf))) goto fail;
-  h->stage_off = (long *)calloc((size_t)h->plan.npieces, sizeof(long));
-  h->stage_stride = (long *)calloc((size_t)h->plan.npieces, sizeof(long));
-  h->stage_mis = (long *)calloc((size_t)h->plan.npieces, sizeof(long));
-  b = (emac_bucket *)calloc((size_t)h->plan.npieces, sizeof(emac_bucket));
-  if (!h->stage_off || !h->stage_stride || !h->stage_mis || !b) {
-    rc = EMAC_ERR_MALLOC;
-    goto fail;
-  }
-  /* peer slots of a piece start at the same 16-byte phase as the chunk in the send buffer,
-     so the fold keeps its dwordx4 path */
-  for (pc = 0; pc < h->plan.npieces; pc++) {
-    long off = h->plan.chunk_off[(size_t)pc * R + h->me_pos], len = h->plan.chunk_len[(size_t)pc * R + h->me_pos];
-    h->stage_mis[pc] = (long)(((unsigned long)h->dsend[0] + (unsigned long)(off * h->plan.tsize)) & 15ul);
-    h->stage_stride[pc] = ((len * h->plan.tsize + 15) / 16) * 16 + 16;
-    h->stage_off[pc] = stage_total;
-    stage_total += (long)(R - 1) * h->stage_stride[pc];
-  }
-  if ((rc = emac_gpu_malloc(&h->staging, (size_t)stage_total))) goto fail;
-  for (pc = 0; pc < h->plan.npieces; pc++) {
-    long off = h->plan.chunk_off[(size_t)pc * R + h->me_pos], len = h->plan.chunk_len[(size_t)pc * R + h->me_pos];
-    emac_bucket *bk = &b[nb];
-    if (len <= 0) continue;
-    for (t = 0; t < R; t++) {
-      int q = h->plan.leaf_rank[h->me_pos][t];
-      if (q == h->me) {
-        bk->src[t] = h->dsend[0];
-      } else {
-        /* shifted back by the chunk offset: split_alignment adds it to every pointer */
-        bk->src[t] = (const char *)h->staging + stage_slot(h, pc, q) - off * h->plan.tsize;
-      }
+  {
+    emac_fold *folds = NULL;
+    int nf = 0, f;
+    if ((rc = emac_comm_program(&h->plan, h->me, (long)((unsigned long)h->dsend[0] & 15ul), &h->ops, &h->nops, &folds,
+                                &nf, &stage_total)))
+      goto fail;
+    b = (emac_bucket *)calloc((size_t)nf + 1, sizeof(emac_bucket));
+    if (!b || (rc = emac_gpu_malloc(&h->staging, (size_t)stage_total))) {
+      free(folds);
+      rc = rc ? rc : EMAC_ERR_MALLOC;
+      goto fail;
     }
-    bk->dst[0] = h->drecv[0];
-    bk->ndst = 1;
-    split_alignment(bk, R, off, len, h->plan.tsize);
-    nb++;
+    for (f = 0; f < nf; f++) {
+      emac_bucket *bk = &b[nb++];
+      long off = folds[f].offset / h->plan.tsize;
+      for (t = 0; t < R; t++) {
+        /* leaf pointers are shifted back by the chunk offset: split_alignment adds it */
+        const char *base = folds[f].buf[t] == EMAC_BUF_SEND ? (const char *)h->dsend[0] : (const char *)h->staging;
+        bk->src[t] = base + folds[f].loff[t] - folds[f].offset;
+      }
+      bk->dst[0] = h->drecv[0];
+      bk->ndst = 1;
+      split_alignment(bk, R, off, folds[f].count, h->plan.tsize);
+    }
+    free(folds);
   }
   if ((rc = upload_buckets(h, b, nb))) goto fail;
   free(b);
@@ -351,70 +337,24 @@ fail:
   return rc;
 }
 
-/* byte offset, inside the staging buffer, of peer q's slice of this rank's chunk of piece pc */
-static long stage_slot(const emac_handle *h, int pc, int q) {
-  int R = h->plan.nranks;
-  long slot = (q - h->me - 1 + R) % R;
-  return h->stage_off[pc] + slot * h->stage_stride[pc] + h->stage_mis[pc];
-}
-
-/* reduce-scatter leg: every rank sends its slice of each owner chunk to the owner */
-static int exchange_reduce_scatter(emac_handle *h) {
+/* Walk the point-to-point program of one leg as ONE RCCL group (all peers at once). */
+static int run_leg(emac_handle *h, int leg) {
   emac_comm *cm = &comms[h->comm];
   hipStream_t s = (hipStream_t)h->stream;
-  int R = cm->size, pc, q;
-  long tsize = h->plan.tsize;
+  int i, bad = 0;
   if (ncclGroupStart() != ncclSuccess) return EMAC_ERR_TRANSPORT;
-  for (pc = 0; pc < h->plan.npieces; pc++) {
-    long mylen = h->plan.chunk_len[(size_t)pc * R + h->me_pos];
-    for (q = 0; q < R; q++) {
-      long qoff, qlen;
-      if (q == h->me) continue;
-      qoff = h->plan.chunk_off[(size_t)pc * R + h->plan.rank_pos[q]];
-      qlen = h->plan.chunk_len[(size_t)pc * R + h->plan.rank_pos[q]];
-      if (qlen > 0 &&
-          ncclSend((const char *)h->dsend[0] + qoff * tsize, (size_t)(qlen * tsize), ncclInt8, q, cm->nccl, s) !=
-              ncclSuccess)
-        goto err;
-      if (mylen > 0) {
-        char *dst = (char *)h->staging + stage_slot(h, pc, q);
-        if (ncclRecv(dst, (size_t)(mylen * tsize), ncclInt8, q, cm->nccl, s) != ncclSuccess) goto err;
-      }
-    }
+  for (i = 0; i < h->nops && !bad; i++) {
+    const emac_p2p *o = &h->ops[i];
+    char *base;
+    if (o->leg != leg) continue;
+    base = o->buf == EMAC_BUF_SEND ? (char *)h->dsend[0] : o->buf == EMAC_BUF_RECV ? (char *)h->drecv[0] : (char *)h->staging;
+    if (o->is_send)
+      bad = ncclSend(base + o->offset, (size_t)o->bytes, ncclInt8, o->peer, cm->nccl, s) != ncclSuccess;
+    else
+      bad = ncclRecv(base + o->offset, (size_t)o->bytes, ncclInt8, o->peer, cm->nccl, s) != ncclSuccess;
   }
-  return ncclGroupEnd() == ncclSuccess ? 0 : EMAC_ERR_TRANSPORT;
-err:
-  ncclGroupEnd();
-  return EMAC_ERR_TRANSPORT;
-}
-
-/* allgather leg: the owned (folded) chunk goes to every peer's receive buffer */
-static int exchange_allgather(emac_handle *h) {
-  emac_comm *cm = &comms[h->comm];
-  hipStream_t s = (hipStream_t)h->stream;
-  int R = cm->size, pc, q;
-  long tsize = h->plan.tsize;
-  if (ncclGroupStart() != ncclSuccess) return EMAC_ERR_TRANSPORT;
-  for (pc = 0; pc < h->plan.npieces; pc++) {
-    long myoff = h->plan.chunk_off[(size_t)pc * R + h->me_pos], mylen = h->plan.chunk_len[(size_t)pc * R + h->me_pos];
-    for (q = 0; q < R; q++) {
-      long qoff, qlen;
-      if (q == h->me) continue;
-      qoff = h->plan.chunk_off[(size_t)pc * R + h->plan.rank_pos[q]];
-      qlen = h->plan.chunk_len[(size_t)pc * R + h->plan.rank_pos[q]];
-      if (mylen > 0 &&
-          ncclSend((const char *)h->drecv[0] + myoff * tsize, (size_t)(mylen * tsize), ncclInt8, q, cm->nccl, s) !=
-              ncclSuccess)
-        goto err;
-      if (qlen > 0 &&
-          ncclRecv((char *)h->drecv[0] + qoff * tsize, (size_t)(qlen * tsize), ncclInt8, q, cm->nccl, s) != ncclSuccess)
-        goto err;
-    }
-  }
-  return ncclGroupEnd() == ncclSuccess ? 0 : EMAC_ERR_TRANSPORT;
-err:
-  ncclGroupEnd();
-  return EMAC_ERR_TRANSPORT;
+  if (ncclGroupEnd() != ncclSuccess) bad = 1;
+  return bad ? EMAC_ERR_TRANSPORT : 0;
 }
 
 static int stage_in(emac_handle *h) {
@@ -446,12 +386,12 @@ int ext_mpi_amd_start_legs(int handle, int legs) {
   multi = h->kind == KIND_COMM && h->plan.nranks > 1;
   if (emac_gpu_set_device(h->device)) return EMAC_ERR_DEVICE;
   if ((legs & EXT_MPI_AMD_LEG_STAGE) && (rc = stage_in(h))) return rc;
-  if ((legs & EXT_MPI_AMD_LEG_REDUCE_SCATTER) && multi && (rc = exchange_reduce_scatter(h))) return rc;
+  if ((legs & EXT_MPI_AMD_LEG_REDUCE_SCATTER) && multi && (rc = run_leg(h, EMAC_LEG_RS))) return rc;
   if ((legs & EXT_MPI_AMD_LEG_FOLD) &&
       (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, &h->plan.codes, h->d_buckets, h->nb, h->ntiles,
                           h->stream)))
     return rc;
-  if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && multi && (rc = exchange_allgather(h))) return rc;
+  if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && multi && (rc = run_leg(h, EMAC_LEG_AG))) return rc;
   if ((legs & EXT_MPI_AMD_LEG_STAGE) && (rc = stage_out(h))) return rc;
   h->started = 1;
   return 0;
@@ -523,6 +463,48 @@ int ext_mpi_amd_plan_describe(int nranks, long count, int dtype, const char *cop
   }
   *nlev = p.codes.nlev;
   rc = p.npieces;
+  emac_plan_free(&p);
+  return rc;
+}
+
+int ext_mpi_amd_comm_program(int nranks, int rank, long count, int dtype, const char *copyin, long send_phase,
+                             ext_mpi_amd_p2p *ops, int max_ops, int *nops, ext_mpi_amd_fold *folds, int max_folds,
+                             int *nfolds, long *staging_bytes) {
+  emac_plan p;
+  emac_copyin cfg;
+  emac_p2p *o = NULL;
+  emac_fold *f = NULL;
+  int rc, i, t, no = 0, nf = 0;
+  if (nranks < 1 || nranks > EMAC_MAX_RANKS || rank < 0 || rank >= nranks) return EMAC_ERR_ARG;
+  if ((rc = parse_cfg(copyin, nranks, &cfg))) return rc;
+  if ((rc = emac_plan_build(&p, nranks, count, dtype, EMAC_SUM, &cfg))) return rc;
+  if ((rc = emac_comm_program(&p, rank, send_phase, &o, &no, &f, &nf, staging_bytes))) goto out;
+  if (no > max_ops || nf > max_folds) {
+    rc = EMAC_ERR_ARG;
+    goto out;
+  }
+  for (i = 0; i < no; i++) {
+    ops[i].leg = o[i].leg;
+    ops[i].peer = o[i].peer;
+    ops[i].is_send = o[i].is_send;
+    ops[i].buf = o[i].buf;
+    ops[i].offset = o[i].offset;
+    ops[i].bytes = o[i].bytes;
+  }
+  for (i = 0; i < nf; i++) {
+    folds[i].piece = f[i].piece;
+    folds[i].offset = f[i].offset;
+    folds[i].count = f[i].count;
+    for (t = 0; t < nranks; t++) {
+      folds[i].buf[t] = f[i].buf[t];
+      folds[i].leaf_offset[t] = f[i].loff[t];
+    }
+  }
+  *nops = no;
+  *nfolds = nf;
+out:
+  free(o);
+  free(f);
   emac_plan_free(&p);
   return rc;
 }

@@ -234,3 +234,74 @@ void emac_plan_free(emac_plan *p) {
   free(p->chunk_len);
   p->chunk_off = p->chunk_len = NULL;
 }
+
+/* Reduce-scatter leg: one all-to-all round -- the slice of every owner chunk goes straight to
+   its owner (the multi-step recursive halving of reduce_copyin.c:687-744 moves the same bytes
+   in log R rounds, each bound by a single xGMI link). Allgather leg: the owned, folded chunk to
+   every peer (reduce_copyin.c:745-838 as one round). Staging holds the R-1 received slices of
+   each owned chunk, one 16-byte aligned slot per peer. */
+int emac_comm_program(const emac_plan *p, int me, long send_phase, emac_p2p **ops_out, int *nops_out,
+                      emac_fold **folds_out, int *nfolds_out, long *staging_bytes) {
+  int R = p->nranks, me_pos = p->rank_pos[me], pc, q, t, nops = 0, nf = 0, leg;
+  long ts = p->tsize, total = 0;
+  long *slot0 = (long *)malloc(sizeof(long) * (size_t)p->npieces);
+  long *stride = (long *)malloc(sizeof(long) * (size_t)p->npieces);
+  emac_p2p *ops = (emac_p2p *)malloc(sizeof(emac_p2p) * (size_t)(4 * p->npieces * R + 1));
+  emac_fold *folds = (emac_fold *)calloc((size_t)p->npieces + 1, sizeof(emac_fold));
+  if (!slot0 || !stride || !ops || !folds) {
+    free(slot0);
+    free(stride);
+    free(ops);
+    free(folds);
+    return EMAC_ERR_MALLOC;
+  }
+  for (pc = 0; pc < p->npieces; pc++) {
+    long off = p->chunk_off[(size_t)pc * R + me_pos], len = p->chunk_len[(size_t)pc * R + me_pos];
+    long phase = (send_phase + off * ts) & 15;
+    stride[pc] = ((len * ts + 15) / 16) * 16 + 16;
+    slot0[pc] = total + phase;
+    total += (long)(R - 1) * stride[pc];
+  }
+#define SLOT(pc, q) (slot0[pc] + (long)(((q) - me - 1 + R) % R) * stride[pc])
+  for (leg = 0; leg < 2; leg++) {
+    for (pc = 0; pc < p->npieces; pc++) {
+      long myoff = p->chunk_off[(size_t)pc * R + me_pos] * ts, mylen = p->chunk_len[(size_t)pc * R + me_pos] * ts;
+      for (q = 0; q < R; q++) {
+        long qoff, qlen;
+        if (q == me) continue;
+        qoff = p->chunk_off[(size_t)pc * R + p->rank_pos[q]] * ts;
+        qlen = p->chunk_len[(size_t)pc * R + p->rank_pos[q]] * ts;
+        if (leg == 0) {
+          if (qlen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_RS, q, 1, EMAC_BUF_SEND, qoff, qlen};
+          if (mylen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_RS, q, 0, EMAC_BUF_STAGE, SLOT(pc, q), mylen};
+        } else {
+          if (mylen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_AG, q, 1, EMAC_BUF_RECV, myoff, mylen};
+          if (qlen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_AG, q, 0, EMAC_BUF_RECV, qoff, qlen};
+        }
+      }
+    }
+  }
+  for (pc = 0; pc < p->npieces; pc++) {
+    long off = p->chunk_off[(size_t)pc * R + me_pos], len = p->chunk_len[(size_t)pc * R + me_pos];
+    emac_fold *f = &folds[nf];
+    if (len <= 0) continue;
+    f->piece = pc;
+    f->offset = off * ts;
+    f->count = len;
+    for (t = 0; t < R; t++) {
+      q = p->leaf_rank[me_pos][t];
+      f->buf[t] = q == me ? EMAC_BUF_SEND : EMAC_BUF_STAGE;
+      f->loff[t] = q == me ? off * ts : SLOT(pc, q);
+    }
+    nf++;
+  }
+#undef SLOT
+  free(slot0);
+  free(stride);
+  *ops_out = ops;
+  *nops_out = nops;
+  *folds_out = folds;
+  *nfolds_out = nf;
+  *staging_bytes = total;
+  return EMAC_OK;
+}

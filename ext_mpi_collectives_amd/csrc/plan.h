@@ -76,6 +76,35 @@ typedef struct {
   emac_codes codes;
 } emac_plan;
 
+/* ---- COMM form (one rank per GPU): the point-to-point legs and the owner's fold, as data ----
+ * Built once per handle; the RCCL executor (engine.c) only walks it. Exported through
+ * ext_mpi_amd_comm_program so the same program can be executed by a host transport in tests. */
+enum { EMAC_BUF_SEND = 0, EMAC_BUF_RECV = 1, EMAC_BUF_STAGE = 2 };
+enum { EMAC_LEG_RS = 2, EMAC_LEG_AG = 8 };
+
+typedef struct {
+  int leg;     /* EMAC_LEG_RS or EMAC_LEG_AG */
+  int peer;    /* node rank */
+  int is_send;
+  int buf;     /* EMAC_BUF_* */
+  long offset; /* bytes */
+  long bytes;
+} emac_p2p;
+
+typedef struct {
+  int piece;
+  long offset;                   /* byte offset of the owned chunk in send / recv buffers */
+  long count;                    /* elements */
+  int buf[EMAC_MAX_RANKS];       /* per leaf (plan leaf order): EMAC_BUF_SEND or EMAC_BUF_STAGE */
+  long loff[EMAC_MAX_RANKS];     /* per leaf: byte offset of the chunk's first element */
+} emac_fold;
+
+/* Program of node rank `me`: ops (reduce-scatter ops first, then allgather ops), one fold per
+   non-empty piece, and the staging bytes. Peer slots in staging start at `send_phase` mod 16
+   so they share the 16-byte phase of the send buffer. Caller frees *ops and *folds. */
+int emac_comm_program(const emac_plan *p, int me, long send_phase, emac_p2p **ops, int *nops, emac_fold **folds,
+                      int *nfolds, long *staging_bytes);
+
 /* Build the plan of an nranks-rank Allreduce of `count` elements. 0 or an EMAC_ERR_* code. */
 int emac_plan_build(emac_plan *p, int nranks, long count, int dtype, int op, const emac_copyin *cfg);
 void emac_plan_free(emac_plan *p);

@@ -96,6 +96,26 @@ int ext_mpi_amd_plan_describe(int nranks, long count, int dtype, const char *cop
                               long *piece_len, int max_pieces, int *owner_rank, int *leaf_ranks,
                               unsigned char *first, unsigned char *close, int *nlev);
 
+/* Program of node rank `rank` in the COMM form (what Start executes, as data): point-to-point
+ * ops of the reduce-scatter leg (leg == EXT_MPI_AMD_LEG_REDUCE_SCATTER) and the allgather leg
+ * (EXT_MPI_AMD_LEG_ALLGATHER), and the owner's folds (leaf buffers/offsets in fold order,
+ * codes as in ext_mpi_amd_plan_describe). Buffers: 0 send, 1 recv, 2 staging. Offsets in
+ * bytes. send_phase = send buffer address mod 16 (staging slots share it). */
+typedef struct {
+  int leg, peer, is_send, buf;
+  long offset, bytes;
+} ext_mpi_amd_p2p;
+typedef struct {
+  int piece;
+  long offset; /* bytes: owned chunk in send / recv */
+  long count;  /* elements */
+  int buf[EXT_MPI_AMD_MAX_RANKS];
+  long leaf_offset[EXT_MPI_AMD_MAX_RANKS];
+} ext_mpi_amd_fold;
+int ext_mpi_amd_comm_program(int nranks, int rank, long count, int dtype, const char *copyin, long send_phase,
+                             ext_mpi_amd_p2p *ops, int max_ops, int *nops, ext_mpi_amd_fold *folds, int max_folds,
+                             int *nfolds, long *staging_bytes);
+
 const char *ext_mpi_amd_version(void);
 
 #ifdef __cplusplus

@@ -1,0 +1,103 @@
+"""The N>1 (COMM form) path on CPU: world-size-2 and -4 gloo process groups execute exactly
+the program the engine hands to RCCL (ext_mpi_amd_comm_program: reduce-scatter p2p ops, the
+owner's folds, allgather p2p ops), with a numpy replay of the fold tree standing in for the
+HIP kernel, and every rank's result is compared bit for bit with the oracle."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import ext_mpi_collectives_amd as emac
+from helpers import NP, xorshift_inputs
+
+LEG_RS, LEG_AG = emac.LEG_REDUCE_SCATTER, emac.LEG_ALLGATHER
+
+
+def _bytes_view(buf, off, n):
+    return torch.from_numpy(buf[off:off + n])
+
+
+def _run_leg(ops, leg, bufs):
+    reqs = []
+    for (lg, peer, is_send, b, off, n) in ops:
+        if lg != leg:
+            continue
+        t = _bytes_view(bufs[b], off, n)
+        reqs.append(dist.isend(t, peer) if is_send else dist.irecv(t, peer))
+    for r in reqs:
+        r.wait()
+
+
+def _fold(folds, bufs, code, desc):
+    dt = NP[code]
+    for off, count, leaves in folds:
+        xs = [bufs[b][lo:lo + count * np.dtype(dt).itemsize].view(dt) for b, lo in leaves]
+        acc, cur = [None] * desc["nlev"], None
+        with np.errstate(over="ignore"):
+            for t, x in enumerate(xs):
+                cur = x
+                for lvl in range(desc["nlev"]):
+                    if lvl == 0 or desc["close"][t] >= lvl:
+                        acc[lvl] = cur.copy() if (desc["first"][t] >> lvl) & 1 else acc[lvl] + cur
+                    cur = acc[lvl]
+        bufs[emac.BUF_RECV][off:off + count * np.dtype(dt).itemsize].view(dt)[:] = cur
+
+
+def _worker(rank, world, port, cases, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle
+    failures = []
+    for code, count, copyin in cases:
+        sends = xorshift_inputs(world, count, code)
+        itemsize = np.dtype(NP[code]).itemsize
+        ops, folds, stage = emac.comm_program(world, rank, count, code, copyin)
+        bufs = {emac.BUF_SEND: sends[rank].view(np.uint8).copy(),
+                emac.BUF_RECV: np.full(count * itemsize, 0xAB, dtype=np.uint8),
+                emac.BUF_STAGE: np.zeros(max(stage, 1), dtype=np.uint8)}
+        desc = emac.plan_describe(world, count, code, copyin, 0)
+        _run_leg(ops, LEG_RS, bufs)
+        _fold(folds, bufs, code, desc)
+        _run_leg(ops, LEG_AG, bufs)
+        want = oracle.allreduce(sends, copyin or f"6;1 -{world} {world}")[rank]
+        if not np.array_equal(bufs[emac.BUF_RECV], want.view(np.uint8)):
+            failures.append((rank, code, count, copyin))
+    q.put(failures)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,cases", [
+    (2, [(emac.FLOAT, 100003, None), (emac.DOUBLE, 7, "6;1 -2 2"), (emac.INT, 4099, "6;3 -2 2"),
+         (emac.LONG, 1000, "6;-5 -2 2"), (emac.FLOAT, 0, None), (emac.FLOAT, 1, None)]),
+    (4, [(emac.FLOAT, 65539, "6;1 -4 4"), (emac.DOUBLE, 4099, "6;1 -2 -2 2 2"), (emac.INT, 1001, "6;2 -2 -2 4"),
+         (emac.LONG, 5000, "6;-7 -4 4")]),
+])
+def test_comm_program_over_gloo(world, cases):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + world * 7 + os.getpid() % 200
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert [f for r in results for f in r] == []
+
+
+def test_comm_program_shape():
+    ops, folds, stage = emac.comm_program(8, 3, 8 * 1000, emac.FLOAT, "6;1 -8 8")
+    rs = [o for o in ops if o[0] == LEG_RS]
+    ag = [o for o in ops if o[0] == LEG_AG]
+    assert len(rs) == 14 and len(ag) == 14  # one send + one recv per peer and leg, one round each
+    assert sorted({o[1] for o in ops}) == [0, 1, 2, 4, 5, 6, 7]
+    assert len(folds) == 1 and folds[0][0] == 3 * 1000 * 4 and folds[0][1] == 1000
+    # leaf 0 of rank 3's chunk is its own send buffer; the others come from staging slots
+    assert folds[0][2][0] == (emac.BUF_SEND, 12000)
+    assert all(b == emac.BUF_STAGE for b, _ in folds[0][2][1:])
+    assert all(off % 16 == 0 for b, off in folds[0][2][1:])
+    assert stage >= 7 * 4000
