@@ -53,6 +53,11 @@ typedef struct {
   emac_bucket *d_buckets;
   int nb;
   long ntiles;
+  long tiles_per_bucket; /* > 0 when every bucket has the same tile count */
+  int fan;               /* fan-out width == nsrc (node form) */
+  emac_edge *d_edges;    /* element-granular work items (device) */
+  int nedges;
+  int unroll;
   int nsrc;
   size_t bytes; /* message bytes per rank */
   int nbuf;     /* ranks with buffers in this process */
@@ -88,6 +93,7 @@ static void release(emac_handle *h) {
     if (h->own_stream) emac_gpu_stream_destroy(h->stream);
   }
   emac_gpu_free(h->d_buckets);
+  emac_gpu_free(h->d_edges);
   emac_gpu_free(h->staging);
   for (r = 0; r < h->nbuf; r++) {
     int same = h->dsend[r] == h->drecv[r];
@@ -126,49 +132,28 @@ static int map_buffers(emac_handle *h, int r, const void *send, void *recv) {
   return 0;
 }
 
-/* head / vector / tail split of one bucket: vectors need every pointer 16-byte aligned at
-   the same element; if the pointers disagree the whole bucket takes the element path. */
-static void split_alignment(emac_bucket *b, int nsrc, long off, long len, int tsize) {
-  long head = 0;
-  int i, ok = 1;
-  unsigned long mis = (unsigned long)((const char *)b->src[0] + off * tsize) & 15ul;
-  if (mis % (unsigned long)tsize == 0) head = (long)((16ul - mis) & 15ul) / tsize;
-  else ok = 0;
-  if (head > len) head = len;
-  for (i = 0; ok && i < nsrc; i++)
-    if (((unsigned long)((const char *)b->src[i] + (off + head) * tsize) & 15ul) != 0) ok = 0;
-  for (i = 0; ok && i < b->ndst; i++)
-    if (((unsigned long)((char *)b->dst[i] + (off + head) * tsize) & 15ul) != 0) ok = 0;
+/* pointers of a bucket are first set at the start of the whole buffers, then moved to the
+   chunk's first element */
+static void place_bucket(emac_bucket *b, int nsrc, long off, long len, int tsize) {
+  int i;
   for (i = 0; i < nsrc; i++) b->src[i] = (const char *)b->src[i] + off * tsize;
   for (i = 0; i < b->ndst; i++) b->dst[i] = (char *)b->dst[i] + off * tsize;
-  if (!ok) {
-    b->scalar = 1;
-    b->head = b->tail = 0;
-    b->nvec = len;
-    return;
-  }
-  b->scalar = 0;
-  b->head = head;
-  b->nvec = (len - head) * tsize / 16;
-  b->tail = len - head - b->nvec * (16 / tsize);
+  emac_split_alignment(b, nsrc, len, tsize);
 }
 
 static int upload_buckets(emac_handle *h, emac_bucket *b, int nb) {
-  long tv = emac_gpu_tile_vectors(h->plan.dtype, h->nsrc), tiles = 0;
-  int i, rc;
-  for (i = 0; i < nb; i++) {
-    long n = b[i].scalar ? b[i].nvec : b[i].nvec;
-    long t = (n + tv - 1) / tv;
-    if (!b[i].scalar && t == 0 && b[i].head + b[i].tail > 0) t = 1;
-    if (t == 0) t = 1;
-    b[i].tile0 = tiles;
-    tiles += t;
-  }
+  emac_edge *edges = NULL;
+  int rc;
+  if ((rc = emac_layout(b, nb, h->nsrc, h->plan.codes.nlev > 1, h->fan, &edges, &h->nedges, &h->ntiles,
+                        &h->tiles_per_bucket, &h->unroll)))
+    return rc;
   h->nb = nb;
-  h->ntiles = tiles;
-  if (!nb) return 0;
-  if ((rc = emac_gpu_malloc((void **)&h->d_buckets, sizeof(emac_bucket) * (size_t)nb))) return rc;
-  return emac_gpu_memcpy(h->d_buckets, b, sizeof(emac_bucket) * (size_t)nb);
+  if (nb && (rc = emac_gpu_malloc((void **)&h->d_buckets, sizeof(emac_bucket) * (size_t)nb)) == 0)
+    rc = emac_gpu_memcpy(h->d_buckets, b, sizeof(emac_bucket) * (size_t)nb);
+  if (!rc && h->nedges && (rc = emac_gpu_malloc((void **)&h->d_edges, sizeof(emac_edge) * (size_t)h->nedges)) == 0)
+    rc = emac_gpu_memcpy(h->d_edges, edges, sizeof(emac_edge) * (size_t)h->nedges);
+  free(edges);
+  return rc;
 }
 
 static int parse_cfg(const char *copyin, int nranks, emac_copyin *cfg) {
@@ -207,6 +192,7 @@ int ext_mpi_amd_node_allreduce_init(int nranks, const void *const *sendbufs, voi
   h->bytes = (size_t)count * (size_t)h->plan.tsize;
   h->nbuf = nranks;
   h->nsrc = nranks;
+  h->fan = nranks > 1;
   for (r = 0; r < nranks; r++)
     if ((rc = map_buffers(h, r, sendbufs[r], recvbufs[r]))) goto fail;
   b = (emac_bucket *)calloc((size_t)h->plan.npieces * nranks, sizeof(emac_bucket));
@@ -222,7 +208,7 @@ int ext_mpi_amd_node_allreduce_init(int nranks, const void *const *sendbufs, voi
       for (t = 0; t < nranks; t++) bk->src[t] = h->dsend[h->plan.leaf_rank[c][t]];
       for (r = 0; r < nranks; r++) bk->dst[r] = h->drecv[r];
       bk->ndst = nranks;
-      split_alignment(bk, nranks, off, len, h->plan.tsize);
+      place_bucket(bk, nranks, off, len, h->plan.tsize);
       nb++;
     }
   }
@@ -321,7 +307,7 @@ int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, i
       }
       bk->dst[0] = h->drecv[0];
       bk->ndst = 1;
-      split_alignment(bk, R, off, folds[f].count, h->plan.tsize);
+      place_bucket(bk, R, off, folds[f].count, h->plan.tsize);
     }
     free(folds);
   }
@@ -388,8 +374,8 @@ int ext_mpi_amd_start_legs(int handle, int legs) {
   if ((legs & EXT_MPI_AMD_LEG_STAGE) && (rc = stage_in(h))) return rc;
   if ((legs & EXT_MPI_AMD_LEG_REDUCE_SCATTER) && multi && (rc = run_leg(h, EMAC_LEG_RS))) return rc;
   if ((legs & EXT_MPI_AMD_LEG_FOLD) &&
-      (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, &h->plan.codes, h->d_buckets, h->nb, h->ntiles,
-                          h->stream)))
+      (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, h->fan, h->unroll, &h->plan.codes, h->d_buckets, h->nb, h->ntiles,
+                          h->tiles_per_bucket, h->d_edges, h->nedges, h->stream)))
     return rc;
   if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && multi && (rc = run_leg(h, EMAC_LEG_AG))) return rc;
   if ((legs & EXT_MPI_AMD_LEG_STAGE) && (rc = stage_out(h))) return rc;

@@ -1,0 +1,254 @@
+// fold.hip -- CDNA4 (gfx950) kernels of the bucket-reduction hot path + the HIP runtime ABI.
+//
+// Replaces gpu_copy_reduce_kernel<T> (reference src/gpu/cuda_core.cu:50-86) and its C-ABI
+// (cuda_core.cu:7-106, include/gpu/gpu_core.h:11-22).
+//
+// The reference kernel walks a per-element descriptor chain in global memory (integer / and %
+// per element), reloads and re-stores dst once per SREDUCE line, and writes each fan-out copy
+// in a separate launch. Here one launch covers every owner chunk ("bucket") of a plan:
+//   * each lane owns 16-byte vectors (dwordx4) of a chunk, U vectors per source in flight;
+//   * all R leaf sources are loaded once into VGPRs, then folded in registers in the exact
+//     order the reference's SMEMCPY + SREDUCE lines apply them (plan.c's fold tree replayed
+//     through per-leaf level codes: a left fold per recursive-halving step, nested);
+//   * the result is stored once per destination (fused copy-out fan-out), never re-read.
+// HBM traffic per bucket is therefore R reads + D writes of the chunk, the algorithmic
+// minimum; the element-wise add is VALU work hidden under the loads (no MFMA: there is no
+// contraction here). Integer sums are computed in unsigned arithmetic (two's complement wrap,
+// bit-identical to the reference's x86 behaviour without signed-overflow UB); float/double
+// keep IEEE round-to-nearest with denormals (no fast-math, no FTZ flags at build time).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gpu.h"
+
+namespace emac {
+
+template <typename T> struct Lane;
+template <> struct Lane<float> {
+  typedef float S;
+  typedef float V __attribute__((ext_vector_type(4)));
+};
+template <> struct Lane<double> {
+  typedef double S;
+  typedef double V __attribute__((ext_vector_type(2)));
+};
+template <> struct Lane<int> {
+  typedef unsigned int S;
+  typedef unsigned int V __attribute__((ext_vector_type(4)));
+};
+template <> struct Lane<long> {
+  typedef unsigned long S;
+  typedef unsigned long V __attribute__((ext_vector_type(2)));
+};
+
+constexpr int kMaxLevels = 4;  // 16 leaves with radix >= 2
+
+// a multi-level tree needs a composite leaf count (every radix >= 2)
+constexpr bool can_tree(int n) {
+  for (int d = 2; d < n; ++d)
+    if (n % d == 0) return true;
+  return false;
+}
+
+// Replay the fold tree over the leaf values x[0..N) (leaf order of plan.c).
+// Linear form (one reduce-scatter radix): ((x0 + x1) + x2) + ...
+// Tree form: nested left folds, level l accumulates the completed level-(l-1) partials.
+template <int N, bool TREE, typename X>
+__device__ __forceinline__ X fold_leaves(const X (&x)[N], const emac_codes &c) {
+  if constexpr (!TREE) {
+    X acc = x[0];
+#pragma unroll
+    for (int t = 1; t < N; ++t) acc = acc + x[t];
+    return acc;
+  } else {
+    X cur = x[0];
+    X acc[kMaxLevels] = {cur, cur, cur, cur};
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
+      cur = x[t];
+#pragma unroll
+      for (int l = 0; l < kMaxLevels; ++l) {
+        if (l < c.nlev) {  // wave-uniform
+          // level l takes a value at leaf t iff levels 0..l-1 all completed at t
+          if (l == 0 || c.close[t] >= l) acc[l] = ((c.first[t] >> l) & 1) ? cur : acc[l] + cur;
+          cur = acc[l];
+        }
+      }
+    }
+    return cur;  // == acc[nlev-1]: the last leaf closes every level
+  }
+}
+
+// D = fan-out width, a compile-time constant: N for the node form (every rank's receive
+// buffer), 1 for the communicator form. All destination pointers are then loaded up front.
+template <typename T, int N, bool TREE, int D>
+__device__ __forceinline__ void fold_scalar_element(const emac_bucket *b, long e, const emac_codes &c) {
+  typedef typename Lane<T>::S S;
+  S x[N];
+#pragma unroll
+  for (int s = 0; s < N; ++s) x[s] = static_cast<const S *>(b->src[s])[e];
+  const S r = fold_leaves<N, TREE>(x, c);
+#pragma unroll
+  for (int d = 0; d < D; ++d) static_cast<S *>(b->dst[d])[e] = r;
+}
+
+// Loads are nontemporal (each leaf byte is read exactly once; keeping it out of L2/MALL leaves
+// room for the concurrent stream), stores too (results are not re-read by this launch).
+// Measured +12 % at 16 MiB x 8 ranks over plain loads/stores (tools/foldbench.hip).
+template <typename T, int N, int U, bool TREE, int D, bool FULL>
+__device__ __forceinline__ void fold_vectors(const emac_bucket *b, long v0, const emac_codes &c) {
+  typedef typename Lane<T>::S S;
+  typedef typename Lane<T>::V V;
+  const long head = b->head, nvec = b->nvec;
+  V x[U][N];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long v = v0 + (long)u * EMAC_BLOCK;
+#pragma unroll
+    for (int s = 0; s < N; ++s) {
+      const V *p = reinterpret_cast<const V *>(static_cast<const S *>(b->src[s]) + head);
+      if (FULL || v < nvec) x[u][s] = __builtin_nontemporal_load(p + v);
+    }
+  }
+  V r[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) r[u] = fold_leaves<N, TREE>(x[u], c);
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    V *q = reinterpret_cast<V *>(static_cast<S *>(b->dst[d]) + head);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long v = v0 + (long)u * EMAC_BLOCK;
+      if (FULL || v < nvec) __builtin_nontemporal_store(r[u], q + v);
+    }
+  }
+}
+
+// Streaming body: one workgroup per tile (grid-stride); a tile is EMAC_BLOCK*U consecutive
+// 16-byte vectors of one bucket. Nothing element-granular runs here (see fold_edge_kernel).
+template <typename T, int N, int U, bool TREE, int D>
+__global__ __launch_bounds__(EMAC_BLOCK) void fold_kernel(const emac_bucket *__restrict__ bk, int nb,
+                                                          long ntiles, long tiles_per_bucket, emac_codes codes) {
+  constexpr long TILE = (long)EMAC_BLOCK * U;
+  for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // bucket of this tile: arithmetic when every bucket has the same tile count (equal chunks:
+    // the common case), else the last bucket whose first tile is <= tile (wave-uniform search;
+    // each probe is a dependent scalar load, so it is avoided whenever possible)
+    int bi;
+    long t;
+    if (tiles_per_bucket > 0) {
+      bi = (int)(tile / tiles_per_bucket);
+      t = tile - (long)bi * tiles_per_bucket;
+    } else {
+      int lo = 0, hi = nb - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (bk[mid].tile0 <= tile)
+          lo = mid;
+        else
+          hi = mid - 1;
+      }
+      bi = lo;
+      t = tile - bk[lo].tile0;
+    }
+    const emac_bucket *b = bk + bi;
+    const long v0 = t * TILE + threadIdx.x;
+    if ((t + 1) * TILE <= b->nvec)
+      fold_vectors<T, N, U, TREE, D, true>(b, v0, codes);
+    else
+      fold_vectors<T, N, U, TREE, D, false>(b, v0, codes);
+  }
+}
+
+// Element-granular work: unaligned heads/tails and misaligned buckets, one workgroup per item.
+template <typename T, int N, bool TREE, int D>
+__global__ __launch_bounds__(EMAC_BLOCK) void fold_edge_kernel(const emac_bucket *__restrict__ bk,
+                                                               const emac_edge *__restrict__ items,
+                                                               emac_codes codes) {
+  constexpr long EPV = 16 / sizeof(typename Lane<T>::S);
+  const emac_edge it = items[blockIdx.x];
+  const emac_bucket *b = bk + it.bucket;
+  if (it.mode == 1) {
+    for (long e = it.start + threadIdx.x; e < it.start + it.count; e += EMAC_BLOCK)
+      fold_scalar_element<T, N, TREE, D>(b, e, codes);
+  } else {
+    const long nsc = b->head + b->tail;
+    for (long i = threadIdx.x; i < nsc; i += EMAC_BLOCK) {
+      const long e = i < b->head ? i : b->head + b->nvec * EPV + (i - b->head);
+      fold_scalar_element<T, N, TREE, D>(b, e, codes);
+    }
+  }
+}
+
+// ---- instantiation policy (keep in sync with emac_gpu_pick_unroll in fold.hip) ----
+// linear, fan-out N (node form):  N <= 8 -> U in {2, 4};  N > 8 -> U = 1
+// linear, fan-out 1 (comm form):  N <= 8 -> U in {1, 2};  N > 8 -> U = 1
+// tree (composite N), either fan-out: U = 4 / 2 / 1 for N <= 4 / <= 8 / > 8
+constexpr int tree_unroll(int n) { return n <= 4 ? 4 : (n <= 8 ? 2 : 1); }
+
+struct Launch {
+  const emac_codes *c;
+  const emac_bucket *b;
+  int nb;
+  long ntiles, tpb;
+  const emac_edge *edges;
+  int nedges;
+  hipStream_t s;
+};
+
+template <typename T, int N, int U, bool TREE, int D>
+int launch_one(const Launch &L) {
+  const long grid = L.ntiles < 8192 ? L.ntiles : 8192;
+  if (grid > 0)
+    hipLaunchKernelGGL((fold_kernel<T, N, U, TREE, D>), dim3((unsigned)grid), dim3(EMAC_BLOCK), 0, L.s, L.b, L.nb,
+                       L.ntiles, L.tpb, *L.c);
+  if (L.nedges > 0)
+    hipLaunchKernelGGL((fold_edge_kernel<T, N, TREE, D>), dim3((unsigned)L.nedges), dim3(EMAC_BLOCK), 0, L.s, L.b,
+                       L.edges, *L.c);
+  return hipGetLastError() == hipSuccess ? 0 : EMAC_ERR_DEVICE;
+}
+
+template <typename T, int N, bool FAN>
+int launch_nf(bool tree, int unroll, const Launch &L) {
+  constexpr int D = FAN ? N : 1;
+  if constexpr (can_tree(N)) {
+    if (tree) return unroll == tree_unroll(N) ? launch_one<T, N, tree_unroll(N), true, D>(L)
+                                              : EMAC_ERR_UNSUPPORTED;
+  }
+  if (tree) return EMAC_ERR_UNSUPPORTED;
+  if constexpr (N > 8) {
+    return unroll == 1 ? launch_one<T, N, 1, false, D>(L) : EMAC_ERR_UNSUPPORTED;
+  } else if constexpr (FAN) {
+    if (unroll == 4) return launch_one<T, N, 4, false, D>(L);
+    if (unroll == 2) return launch_one<T, N, 2, false, D>(L);
+  } else {
+    if (unroll == 2) return launch_one<T, N, 2, false, D>(L);
+    if (unroll == 1) return launch_one<T, N, 1, false, D>(L);
+  }
+  return EMAC_ERR_UNSUPPORTED;
+}
+
+template <typename T, int N>
+int launch_n(bool tree, bool fan, int unroll, const Launch &L) {
+  if constexpr (N == 1) {
+    return launch_nf<T, 1, false>(false, unroll, L);
+  } else {
+    return fan ? launch_nf<T, N, true>(tree, unroll, L)
+               : launch_nf<T, N, false>(tree, unroll, L);
+  }
+}
+
+template <typename T>
+int launch_t(int nsrc, bool tree, bool fan, int unroll, const Launch &L) {
+  switch (nsrc) {
+#define EMAC_CASE(n) \
+  case n: return launch_n<T, n>(tree, fan, unroll, L);
+    EMAC_CASE(1) EMAC_CASE(2) EMAC_CASE(3) EMAC_CASE(4) EMAC_CASE(5) EMAC_CASE(6) EMAC_CASE(7) EMAC_CASE(8)
+    EMAC_CASE(9) EMAC_CASE(10) EMAC_CASE(11) EMAC_CASE(12) EMAC_CASE(13) EMAC_CASE(14) EMAC_CASE(15) EMAC_CASE(16)
+#undef EMAC_CASE
+  }
+  return EMAC_ERR_UNSUPPORTED;
+}
+
+}  // namespace emac

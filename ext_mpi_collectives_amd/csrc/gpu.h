@@ -22,13 +22,23 @@ extern "C" {
 typedef struct {
   const void *src[EMAC_MAX_RANKS];
   void *dst[EMAC_MAX_RANKS];
-  long head;   /* leading elements before the first 16-byte aligned vector (scalar path) */
-  long nvec;   /* 16-byte vectors after the head (or, if scalar, all elements) */
-  long tail;   /* trailing elements after the vectors (scalar path) */
-  long tile0;  /* first tile index of this bucket inside the launch */
+  long count;  /* elements */
+  long head;   /* leading elements before the first 16-byte aligned vector (edge path) */
+  long nvec;   /* 16-byte vectors after the head (0 if the bucket is misaligned) */
+  long tail;   /* trailing elements after the vectors (edge path) */
+  long tile0;  /* first tile index of this bucket inside the vector launch */
   int ndst;
-  int scalar;  /* 1: pointers disagree on 16-byte alignment -> element-granular path */
+  int scalar;  /* 1: pointers disagree on 16-byte alignment -> every element on the edge path */
 } emac_bucket;
+
+/* Element-granular work kept out of the streaming kernel: the unaligned head and tail of a
+   bucket (mode 0), or a range of a misaligned bucket (mode 1). One workgroup per item. */
+typedef struct {
+  int bucket;
+  int mode;
+  long start, count;
+} emac_edge;
+#define EMAC_EDGE_RANGE 65536
 
 #define EMAC_BLOCK 256
 
@@ -49,12 +59,21 @@ int emac_gpu_stream_sync(void *stream);
 int emac_gpu_stream_query(void *stream); /* 1 idle, 0 busy, <0 error */
 int emac_gpu_device_sync(void);
 
-/* vectors (16 B) one tile covers for an nsrc-leaf fold of dtype */
-long emac_gpu_tile_vectors(int dtype, int nsrc);
+/* Unroll (16-byte vectors per lane per leaf) of a launch: a tile covers EMAC_BLOCK * unroll
+   vectors. fan: the fan-out width equals nsrc (node form) instead of 1. */
+int emac_gpu_pick_unroll(int nsrc, int tree, int fan, long total_vectors);
 
-/* Launch the fold over nb device-resident buckets (ntiles tiles in total) on `stream`. */
-int emac_gpu_fold(int dtype, int op, int nsrc, const emac_codes *codes, const emac_bucket *d_buckets,
-                  int nb, long ntiles, void *stream);
+/* Launch the fold over nb device-resident buckets (ntiles tiles in total) on `stream`.
+   tiles_per_bucket > 0 declares that every bucket spans exactly that many tiles. */
+int emac_gpu_fold(int dtype, int op, int nsrc, int fan, int unroll, const emac_codes *codes,
+                  const emac_bucket *d_buckets, int nb, long ntiles, long tiles_per_bucket,
+                  const emac_edge *d_edges, int nedges, void *stream);
+
+/* layout.c: alignment split of a bucket whose pointers sit at its first element, and the
+   launch layout (tiles, uniform tiles per bucket, unroll, edge items; caller frees edges). */
+void emac_split_alignment(emac_bucket *b, int nsrc, long len, int tsize);
+int emac_layout(emac_bucket *b, int nb, int nsrc, int tree, int fan, emac_edge **edges, int *nedges,
+                long *ntiles, long *tiles_per_bucket, int *unroll);
 
 #ifdef __cplusplus
 }

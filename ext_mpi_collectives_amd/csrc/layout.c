@@ -1,0 +1,83 @@
+/*
+ * layout.c -- turns owner chunks into device launch layouts (host C, no HIP calls):
+ * alignment split of each bucket, tile numbering of the streaming kernel, and the
+ * element-granular edge items. Shared by the engine and the one-chunk device ABI.
+ */
+#include <stdlib.h>
+
+#include "gpu.h"
+
+/* head / vector / tail split of one bucket whose pointers are at element 0 of the chunk:
+   vectors need every pointer 16-byte aligned at the same element; if they disagree the whole
+   bucket is element-granular (edge path). */
+void emac_split_alignment(emac_bucket *b, int nsrc, long len, int tsize) {
+  long head = 0;
+  int i, ok = 1;
+  unsigned long mis = (unsigned long)b->src[0] & 15ul;
+  if (mis % (unsigned long)tsize == 0)
+    head = (long)((16ul - mis) & 15ul) / tsize;
+  else
+    ok = 0;
+  if (head > len) head = len;
+  for (i = 0; ok && i < nsrc; i++)
+    if (((unsigned long)((const char *)b->src[i] + head * tsize) & 15ul) != 0) ok = 0;
+  for (i = 0; ok && i < b->ndst; i++)
+    if (((unsigned long)((char *)b->dst[i] + head * tsize) & 15ul) != 0) ok = 0;
+  b->count = len;
+  if (!ok) {
+    b->scalar = 1;
+    b->head = b->tail = b->nvec = 0;
+    return;
+  }
+  b->scalar = 0;
+  b->head = head;
+  b->nvec = (len - head) * tsize / 16;
+  b->tail = len - head - b->nvec * (16 / tsize);
+}
+
+int emac_layout(emac_bucket *b, int nb, int nsrc, int tree, int fan, emac_edge **edges_out, int *nedges,
+                long *ntiles_out, long *tpb_out, int *unroll_out) {
+  long total = 0, tv, tiles = 0, uniform = -1;
+  int i, ne = 0, unroll;
+  emac_edge *edges;
+  for (i = 0; i < nb; i++) total += b[i].nvec;
+  unroll = emac_gpu_pick_unroll(nsrc, tree, fan, total);
+  tv = (long)EMAC_BLOCK * unroll;
+  for (i = 0; i < nb; i++) {
+    long t = (b[i].nvec + tv - 1) / tv;
+    b[i].tile0 = tiles;
+    tiles += t;
+    uniform = (uniform == -1 || uniform == t) ? t : 0;
+    if (b[i].scalar)
+      ne += (int)((b[i].count + EMAC_EDGE_RANGE - 1) / EMAC_EDGE_RANGE);
+    else if (b[i].head + b[i].tail > 0)
+      ne++;
+  }
+  edges = (emac_edge *)malloc(sizeof(emac_edge) * (size_t)(ne + 1));
+  if (!edges) return EMAC_ERR_MALLOC;
+  ne = 0;
+  for (i = 0; i < nb; i++) {
+    if (b[i].scalar) {
+      long s;
+      for (s = 0; s < b[i].count; s += EMAC_EDGE_RANGE) {
+        edges[ne].bucket = i;
+        edges[ne].mode = 1;
+        edges[ne].start = s;
+        edges[ne].count = b[i].count - s < EMAC_EDGE_RANGE ? b[i].count - s : EMAC_EDGE_RANGE;
+        ne++;
+      }
+    } else if (b[i].head + b[i].tail > 0) {
+      edges[ne].bucket = i;
+      edges[ne].mode = 0;
+      edges[ne].start = 0;
+      edges[ne].count = b[i].head + b[i].tail;
+      ne++;
+    }
+  }
+  *edges_out = edges;
+  *nedges = ne;
+  *ntiles_out = tiles;
+  *tpb_out = uniform > 0 ? uniform : 0;
+  *unroll_out = unroll;
+  return 0;
+}
