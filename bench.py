@@ -19,6 +19,7 @@ stream it runs on. cpu_baseline times the oracle's threaded restatement of the r
 CPU path (oracle/ref_cpu_threads.c) on this host, rank 0 at N = 1 only.
 """
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -50,6 +51,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the 256 MiB and host-buffer points")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU baseline sample")
+    ap.add_argument("--alloc", default="hip", choices=["hip", "torch"],
+                    help="device buffers from hipMalloc (library device ABI, like the reference's "
+                         "tests/benchmark_gpu.c cudaMalloc) or torch's caching allocator")
     return ap.parse_args()
 
 
@@ -81,7 +85,43 @@ def traffic_from_profiles(tag):
     return None
 
 
-def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * MIB, host=False):
+class DevBuf:
+    """A device buffer from the library's device ABI (hipMalloc), filled from host data."""
+
+    def __init__(self, nbytes):
+        import ext_mpi_collectives_amd as emac
+        self.ptr = ctypes.c_void_p()
+        self.nbytes = nbytes
+        L = emac.lib()
+        if L.ext_mpi_amd_gpu_malloc(ctypes.byref(self.ptr), ctypes.c_size_t(nbytes)) != 0:
+            raise MemoryError("ext_mpi_amd_gpu_malloc failed")
+
+    def data_ptr(self):
+        return self.ptr.value
+
+    def upload(self, arr):
+        import ext_mpi_collectives_amd as emac
+        emac.lib().ext_mpi_amd_gpu_memcpy_hd(self.ptr, arr.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(arr.nbytes))
+
+    def download(self, arr):
+        import ext_mpi_collectives_amd as emac
+        emac.lib().ext_mpi_amd_gpu_memcpy_dh(arr.ctypes.data_as(ctypes.c_void_p), self.ptr, ctypes.c_size_t(arr.nbytes))
+
+    def free(self):
+        import ext_mpi_collectives_amd as emac
+        if self.ptr.value:
+            emac.lib().ext_mpi_amd_gpu_free(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+
+def host_random(count, np_dtype, seed):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    if np.dtype(np_dtype).kind == "f":
+        return (rng.random(count, dtype=np.float64) * 2 - 1).astype(np_dtype)
+    return rng.integers(-(1 << 20), 1 << 20, count).astype(np_dtype)
+
+
+def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * MIB, host=False, alloc="torch"):
     """Time `steps` node-form Allreduces (R ranks in this GPU). Returns dict of timings."""
     import torch
     import ext_mpi_collectives_amd as emac
@@ -96,6 +136,15 @@ def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * 
             recvs = [torch.empty(count, dtype=tdtype).pin_memory() for _ in range(R)]
             for r, t in enumerate(sends):
                 t.copy_(torch.rand(count, dtype=torch.float64).mul_(2).sub_(1).to(tdtype))
+        elif alloc == "hip":
+            np_dtype = {torch.float32: np.float32, torch.float64: np.float64, torch.int32: np.int32,
+                        torch.int64: np.int64}[tdtype]
+            sends, recvs = [], []
+            for r in range(R):
+                b = DevBuf(count * tsize)
+                b.upload(host_random(count, np_dtype, 0x5EED0000 + 97 * s + r))
+                sends.append(b)
+                recvs.append(DevBuf(count * tsize))
         else:
             sends = [torch.empty(count, dtype=tdtype, device="cuda") for _ in range(R)]
             recvs = [torch.empty(count, dtype=tdtype, device="cuda") for _ in range(R)]
@@ -113,6 +162,17 @@ def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * 
     emac.start(handles[0])
     stream.synchronize()
     sends, recvs = sets[0]
+    if isinstance(sends[0], DevBuf):
+        np_dtype = {torch.float32: np.float32, torch.float64: np.float64, torch.int32: np.int32,
+                    torch.int64: np.int64}[tdtype]
+        hs = [np.empty(count, np_dtype) for _ in range(R)]
+        hr = [np.empty(count, np_dtype) for _ in range(R)]
+        for b, a in zip(sends, hs):
+            b.download(a)
+        for b, a in zip(recvs, hr):
+            b.download(a)
+        sends = [torch.from_numpy(a) for a in hs]
+        recvs = [torch.from_numpy(a) for a in hr]
     ref = torch.stack([t.to("cuda", torch.float64) for t in sends]).sum(0)
     got = recvs[0].to("cuda", torch.float64)
     tol = 1e-5 * R if tdtype.is_floating_point else 0.0
@@ -129,6 +189,10 @@ def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * 
     t1 = time.perf_counter()
     for h in handles:
         emac.done(h)
+    for sends, recvs in sets:
+        for b in list(sends) + list(recvs):
+            if isinstance(b, DevBuf):
+                b.free()
     del sets
     return {"wall_s": t1 - t0, "event_ms": e0.elapsed_time(e1), "nsets": nsets, "checked": checked,
             "set_bytes": set_bytes}
@@ -188,7 +252,7 @@ def single_gpu(args):
     S = count * tsize
     copyin = args.copyin or f"6;1 -{R} {R}"
     emac.lib()
-    main = node_run(R, count, tdtype, code, copyin, args.steps, args.warmup)
+    main = node_run(R, count, tdtype, code, copyin, args.steps, args.warmup, alloc=args.alloc)
     kernel_s = main["event_ms"] * 1e-3 / args.steps
     bytes_reduced_per_step = R * S
     algo_bytes = 2 * R * S  # R buckets x (R leaf reads + R fan-out writes) x chunk S/R
@@ -211,6 +275,7 @@ def single_gpu(args):
                                f"resident in one MI355X (BASELINE configs[1]), EXT_MPI_COPYIN '{copyin}', fused "
                                f"reduce_copyin + reduce_copyout fold",
                    "ranks": R, "message_bytes_per_rank": S, "copyin": copyin, "layout": "node-in-one-HBM",
+                   "buffers": "hipMalloc" if args.alloc == "hip" else "torch caching allocator",
                    "checked_vs_fp64_sum": main["checked"]},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4),
@@ -226,7 +291,7 @@ def single_gpu(args):
         except RuntimeError as e:
             log("stream copy peak failed:", e)
         big = (256 * MIB) // tsize
-        r256 = node_run(R, big, tdtype, code, copyin, max(4, args.steps // 5), 2)
+        r256 = node_run(R, big, tdtype, code, copyin, max(4, args.steps // 5), 2, alloc=args.alloc)
         k256 = r256["event_ms"] * 1e-3 / max(4, args.steps // 5)
         extras["point_256MiB"] = {
             "gbps_reduced": round(R * big * tsize / k256 / 1e9, 1),

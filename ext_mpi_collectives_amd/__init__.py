@@ -87,6 +87,10 @@ def lib():
         L.ext_mpi_amd_comm_program.argtypes = [c_int, c_int, c_long, c_int, ctypes.c_char_p, c_long,
                                                P(P2P), c_int, P(c_int), P(FoldDesc), c_int, P(c_int), P(c_long)]
         L.ext_mpi_amd_version.restype = ctypes.c_char_p
+        L.ext_mpi_amd_gpu_malloc.argtypes = [P(c_void_p), ctypes.c_size_t]
+        L.ext_mpi_amd_gpu_free.argtypes = [c_void_p]
+        L.ext_mpi_amd_gpu_memcpy_hd.argtypes = [c_void_p, c_void_p, ctypes.c_size_t]
+        L.ext_mpi_amd_gpu_memcpy_dh.argtypes = [c_void_p, c_void_p, ctypes.c_size_t]
         _lib = L
     return _lib
 

@@ -96,31 +96,42 @@ __device__ __forceinline__ void fold_scalar_element(const emac_bucket *b, long e
 // Loads are nontemporal (each leaf byte is read exactly once; keeping it out of L2/MALL leaves
 // room for the concurrent stream), stores too (results are not re-read by this launch).
 // Measured +12 % at 16 MiB x 8 ranks over plain loads/stores (tools/foldbench.hip).
+// All leaf / destination pointers of the bucket are read into scalar registers once, before
+// any load is issued, and used as global (address space 1) bases: the loads become
+// `global_load_dwordx4 v, v_off, s_base nt` issued back to back, instead of flat loads each
+// waiting on its own descriptor read.
 template <typename T, int N, int U, bool TREE, int D, bool FULL>
-__device__ __forceinline__ void fold_vectors(const emac_bucket *b, long v0, const emac_codes &c) {
+__device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_base, const emac_codes &c) {
   typedef typename Lane<T>::S S;
   typedef typename Lane<T>::V V;
-  const long head = b->head, nvec = b->nvec;
+  typedef __attribute__((address_space(1))) V GV;
+  const long head = b->head;
+  // vectors of this tile still inside the bucket (wave-uniform); lane offsets are 32-bit so
+  // every access is `global_*_dwordx4 v, v_off, s_base` with the tile base in SGPRs
+  const long left = b->nvec - tile_base;
+  const GV *src[N];
+  GV *dst[D];
+#pragma unroll
+  for (int s = 0; s < N; ++s) src[s] = (const GV *)(static_cast<const S *>(b->src[s]) + head) + tile_base;
+#pragma unroll
+  for (int d = 0; d < D; ++d) dst[d] = (GV *)(static_cast<S *>(b->dst[d]) + head) + tile_base;
   V x[U][N];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const long v = v0 + (long)u * EMAC_BLOCK;
+    const unsigned v = threadIdx.x + (unsigned)(u * EMAC_BLOCK);
 #pragma unroll
-    for (int s = 0; s < N; ++s) {
-      const V *p = reinterpret_cast<const V *>(static_cast<const S *>(b->src[s]) + head);
-      if (FULL || v < nvec) x[u][s] = __builtin_nontemporal_load(p + v);
-    }
+    for (int s = 0; s < N; ++s)
+      if (FULL || (long)v < left) x[u][s] = __builtin_nontemporal_load(src[s] + v);
   }
   V r[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) r[u] = fold_leaves<N, TREE>(x[u], c);
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    V *q = reinterpret_cast<V *>(static_cast<S *>(b->dst[d]) + head);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const long v = v0 + (long)u * EMAC_BLOCK;
-      if (FULL || v < nvec) __builtin_nontemporal_store(r[u], q + v);
+      const unsigned v = threadIdx.x + (unsigned)(u * EMAC_BLOCK);
+      if (FULL || (long)v < left) __builtin_nontemporal_store(r[u], dst[d] + v);
     }
   }
 }
@@ -138,7 +149,8 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_kernel(const emac_bucket *__r
     int bi;
     long t;
     if (tiles_per_bucket > 0) {
-      bi = (int)(tile / tiles_per_bucket);
+      // tile counts fit 32 bits (< 2^31 tiles of >= 4 KiB); 32-bit division is a short sequence
+      bi = (int)((unsigned)tile / (unsigned)tiles_per_bucket);
       t = tile - (long)bi * tiles_per_bucket;
     } else {
       int lo = 0, hi = nb - 1;
@@ -153,11 +165,10 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_kernel(const emac_bucket *__r
       t = tile - bk[lo].tile0;
     }
     const emac_bucket *b = bk + bi;
-    const long v0 = t * TILE + threadIdx.x;
     if ((t + 1) * TILE <= b->nvec)
-      fold_vectors<T, N, U, TREE, D, true>(b, v0, codes);
+      fold_vectors<T, N, U, TREE, D, true>(b, t * TILE, codes);
     else
-      fold_vectors<T, N, U, TREE, D, false>(b, v0, codes);
+      fold_vectors<T, N, U, TREE, D, false>(b, t * TILE, codes);
   }
 }
 

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "ext_mpi_amd.h"
+#include "../ext_mpi_collectives_amd/csrc/fold_kernel.hpp"
 
 #define CHECK(x)                                                                  \
   do {                                                                            \
@@ -143,6 +144,7 @@ int main(int argc, char **argv) {
   long S = mib << 20, nvec_rank = S / 16, C = nvec_rank / R;  // vectors per chunk
   int nsets = std::max<long>(2, (640L << 20) / (2 * R * S) + 1);
   std::vector<Bucket *> dbk(nsets);
+  std::vector<emac_bucket *> ebk_rot(nsets), ebk_prod(nsets);
   std::vector<f4 *> bufs;
   std::vector<int> prod_handles;
   for (int st = 0; st < nsets; st++) {
@@ -174,13 +176,37 @@ int main(int argc, char **argv) {
       for (int d = 0; d < R; d++) hb[c].dst[d] = recv[d] + c * C;
       hb[c].nvec = C;
     }
+    {  // production kernel template on harness-built descriptors: rotated and production leaf order
+      emac_bucket eb[2][R];
+      memset(eb, 0, sizeof(eb));
+      for (int o = 0; o < 2; o++)
+        for (int c = 0; c < R; c++) {
+          for (int t = 0; t < R; t++) {
+            int leaf = o == 0 ? (c + t) % R : (t == 0 ? c : (t <= c ? t - 1 : t));
+            eb[o][c].src[t] = send[leaf] + c * C;
+          }
+          for (int d = 0; d < R; d++) eb[o][c].dst[d] = recv[d] + c * C;
+          eb[o][c].count = C * 4;
+          eb[o][c].nvec = C;
+          eb[o][c].ndst = R;
+          eb[o][c].tile0 = (long)c * (C / 512);
+        }
+      CHECK(hipMalloc(&ebk_rot[st], sizeof(eb[0])));
+      CHECK(hipMalloc(&ebk_prod[st], sizeof(eb[1])));
+      CHECK(hipMemcpy(ebk_rot[st], eb[0], sizeof(eb[0]), hipMemcpyHostToDevice));
+      CHECK(hipMemcpy(ebk_prod[st], eb[1], sizeof(eb[1]), hipMemcpyHostToDevice));
+    }
     CHECK(hipMalloc(&dbk[st], sizeof(hb)));
     CHECK(hipMemcpy(dbk[st], hb, sizeof(hb), hipMemcpyHostToDevice));
   }
   hipStream_t s;
   CHECK(hipStreamCreate(&s));
   for (int h : prod_handles) ext_mpi_amd_set_stream(h, s);
-  std::vector<float> prod_us;
+  std::vector<float> prod_us, tmpl_rot_us, tmpl_prod_us;
+  emac_codes codes;
+  memset(&codes, 0, sizeof(codes));
+  codes.nlev = 1;
+  codes.nleaf = R;
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
@@ -247,6 +273,18 @@ int main(int argc, char **argv) {
       CHECK(hipEventElapsedTime(&ms, e0, e1));
       v.us.push_back(ms * 1000 / per);
     }
+    for (int o = 0; o < 2; o++) {
+      CHECK(hipEventRecord(e0, s));
+      for (int i = 0; i < per; i++) {
+        emac::Launch L = {&codes, (o ? ebk_prod : ebk_rot)[(k++) % nsets], R, (long)R * (C / 512), C / 512, nullptr, 0, s};
+        emac::launch_one<float, R, 2, false, R>(L);
+      }
+      CHECK(hipEventRecord(e1, s));
+      CHECK(hipEventSynchronize(e1));
+      float ms;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      (o ? tmpl_prod_us : tmpl_rot_us).push_back(ms * 1000 / per);
+    }
     {
       CHECK(hipEventRecord(e0, s));
       for (int i = 0; i < per; i++) ext_mpi_amd_start(prod_handles[(k++) % nsets]);
@@ -284,6 +322,10 @@ int main(int argc, char **argv) {
            bytes / med(v.us) / 1e3, bytes / mn(v.us) / 1e3);
   printf("%-20s median %8.2f us  min %8.2f us  %7.1f GB/s\n", "PRODUCTION C-ABI", med(prod_us), mn(prod_us),
          bytes / med(prod_us) / 1e3);
+  printf("%-20s median %8.2f us  min %8.2f us  %7.1f GB/s\n", "prod tmpl, rot order", med(tmpl_rot_us),
+         mn(tmpl_rot_us), bytes / med(tmpl_rot_us) / 1e3);
+  printf("%-20s median %8.2f us  min %8.2f us  %7.1f GB/s\n", "prod tmpl, prod order", med(tmpl_prod_us),
+         mn(tmpl_prod_us), bytes / med(tmpl_prod_us) / 1e3);
   printf("%-20s median %8.2f us  %7.1f GB/s (read+write of %.0f MiB)\n", "copy float4", med(copy_us),
          bytes / med(copy_us) / 1e3, R * S / 1048576.0);
   printf("%-20s median %8.2f us  %7.1f GB/s (read of %.0f MiB)\n", "read float4", med(read_us),
