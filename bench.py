@@ -127,7 +127,10 @@ def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * 
     import ext_mpi_collectives_amd as emac
     tsize = torch.empty((), dtype=tdtype).element_size()
     set_bytes = 2 * R * count * tsize
-    nsets = 1 if host else max(2, math.ceil(min_set_bytes / max(1, set_bytes)))
+    if host or min_set_bytes <= 0:
+        nsets = 1
+    else:
+        nsets = max(2, math.ceil(min_set_bytes / max(1, set_bytes)))
     stream = torch.cuda.Stream()
     sets, handles = [], []
     for s in range(nsets):
@@ -196,6 +199,47 @@ def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * 
     del sets
     return {"wall_s": t1 - t0, "event_ms": e0.elapsed_time(e1), "nsets": nsets, "checked": checked,
             "set_bytes": set_bytes}
+
+
+def comm_shape_fold(R, chunk, tdtype, code, steps):
+    """The COMM form's per-GPU fold (R leaves of one chunk -> 1 destination) on this one GPU, at
+    the chunk size an R-GPU run of the same message uses: the 1-GPU reference for the
+    'per-GPU rate retained at N GPUs' comparison. Buffer sets rotate past the
+    Infinity Cache."""
+    import torch
+    import ext_mpi_collectives_amd as emac
+    tsize = torch.empty((), dtype=tdtype).element_size()
+    nbytes = chunk * tsize
+    nsets = max(2, math.ceil(640 * MIB / ((R + 1) * nbytes)))
+    np_dtype = {torch.float32: np.float32, torch.float64: np.float64, torch.int32: np.int32,
+                torch.int64: np.int64}[tdtype]
+    bufs, handles = [], []
+    stream = torch.cuda.Stream()
+    for st in range(nsets):
+        srcs = [DevBuf(nbytes) for _ in range(R)]
+        for i, b in enumerate(srcs):
+            b.upload(host_random(chunk, np_dtype, 77 * st + i))
+        dst = DevBuf(nbytes)
+        h = emac.fold_init([b.data_ptr() for b in srcs], [dst.data_ptr()], chunk, code)
+        emac.set_stream(h, stream.cuda_stream)
+        bufs += srcs + [dst]
+        handles.append(h)
+    for k in range(10):
+        emac.start(handles[k % nsets])
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    stream.synchronize()
+    e0.record(stream)
+    for k in range(steps):
+        emac.start(handles[k % nsets])
+    e1.record(stream)
+    stream.synchronize()
+    t = e0.elapsed_time(e1) * 1e-3 / steps
+    for h in handles:
+        emac.done(h)
+    for b in bufs:
+        b.free()
+    return {"chunk_bytes": nbytes, "leaves": R, "avg_launch_us": round(t * 1e6, 2),
+            "gbps_reduced": round(R * nbytes / t / 1e9, 1), "achieved_gbps": round((R + 1) * nbytes / t / 1e9, 1)}
 
 
 def stream_copy_peak():
@@ -299,6 +343,27 @@ def single_gpu(args):
             "frac_of_peak": round(2 * R * big * tsize / k256 / 1e9 / HBM_PEAK_GBPS, 4),
             "read_gbps": round(R * big * tsize / k256 / 1e9, 1),
             "avg_launch_us": round(k256 * 1e6, 1), "checked": r256["checked"]}
+        # latency -> bandwidth crossover of the node form (cf. BASELINE configs[4] on 8 GPUs);
+        # small points reuse one buffer set (as the reference's latency runs do), large ones rotate
+        sweep = []
+        for nbytes in (8, 1024, 64 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20):
+            cnt = max(1, nbytes // tsize)
+            st = 200 if nbytes <= (1 << 20) else 40
+            r = node_run(R, cnt, tdtype, code, copyin, st, 5, min_set_bytes=0 if nbytes < (16 << 20) else 640 * MIB,
+                         alloc=args.alloc)
+            sweep.append({"bytes_per_rank": cnt * tsize, "us_per_allreduce": round(r["wall_s"] * 1e6 / st, 2),
+                          "gpu_us_per_allreduce": round(r["event_ms"] * 1e3 / st, 2),
+                          "gbps_reduced": round(R * cnt * tsize * st / r["wall_s"] / 1e9, 2),
+                          "checked": r["checked"]})
+        extras["sweep_node_form"] = sweep
+        chains = {}
+        for cp in ("6;1 -2 -2 -2 2 2 2", "6;1 -4 -2 2 4", "6;-64 -8 8"):
+            r = node_run(R, count, tdtype, code, cp, 20, 3, alloc=args.alloc)
+            k = r["event_ms"] * 1e-3 / 20
+            chains[cp] = {"gbps_reduced": round(R * S / k / 1e9, 1), "avg_launch_us": round(k * 1e6, 2),
+                          "checked": r["checked"]}
+        extras["radix_chains_16MiB"] = chains
+        extras["fold_comm_shape"] = comm_shape_fold(R, count // R, tdtype, code, 200)
         hst = node_run(R, count, tdtype, code, copyin, 5, 1, host=True)
         extras["host_buffers_pcie_inclusive"] = {
             "gbps_reduced": round(R * S * 5 / hst["wall_s"] / 1e9, 2),
@@ -317,6 +382,9 @@ def multi_gpu(args):
     import ext_mpi_collectives_amd as emac
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
+    import signal
+    signal.signal(signal.SIGALRM, lambda *_: (log(f"rank {rank}: watchdog expired"), os._exit(3)))
+    signal.alarm(900)  # a rank stuck in a collective must not hang the job
     torch.cuda.set_device(local)
     dist.init_process_group("gloo")
     tdtype, code, dname, tsize = dtype_info(args.dtype)
@@ -361,7 +429,49 @@ def multi_gpu(args):
     stream.synchronize()
     fold_s = torch.tensor([e0.elapsed_time(e1) * 1e-3 / args.steps], dtype=torch.float64)
     dist.all_reduce(fold_s, op=dist.ReduceOp.MAX)
+    # the same fold on rank 0's GPU while every other GPU idles: the 1-GPU reference at equal C
+    dist.barrier()
+    alone_s = torch.zeros(1, dtype=torch.float64)
+    if rank == 0:
+        e0.record(stream)
+        for _ in range(args.steps):
+            emac.start_legs(h, emac.LEG_FOLD)
+        e1.record(stream)
+        stream.synchronize()
+        alone_s[0] = e0.elapsed_time(e1) * 1e-3 / args.steps
+    dist.barrier()
     emac.done(h)
+    # BASELINE configs[3] (double, 256 MiB per rank) and a configs[4]-style size sweep, bounded
+    extra_points = []
+    points = [(args.dtype, n) for n in (8, 64 << 10, 1 << 20, 64 << 20, 256 << 20)] + [("double", 256 << 20)]
+    for dname_p, nbytes in points:
+        tdt, cde, _, tsz = dtype_info(dname_p)
+        cnt = max(1, nbytes // tsz)
+        try:
+            sb = torch.empty(cnt, dtype=tdt, device="cuda")
+            rb = torch.empty(cnt, dtype=tdt, device="cuda")
+            fill(sb, 0x5EED0000 + rank)
+            hp = emac.allreduce_init(sb.data_ptr(), rb.data_ptr(), cnt, cde, comm, copyin)
+            emac.set_stream(hp, stream.cuda_stream)
+            st = 50 if nbytes <= (1 << 20) else 10
+            for _ in range(3):
+                emac.start(hp)
+            stream.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(st):
+                emac.start(hp)
+            stream.synchronize()
+            dist.barrier()
+            el_p = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+            dist.all_reduce(el_p, op=dist.ReduceOp.MAX)
+            emac.done(hp)
+            extra_points.append({"dtype": dname_p, "bytes_per_rank": cnt * tsz,
+                                 "us_per_allreduce": round(el_p.item() * 1e6 / st, 2),
+                                 "algbw_gbps": round(cnt * tsz * st / el_p.item() / 1e9, 2)})
+            del sb, rb
+        except Exception as e:  # a failing extra point must not lose the headline line
+            extra_points.append({"dtype": dname_p, "bytes_per_rank": nbytes, "error": str(e)})
     emac.comm_free(comm)
     if rank == 0:
         wall = el.item()
@@ -385,11 +495,16 @@ def multi_gpu(args):
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None, "kernel": "fold_kernel",
                          "algorithmic_bytes_per_launch": int(algo), "avg_launch_us": round(kf * 1e6, 2)},
             "extras": {"fold_gbps_reduced_per_gpu": round(S / kf / 1e9, 1),
-                       "end_to_end_algbw_gbps_per_gpu": round(S * args.steps / wall / 1e9, 2)},
+                       "fold_alone_on_one_gpu_us": round(alone_s.item() * 1e6, 2),
+                       "per_gpu_fold_rate_retained": round(alone_s.item() / kf, 3),
+                       "end_to_end_algbw_gbps_per_gpu": round(S * args.steps / wall / 1e9, 2),
+                       "xgmi_bound_us": round(2 * (world - 1) / world * S / (min(world - 1, 7) * 153e9) * 1e6, 1),
+                       "sweep_comm_form": extra_points},
         }
         print(json.dumps(out), flush=True)
     dist.barrier()
     dist.destroy_process_group()
+    signal.alarm(0)
 
 
 def main():

@@ -69,6 +69,7 @@ def lib():
         P = ctypes.POINTER
         L.ext_mpi_amd_node_allreduce_init.argtypes = [c_int, P(c_void_p), P(c_void_p), c_long, c_int, c_int,
                                                       ctypes.c_char_p, P(c_int)]
+        L.ext_mpi_amd_fold_init.argtypes = [c_int, P(c_void_p), c_int, P(c_void_p), c_long, c_int, c_int, P(c_int)]
         L.ext_mpi_amd_get_unique_id.argtypes = [c_void_p]
         L.ext_mpi_amd_comm_init.argtypes = [c_int, c_int, c_void_p, c_int, P(c_int)]
         L.ext_mpi_amd_comm_free.argtypes = [c_int]
@@ -124,6 +125,16 @@ def node_allreduce_init(sendptrs, recvptrs, count, dtype, copyin=None, op=SUM):
     h = ctypes.c_int(-1)
     _check("ext_mpi_amd_node_allreduce_init",
            lib().ext_mpi_amd_node_allreduce_init(n, s, r, count, dtype, op, _enc(copyin), ctypes.byref(h)))
+    return h.value
+
+
+def fold_init(srcptrs, dstptrs, count, dtype, op=SUM):
+    """Persistent fold of one chunk: every dst = ((src0 + src1) + src2) + ... (device pointers)."""
+    s = (ctypes.c_void_p * len(srcptrs))(*srcptrs)
+    d = (ctypes.c_void_p * len(dstptrs))(*dstptrs)
+    h = ctypes.c_int(-1)
+    _check("ext_mpi_amd_fold_init",
+           lib().ext_mpi_amd_fold_init(len(srcptrs), s, len(dstptrs), d, count, dtype, op, ctypes.byref(h)))
     return h.value
 
 

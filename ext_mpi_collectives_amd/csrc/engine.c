@@ -224,6 +224,50 @@ fail:
   return rc;
 }
 
+/* One owner chunk as a persistent handle: the persistent form of the device C-ABI's
+   ext_mpi_amd_gpu_copy_reduce (the reference launches one such descriptor per GPU stream,
+   byte_code.c:936-992). Leaves are folded in the given order, left to right. */
+int ext_mpi_amd_fold_init(int nsrc, const void *const *srcs, int ndst, void *const *dsts, long count, int dtype,
+                          int op, int *handle) {
+  emac_handle *h;
+  emac_bucket b;
+  emac_copyin cfg;
+  int rc, i;
+  if (!handle || !srcs || nsrc < 1 || nsrc > EMAC_MAX_RANKS || ndst < 1 || count < 0) return EMAC_ERR_ARG;
+  if (ndst > 1 && ndst != nsrc) return EMAC_ERR_UNSUPPORTED; /* fan-out width is 1 or nsrc */
+  *handle = -1;
+  if (emac_gpu_device_count() <= 0) return EMAC_ERR_DEVICE;
+  for (i = 0; i < nsrc; i++)
+    if (!emac_gpu_is_device_pointer(srcs[i])) return EMAC_ERR_ARG;
+  for (i = 0; i < ndst; i++)
+    if (!emac_gpu_is_device_pointer(dsts[i])) return EMAC_ERR_ARG;
+  h = (emac_handle *)calloc(1, sizeof(emac_handle));
+  if (!h) return EMAC_ERR_MALLOC;
+  h->kind = KIND_NODE;
+  /* a linear plan over nsrc leaves supplies the codes (one level, leaves in given order) */
+  memset(&cfg, 0, sizeof(cfg));
+  cfg.method = 6;
+  cfg.split = 1;
+  cfg.nrs = 1;
+  cfg.rs[0] = nsrc;
+  if ((rc = emac_plan_build(&h->plan, nsrc, count, dtype, op, nsrc > 1 ? &cfg : NULL))) goto fail;
+  emac_gpu_get_device(&h->device);
+  h->nsrc = nsrc;
+  h->fan = ndst > 1;
+  memset(&b, 0, sizeof(b));
+  for (i = 0; i < nsrc; i++) b.src[i] = srcs[i];
+  for (i = 0; i < ndst; i++) b.dst[i] = dsts[i];
+  b.ndst = ndst;
+  place_bucket(&b, nsrc, 0, count, h->plan.tsize);
+  if ((rc = upload_buckets(h, &b, count > 0 ? 1 : 0))) goto fail;
+  if ((rc = emac_gpu_stream_create(&h->stream))) goto fail;
+  if ((rc = finish_init(h, handle))) goto fail;
+  return 0;
+fail:
+  release(h);
+  return rc;
+}
+
 /* ------------------------------ COMM form (RCCL) ------------------------------ */
 
 int ext_mpi_amd_get_unique_id(void *id) {

@@ -63,6 +63,13 @@ extern "C" {
 int ext_mpi_amd_node_allreduce_init(int nranks, const void *const *sendbufs, void *const *recvbufs, long count,
                                     int dtype, int op, const char *copyin, int *handle);
 
+/* ---- one owner chunk as a persistent handle (device pointers): dsts[d] = fold of srcs in the
+ * given order, ((srcs[0] + srcs[1]) + srcs[2]) + ... ; ndst is 1 or nsrc. The persistent form of
+ * the reference's per-stream copy/reduce descriptor (src/core/byte_code.c:936-992,
+ * src/gpu/cuda_core.cu:88-106). */
+int ext_mpi_amd_fold_init(int nsrc, const void *const *srcs, int ndst, void *const *dsts, long count, int dtype,
+                          int op, int *handle);
+
 /* ---- node communicator: one rank per GPU, reduce-scatter / allgather legs over RCCL ---- */
 int ext_mpi_amd_get_unique_id(void *id /* EXT_MPI_AMD_UNIQUE_ID_BYTES */);
 int ext_mpi_amd_comm_init(int rank, int size, const void *id, int device, int *comm);

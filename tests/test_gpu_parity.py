@@ -193,3 +193,34 @@ def test_comm_single_rank_rccl():
     emac.done(h)
     emac.comm_free(comm)
     assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("code", CODES)
+@pytest.mark.parametrize("nsrc,ndst", [(1, 1), (3, 1), (8, 1), (8, 8), (16, 1)])
+def test_fold_handle_and_copy_reduce(code, nsrc, ndst):
+    """The persistent one-chunk fold and the device C-ABI copy_reduce: left fold in the given
+    leaf order, every destination identical; compared with a sequential numpy fold."""
+    count = 70001
+    srcs_np = xorshift_inputs(nsrc, count, code, seed_base=991 + nsrc)
+    want = srcs_np[0].copy()
+    with np.errstate(over="ignore"):
+        for x in srcs_np[1:]:
+            want = want + x
+    srcs = [_dev(x) for x in srcs_np]
+    for how in ("handle", "copy_reduce"):
+        dsts = [torch.full((count,), -1, dtype=TORCH[code], device="cuda") for _ in range(ndst)]
+        if how == "handle":
+            h = emac.fold_init([t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts], count, code)
+            emac.start(h)
+            emac.wait(h)
+            emac.done(h)
+        else:
+            L = emac.lib()
+            L.ext_mpi_amd_gpu_copy_reduce.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                      ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
+                                                      ctypes.POINTER(ctypes.c_void_p), ctypes.c_long, ctypes.c_void_p]
+            sp = (ctypes.c_void_p * nsrc)(*[t.data_ptr() for t in srcs])
+            dp = (ctypes.c_void_p * ndst)(*[t.data_ptr() for t in dsts])
+            assert L.ext_mpi_amd_gpu_copy_reduce(code, emac.SUM, nsrc, sp, ndst, dp, count, None) == 0
+        for d in dsts:
+            assert np.array_equal(d.cpu().numpy().view(np.uint8), want.view(np.uint8)), (how, nsrc, ndst)

@@ -75,6 +75,85 @@ __global__ __launch_bounds__(BLOCK) void fold(const Bucket *__restrict__ bk, lon
   }
 }
 
+// harness kernel with global (address space 1) accesses, pointers still read lazily
+template <int BLOCK, int U>
+__global__ __launch_bounds__(BLOCK) void fold_glob(const Bucket *__restrict__ bk, long tiles_per_bucket, long ntiles) {
+  typedef __attribute__((address_space(1))) f4 G;
+  for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const Bucket *b = bk + tile / tiles_per_bucket;
+    const long v0 = (tile % tiles_per_bucket) * (long)BLOCK * U + threadIdx.x;
+    f4 x[U][R];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int s = 0; s < R; ++s) {
+        long v = v0 + (long)u * BLOCK;
+        x[u][s] = v < b->nvec ? __builtin_nontemporal_load((const G *)b->src[s] + v) : f4{0, 0, 0, 0};
+      }
+    f4 r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      r[u] = x[u][0];
+#pragma unroll
+      for (int s = 1; s < R; ++s) r[u] = r[u] + x[u][s];
+    }
+#pragma unroll
+    for (int d = 0; d < R; ++d)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        long v = v0 + (long)u * BLOCK;
+        if (v < b->nvec) __builtin_nontemporal_store(r[u], (G *)b->dst[d] + v);
+      }
+  }
+}
+
+// hoisted pointers + global accesses, loads issued source-major with a wave-level stagger
+// (s_sleep after each group of 4 loads) to test whether burst issue hurts
+template <int BLOCK, int U, int STAGGER>
+__global__ __launch_bounds__(BLOCK) void fold_hoist(const Bucket *__restrict__ bk, long tiles_per_bucket, long ntiles) {
+  typedef __attribute__((address_space(1))) f4 G;
+  for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const Bucket *b = bk + (unsigned)tile / (unsigned)tiles_per_bucket;
+    const long base = (long)((unsigned)tile % (unsigned)tiles_per_bucket) * BLOCK * U;
+    const G *sp[R];
+    G *dp[R];
+#pragma unroll
+    for (int s = 0; s < R; ++s) sp[s] = (const G *)b->src[s] + base;
+#pragma unroll
+    for (int s = 0; s < R; ++s) dp[s] = (G *)b->dst[s] + base;
+    f4 x[U][R];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int s = 0; s < R; ++s) {
+        x[u][s] = __builtin_nontemporal_load(sp[s] + threadIdx.x + u * BLOCK);
+        if (STAGGER && (s & 3) == 3) __builtin_amdgcn_s_sleep(STAGGER);
+      }
+    f4 r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      r[u] = x[u][0];
+#pragma unroll
+      for (int s = 1; s < R; ++s) r[u] = r[u] + x[u][s];
+    }
+#pragma unroll
+    for (int d = 0; d < R; ++d)
+#pragma unroll
+      for (int u = 0; u < U; ++u) __builtin_nontemporal_store(r[u], dp[d] + threadIdx.x + u * BLOCK);
+  }
+}
+
+template <int BLOCK, int U>
+void launch_glob(const Bucket *b, long tpb, long ntiles, hipStream_t s, int grid_cap) {
+  long g = std::min<long>(ntiles, grid_cap);
+  hipLaunchKernelGGL((fold_glob<BLOCK, U>), dim3(g), dim3(BLOCK), 0, s, b, tpb, ntiles);
+}
+template <int BLOCK, int U, int ST>
+void launch_hoist(const Bucket *b, long tpb, long ntiles, hipStream_t s, int grid_cap) {
+  long g = std::min<long>(ntiles, grid_cap);
+  hipLaunchKernelGGL((fold_hoist<BLOCK, U, ST>), dim3(g), dim3(BLOCK), 0, s, b, tpb, ntiles);
+}
+
 // destination-major variant: each lane stores its U vectors to one destination before the next
 template <int BLOCK, int U>
 __global__ __launch_bounds__(BLOCK) void fold_wide(const Bucket *__restrict__ bk, long tiles_per_bucket, long ntiles) {
@@ -220,19 +299,17 @@ int main(int argc, char **argv) {
   std::vector<V> vs = {
       {"b256_u2 (r1 prod)", launch_fold<256, 2, false, false>, 512, 8192, {}},
       {"b256_u2_ntls", launch_fold<256, 2, true, true>, 512, 8192, {}},
+      {"glob_u2", launch_glob<256, 2>, 512, 8192, {}},
+      {"hoist_u2", launch_hoist<256, 2, 0>, 512, 8192, {}},
+      {"hoist_u2_sleep1", launch_hoist<256, 2, 1>, 512, 8192, {}},
+      {"hoist_u2_sleep4", launch_hoist<256, 2, 4>, 512, 8192, {}},
+      {"hoist_u2_g1792", launch_hoist<256, 2, 0>, 512, 1792, {}},
+      {"b256_u2_ntls_g1792", launch_fold<256, 2, true, true>, 512, 1792, {}},
+      {"hoist_u4", launch_hoist<256, 4, 0>, 1024, 8192, {}},
+      {"hoist_u1", launch_hoist<256, 1, 0>, 256, 8192, {}},
       {"b256_u4_ntls", launch_fold<256, 4, true, true>, 1024, 8192, {}},
-      {"b256_u1_ntls", launch_fold<256, 1, true, true>, 256, 8192, {}},
       {"b512_u2_ntls", launch_fold<512, 2, true, true>, 1024, 8192, {}},
-      {"b512_u1_ntls", launch_fold<512, 1, true, true>, 512, 8192, {}},
-      {"b1024_u1_ntls", launch_fold<1024, 1, true, true>, 1024, 8192, {}},
-      {"b256_u2_ntls_g1024", launch_fold<256, 2, true, true>, 512, 1024, {}},
-      {"b256_u2_ntls_g1536", launch_fold<256, 2, true, true>, 512, 1536, {}},
-      {"b256_u4_ntls_g1024", launch_fold<256, 4, true, true>, 1024, 1024, {}},
-      {"b256_u2_ntl", launch_fold<256, 2, true, false>, 512, 8192, {}},
-      {"b256_u2_nts", launch_fold<256, 2, false, true>, 512, 8192, {}},
       {"b256_u2_ntls", launch_fold<256, 2, true, true>, 512, 8192, {}},
-      {"b256_u2_grid1024", launch_fold<256, 2, false, false>, 512, 1024, {}},
-      {"wide_b256_u4", launch_wide<256, 4>, 1024, 8192, {}},
   };
   // copy / read ceilings over the same bytes per launch as the fold (2RS: R*S read + R*S write)
   f4 *ca, *cb;
