@@ -54,6 +54,7 @@ typedef struct {
   int nb;
   long ntiles;
   long tiles_per_bucket; /* > 0 when every bucket has the same tile count */
+  int all_full;          /* every bucket is a whole number of tiles */
   int fan;               /* fan-out width == nsrc (node form) */
   emac_edge *d_edges;    /* element-granular work items (device) */
   int nedges;
@@ -145,7 +146,7 @@ static int upload_buckets(emac_handle *h, emac_bucket *b, int nb) {
   emac_edge *edges = NULL;
   int rc;
   if ((rc = emac_layout(b, nb, h->nsrc, h->plan.codes.nlev > 1, h->fan, &edges, &h->nedges, &h->ntiles,
-                        &h->tiles_per_bucket, &h->unroll)))
+                        &h->tiles_per_bucket, &h->all_full, &h->unroll)))
     return rc;
   h->nb = nb;
   if (nb && (rc = emac_gpu_malloc((void **)&h->d_buckets, sizeof(emac_bucket) * (size_t)nb)) == 0)
@@ -419,7 +420,7 @@ int ext_mpi_amd_start_legs(int handle, int legs) {
   if ((legs & EXT_MPI_AMD_LEG_REDUCE_SCATTER) && multi && (rc = run_leg(h, EMAC_LEG_RS))) return rc;
   if ((legs & EXT_MPI_AMD_LEG_FOLD) &&
       (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, h->fan, h->unroll, &h->plan.codes, h->d_buckets, h->nb, h->ntiles,
-                          h->tiles_per_bucket, h->d_edges, h->nedges, h->stream)))
+                          h->tiles_per_bucket, h->all_full, h->d_edges, h->nedges, h->stream)))
     return rc;
   if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && multi && (rc = run_leg(h, EMAC_LEG_AG))) return rc;
   if ((legs & EXT_MPI_AMD_LEG_STAGE) && (rc = stage_out(h))) return rc;

@@ -52,10 +52,10 @@ int emac_gpu_pick_unroll(int nsrc, int tree, int fan, long total_vectors) {
 }
 
 int emac_gpu_fold(int dtype, int op, int nsrc, int fan, int unroll, const emac_codes *codes,
-                  const emac_bucket *d_buckets, int nb, long ntiles, long tiles_per_bucket,
+                  const emac_bucket *d_buckets, int nb, long ntiles, long tiles_per_bucket, int all_full,
                   const emac_edge *d_edges, int nedges, void *stream) {
   const bool tree = codes->nlev > 1;
-  const emac::Launch L = {codes, d_buckets, nb, ntiles, tiles_per_bucket, d_edges, nedges,
+  const emac::Launch L = {codes, d_buckets, nb, ntiles, tiles_per_bucket, all_full, d_edges, nedges,
                           static_cast<hipStream_t>(stream)};
   if (op != EMAC_SUM) return EMAC_ERR_UNSUPPORTED;
   if (nb <= 0 || (ntiles <= 0 && nedges <= 0)) return 0;
@@ -181,11 +181,11 @@ int ext_mpi_amd_gpu_copy_reduce(int dtype, int op, int nsrc, const void *const *
   b.ndst = ndst;
   emac_split_alignment(&b, nsrc, count, tsize);
   emac_edge *edges = nullptr, *d_edges = nullptr;
-  int nedges = 0, unroll = 1;
+  int nedges = 0, unroll = 1, all_full = 0;
   long ntiles = 0, tpb = 0;
   const int fan = ndst > 1;
   if (ndst > 1 && ndst != nsrc) return EMAC_ERR_UNSUPPORTED; /* fan-out width is 1 or nsrc */
-  if ((rc = emac_layout(&b, 1, nsrc, 0, fan, &edges, &nedges, &ntiles, &tpb, &unroll))) return rc;
+  if ((rc = emac_layout(&b, 1, nsrc, 0, fan, &edges, &nedges, &ntiles, &tpb, &all_full, &unroll))) return rc;
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
   if (hipMallocAsync((void **)&d, sizeof(b) + sizeof(emac_edge) * (nedges + 1), s) != hipSuccess) {
     free(edges);
@@ -194,7 +194,7 @@ int ext_mpi_amd_gpu_copy_reduce(int dtype, int op, int nsrc, const void *const *
   d_edges = reinterpret_cast<emac_edge *>(d + 1);
   rc = ok(hipMemcpyAsync(d, &b, sizeof(b), hipMemcpyHostToDevice, s));
   if (!rc && nedges) rc = ok(hipMemcpyAsync(d_edges, edges, sizeof(emac_edge) * nedges, hipMemcpyHostToDevice, s));
-  if (!rc) rc = emac_gpu_fold(dtype, op, nsrc, fan, unroll, &codes, d, 1, ntiles, tpb, d_edges, nedges, hip_stream);
+  if (!rc) rc = emac_gpu_fold(dtype, op, nsrc, fan, unroll, &codes, d, 1, ntiles, tpb, all_full, d_edges, nedges, hip_stream);
   (void)hipFreeAsync(d, s);
   if (!rc) rc = ok(hipStreamSynchronize(s));  // the host descriptor lives on this stack frame
   free(edges);

@@ -85,12 +85,13 @@ __device__ __forceinline__ X fold_leaves(const X (&x)[N], const emac_codes &c) {
 template <typename T, int N, bool TREE, int D>
 __device__ __forceinline__ void fold_scalar_element(const emac_bucket *b, long e, const emac_codes &c) {
   typedef typename Lane<T>::S S;
+  const long k = e - b->head;  // bucket pointers sit at element `head`
   S x[N];
 #pragma unroll
-  for (int s = 0; s < N; ++s) x[s] = static_cast<const S *>(b->src[s])[e];
+  for (int s = 0; s < N; ++s) x[s] = static_cast<const S *>(b->src[s])[k];
   const S r = fold_leaves<N, TREE>(x, c);
 #pragma unroll
-  for (int d = 0; d < D; ++d) static_cast<S *>(b->dst[d])[e] = r;
+  for (int d = 0; d < D; ++d) static_cast<S *>(b->dst[d])[k] = r;
 }
 
 // Loads are nontemporal (each leaf byte is read exactly once; keeping it out of L2/MALL leaves
@@ -101,37 +102,33 @@ __device__ __forceinline__ void fold_scalar_element(const emac_bucket *b, long e
 // `global_load_dwordx4 v, v_off, s_base nt` issued back to back, instead of flat loads each
 // waiting on its own descriptor read.
 template <typename T, int N, int U, bool TREE, int D, bool FULL>
-__device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_base, const emac_codes &c) {
-  typedef typename Lane<T>::S S;
+__device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_base, long nvec, const emac_codes &c) {
   typedef typename Lane<T>::V V;
   typedef __attribute__((address_space(1))) V GV;
-  const long head = b->head;
   // vectors of this tile still inside the bucket (wave-uniform); lane offsets are 32-bit so
   // every access is `global_*_dwordx4 v, v_off, s_base` with the tile base in SGPRs
-  const long left = b->nvec - tile_base;
-  const GV *src[N];
-  GV *dst[D];
-#pragma unroll
-  for (int s = 0; s < N; ++s) src[s] = (const GV *)(static_cast<const S *>(b->src[s]) + head) + tile_base;
-#pragma unroll
-  for (int d = 0; d < D; ++d) dst[d] = (GV *)(static_cast<S *>(b->dst[d]) + head) + tile_base;
+  const long left = nvec - tile_base;
   V x[U][N];
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const unsigned v = threadIdx.x + (unsigned)(u * EMAC_BLOCK);
+  for (int s = 0; s < N; ++s) {
+    const GV *src = (const GV *)b->src[s] + tile_base;
 #pragma unroll
-    for (int s = 0; s < N; ++s)
-      if (FULL || (long)v < left) x[u][s] = __builtin_nontemporal_load(src[s] + v);
+    for (int u = 0; u < U; ++u) {
+      const unsigned v = threadIdx.x + (unsigned)(u * EMAC_BLOCK);
+      if (FULL || (long)v < left) x[u][s] = __builtin_nontemporal_load(src + v);
+    }
   }
   V r[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) r[u] = fold_leaves<N, TREE>(x[u], c);
+  // destination pointers are only needed now: their descriptor read overlaps the loads
 #pragma unroll
   for (int d = 0; d < D; ++d) {
+    GV *dst = (GV *)b->dst[d] + tile_base;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const unsigned v = threadIdx.x + (unsigned)(u * EMAC_BLOCK);
-      if (FULL || (long)v < left) __builtin_nontemporal_store(r[u], dst[d] + v);
+      if (FULL || (long)v < left) __builtin_nontemporal_store(r[u], dst + v);
     }
   }
 }
@@ -140,7 +137,8 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
 // 16-byte vectors of one bucket. Nothing element-granular runs here (see fold_edge_kernel).
 template <typename T, int N, int U, bool TREE, int D>
 __global__ __launch_bounds__(EMAC_BLOCK) void fold_kernel(const emac_bucket *__restrict__ bk, int nb,
-                                                          long ntiles, long tiles_per_bucket, emac_codes codes) {
+                                                          long ntiles, long tiles_per_bucket, int all_full,
+                                                          emac_codes codes) {
   constexpr long TILE = (long)EMAC_BLOCK * U;
   for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     // bucket of this tile: arithmetic when every bucket has the same tile count (equal chunks:
@@ -165,10 +163,12 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_kernel(const emac_bucket *__r
       t = tile - bk[lo].tile0;
     }
     const emac_bucket *b = bk + bi;
-    if ((t + 1) * TILE <= b->nvec)
-      fold_vectors<T, N, U, TREE, D, true>(b, t * TILE, codes);
+    // all_full (host-known: every bucket a whole number of tiles) skips the dependent read of
+    // nvec before the first load of the tile
+    if (all_full || (t + 1) * TILE <= b->nvec)
+      fold_vectors<T, N, U, TREE, D, true>(b, t * TILE, 0, codes);
     else
-      fold_vectors<T, N, U, TREE, D, false>(b, t * TILE, codes);
+      fold_vectors<T, N, U, TREE, D, false>(b, t * TILE, b->nvec, codes);
   }
 }
 
@@ -203,6 +203,7 @@ struct Launch {
   const emac_bucket *b;
   int nb;
   long ntiles, tpb;
+  int all_full;
   const emac_edge *edges;
   int nedges;
   hipStream_t s;
@@ -213,7 +214,7 @@ int launch_one(const Launch &L) {
   const long grid = L.ntiles < 8192 ? L.ntiles : 8192;
   if (grid > 0)
     hipLaunchKernelGGL((fold_kernel<T, N, U, TREE, D>), dim3((unsigned)grid), dim3(EMAC_BLOCK), 0, L.s, L.b, L.nb,
-                       L.ntiles, L.tpb, *L.c);
+                       L.ntiles, L.tpb, L.all_full, *L.c);
   if (L.nedges > 0)
     hipLaunchKernelGGL((fold_edge_kernel<T, N, TREE, D>), dim3((unsigned)L.nedges), dim3(EMAC_BLOCK), 0, L.s, L.b,
                        L.edges, *L.c);

@@ -20,13 +20,13 @@ extern "C" {
 /* One owner chunk of a launch: `nsrc` leaves (plan leaf order) folded element-wise and the
    result stored to `ndst` destinations. Element e of the chunk is at src[t] + e (elements). */
 typedef struct {
-  const void *src[EMAC_MAX_RANKS];
-  void *dst[EMAC_MAX_RANKS];
+  const void *src[EMAC_MAX_RANKS]; /* leaf pointers at element `head` (the first full vector) */
+  long nvec;   /* 16-byte vectors from there (0 if the bucket is misaligned) */
+  long tile0;  /* first tile index of this bucket inside the vector launch */
+  void *dst[EMAC_MAX_RANKS];       /* destination pointers at element `head` */
   long count;  /* elements */
   long head;   /* leading elements before the first 16-byte aligned vector (edge path) */
-  long nvec;   /* 16-byte vectors after the head (0 if the bucket is misaligned) */
   long tail;   /* trailing elements after the vectors (edge path) */
-  long tile0;  /* first tile index of this bucket inside the vector launch */
   int ndst;
   int scalar;  /* 1: pointers disagree on 16-byte alignment -> every element on the edge path */
 } emac_bucket;
@@ -66,14 +66,14 @@ int emac_gpu_pick_unroll(int nsrc, int tree, int fan, long total_vectors);
 /* Launch the fold over nb device-resident buckets (ntiles tiles in total) on `stream`.
    tiles_per_bucket > 0 declares that every bucket spans exactly that many tiles. */
 int emac_gpu_fold(int dtype, int op, int nsrc, int fan, int unroll, const emac_codes *codes,
-                  const emac_bucket *d_buckets, int nb, long ntiles, long tiles_per_bucket,
+                  const emac_bucket *d_buckets, int nb, long ntiles, long tiles_per_bucket, int all_full,
                   const emac_edge *d_edges, int nedges, void *stream);
 
 /* layout.c: alignment split of a bucket whose pointers sit at its first element, and the
    launch layout (tiles, uniform tiles per bucket, unroll, edge items; caller frees edges). */
 void emac_split_alignment(emac_bucket *b, int nsrc, long len, int tsize);
 int emac_layout(emac_bucket *b, int nb, int nsrc, int tree, int fan, emac_edge **edges, int *nedges,
-                long *ntiles, long *tiles_per_bucket, int *unroll);
+                long *ntiles, long *tiles_per_bucket, int *all_full, int *unroll);
 
 #ifdef __cplusplus
 }

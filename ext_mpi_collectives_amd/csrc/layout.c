@@ -9,7 +9,8 @@
 
 /* head / vector / tail split of one bucket whose pointers are at element 0 of the chunk:
    vectors need every pointer 16-byte aligned at the same element; if they disagree the whole
-   bucket is element-granular (edge path). */
+   bucket is element-granular (edge path). On return the pointers sit at element `head`, the
+   first full vector, so the streaming kernel adds no offset. */
 void emac_split_alignment(emac_bucket *b, int nsrc, long len, int tsize) {
   long head = 0;
   int i, ok = 1;
@@ -33,12 +34,14 @@ void emac_split_alignment(emac_bucket *b, int nsrc, long len, int tsize) {
   b->head = head;
   b->nvec = (len - head) * tsize / 16;
   b->tail = len - head - b->nvec * (16 / tsize);
+  for (i = 0; i < nsrc; i++) b->src[i] = (const char *)b->src[i] + head * tsize;
+  for (i = 0; i < b->ndst; i++) b->dst[i] = (char *)b->dst[i] + head * tsize;
 }
 
 int emac_layout(emac_bucket *b, int nb, int nsrc, int tree, int fan, emac_edge **edges_out, int *nedges,
-                long *ntiles_out, long *tpb_out, int *unroll_out) {
+                long *ntiles_out, long *tpb_out, int *all_full_out, int *unroll_out) {
   long total = 0, tv, tiles = 0, uniform = -1;
-  int i, ne = 0, unroll;
+  int i, ne = 0, unroll, all_full = 1;
   emac_edge *edges;
   for (i = 0; i < nb; i++) total += b[i].nvec;
   unroll = emac_gpu_pick_unroll(nsrc, tree, fan, total);
@@ -48,6 +51,7 @@ int emac_layout(emac_bucket *b, int nb, int nsrc, int tree, int fan, emac_edge *
     b[i].tile0 = tiles;
     tiles += t;
     uniform = (uniform == -1 || uniform == t) ? t : 0;
+    if (b[i].nvec % tv) all_full = 0;
     if (b[i].scalar)
       ne += (int)((b[i].count + EMAC_EDGE_RANGE - 1) / EMAC_EDGE_RANGE);
     else if (b[i].head + b[i].tail > 0)
@@ -78,6 +82,7 @@ int emac_layout(emac_bucket *b, int nb, int nsrc, int tree, int fan, emac_edge *
   *nedges = ne;
   *ntiles_out = tiles;
   *tpb_out = uniform > 0 ? uniform : 0;
+  *all_full_out = all_full;
   *unroll_out = unroll;
   return 0;
 }

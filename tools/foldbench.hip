@@ -353,7 +353,7 @@ int main(int argc, char **argv) {
     for (int o = 0; o < 2; o++) {
       CHECK(hipEventRecord(e0, s));
       for (int i = 0; i < per; i++) {
-        emac::Launch L = {&codes, (o ? ebk_prod : ebk_rot)[(k++) % nsets], R, (long)R * (C / 512), C / 512, nullptr, 0, s};
+        emac::Launch L = {&codes, (o ? ebk_prod : ebk_rot)[(k++) % nsets], R, (long)R * (C / 512), C / 512, 1, nullptr, 0, s};
         emac::launch_one<float, R, 2, false, R>(L);
       }
       CHECK(hipEventRecord(e1, s));
