@@ -73,6 +73,7 @@ def lib():
         L.ext_mpi_amd_get_unique_id.argtypes = [c_void_p]
         L.ext_mpi_amd_comm_init.argtypes = [c_int, c_int, c_void_p, c_int, P(c_int)]
         L.ext_mpi_amd_comm_free.argtypes = [c_int]
+        L.ext_mpi_amd_comm_init_loopback.argtypes = [c_int, P(c_int)]
         L.ext_mpi_amd_allreduce_init.argtypes = [c_void_p, c_void_p, c_long, c_int, c_int, c_int,
                                                  ctypes.c_char_p, P(c_int)]
         for name in ("start", "test", "wait", "done"):
@@ -151,6 +152,13 @@ def comm_init(rank, size, unique_id, device=-1):
     return c.value
 
 
+def comm_init_loopback(size):
+    """Testing transport: one communicator per rank, all in this process on the current device."""
+    comms = (ctypes.c_int * size)()
+    _check("ext_mpi_amd_comm_init_loopback", lib().ext_mpi_amd_comm_init_loopback(size, comms))
+    return list(comms)
+
+
 def comm_free(comm):
     _check("ext_mpi_amd_comm_free", lib().ext_mpi_amd_comm_free(comm))
 
@@ -179,7 +187,8 @@ def done(h):
     return _check("ext_mpi_amd_done", lib().ext_mpi_amd_done(h))
 
 
-LEG_STAGE, LEG_REDUCE_SCATTER, LEG_FOLD, LEG_ALLGATHER, LEG_ALL = 1, 2, 4, 8, 15
+LEG_STAGE_IN, LEG_REDUCE_SCATTER, LEG_FOLD, LEG_ALLGATHER, LEG_STAGE_OUT = 1, 2, 4, 8, 16
+LEG_STAGE, LEG_ALL = 17, 31
 
 
 def start_legs(h, legs):

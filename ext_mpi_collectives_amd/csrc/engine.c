@@ -43,7 +43,19 @@ typedef struct {
   int used;
   int rank, size, device;
   ncclComm_t nccl;
+  int loop_group; /* >= 0: in-process loopback communicator (testing transport), no RCCL */
 } emac_comm;
+
+/* Loopback groups: every rank of the communicator lives in this process; the i-th handle a
+   rank creates on it matches the i-th handle of every other rank (collective call order). */
+#define MAX_LOOP_GROUPS 8
+#define MAX_LOOP_HANDLES 256
+typedef struct {
+  int used, size;
+  int nh[EMAC_MAX_RANKS];
+  int handle[EMAC_MAX_RANKS][MAX_LOOP_HANDLES];
+} loop_group;
+static loop_group loops[MAX_LOOP_GROUPS];
 
 typedef struct {
   int kind;
@@ -73,6 +85,7 @@ typedef struct {
   emac_p2p *ops; /* reduce-scatter and allgather point-to-point program (plan.c) */
   int nops;
   int started;
+  int loop_index; /* position in the loopback group's per-rank handle list */
   int own_stream; /* 0 once the caller supplied the stream (ext_mpi_amd_set_stream) */
 } emac_handle;
 
@@ -246,11 +259,7 @@ int ext_mpi_amd_fold_init(int nsrc, const void *const *srcs, int ndst, void *con
   if (!h) return EMAC_ERR_MALLOC;
   h->kind = KIND_NODE;
   /* a linear plan over nsrc leaves supplies the codes (one level, leaves in given order) */
-  memset(&cfg, 0, sizeof(cfg));
-  cfg.method = 6;
-  cfg.split = 1;
-  cfg.nrs = 1;
-  cfg.rs[0] = nsrc;
+  emac_default_copyin(nsrc, &cfg);
   if ((rc = emac_plan_build(&h->plan, nsrc, count, dtype, op, nsrc > 1 ? &cfg : NULL))) goto fail;
   emac_gpu_get_device(&h->device);
   h->nsrc = nsrc;
@@ -293,13 +302,50 @@ int ext_mpi_amd_comm_init(int rank, int size, const void *id, int device, int *c
   comms[i].used = 1;
   comms[i].rank = rank;
   comms[i].size = size;
+  comms[i].loop_group = -1;
   *comm = i;
+  return 0;
+}
+
+/* Testing transport: `size` communicators, one per rank, all in this process on the current
+   device. Their point-to-point ops are matched in order (as RCCL matches ops between a pair
+   inside a group) and executed as device copies when the RECEIVING rank runs the leg, so the
+   caller must run each leg on every rank before the next one (ext_mpi_amd_start_legs). */
+int ext_mpi_amd_comm_init_loopback(int size, int *comm_of_rank) {
+  int g, r, i;
+  if (!comm_of_rank || size < 1 || size > EMAC_MAX_RANKS) return EMAC_ERR_ARG;
+  if (emac_gpu_device_count() <= 0) return EMAC_ERR_DEVICE;
+  for (g = 0; g < MAX_LOOP_GROUPS && loops[g].used; g++);
+  if (g == MAX_LOOP_GROUPS) return EMAC_ERR_MALLOC;
+  memset(&loops[g], 0, sizeof(loops[g]));
+  loops[g].used = 1;
+  loops[g].size = size;
+  for (r = 0; r < size; r++) {
+    for (i = 0; i < MAX_COMMS && comms[i].used; i++);
+    if (i == MAX_COMMS) return EMAC_ERR_MALLOC;
+    memset(&comms[i], 0, sizeof(comms[i]));
+    comms[i].used = 1;
+    comms[i].rank = r;
+    comms[i].size = size;
+    comms[i].loop_group = g;
+    emac_gpu_get_device(&comms[i].device);
+    comm_of_rank[r] = i;
+  }
   return 0;
 }
 
 int ext_mpi_amd_comm_free(int comm) {
   if (comm < 0 || comm >= MAX_COMMS || !comms[comm].used) return EMAC_ERR_ARG;
-  ncclCommDestroy(comms[comm].nccl);
+  if (comms[comm].loop_group >= 0) {
+    loop_group *g = &loops[comms[comm].loop_group];
+    g->nh[comms[comm].rank] = -1; /* this rank left */
+    for (int r = 0; r < g->size; r++)
+      if (g->nh[r] >= 0) goto keep;
+    g->used = 0;
+  keep:;
+  } else {
+    ncclCommDestroy(comms[comm].nccl);
+  }
   comms[comm].used = 0;
   return 0;
 }
@@ -360,7 +406,16 @@ int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, i
   free(b);
   b = NULL;
   if ((rc = emac_gpu_stream_create(&h->stream))) goto fail;
+  if (cm->loop_group >= 0) {
+    loop_group *g = &loops[cm->loop_group];
+    if (g->nh[h->me] < 0 || g->nh[h->me] >= MAX_LOOP_HANDLES) {
+      rc = EMAC_ERR_MALLOC;
+      goto fail;
+    }
+    h->loop_index = g->nh[h->me];
+  }
   if ((rc = finish_init(h, handle))) goto fail;
+  if (cm->loop_group >= 0) loops[cm->loop_group].handle[h->me][loops[cm->loop_group].nh[h->me]++] = *handle;
   return 0;
 fail:
   free(b);
@@ -368,17 +423,54 @@ fail:
   return rc;
 }
 
+static char *leg_base(const emac_handle *h, int buf) {
+  return buf == EMAC_BUF_SEND ? (char *)h->dsend[0] : buf == EMAC_BUF_RECV ? (char *)h->drecv[0] : (char *)h->staging;
+}
+
+static emac_handle *get(int handle);
+
+/* Loopback transport: every receive of this leg copies the matching send of the peer (the
+   k-th send of q to me in this leg matches my k-th receive from q). */
+static int run_leg_loopback(emac_handle *h, int leg) {
+  loop_group *g = &loops[comms[h->comm].loop_group];
+  int seen[EMAC_MAX_RANKS] = {0}, i, j, rc;
+  for (i = 0; i < h->nops; i++) {
+    const emac_p2p *o = &h->ops[i];
+    emac_handle *hq;
+    int q = o->peer, k, found = 0;
+    if (o->leg != leg || o->is_send) continue;
+    k = seen[q]++;
+    if (h->loop_index >= g->nh[q]) return EMAC_ERR_TRANSPORT; /* peer has no matching handle */
+    hq = get(g->handle[q][h->loop_index]);
+    if (!hq) return EMAC_ERR_TRANSPORT;
+    for (j = 0; j < hq->nops; j++) {
+      const emac_p2p *so = &hq->ops[j];
+      if (so->leg == leg && so->is_send && so->peer == h->me && k-- == 0) {
+        if (so->bytes != o->bytes) return EMAC_ERR_TRANSPORT;
+        if ((rc = emac_gpu_memcpy_async(leg_base(h, o->buf) + o->offset, leg_base(hq, so->buf) + so->offset,
+                                        (size_t)o->bytes, h->stream)))
+          return rc;
+        found = 1;
+        break;
+      }
+    }
+    if (!found) return EMAC_ERR_TRANSPORT;
+  }
+  return 0;
+}
+
 /* Walk the point-to-point program of one leg as ONE RCCL group (all peers at once). */
 static int run_leg(emac_handle *h, int leg) {
   emac_comm *cm = &comms[h->comm];
   hipStream_t s = (hipStream_t)h->stream;
   int i, bad = 0;
+  if (cm->loop_group >= 0) return run_leg_loopback(h, leg);
   if (ncclGroupStart() != ncclSuccess) return EMAC_ERR_TRANSPORT;
   for (i = 0; i < h->nops && !bad; i++) {
     const emac_p2p *o = &h->ops[i];
     char *base;
     if (o->leg != leg) continue;
-    base = o->buf == EMAC_BUF_SEND ? (char *)h->dsend[0] : o->buf == EMAC_BUF_RECV ? (char *)h->drecv[0] : (char *)h->staging;
+    base = leg_base(h, o->buf);
     if (o->is_send)
       bad = ncclSend(base + o->offset, (size_t)o->bytes, ncclInt8, o->peer, cm->nccl, s) != ncclSuccess;
     else
@@ -416,14 +508,14 @@ int ext_mpi_amd_start_legs(int handle, int legs) {
   if (!h) return EMAC_ERR_ARG;
   multi = h->kind == KIND_COMM && h->plan.nranks > 1;
   if (emac_gpu_set_device(h->device)) return EMAC_ERR_DEVICE;
-  if ((legs & EXT_MPI_AMD_LEG_STAGE) && (rc = stage_in(h))) return rc;
+  if ((legs & EXT_MPI_AMD_LEG_STAGE_IN) && (rc = stage_in(h))) return rc;
   if ((legs & EXT_MPI_AMD_LEG_REDUCE_SCATTER) && multi && (rc = run_leg(h, EMAC_LEG_RS))) return rc;
   if ((legs & EXT_MPI_AMD_LEG_FOLD) &&
       (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, h->fan, h->unroll, &h->plan.codes, h->d_buckets, h->nb, h->ntiles,
                           h->tiles_per_bucket, h->all_full, h->d_edges, h->nedges, h->stream)))
     return rc;
   if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && multi && (rc = run_leg(h, EMAC_LEG_AG))) return rc;
-  if ((legs & EXT_MPI_AMD_LEG_STAGE) && (rc = stage_out(h))) return rc;
+  if ((legs & EXT_MPI_AMD_LEG_STAGE_OUT) && (rc = stage_out(h))) return rc;
   h->started = 1;
   return 0;
 }

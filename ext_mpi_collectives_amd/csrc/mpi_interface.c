@@ -14,9 +14,18 @@
  * Configuration as the reference reads it (ext_mpi.c:43-187; rank 0 reads the environment and
  * broadcasts): EXT_MPI_COPYIN, EXT_MPI_VERBOSE, EXT_MPI_DEBUG (default 1: the known-answer
  * self-test of debug_persistent.c:393-568 runs inside every Allreduce_init),
- * EXT_MPI_NUM_SOCKETS_PER_NODE / EXT_MPI_NUM_TASKS_PER_SOCKET (one socket supported). MPI_Info
+ * EXT_MPI_NUM_SOCKETS_PER_NODE (any divisor of the node size: sockets change the reference's
+ * partner encoding and barrier scope, not the fold arithmetic -- see oracle/ref_schedule.c). MPI_Info
  * key "ext_mpi_copyin" overrides nothing the environment sets (num_ports_factors.c:25-36:
  * env > info > default).
+ *
+ * Blocking front end (EXT_MPI_BLOCKING; ext_mpi_interface.c:507-535, ext_mpi_native_blocking.c:
+ * 189-290, 662-741): MPI_Allreduce on MPI_COMM_WORLD and on communicators made by
+ * MPI_Comm_dup/create/create_group/split/split_type (:640-729) runs the same persistent engine
+ * through a per-communicator cache of handles keyed on (buffers, count, type, parameter row).
+ * The copy-in factors come from the reference's parameter file
+ * ext_mpi_allreduce_blocking_<nodes>_<cores>.txt (/dev/shm first, then the working directory):
+ * one row per message-size threshold, host rows then device rows (README "blocking").
  *
  * Transport: one RCCL communicator per MPI communicator, cached as an MPI attribute and
  * destroyed with it; bootstrapped with PMPI_Bcast of the unique id. The communicator must lie
@@ -39,8 +48,10 @@ static int cfg_has_copyin = 0;
 static int cfg_verbose = 0;
 static int cfg_debug = 1;
 static int cfg_num_sockets = -1;
+static int cfg_blocking = 0;
 static int initialised = 0;
 static int comm_keyval = MPI_KEYVAL_INVALID;
+static int blocking_keyval = MPI_KEYVAL_INVALID;
 
 static int env_int(const char *name, int *out) {
   const char *c = getenv(name);
@@ -58,6 +69,7 @@ static void read_env(void) {
   if (rank == 0) {
     const char *c = getenv("EXT_MPI_COPYIN");
     cfg_verbose = getenv("EXT_MPI_VERBOSE") != NULL;
+    cfg_blocking = getenv("EXT_MPI_BLOCKING") != NULL; /* ext_mpi_interface.c:46-51 */
     env_int("EXT_MPI_DEBUG", &cfg_debug);
     env_int("EXT_MPI_NUM_SOCKETS_PER_NODE", &cfg_num_sockets);
     if (c) {
@@ -66,6 +78,7 @@ static void read_env(void) {
     }
   }
   PMPI_Bcast(&cfg_verbose, 1, MPI_INT, 0, MPI_COMM_WORLD);
+  PMPI_Bcast(&cfg_blocking, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_debug, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_num_sockets, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&len, 1, MPI_INT, 0, MPI_COMM_WORLD);
@@ -257,13 +270,228 @@ out:
   return rc;
 }
 
+
+/* ------------------------------------------- blocking MPI_Allreduce (EXT_MPI_BLOCKING) */
+
+#define BROWS 64
+#define BCACHE 16
+#define BLOCKING_MAX_BYTES (1024L * 1024L * 100L) /* ext_mpi_interface.c:517 */
+
+typedef struct {
+  long msize;  /* message size in bytes from which the row applies */
+  int sockets; /* logical sockets per node */
+  int nodes;   /* "<nodes>(ports)" field: 1 = single node */
+  char copyin[256];
+} brow;
+
+typedef struct {
+  const void *send;
+  void *recv;
+  int count, dtype, side, row, handle;
+  unsigned long used;
+} bentry;
+
+/* Per-communicator state of the blocking path (comm_comm_blocking, ext_mpi_native_blocking.c). */
+typedef struct {
+  int status; /* 0 not yet bound, 1 bound to ext_comm, <0 engine error, 2 not for this path */
+  int ext_comm;
+  int loaded, nrow[2]; /* [0] host rows, [1] device rows */
+  brow row[2][BROWS];
+  bentry cache[BCACHE];
+  unsigned long clock;
+  void *scratch;
+  size_t scratch_bytes;
+} bcomm;
+
+static void bcomm_drop(bcomm *b, int i) {
+  if (b->cache[i].handle >= 0) ext_mpi_amd_done(b->cache[i].handle);
+  memset(&b->cache[i], 0, sizeof(bentry));
+  b->cache[i].handle = -1;
+}
+
+static int bcomm_delete(MPI_Comm comm, int keyval, void *attr, void *extra) {
+  bcomm *b = (bcomm *)attr;
+  int i;
+  (void)comm;
+  (void)keyval;
+  (void)extra;
+  if (b) {
+    for (i = 0; i < BCACHE; i++) bcomm_drop(b, i);
+    ext_mpi_amd_gpu_free(b->scratch);
+    free(b);
+  }
+  return MPI_SUCCESS;
+}
+
+/* add_comm_to_blocking (ext_mpi_interface.c:640-651); MPI_COMM_WORLD is added whatever its
+   size (:57-60). */
+static void blocking_register(MPI_Comm comm, int any_size) {
+  bcomm *b;
+  int size, i;
+  if (!cfg_blocking || blocking_keyval == MPI_KEYVAL_INVALID || comm == MPI_COMM_NULL) return;
+  PMPI_Comm_size(comm, &size);
+  if (size <= 1 && !any_size) return;
+  b = (bcomm *)calloc(1, sizeof(bcomm));
+  if (!b) return;
+  for (i = 0; i < BCACHE; i++) b->cache[i].handle = -1;
+  PMPI_Comm_set_attr(comm, blocking_keyval, b);
+}
+
+/* init_blocking_native (ext_mpi_native_blocking.c:189-290): "<bytes> <sockets> <ports>
+   <copyin>" per line, '_' standing for ' '; a non-increasing size starts the device rows. */
+static void blocking_load_rows(bcomm *b, MPI_Comm comm) {
+  char fname[256], ports[1000], cf[1000];
+  long ms, prev = -1;
+  int so, size, rank, side = 0, i;
+  FILE *f;
+  PMPI_Comm_size(comm, &size);
+  PMPI_Comm_rank(comm, &rank);
+  b->loaded = 1;
+  /* single node: <nodes> = 1, <cores> = every rank of the communicator */
+  snprintf(fname, sizeof(fname), "/dev/shm/ext_mpi_allreduce_blocking_%d_%d.txt", 1, size);
+  f = fopen(fname, "r");
+  if (!f) {
+    snprintf(fname, sizeof(fname), "ext_mpi_allreduce_blocking_%d_%d.txt", 1, size);
+    f = fopen(fname, "r");
+  }
+  if (!f) {
+    if (rank == 0 && cfg_verbose) printf("# EXT_MPI blocking: file %s missing, using the persistent copyin\n", fname);
+    return;
+  }
+  while (fscanf(f, "%ld %d %999s %999s", &ms, &so, ports, cf) == 4) {
+    brow *r;
+    if (ms <= prev) side = 1;
+    prev = ms;
+    if (b->nrow[side] == BROWS) continue;
+    r = &b->row[side][b->nrow[side]++];
+    r->msize = ms;
+    r->sockets = so;
+    r->nodes = atoi(ports);
+    for (i = 0; cf[i]; i++)
+      if (cf[i] == '_') cf[i] = ' ';
+    snprintf(r->copyin, sizeof(r->copyin), "%.255s", cf);
+  }
+  fclose(f);
+}
+
+/* Row choice of EXT_MPI_Allreduce_native (ext_mpi_native_blocking.c:687-688): the last row whose
+   size does not exceed the message, else the first. */
+static int blocking_select_row(const bcomm *b, int side, long bytes) {
+  int n = b->nrow[side], i = 0;
+  if (!n) return -1;
+  while (b->row[side][i].msize <= bytes && i + 1 < n) i++;
+  if (b->row[side][i].msize > bytes && i > 0) i--;
+  return i;
+}
+
+/* 0: done, 1: not for this path (caller uses PMPI_Allreduce), <0: engine error. */
+static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int dtype, int tsize, bcomm *b,
+                              MPI_Comm comm) {
+  size_t bytes = (size_t)count * (size_t)tsize, need, stride;
+  int on_dev, side, row, i, rc, slot = -1, in_place, rank;
+  const char *copyin = NULL;
+  const void *s;
+  void *r;
+  bentry *e;
+  if (sendbuf == MPI_IN_PLACE) sendbuf = recvbuf; /* ext_mpi_blocking.c:427-429 */
+  in_place = sendbuf == recvbuf;
+  if (b->status == 0) {
+    rc = node_comm(comm, recvbuf, &b->ext_comm);
+    b->status = rc == 0 ? 1 : rc == EXT_MPI_AMD_ERROR_UNSUPPORTED ? 2 : rc;
+  }
+  if (b->status != 1) return b->status == 2 ? 1 : b->status;
+  if (!b->loaded) blocking_load_rows(b, comm);
+  on_dev = ext_mpi_amd_gpu_is_device_pointer(recvbuf) && ext_mpi_amd_gpu_is_device_pointer(sendbuf);
+  side = on_dev && b->nrow[1] ? 1 : 0;
+  row = blocking_select_row(b, side, (long)bytes);
+  if (row >= 0) {
+    int size;
+    PMPI_Comm_size(comm, &size);
+    if (b->row[side][row].nodes != 1) return 1; /* inter-node row: not this path */
+    if (b->row[side][row].sockets < 1 || size % b->row[side][row].sockets) return 1;
+    copyin = b->row[side][row].copyin;
+  } else if (cfg_has_copyin) {
+    copyin = cfg_copyin;
+  }
+  if (on_dev) {
+    s = sendbuf;
+    r = recvbuf;
+  } else {
+    /* host buffers go through device scratch (no page-locking of caller memory that may be
+       freed between calls) */
+    stride = (bytes + 255) & ~(size_t)255;
+    need = in_place ? stride : 2 * stride;
+    if (need < 256) need = 256;
+    if (b->scratch_bytes < need) {
+      for (i = 0; i < BCACHE; i++)
+        if (b->cache[i].handle >= 0 && b->cache[i].send == b->scratch) bcomm_drop(b, i);
+      ext_mpi_amd_gpu_free(b->scratch);
+      b->scratch = NULL;
+      b->scratch_bytes = 0;
+      if ((rc = ext_mpi_amd_gpu_malloc(&b->scratch, need))) return rc;
+      b->scratch_bytes = need;
+    }
+    s = b->scratch;
+    r = in_place ? b->scratch : (char *)b->scratch + stride;
+    if (bytes && (rc = ext_mpi_amd_gpu_memcpy_hd((void *)s, sendbuf, bytes))) return rc;
+  }
+  for (i = 0; i < BCACHE; i++) {
+    e = &b->cache[i];
+    if (e->handle >= 0 && e->send == s && e->recv == r && e->count == count && e->dtype == dtype && e->side == side &&
+        e->row == row) {
+      slot = i;
+      break;
+    }
+  }
+  if (slot < 0) {
+    slot = 0;
+    for (i = 0; i < BCACHE; i++) {
+      if (b->cache[i].handle < 0) {
+        slot = i;
+        break;
+      }
+      if (b->cache[i].used < b->cache[slot].used) slot = i;
+    }
+    bcomm_drop(b, slot);
+    e = &b->cache[slot];
+    if ((rc = ext_mpi_amd_allreduce_init(s, r, count, dtype, EXT_MPI_AMD_SUM, b->ext_comm, copyin, &e->handle))) {
+      e->handle = -1;
+      return rc;
+    }
+    e->send = s;
+    e->recv = r;
+    e->count = count;
+    e->dtype = dtype;
+    e->side = side;
+    e->row = row;
+    if (cfg_verbose) {
+      PMPI_Comm_rank(comm, &rank);
+      if (rank == 0)
+        printf("# EXT_MPI blocking allreduce %zu bytes %s copyin %s\n", bytes, on_dev ? "device" : "host",
+               copyin ? copyin : "(default 6;1 -R R)");
+    }
+  }
+  e = &b->cache[slot];
+  e->used = ++b->clock;
+  if ((rc = ext_mpi_amd_start(e->handle)) || (rc = ext_mpi_amd_wait(e->handle))) return rc;
+  if (!on_dev && bytes && (rc = ext_mpi_amd_gpu_memcpy_dh(recvbuf, r, bytes))) return rc;
+  return 0;
+}
+
 /* ------------------------------------------------------------------- native API */
 
 int EXT_MPI_Init(void) {
   if (initialised) return 0;
   read_env();
   PMPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, comm_attr_delete, &comm_keyval, NULL);
+  PMPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, bcomm_delete, &blocking_keyval, NULL);
   initialised = 1;
+  if (cfg_blocking) {
+    int rank;
+    PMPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    if (rank == 0 && cfg_verbose) printf("# EXT_MPI blocking\n"); /* ext_mpi_interface.c:52-54 */
+    blocking_register(MPI_COMM_WORLD, 1);
+  }
   return 0;
 }
 
@@ -275,7 +503,12 @@ int EXT_MPI_Initialized(int *flag) {
 int EXT_MPI_Finalize(void) {
   if (!initialised) return 0;
   initialised = 0;
-  return 0; /* the RCCL communicators go with their MPI communicators' attributes */
+  /* MPI_COMM_WORLD's attributes are not deleted by MPI_Finalize: release the blocking cache
+     first (its handles use the RCCL communicator), then the RCCL communicator; the other
+     communicators' go with MPI_Comm_free. */
+  PMPI_Comm_delete_attr(MPI_COMM_WORLD, blocking_keyval);
+  PMPI_Comm_delete_attr(MPI_COMM_WORLD, comm_keyval);
+  return 0;
 }
 
 int EXT_MPI_Allreduce_init(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
@@ -287,7 +520,12 @@ int EXT_MPI_Allreduce_init(const void *sendbuf, void *recvbuf, int count, MPI_Da
   if (!initialised) EXT_MPI_Init();
   if (dtype < 0 || op != MPI_SUM || count < 0) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
   if (sendbuf == MPI_IN_PLACE) sendbuf = recvbuf; /* ext_mpi.c:651-653 */
-  if (cfg_num_sockets > 1) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
+  /* sockets only change the reference's partner encoding, not the arithmetic (plan.h) */
+  if (cfg_num_sockets > 1) {
+    int size;
+    PMPI_Comm_size(comm, &size);
+    if (size % cfg_num_sockets) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
+  }
   if (cfg_has_copyin) {
     copyin = cfg_copyin;
   } else if (info != MPI_INFO_NULL) {
@@ -460,5 +698,59 @@ int MPI_Testsome(int incount, MPI_Request array_of_requests[], int *outcount, in
   ret = MPI_Testany(incount, array_of_requests, &array_of_indices[0], &flag,
                     array_of_statuses == MPI_STATUSES_IGNORE ? MPI_STATUS_IGNORE : &array_of_statuses[0]);
   *outcount = flag ? 1 : 0;
+  return ret;
+}
+
+/* Blocking MPI_Allreduce (ext_mpi_interface.c:507-535): SUM over the four types below 100 MB on
+   a registered communicator; anything else goes to PMPI_Allreduce. */
+int MPI_Allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op, MPI_Comm comm) {
+  int dtype = map_type(datatype), tsize, flag = 0, rc, rank;
+  bcomm *b = NULL;
+  if (cfg_blocking && initialised && dtype >= 0 && op == MPI_SUM && count >= 0) {
+    PMPI_Type_size(datatype, &tsize);
+    if ((long)count * tsize < BLOCKING_MAX_BYTES) {
+      PMPI_Comm_get_attr(comm, blocking_keyval, &b, &flag);
+      if (flag && b) {
+        rc = blocking_allreduce(sendbuf, recvbuf, count, dtype, tsize, b, comm);
+        if (rc == 0) return MPI_SUCCESS;
+        if (rc < 0) {
+          PMPI_Comm_rank(comm, &rank);
+          fprintf(stderr, "EXT_MPI blocking allreduce failed on rank %d: %d\n", rank, rc);
+          return MPI_ERR_OTHER;
+        }
+      }
+    }
+  }
+  return PMPI_Allreduce(sendbuf, recvbuf, count, datatype, op, comm);
+}
+
+/* Communicators the blocking path serves (ext_mpi_interface.c:663-721). */
+int MPI_Comm_dup(MPI_Comm comm, MPI_Comm *newcomm) {
+  int ret = PMPI_Comm_dup(comm, newcomm);
+  if (ret == MPI_SUCCESS) blocking_register(*newcomm, 0);
+  return ret;
+}
+
+int MPI_Comm_create(MPI_Comm comm, MPI_Group group, MPI_Comm *newcomm) {
+  int ret = PMPI_Comm_create(comm, group, newcomm);
+  if (ret == MPI_SUCCESS) blocking_register(*newcomm, 0);
+  return ret;
+}
+
+int MPI_Comm_create_group(MPI_Comm comm, MPI_Group group, int tag, MPI_Comm *newcomm) {
+  int ret = PMPI_Comm_create_group(comm, group, tag, newcomm);
+  if (ret == MPI_SUCCESS) blocking_register(*newcomm, 0);
+  return ret;
+}
+
+int MPI_Comm_split(MPI_Comm comm, int color, int key, MPI_Comm *newcomm) {
+  int ret = PMPI_Comm_split(comm, color, key, newcomm);
+  if (ret == MPI_SUCCESS) blocking_register(*newcomm, 0);
+  return ret;
+}
+
+int MPI_Comm_split_type(MPI_Comm comm, int split_type, int key, MPI_Info info, MPI_Comm *newcomm) {
+  int ret = PMPI_Comm_split_type(comm, split_type, key, info, newcomm);
+  if (ret == MPI_SUCCESS) blocking_register(*newcomm, 0);
   return ret;
 }

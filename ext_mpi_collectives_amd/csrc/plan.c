@@ -17,13 +17,15 @@ int emac_type_size(int dtype) {
 }
 
 /* Grammar "method;f0 f1 f2 ..." of EXT_MPI_COPYIN / MPI_Info "ext_mpi_copyin"
-   (src/core/ports_groups.c:18-35): f0 = split, then negative reduce-scatter radices,
-   then positive allgather radices. */
+   (src/core/ports_groups.c:18-35): f0 = split, then negative reduce-scatter radices, then
+   positive allgather radices; a "1" (never a radix) opens a sub-split "1 <members> <level>"
+   whose level has the same grammar (reduce_copyin.c:974-981). */
 int emac_parse_copyin(const char *s, emac_copyin *out) {
-  long v[2 + 2 * EMAC_MAX_LEVELS];
-  int n = 0, i;
+  long v[4 * (2 + 2 * EMAC_MAX_LEVELS)];
+  int n = 0, i, L = 0;
   const char *c = s;
   char *end;
+  emac_level *lv;
   if (!s) return EMAC_ERR_ARG;
   memset(out, 0, sizeof(*out));
   while (*c == ' ') c++;
@@ -42,47 +44,79 @@ int emac_parse_copyin(const char *s, emac_copyin *out) {
   }
   if (n < 3) return EMAC_ERR_ARG; /* method, split and at least one radix */
   out->method = (int)v[0];
-  out->split = (int)v[1];
-  for (i = 2; i < n; i++) {
-    if (v[i] < 0) {
-      if (out->nag) return EMAC_ERR_ARG; /* reduce-scatter radices come first */
-      if (out->nrs >= EMAC_MAX_LEVELS) return EMAC_ERR_UNSUPPORTED;
-      out->rs[out->nrs++] = (int)-v[i];
-    } else {
-      if (out->nag >= EMAC_MAX_LEVELS) return EMAC_ERR_UNSUPPORTED;
-      out->ag[out->nag++] = (int)v[i];
+  i = 1;
+  for (;;) {
+    if (L >= EMAC_MAX_SPLITS) return EMAC_ERR_UNSUPPORTED;
+    lv = &out->lv[L++];
+    if (i >= n) return EMAC_ERR_ARG;
+    lv->split = (int)v[i++];
+    for (; i < n && v[i] != 1; i++) {
+      if (v[i] < 0) {
+        if (lv->nag) return EMAC_ERR_ARG; /* reduce-scatter radices come first */
+        if (lv->nrs >= EMAC_MAX_LEVELS) return EMAC_ERR_UNSUPPORTED;
+        lv->rs[lv->nrs++] = (int)-v[i];
+      } else {
+        if (lv->nag >= EMAC_MAX_LEVELS) return EMAC_ERR_UNSUPPORTED;
+        lv->ag[lv->nag++] = (int)v[i];
+      }
     }
+    if (i == n) break;
+    /* "1 <members>": the next level follows */
+    if (i + 2 >= n) return EMAC_ERR_ARG;
+    lv->sub = (int)v[i + 1];
+    if (lv->sub < 1) return EMAC_ERR_ARG;
+    i += 2;
   }
+  out->nlv = L;
   return EMAC_OK;
 }
 
 void emac_default_copyin(int nranks, emac_copyin *out) {
   memset(out, 0, sizeof(*out));
   out->method = 6;
-  out->split = 1;
-  out->nrs = 1;
-  out->rs[0] = nranks;
-  out->nag = 1;
-  out->ag[0] = nranks;
+  out->nlv = 1;
+  out->lv[0].split = 1;
+  out->lv[0].nrs = 1;
+  out->lv[0].rs[0] = nranks;
+  out->lv[0].nag = 1;
+  out->lv[0].ag[0] = nranks;
 }
 
 int emac_validate_copyin(const emac_copyin *c, int nranks) {
-  int i, prs = 1, pag = 1;
+  int i, L, size = nranks, nlev = 0;
   if (c->method != 6 && c->method != 9) return EMAC_ERR_UNSUPPORTED;
-  if (c->split == 0 || c->nrs < 1) return EMAC_ERR_ARG;
-  if (c->split > EMAC_MAX_PIECES) return EMAC_ERR_UNSUPPORTED;
-  for (i = 0; i < c->nrs; i++) {
-    if (c->rs[i] < 2) return EMAC_ERR_ARG;
-    prs *= c->rs[i];
+  if (c->nlv < 1) return EMAC_ERR_ARG;
+  for (L = 0; L < c->nlv; L++) {
+    const emac_level *v = &c->lv[L];
+    int prs = 1, pag = 1, members = size;
+    if (v->split == 0 || v->nrs < 1) return EMAC_ERR_ARG;
+    if (v->split > EMAC_MAX_PIECES) return EMAC_ERR_UNSUPPORTED;
+    if (L < c->nlv - 1) {
+      /* a sub-split needs members dividing the level, and the next level at least 2 wide */
+      if (v->sub < 2 || size % v->sub || size / v->sub < 2) return EMAC_ERR_ARG;
+      /* reduce_copyin.c:1035-1067 reuse the piece loop's variable inside a sub-split: more
+         than one equal piece above a sub-split never terminates in the reference */
+      if (v->split > 1) return EMAC_ERR_UNSUPPORTED;
+      members = v->sub;
+    } else if (v->sub) {
+      return EMAC_ERR_ARG;
+    }
+    for (i = 0; i < v->nrs; i++) {
+      if (v->rs[i] < 2) return EMAC_ERR_ARG;
+      prs *= v->rs[i];
+    }
+    for (i = 0; i < v->nag; i++) {
+      if (v->ag[i] < 2) return EMAC_ERR_ARG;
+      pag *= v->ag[i];
+    }
+    /* every radix chain must cover its level exactly: the reference silently produces a
+       partial reduction otherwise; here it is rejected */
+    if (prs != members) return EMAC_ERR_ARG;
+    if (v->nag && pag != members) return EMAC_ERR_ARG;
+    nlev += v->nrs;
+    size /= members;
   }
-  for (i = 0; i < c->nag; i++) {
-    if (c->ag[i] < 2) return EMAC_ERR_UNSUPPORTED; /* a "1" opens a multi-socket sub-split */
-    pag *= c->ag[i];
-  }
-  /* every radix chain must cover the node exactly: the reference silently produces a partial
-     reduction otherwise; here it is rejected */
-  if (prs != nranks) return EMAC_ERR_ARG;
-  if (c->nag && pag != nranks) return EMAC_ERR_ARG;
+  if (nlev > EMAC_MAX_LEVELS) return EMAC_ERR_UNSUPPORTED;
   return EMAC_OK;
 }
 
@@ -121,36 +155,63 @@ static void position_order(int size, int nf, const int *f, int *ranks) {
   }
 }
 
-/* Leaves, in evaluation order, of the value position p holds for its chunk after
-   reduce-scatter step s. Step s combines f[s] partials of step s-1: p's own first, then
-   the partners of p's radix group in ascending group index. */
-static void tree_leaves(const emac_plan *pl, int s, int p, int *out, int *k) {
-  int gb = 1, i, q, base, qme;
-  if (s < 0) {
-    out[(*k)++] = pl->pos_rank[p];
-    return;
+/* Block of level L holding absolute position P: its first position and width, P's offset in it,
+   and the stride g of the level's member groups (g = 1 without a sub-split). */
+static void level_block(const emac_copyin *c, int R, int L, int P, int *base, int *size, int *p, int *g) {
+  int l, b = 0, sz = R, gg;
+  for (l = 0;; l++) {
+    gg = c->lv[l].sub ? sz / c->lv[l].sub : 1;
+    if (l == L) break;
+    b += ((P - b) / gg) * gg;
+    sz = gg;
   }
-  for (i = s + 1; i < pl->cfg.nrs; i++) gb *= pl->cfg.rs[i];
-  base = (p / (gb * pl->cfg.rs[s])) * (gb * pl->cfg.rs[s]);
-  qme = (p - base) / gb;
-  tree_leaves(pl, s - 1, p, out, k);
-  for (q = 0; q < pl->cfg.rs[s]; q++)
-    if (q != qme) tree_leaves(pl, s - 1, base + gb * q + p % gb, out, k);
+  *base = b;
+  *size = sz;
+  *p = P - b;
+  *g = gg;
 }
 
+/* Leaves, in evaluation order, of the value absolute position P holds for its chunk after
+   reduce-scatter step s of level L. Step s combines rs[s] partials of step s-1: P's own first,
+   then the partners of its radix group in ascending group index (reduce_copyin.c:687-744).
+   Below step 0 of a level L > 0 the partial is level L-1's complete value of that position. */
+static void tree_leaves(const emac_plan *pl, int L, int s, int P, int *out, int *k) {
+  const emac_level *v = &pl->cfg.lv[L];
+  int base, size, p, g, m, o, gb = 1, i, q, mbase, qme;
+  if (s < 0) {
+    if (L == 0)
+      out[(*k)++] = pl->pos_rank[P];
+    else
+      tree_leaves(pl, L - 1, pl->cfg.lv[L - 1].nrs - 1, P, out, k);
+    return;
+  }
+  level_block(&pl->cfg, pl->nranks, L, P, &base, &size, &p, &g);
+  m = p / g; /* member index within the strided group (rank_loc) */
+  o = p % g;
+  for (i = s + 1; i < v->nrs; i++) gb *= v->rs[i];
+  mbase = (m / (gb * v->rs[s])) * (gb * v->rs[s]);
+  qme = (m - mbase) / gb;
+  tree_leaves(pl, L, s - 1, P, out, k);
+  for (q = 0; q < v->rs[s]; q++)
+    if (q != qme) tree_leaves(pl, L, s - 1, base + (mbase + gb * q + m % gb) * g + o, out, k);
+}
+
+/* Replay codes of the composite tree: its levels are the reduce-scatter radices of level 0,
+   then of level 1, ... (level 0's are the fastest-varying digits of the leaf index). */
 static void build_codes(const emac_copyin *c, emac_codes *codes) {
-  int t, l;
+  int t, l, L, rad[EMAC_MAX_LEVELS];
   memset(codes, 0, sizeof(*codes));
-  codes->nlev = c->nrs;
+  for (L = 0; L < c->nlv; L++)
+    for (l = 0; l < c->lv[L].nrs; l++) rad[codes->nlev++] = c->lv[L].rs[l];
   codes->nleaf = 1;
-  for (l = 0; l < c->nrs; l++) codes->nleaf *= c->rs[l];
+  for (l = 0; l < codes->nlev; l++) codes->nleaf *= rad[l];
   for (t = 0; t < codes->nleaf; t++) {
     int rem = t, closing = 1;
-    for (l = 0; l < c->nrs; l++) {
-      int d = rem % c->rs[l];
-      rem /= c->rs[l];
+    for (l = 0; l < codes->nlev; l++) {
+      int d = rem % rad[l];
+      rem /= rad[l];
       if (d == 0) codes->first[t] |= (unsigned char)(1u << l);
-      if (closing && d == c->rs[l] - 1)
+      if (closing && d == rad[l] - 1)
         codes->close[t]++;
       else
         closing = 0;
@@ -158,9 +219,36 @@ static void build_codes(const emac_copyin *c, emac_codes *codes) {
   }
 }
 
+static int level_pieces(const emac_level *v) { return v->split > 0 ? v->split : 1; }
+
+/* Final chunks of relative position p in the level-L block of width `size`, inside the region
+   [off, off+len) this block works on, appended in piece order (reduce_copyin.c:994-1081). */
+static void level_chunks(const emac_copyin *c, int L, int size, int p, long off, long len, long *coff, long *clen,
+                         int *k) {
+  const emac_level *v = &c->lv[L];
+  int members = v->sub ? v->sub : size, g = size / members, pc;
+  long o[EMAC_MAX_RANKS], l[EMAC_MAX_RANKS], frac = v->split < 0 ? -(long)v->split : 0;
+  for (pc = 0; pc < level_pieces(v); pc++) {
+    long plen = len, poff = off;
+    if (v->split > 0) { /* piece pc of an equal split (:1035-1044) */
+      long base = len / v->split, extra = len % v->split;
+      plen = base + (pc < extra);
+      poff = off + base * pc + (pc < extra ? pc : extra);
+    }
+    partition(members, plen, frac, o, l);
+    if (v->sub) {
+      level_chunks(c, L + 1, g, p % g, poff + o[p / g], l[p / g], coff, clen, k);
+    } else {
+      coff[*k] = poff + o[p];
+      clen[*k] = l[p];
+      (*k)++;
+    }
+  }
+}
+
 int emac_plan_build(emac_plan *p, int nranks, long count, int dtype, int op, const emac_copyin *cfg) {
-  int i, pc, k;
-  long frac = 0;
+  int i, pc, k, L;
+  long *coff, *clen;
   memset(p, 0, sizeof(*p));
   if (nranks < 1 || nranks > EMAC_MAX_RANKS || count < 0) return EMAC_ERR_ARG;
   if (emac_type_size(dtype) < 0 || op < EMAC_SUM || op > EMAC_MAX) return EMAC_ERR_ARG;
@@ -175,57 +263,50 @@ int emac_plan_build(emac_plan *p, int nranks, long count, int dtype, int op, con
     emac_default_copyin(nranks, &p->cfg);
   }
   if (nranks == 1) { /* one rank: the allreduce is a copy; one leaf, one level */
-    p->cfg.nrs = 1;
-    p->cfg.rs[0] = 1;
-    p->cfg.nag = 0;
-    p->cfg.split = 1;
+    memset(&p->cfg.lv, 0, sizeof(p->cfg.lv));
+    p->cfg.nlv = 1;
+    p->cfg.lv[0].split = 1;
+    p->cfg.lv[0].nrs = 1;
+    p->cfg.lv[0].rs[0] = 1;
   } else {
     int rc = emac_validate_copyin(&p->cfg, nranks);
     if (rc) return rc;
   }
+  /* rank order from the leading reduce-scatter radices (ext_mpi_native.c:715-724) */
   for (i = 0; i < nranks; i++) p->pos_rank[i] = i;
-  position_order(nranks, p->cfg.nrs, p->cfg.rs, p->pos_rank);
+  position_order(nranks, p->cfg.lv[0].nrs, p->cfg.lv[0].rs, p->pos_rank);
   for (i = 0; i < nranks; i++) p->rank_pos[p->pos_rank[i]] = i;
 
-  if (p->cfg.split > 0) {
-    p->npieces = p->cfg.split;
-  } else {
-    p->npieces = 1;
-    frac = -(long)p->cfg.split;
-  }
+  p->npieces = 1;
+  for (L = 0; L < p->cfg.nlv; L++) p->npieces *= level_pieces(&p->cfg.lv[L]);
   p->chunk_off = (long *)malloc(sizeof(long) * (size_t)p->npieces * nranks);
   p->chunk_len = (long *)malloc(sizeof(long) * (size_t)p->npieces * nranks);
-  if (!p->chunk_off || !p->chunk_len) {
+  coff = (long *)malloc(sizeof(long) * (size_t)p->npieces);
+  clen = (long *)malloc(sizeof(long) * (size_t)p->npieces);
+  if (!p->chunk_off || !p->chunk_len || !coff || !clen) {
+    free(coff);
+    free(clen);
     emac_plan_free(p);
     return EMAC_ERR_MALLOC;
   }
-  for (pc = 0; pc < p->npieces; pc++) {
-    /* piece pc of an equal split (reduce_copyin.c:1035-1044), then its own partition */
-    long plen = count, poff = 0;
-    if (p->cfg.split > 0) {
-      long base = count / p->cfg.split, extra = count % p->cfg.split;
-      plen = base + (pc < extra);
-      poff = base * pc + (pc < extra ? pc : extra);
+  for (i = 0; i < nranks; i++) {
+    k = 0;
+    level_chunks(&p->cfg, 0, nranks, i, 0, count, coff, clen, &k);
+    for (pc = 0; pc < p->npieces; pc++) {
+      p->chunk_off[(size_t)pc * nranks + i] = coff[pc];
+      p->chunk_len[(size_t)pc * nranks + i] = clen[pc];
     }
-    partition(nranks, plen, frac, p->chunk_off + (size_t)pc * nranks, p->chunk_len + (size_t)pc * nranks);
-    for (i = 0; i < nranks; i++) p->chunk_off[(size_t)pc * nranks + i] += poff;
   }
+  free(coff);
+  free(clen);
   for (i = 0; i < nranks; i++) {
     k = 0;
     if (nranks == 1)
       p->leaf_rank[0][k++] = 0;
     else
-      tree_leaves(p, p->cfg.nrs - 1, i, p->leaf_rank[i], &k);
+      tree_leaves(p, p->cfg.nlv - 1, p->cfg.lv[p->cfg.nlv - 1].nrs - 1, i, p->leaf_rank[i], &k);
   }
-  if (nranks == 1) {
-    memset(&p->codes, 0, sizeof(p->codes));
-    p->codes.nlev = 1;
-    p->codes.nleaf = 1;
-    p->codes.first[0] = 1;
-    p->codes.close[0] = 1;
-  } else {
-    build_codes(&p->cfg, &p->codes);
-  }
+  build_codes(&p->cfg, &p->codes);
   return EMAC_OK;
 }
 

@@ -5,7 +5,8 @@
  * (src/core/reduce_copyin.c:674-842), assembles it into bytecode (src/core/byte_code.c) and
  * interprets it line by line. This planner computes the same arithmetic directly:
  *
- *   - the chunk partition of the message (reduce_copyin.c:396-427),
+ *   - the chunk partition of the message (reduce_copyin.c:396-427), nested through the "1"
+ *     sub-splits of the factor list (reduce_copies_one_socket, reduce_copyin.c:970-1084),
  *   - the permuted rank order of radix chains (reduce_copyin.c:375-394),
  *   - for every owner chunk, the exact fold tree its elements are summed in: the left fold
  *     of each recursive-halving step (own partial first, partners by ascending substep) nested
@@ -25,6 +26,7 @@ extern "C" {
 
 #define EMAC_MAX_RANKS 16  /* ranks of one node fold (sources and fan-out destinations) */
 #define EMAC_MAX_LEVELS 8  /* radices in one leg */
+#define EMAC_MAX_SPLITS 4  /* nested "1 <members>" sub-split levels of one copy-in string */
 #define EMAC_MAX_PIECES 65536
 
 /* element types: same codes as include/ext_mpi_amd.h */
@@ -42,11 +44,21 @@ enum {
   EMAC_ERR_TRANSPORT = -6
 };
 
+/* One level of "split radices... [1 <members> <next level>]". Level 0 spans the node. A level
+   followed by a sub-split runs over `sub` members strided by g = size/sub (the positions that
+   share p mod g); the next level spans the contiguous block of g positions holding p, on the
+   chunk this level assigned to p (reduce_copyin.c:976-981, :1011-1020). */
 typedef struct {
-  int method;                  /* 6 (recursive); 9 is accepted as its shm-staged alias */
-  int split;                   /* factors[0]: k>0 equal pieces, -k fixed k-element fractions */
+  int split;                    /* k>0 equal pieces, -k fixed k-element fractions */
   int nrs, rs[EMAC_MAX_LEVELS]; /* reduce-scatter radices, in application order */
   int nag, ag[EMAC_MAX_LEVELS]; /* allgather radices (0 of them = direct push) */
+  int sub;                      /* members per group when a sub-split follows, else 0 */
+} emac_level;
+
+typedef struct {
+  int method; /* 6 (recursive); 9 is accepted as its shm-staged alias */
+  int nlv;
+  emac_level lv[EMAC_MAX_SPLITS];
 } emac_copyin;
 
 int emac_parse_copyin(const char *s, emac_copyin *out);
@@ -58,6 +70,7 @@ int emac_type_size(int dtype);
 typedef struct {
   unsigned char first[EMAC_MAX_RANKS]; /* bit l: leaf t opens a fresh level-l accumulator */
   unsigned char close[EMAC_MAX_RANKS]; /* levels completed right after leaf t */
+  /* levels are the reduce-scatter radices of every split level, level 0's first */
   int nlev;
   int nleaf;
 } emac_codes;

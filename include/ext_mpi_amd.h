@@ -74,6 +74,10 @@ int ext_mpi_amd_fold_init(int nsrc, const void *const *srcs, int ndst, void *con
 int ext_mpi_amd_get_unique_id(void *id /* EXT_MPI_AMD_UNIQUE_ID_BYTES */);
 int ext_mpi_amd_comm_init(int rank, int size, const void *id, int device, int *comm);
 int ext_mpi_amd_comm_free(int comm);
+/* Testing transport: `size` communicators (one per rank) living in this process on the current
+ * device; point-to-point ops become device copies executed by the receiving rank. Run each leg
+ * on every rank before the next one (ext_mpi_amd_start_legs). Not for production. */
+int ext_mpi_amd_comm_init_loopback(int size, int *comm_of_rank);
 int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, int dtype, int op, int comm,
                                const char *copyin, int *handle);
 
@@ -87,11 +91,13 @@ void *ext_mpi_amd_stream(int handle); /* hipStream_t the handle runs on */
 int ext_mpi_amd_set_stream(int handle, void *hip_stream);
 /* Start a subset of the legs (benchmarking / profiling): the reference interleaves them in one
    byte-code stream (src/mpi/ext_mpi_native_exec.c:345-587); here they are separable. */
-#define EXT_MPI_AMD_LEG_STAGE 1          /* H2D / D2H of host buffers */
+#define EXT_MPI_AMD_LEG_STAGE_IN 1       /* H2D of host send buffers */
 #define EXT_MPI_AMD_LEG_REDUCE_SCATTER 2 /* COMM form: slice exchange (reduce_copyin transport) */
 #define EXT_MPI_AMD_LEG_FOLD 4           /* the bucket fold kernel (+ node fan-out) */
 #define EXT_MPI_AMD_LEG_ALLGATHER 8      /* COMM form: owned chunk to every peer (reduce_copyout) */
-#define EXT_MPI_AMD_LEG_ALL 15
+#define EXT_MPI_AMD_LEG_STAGE_OUT 16     /* D2H of host receive buffers */
+#define EXT_MPI_AMD_LEG_STAGE 17         /* both staging copies */
+#define EXT_MPI_AMD_LEG_ALL 31
 int ext_mpi_amd_start_legs(int handle, int legs);
 
 /* ---- introspection (no GPU needed) ----

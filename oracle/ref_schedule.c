@@ -4,8 +4,13 @@
  * Restatement of the method-6 ("recursive") single-node schedule generator of
  * src/core/reduce_copyin.c. Only the SMEMCPY / SREDUCE lines and the SET_NODE_BARRIER
  * markers are emitted; WAIT_NODE_BARRIER and memory-fence lines carry no data semantics
- * once phases are executed in lock-step (ref_emulate.c). Scope: one socket, one node,
- * no "1" sub-split inside the factor list (reduce_copies_one_socket's multi-level form).
+ * once phases are executed in lock-step (ref_emulate.c). Scope: one node, including the "1"
+ * sub-split of the factor list (reduce_copies_one_socket's multi-level form, :970-1084).
+ *
+ * Sockets: with EXT_MPI_NUM_SOCKETS_PER_NODE > 1 the generator runs over the same node-wide
+ * positions (ext_mpi_native.c:700-724); num_sockets only changes get_rank_cyclic's encoding of
+ * a partner (:482-486), which the buffer table decodes back to the same node rank, and the
+ * barrier/fence lines. The SMEMCPY / SREDUCE arithmetic restated here is therefore the same.
  *
  * Positions vs node ranks: the generator works on positions p in a permuted rank order
  * (ranks[p] is the node rank at position p, ext_mpi_rank_order); buffer indices in the
@@ -116,8 +121,9 @@ static void phase(prog_t *p) { emit(p, REF_OP_PHASE, 0, 0, 0, 0, 0, 0, 0); }
  * (:745-838). f[0..nf) are the radices after factors[0]: negative = reduce-scatter,
  * positive = allgather. pos is this rank's position.
  */
-static void recursive_legs(prog_t *p, int R, int nf, const int *f, long bytes, int tsize, int pos,
+static void recursive_legs(prog_t *p, int NR, int R, int nf, const int *f, long bytes, int tsize, int pos,
                            const int *ranks, long size_l, long off0, int stage, int first_call) {
+  /* NR: ranks of the node (buffer-index modulus); R: members of this level (socket_size) */
   long sizes[R], displs[R + 1];
   int nrs, s, q, i, base, gb, copied = 0;
   int *ag_base = (int *)calloc(nf > 0 ? nf : 1, sizeof(int));
@@ -147,10 +153,10 @@ static void recursive_legs(prog_t *p, int R, int nf, const int *f, long bytes, i
             emit(p, REF_OP_COPY, REF_BUF_RECV, 0, off, REF_BUF_SEND, 0, off, len);
             copied = 1;
           }
-          emit(p, REF_OP_SUM, REF_BUF_RECV, 0, off, REF_BUF_SEND, rel_index(R, ranks, pos, partner),
+          emit(p, REF_OP_SUM, REF_BUF_RECV, 0, off, REF_BUF_SEND, rel_index(NR, ranks, pos, partner),
                off, len);
         } else {
-          emit(p, REF_OP_SUM, REF_BUF_RECV, 0, off, REF_BUF_RECV, rel_index(R, ranks, pos, partner),
+          emit(p, REF_OP_SUM, REF_BUF_RECV, 0, off, REF_BUF_RECV, rel_index(NR, ranks, pos, partner),
                off, len);
         }
       }
@@ -186,7 +192,7 @@ static void recursive_legs(prog_t *p, int R, int nf, const int *f, long bytes, i
         for (i = 0; i < gb; i++) len += sizes[(pos / gb) * gb + i];
         target = ag_base[s] + gb * q + pos % gb;
         if (len > 0)
-          emit(p, REF_OP_COPY, REF_BUF_RECV, rel_index(R, ranks, pos, target), off, REF_BUF_RECV, 0,
+          emit(p, REF_OP_COPY, REF_BUF_RECV, rel_index(NR, ranks, pos, target), off, REF_BUF_RECV, 0,
                off, len);
       }
     }
@@ -196,7 +202,7 @@ static void recursive_legs(prog_t *p, int R, int nf, const int *f, long bytes, i
     for (i = 1; i < R; i++) {
       long off = displs[pos] + off0, len = sizes[pos];
       if (len > 0)
-        emit(p, REF_OP_COPY, REF_BUF_RECV, rel_index(R, ranks, pos, (pos + i) % R), off, REF_BUF_RECV,
+        emit(p, REF_OP_COPY, REF_BUF_RECV, rel_index(NR, ranks, pos, (pos + i) % R), off, REF_BUF_RECV,
              0, off, len);
     }
     phase(p);
@@ -204,17 +210,50 @@ static void recursive_legs(prog_t *p, int R, int nf, const int *f, long bytes, i
   free(ag_base);
 }
 
-/* reduce_copies_one_socket (reduce_copyin.c:970-1084) for one socket and no sub-splits */
-static int one_socket(prog_t *p, int R, int nfactors, const int *factors, long bytes, int tsize,
+/* reduce_copies_one_socket (reduce_copyin.c:970-1084). A "1" at index nloc of the factor list
+   opens a sub-split: factors[nloc+1] = sloc members per group. This level then runs over the
+   sloc positions strided by g = size / sloc that share pos % g (:976-981), and the level named
+   by the factors after nloc+1 runs over the contiguous block of g positions holding pos, on the
+   chunk this level assigned to pos (:1011-1020 / :1058-1067); the copy-out nests the other way
+   round (:1020-1031). */
+static int one_socket(prog_t *p, int NR, int size, int nfactors, const int *factors, long add, long bytes, int tsize,
                       int pos, const int *ranks, int first_call, int stage) {
-  int i;
-  if (R <= 1) return 0;
-  for (i = 1; i < nfactors; i++)
-    if (factors[i] == 1) return -1; /* multi-level split: out of the oracle's scope */
+  int nloc, sloc, g, i, rank_loc = -1, rank_loci = -1;
+  int ranks_loc[size > 0 ? size : 1], ranks_loci[size > 0 ? size : 1];
+  long sizes[size + 1], displs[size + 2];
+  if (size <= 1) return 0;
+  if (nfactors < 2) return -1;
+  for (nloc = 1; nloc < nfactors && factors[nloc] != 1; nloc++);
+  if (nloc != nfactors) {
+    if (nloc + 2 >= nfactors) return -1;
+    sloc = factors[nloc + 1];
+    if (sloc < 1 || size % sloc) return -1;
+    /* :1066-1067 reuse the piece loop's variable: an equal split into >1 pieces above a
+       sub-split does not terminate in the reference's generator */
+    if (factors[0] > 1) return -1;
+  } else {
+    sloc = size;
+  }
+  g = size / sloc;
+  for (i = 0; i < sloc; i++) ranks_loc[i] = ranks[i * g + pos % g];
+  for (i = 0; i < sloc; i++)
+    if (ranks_loc[i] == ranks[pos]) rank_loc = i;
+  for (i = 0; i < g; i++) ranks_loci[i] = ranks[i + pos / g * g];
+  for (i = 0; i < g; i++)
+    if (ranks_loci[i] == ranks[pos]) rank_loci = i;
   if (factors[0] < 0) {
-    /* fixed fraction of -factors[0] elements per rank (:994-1033) */
-    recursive_legs(p, R, nfactors - 1, factors + 1, bytes, tsize, pos, ranks, -factors[0], 0, stage,
-                   stage == 1 ? first_call : 0);
+    /* fixed fraction of -factors[0] elements per member (:994-1033) */
+    if (stage == 1)
+      recursive_legs(p, NR, sloc, nloc - 1, factors + 1, bytes, tsize, rank_loc, ranks_loc, -factors[0], add, 1,
+                     first_call);
+    if (nloc != nfactors) {
+      ref_sizes_displs(sloc, bytes, tsize, -factors[0], sizes, displs);
+      if (one_socket(p, NR, g, nfactors - nloc - 2, factors + nloc + 2, add + displs[rank_loc], sizes[rank_loc], tsize,
+                     rank_loci, ranks_loci, 0, stage))
+        return -1;
+    }
+    if (stage == 2)
+      recursive_legs(p, NR, sloc, nloc - 1, factors + 1, bytes, tsize, rank_loc, ranks_loc, -factors[0], add, 2, 0);
   } else {
     /* factors[0] equal pieces, each with its own schedule (:1035-1081) */
     long nelem = bytes / tsize;
@@ -226,18 +265,39 @@ static int one_socket(prog_t *p, int R, int nfactors, const int *factors, long b
         first = len * i + i;
         len++;
       }
-      if (len > 0)
-        recursive_legs(p, R, nfactors - 1, factors + 1, len * tsize, tsize, pos, ranks, 0,
-                       first * tsize, stage, stage == 1 ? first_call : 0);
+      if (len > 0 || size != NR) {
+        if (stage == 1)
+          recursive_legs(p, NR, sloc, nloc - 1, factors + 1, len * tsize, tsize, rank_loc, ranks_loc, 0,
+                         add + first * tsize, 1, first_call);
+        if (nloc != nfactors) {
+          ref_sizes_displs(sloc, len * tsize, tsize, 0, sizes, displs);
+          if (one_socket(p, NR, g, nfactors - nloc - 2, factors + nloc + 2, add + first * tsize + displs[rank_loc],
+                         sizes[rank_loc], tsize, rank_loci, ranks_loci, 0, stage))
+            return -1;
+        }
+        if (stage == 2)
+          recursive_legs(p, NR, sloc, nloc - 1, factors + 1, len * tsize, tsize, rank_loc, ranks_loc, 0,
+                         add + first * tsize, 2, 0);
+      }
     }
   }
   return 0;
 }
 
-static int check_factors(int R, const int *factors, int nfactors) {
-  int prod_rs = 1, prod_ag = 1, i, nrs = 0, nag = 0;
-  if (nfactors < 1 || factors[0] == 0) return -1;
-  for (i = 1; i < nfactors; i++) {
+/* Every level's radix chain must cover its members exactly (the reference silently produces a
+   partial reduction otherwise). Returns 0 if the factor list is a valid method-6 list. */
+static int check_level(int size, const int *factors, int nfactors) {
+  int prod_rs = 1, prod_ag = 1, i, nrs = 0, nag = 0, nloc, sloc;
+  if (nfactors < 2 || factors[0] == 0) return -1;
+  for (nloc = 1; nloc < nfactors && factors[nloc] != 1; nloc++);
+  sloc = size;
+  if (nloc != nfactors) {
+    if (nloc + 2 >= nfactors) return -1;
+    sloc = factors[nloc + 1];
+    if (sloc < 2 || size % sloc || size / sloc < 2 || factors[0] > 1) return -1;
+    if (check_level(size / sloc, factors + nloc + 2, nfactors - nloc - 2)) return -1;
+  }
+  for (i = 1; i < nloc; i++) {
     if (factors[i] < 0) {
       if (nag) return -1; /* radices must be all reduce-scatter first, then allgather */
       prod_rs *= -factors[i];
@@ -249,8 +309,8 @@ static int check_factors(int R, const int *factors, int nfactors) {
       return -1;
     }
   }
-  if (!nrs || prod_rs != R) return -1;
-  if (nag && prod_ag != R) return -1;
+  if (!nrs || prod_rs != sloc) return -1;
+  if (nag && prod_ag != sloc) return -1;
   return 0;
 }
 
@@ -259,7 +319,7 @@ int ref_schedule(int R, int node_rank, long bytes, int dtype, const int *factors
                  int in_place, int stage, ref_op *out, int cap) {
   prog_t prog;
   int ranks[R], pos = -1, i, nrs, tsize = ref_type_size(dtype);
-  if (tsize <= 0 || check_factors(R, factors, nfactors)) return -1;
+  if (tsize <= 0 || check_level(R, factors, nfactors)) return -1;
   prog.ops = out;
   prog.n = 0;
   prog.cap = cap;
@@ -270,7 +330,7 @@ int ref_schedule(int R, int node_rank, long bytes, int dtype, const int *factors
   for (i = 0; i < R; i++)
     if (ranks[i] == node_rank) pos = i;
   if (pos < 0) return -1;
-  if (one_socket(&prog, R, nfactors, factors, bytes, tsize, pos, ranks, !in_place, stage) < 0) return -1;
+  if (one_socket(&prog, R, R, nfactors, factors, 0, bytes, tsize, pos, ranks, !in_place, stage) < 0) return -1;
   if (prog.overflow) return -1;
   return prog.n;
 }

@@ -1,6 +1,7 @@
 /* Drop-in check of libext_mpi_collectives.so, written like an application of the reference
  * (tests/benchmark.c shape): only MPI calls plus the MPI-4 prototype from ext_mpi_interface.h.
- * argv: count dtype(f|d|i|l) mem(dev|host) [inplace]. Prints "RESULT ok" / "RESULT no-device"
+ * argv: count dtype(f|d|i|l) mem(dev|host) [inplace] [blocking]. "blocking" drives MPI_Allreduce
+ * (run with EXT_MPI_BLOCKING set) instead of MPI_Allreduce_init. Prints "RESULT ok" / "RESULT no-device"
  * / "RESULT fail ...". Integer inputs are checked exactly against PMPI_Allreduce; float inputs
  * are integer-valued (exact in any order) so the same comparison applies. */
 #include <mpi.h>
@@ -13,12 +14,16 @@
 int main(int argc, char **argv) {
   int rank, size, count = argc > 1 ? atoi(argv[1]) : 1000, rc, i, bad = 0, flag;
   char t = argc > 2 ? argv[2][0] : 'f';
-  int dev = argc > 3 ? !strcmp(argv[3], "dev") : 1, inplace = argc > 4 && !strcmp(argv[4], "inplace");
+  int dev = argc > 3 ? !strcmp(argv[3], "dev") : 1, inplace = 0, blocking = 0;
   MPI_Datatype dt = t == 'd' ? MPI_DOUBLE : t == 'i' ? MPI_INT : t == 'l' ? MPI_LONG : MPI_FLOAT;
   int ts = (t == 'd' || t == 'l') ? 8 : 4;
   size_t bytes = (size_t)count * ts;
   void *hs, *hr, *ref, *s = NULL, *r = NULL;
   MPI_Request req, p2p[2];
+  for (i = 4; i < argc; i++) {
+    inplace |= !strcmp(argv[i], "inplace");
+    blocking |= !strcmp(argv[i], "blocking");
+  }
   MPI_Init(&argc, &argv);
   MPI_Comm_rank(MPI_COMM_WORLD, &rank);
   MPI_Comm_size(MPI_COMM_WORLD, &size);
@@ -45,7 +50,8 @@ int main(int argc, char **argv) {
     if (b != from) bad |= 1;
   }
   if (ext_mpi_amd_gpu_device_count() <= 0) {
-    rc = MPI_Allreduce_init(hs, hr, count, dt, MPI_SUM, MPI_COMM_WORLD, MPI_INFO_NULL, &req);
+    if (blocking) rc = MPI_Allreduce(hs, hr, count, dt, MPI_SUM, MPI_COMM_WORLD) == MPI_SUCCESS ? 0 : -5;
+    else rc = MPI_Allreduce_init(hs, hr, count, dt, MPI_SUM, MPI_COMM_WORLD, MPI_INFO_NULL, &req);
     if (rank == 0) printf("RESULT %s rc=%d\n", (rc == -5 && !bad) ? "no-device" : "fail", rc);
     MPI_Finalize();
     return 0;
@@ -58,6 +64,47 @@ int main(int argc, char **argv) {
     r = hr;
     s = hs;
     if (inplace) memcpy(hr, hs, bytes);
+  }
+  if (blocking) {
+    /* repeated calls (handle cache hits), a second buffer pair (a miss), a derived communicator */
+    void *s2 = NULL, *r2 = NULL;
+    MPI_Comm dup;
+    MPI_Comm_dup(MPI_COMM_WORLD, &dup);
+    if (dev) {
+      ext_mpi_amd_gpu_malloc(&r2, bytes);
+      ext_mpi_amd_gpu_malloc(&s2, bytes);
+      ext_mpi_amd_gpu_memcpy_hd(s2, hs, bytes);
+    } else {
+      r2 = malloc(bytes);
+      s2 = malloc(bytes);
+      memcpy(s2, hs, bytes);
+    }
+    for (int it = 0; it < 6; it++) {
+      int second = it == 3 || it == 4;
+      void *rr = second ? r2 : r, *ss = second ? s2 : s;
+      MPI_Comm c = it == 5 ? dup : MPI_COMM_WORLD;
+      if (inplace) {
+        if (dev) ext_mpi_amd_gpu_memcpy_hd(rr, hs, bytes);
+        else memcpy(rr, hs, bytes);
+      }
+      rc = MPI_Allreduce(inplace ? MPI_IN_PLACE : ss, rr, count, dt, MPI_SUM, c);
+      if (rc != MPI_SUCCESS) {
+        printf("RESULT fail blocking rc=%d\n", rc);
+        MPI_Abort(MPI_COMM_WORLD, 1);
+      }
+      if (dev) ext_mpi_amd_gpu_memcpy_dh(hr, rr, bytes);
+      else if (rr != hr) memcpy(hr, rr, bytes);
+      if (memcmp(hr, ref, bytes)) bad |= 4 << it;
+    }
+    MPI_Comm_free(&dup);
+    if (dev) {
+      ext_mpi_amd_gpu_free(r2);
+      ext_mpi_amd_gpu_free(s2);
+    } else {
+      free(r2);
+      free(s2);
+    }
+    goto report;
   }
   rc = MPI_Allreduce_init(inplace ? MPI_IN_PLACE : s, r, count, dt, MPI_SUM, MPI_COMM_WORLD, MPI_INFO_NULL, &req);
   if (rc) {
@@ -79,9 +126,10 @@ int main(int argc, char **argv) {
     if (memcmp(hr, ref, bytes)) bad |= 2;
   }
   MPI_Request_free(&req);
+report:
   MPI_Allreduce(MPI_IN_PLACE, &bad, 1, MPI_INT, MPI_BOR, MPI_COMM_WORLD);
-  if (rank == 0) printf("RESULT %s (size=%d count=%d type=%c mem=%s%s)\n", bad ? "fail" : "ok", size, count, t,
-                        dev ? "dev" : "host", inplace ? " inplace" : "");
+  if (rank == 0) printf("RESULT %s (size=%d count=%d type=%c mem=%s%s%s) bad=%d\n", bad ? "fail" : "ok", size, count, t,
+                        dev ? "dev" : "host", inplace ? " inplace" : "", blocking ? " blocking" : "", bad);
   if (dev) {
     ext_mpi_amd_gpu_free(r);
     ext_mpi_amd_gpu_free(s);

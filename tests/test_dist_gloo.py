@@ -73,7 +73,8 @@ def _worker(rank, world, port, cases, q):
     (2, [(emac.FLOAT, 100003, None), (emac.DOUBLE, 7, "6;1 -2 2"), (emac.INT, 4099, "6;3 -2 2"),
          (emac.LONG, 1000, "6;-5 -2 2"), (emac.FLOAT, 0, None), (emac.FLOAT, 1, None)]),
     (4, [(emac.FLOAT, 65539, "6;1 -4 4"), (emac.DOUBLE, 4099, "6;1 -2 -2 2 2"), (emac.INT, 1001, "6;2 -2 -2 4"),
-         (emac.LONG, 5000, "6;-7 -4 4")]),
+         (emac.LONG, 5000, "6;-7 -4 4"), (emac.FLOAT, 30011, "6;1 -2 2 1 2 1 -2 2"),
+         (emac.DOUBLE, 999, "6;-5 -2 2 1 2 3 -2 2")]),
 ])
 def test_comm_program_over_gloo(world, cases):
     ctx = mp.get_context("spawn")

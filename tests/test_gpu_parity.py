@@ -60,6 +60,8 @@ CONFIGS = [
     (2, "6;1 -2 2"), (3, "6;1 -3 3"), (4, "6;1 -4 4"), (4, "6;1 -2 -2 2 2"), (6, "6;1 -2 -3 3 2"),
     (8, "6;1 -8 8"), (8, "6;1 -2 -2 -2 2 2 2"), (8, "6;1 -4 -2 2 4"), (8, "6;-64 -8 8"), (8, "6;3 -8 8"),
     (8, "9;1 -8 8"), (12, "6;1 -3 -4 4 3"), (16, "6;1 -16 16"), (16, "6;1 -2 -2 -2 -2 2 2 2 2"),
+    # "1 <members>" sub-splits (two-level trees, reduce_copyin.c:970-1084)
+    (8, "6;1 -4 4 1 4 1 -2 2"), (8, "6;-3 -2 -2 2 2 1 4 2 -2 2"), (16, "6;1 -4 4 1 4 1 -2 -2 2 2"),
 ]
 CODES = [emac.FLOAT, emac.DOUBLE, emac.INT, emac.LONG]
 
@@ -224,3 +226,66 @@ def test_fold_handle_and_copy_reduce(code, nsrc, ndst):
             assert L.ext_mpi_amd_gpu_copy_reduce(code, emac.SUM, nsrc, sp, ndst, dp, count, None) == 0
         for d in dsts:
             assert np.array_equal(d.cpu().numpy().view(np.uint8), want.view(np.uint8)), (how, nsrc, ndst)
+
+
+def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=None):
+    """COMM form (one rank per communicator) on the in-process loopback transport: the legs run
+    on every rank in lock-step -- stage-in, reduce-scatter, fold, all-gather, stage-out -- so
+    the staging slots, fold buckets and leg programs of the multi-GPU path execute on one GPU."""
+    R, count = len(sends), sends[0].size
+    comms = emac.comm_init_loopback(R)
+    phase = phase or [0] * R
+    keep = []
+    if host:
+        sbufs = [s.copy() for s in sends]
+        rbufs = sbufs if in_place else [np.full(count, -1, dtype=s.dtype) for s in sends]
+        ptrs = [(s.ctypes.data, r.ctypes.data) for s, r in zip(sbufs, rbufs)]
+    else:
+        # element offsets shift the 16-byte phase of each rank's buffers independently
+        sb = [torch.zeros(count + 4, dtype=TORCH[code], device="cuda") for _ in range(R)]
+        sbufs = [b[p:p + count] for b, p in zip(sb, phase)]
+        for t, s in zip(sbufs, sends):
+            t.copy_(torch.from_numpy(s))
+        rbufs = sbufs if in_place else [torch.full((count,), -1, dtype=TORCH[code], device="cuda") for _ in range(R)]
+        keep += sb
+        ptrs = [(s.data_ptr(), r.data_ptr()) for s, r in zip(sbufs, rbufs)]
+    hs = []
+    try:
+        for r in range(R):
+            hs.append(emac.allreduce_init(ptrs[r][0], ptrs[r][1], count, code, comms[r], copyin))
+        torch.cuda.synchronize()
+        for leg in (emac.LEG_STAGE_IN, emac.LEG_REDUCE_SCATTER, emac.LEG_FOLD, emac.LEG_ALLGATHER, emac.LEG_STAGE_OUT):
+            for h in hs:
+                emac.start_legs(h, leg)
+            for h in hs:
+                emac.wait(h)
+    finally:
+        for h in hs:
+            emac.done(h)
+        for c in comms:
+            emac.comm_free(c)
+    return [np.asarray(r) if host else r.cpu().numpy() for r in rbufs]
+
+
+COMM_CONFIGS = [(2, "6;1 -2 2"), (3, "6;1 -3 3"), (4, "6;1 -2 -2 2 2"), (6, "6;1 -3 -2 2 3"), (8, "6;1 -8 8"),
+                (8, "6;1 -2 -4 4 2"), (8, "6;-64 -8 8"), (16, "6;1 -4 -4 4 4"), (8, "6;1 -2 2 1 2 1 -4 4"),
+                (8, "6;1 -2 2 1 2 1 -2 2 1 2 1 -2 2")]
+
+
+@pytest.mark.parametrize("R,copyin", COMM_CONFIGS)
+@pytest.mark.parametrize("code", CODES)
+def test_comm_form_loopback_parity(oracle, R, copyin, code):
+    for count in (0, 1, 7, 1031, 65536 + 5):
+        sends = xorshift_inputs(R, count, code, seed_base=0xC0AA0000 + count)
+        want = oracle.allreduce(sends, copyin)
+        got = run_comm_loopback(sends, code, copyin, phase=[(r * 3) % 4 for r in range(R)])
+        assert_bitwise(got, want, f"comm R={R} {copyin} code={code} n={count}")
+
+
+@pytest.mark.parametrize("in_place", [False, True])
+def test_comm_form_loopback_host_and_in_place(oracle, in_place):
+    sends = xorshift_inputs(4, 200003, emac.DOUBLE)
+    want = oracle.allreduce(sends, "6;1 -4 4", in_place=in_place)
+    for host in (False, True):
+        got = run_comm_loopback(sends, emac.DOUBLE, "6;1 -4 4", host=host, in_place=in_place)
+        assert_bitwise(got, want, f"comm host={host} in_place={in_place}")

@@ -32,10 +32,10 @@ def _build(tmp_path):
     return exe
 
 
-def _run(exe, n, args, env=None, timeout=240):
+def _run(exe, n, args, env=None, timeout=240, cwd=None):
     e = dict(os.environ, **(env or {}))
     p = subprocess.run([os.path.join(MPI_HOME, "bin", "mpiexec"), "-n", str(n), exe] + [str(a) for a in args],
-                       capture_output=True, text=True, timeout=timeout, env=e)
+                       capture_output=True, text=True, timeout=timeout, env=e, cwd=cwd)
     out = p.stdout + p.stderr
     return [l for l in out.splitlines() if l.startswith("RESULT")], out
 
@@ -56,3 +56,42 @@ def test_mpi_layer_single_rank_gpu(tmp_path, args):
     exe = _build(tmp_path)
     res, out = _run(exe, 1, args, env={"EXT_MPI_DEBUG": "1"})
     assert res and res[0].startswith("RESULT ok"), out
+
+
+def test_mpi_blocking_without_gpu(tmp_path):
+    """EXT_MPI_BLOCKING routes MPI_Allreduce(SUM) to the engine, which fails loudly without a GPU."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by the gpu test")
+    exe = _build(tmp_path)
+    res, out = _run(exe, 2, [1000, "f", "host", "blocking"], env={"EXT_MPI_BLOCKING": "1"})
+    assert res and res[0].startswith("RESULT no-device"), out
+
+
+# ext_mpi_allreduce_blocking_<nodes>_<cores>.txt as the reference's README shows it: host rows,
+# then device rows (the size column restarts); '_' stands for ' ' in the copy-in column.
+PARAMS_1_1 = """8 1 1(-1) 9;-64_-1_1
+1024 1 1(-1) 6;1_-1_1
+8 1 1(-1) 6;-64_-1_1
+4096 1 1(-1) 9;1_-1_1
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args,copyin", [
+    ([100003, "f", "dev", "blocking"], "9;1 -1 1"),             # 400012 B: device row 2
+    ([100, "f", "dev", "blocking"], "6;-64 -1 1"),              # 400 B: device row 1
+    ([4099, "d", "dev", "inplace", "blocking"], "9;1 -1 1"),
+    ([100, "i", "host", "blocking"], "9;-64 -1 1"),             # 400 B: host row 1
+    ([777, "l", "host", "inplace", "blocking"], "6;1 -1 1"),    # 6216 B: host row 2
+    ([0, "f", "dev", "blocking"], "9;-64 -1 1"),                # no allocation: host rows
+])
+def test_mpi_blocking_single_rank_gpu(tmp_path, args, copyin):
+    """Blocking MPI_Allreduce: parameter-file row choice, handle cache hits and misses, in place,
+    host and device buffers, a derived communicator."""
+    exe = _build(tmp_path)
+    (tmp_path / "ext_mpi_allreduce_blocking_1_1.txt").write_text(PARAMS_1_1)
+    res, out = _run(exe, 1, args, env={"EXT_MPI_BLOCKING": "1", "EXT_MPI_VERBOSE": "1"}, cwd=str(tmp_path))
+    assert res and res[0].startswith("RESULT ok"), out
+    chosen = [l for l in out.splitlines() if l.startswith("# EXT_MPI blocking allreduce")]
+    assert chosen and all(l.endswith("copyin " + copyin) for l in chosen), out

@@ -16,6 +16,14 @@ CONFIGS = [
     (8, "6;-64 -8 8"), (8, "6;3 -8 8"), (8, "9;1 -8 8"),
     (12, "6;1 -2 -2 -3 3 2 2"), (16, "6;1 -16 16"), (16, "6;1 -2 -2 -2 -2 2 2 2 2"), (16, "6;1 -4 -4 4 4"),
 ]
+# "1 <members> <level>" sub-splits (reduce_copies_one_socket's multi-level form, reduce_copyin.c:970-1084)
+SUBSPLITS = [
+    (4, "6;1 -2 2 1 2 1 -2 2"), (6, "6;1 -3 3 1 3 1 -2 2"), (6, "6;1 -2 2 1 2 -4 -3 3"),
+    (8, "6;1 -4 4 1 4 1 -2 2"), (8, "6;1 -2 2 1 2 1 -4 4"), (8, "6;1 -2 2 1 2 3 -2 -2 2 2"),
+    (8, "6;-3 -2 -2 2 2 1 4 1 -2 2"), (8, "6;1 -2 1 2 -5 -4"), (8, "6;1 -2 2 1 2 1 -2 2 1 2 1 -2 2"),
+    (12, "6;1 -3 3 1 3 1 -2 -2 2 2"), (16, "6;1 -4 4 1 4 1 -2 -2 2 2"), (16, "6;-9 -2 -2 2 2 1 4 2 -4 4"),
+]
+CONFIGS += SUBSPLITS
 CODES = [emac.FLOAT, emac.DOUBLE, emac.INT, emac.LONG]
 
 
@@ -46,7 +54,25 @@ def test_chain_leaf_order():
     assert d5["owner"] == 5 and d5["pieces"] == [(10240, 2048)]
 
 
-@pytest.mark.parametrize("bad", ["6;1 -3 3", "6;1 -2 -2 2", "5;1 -4 4", "6;1 4 -4", "6;1 -4 1 4", "garbage", "6;"])
+@pytest.mark.parametrize("bad", ["6;1 -3 3", "6;1 -2 -2 2", "5;1 -4 4", "6;1 4 -4", "6;1 -4 1 4", "garbage", "6;",
+                                 "6;1 -2 2 1 2 1 -4 4", "6;1 -2 2 1 3 1 -2 2", "6;1 -4 4 1 4 1 -1 1"])
 def test_invalid_copyin_rejected(bad):
+    # (R=4) chain/level size mismatches, a sub-split whose members do not divide the level
     with pytest.raises(emac.ExtMpiError):
         emac.plan_describe(4, 100, emac.FLOAT, bad, 0)
+
+
+def test_subsplit_equal_pieces_above_a_subsplit_unsupported():
+    """reduce_copyin.c:1035-1067 reuse the piece loop's variable inside a sub-split, so the
+    reference's generator never terminates for k>1 equal pieces above one: rejected here."""
+    with pytest.raises(emac.ExtMpiError):
+        emac.plan_describe(8, 100, emac.FLOAT, "6;2 -4 4 1 4 1 -2 2", 0)
+
+
+def test_subsplit_leaf_order():
+    """'6;1 -4 4 1 4 1 -2 2' on 8 ranks: the strided groups {p%2, p%2+2, ...} fold first (own partial,
+    then partners ascending), then each contiguous pair folds the two group partials."""
+    d = emac.plan_describe(8, 8000, emac.FLOAT, "6;1 -4 4 1 4 1 -2 2", 3)
+    # position 3: outer member 1 of group {1,3,5,7}; inner member 1 of block {2,3}
+    assert d["leaves"] == [3, 1, 5, 7, 2, 0, 4, 6]
+    assert d["nlev"] == 2 and d["pieces"] == [(3000, 1000)]  # outer quarter [2000, 4000), inner half 1
