@@ -171,7 +171,8 @@ static int upload_buckets(emac_handle *h, emac_bucket *b, int nb) {
 }
 
 static int parse_cfg(const char *copyin, int nranks, emac_copyin *cfg) {
-  if (!copyin || !*copyin) {
+  /* one rank: the generator returns before reading the factors (reduce_copyin.c:975) */
+  if (!copyin || !*copyin || nranks == 1) {
     emac_default_copyin(nranks, cfg);
     return 0;
   }
