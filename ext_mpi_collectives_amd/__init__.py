@@ -41,6 +41,10 @@ class FoldDesc(ctypes.Structure):
 
 BUF_SEND, BUF_RECV, BUF_STAGE = 0, 1, 2
 
+# int (*)(void *ctx, const void *send, void *recv, long bytes) -- include/ext_mpi_amd.h
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long)
+_ipc_callbacks = {}  # comm -> the ctypes callback (must outlive the communicator)
+
 
 class ExtMpiError(RuntimeError):
     def __init__(self, what, code):
@@ -74,6 +78,7 @@ def lib():
         L.ext_mpi_amd_comm_init.argtypes = [c_int, c_int, c_void_p, c_int, P(c_int)]
         L.ext_mpi_amd_comm_free.argtypes = [c_int]
         L.ext_mpi_amd_comm_init_loopback.argtypes = [c_int, P(c_int)]
+        L.ext_mpi_amd_comm_init_ipc.argtypes = [c_int, c_int, ALLGATHER_FN, c_void_p, c_int, P(c_int)]
         L.ext_mpi_amd_allreduce_init.argtypes = [c_void_p, c_void_p, c_long, c_int, c_int, c_int,
                                                  ctypes.c_char_p, P(c_int)]
         for name in ("start", "test", "wait", "done"):
@@ -159,8 +164,42 @@ def comm_init_loopback(size):
     return list(comms)
 
 
+def comm_init_ipc(rank, size, allgather, device=-1):
+    """Peer-mapped communicator (hipIpc over xGMI): one rank per GPU, or several processes on one.
+
+    ``allgather(payload: bytes) -> list[bytes]`` must return every rank's payload in rank order
+    (a bootstrap exchange, called collectively at communicator and handle set-up only)."""
+    def _cb(ctx, send, recv, nbytes):
+        try:
+            parts = allgather(ctypes.string_at(send, nbytes))
+            blob = b"".join(bytes(x) for x in parts)
+            if len(parts) != size or len(blob) != nbytes * size:
+                return -1
+            ctypes.memmove(recv, blob, len(blob))
+            return 0
+        except Exception:  # noqa: BLE001 -- reported to the C side as a transport failure
+            return -1
+    cb = ALLGATHER_FN(_cb)
+    c = ctypes.c_int(-1)
+    _check("ext_mpi_amd_comm_init_ipc", lib().ext_mpi_amd_comm_init_ipc(rank, size, cb, None, device, ctypes.byref(c)))
+    _ipc_callbacks[c.value] = cb
+    return c.value
+
+
+def torch_allgather(group=None):
+    """Bootstrap exchange for :func:`comm_init_ipc` over an initialised torch.distributed group."""
+    import torch.distributed as dist
+
+    def ag(payload):
+        out = [None] * dist.get_world_size(group)
+        dist.all_gather_object(out, payload, group=group)
+        return out
+    return ag
+
+
 def comm_free(comm):
     _check("ext_mpi_amd_comm_free", lib().ext_mpi_amd_comm_free(comm))
+    _ipc_callbacks.pop(comm, None)
 
 
 def allreduce_init(sendptr, recvptr, count, dtype, comm, copyin=None, op=SUM):

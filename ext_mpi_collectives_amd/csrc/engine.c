@@ -37,13 +37,36 @@
 #define MAX_HANDLES 4096
 #define MAX_COMMS 64
 
-enum { KIND_NODE = 1, KIND_COMM = 2 };
+enum { KIND_NODE = 1, KIND_COMM = 2, KIND_IPC = 3 };
+
+/* one peer allocation mapped into this process (hipIpcOpenMemHandle), shared by the handles
+   that reference it */
+typedef struct {
+  int peer;
+  unsigned char handle[EMAC_IPC_HANDLE_BYTES];
+  void *base;
+  int refs;
+} ipc_map;
 
 typedef struct {
   int used;
   int rank, size, device;
   ncclComm_t nccl;
   int loop_group; /* >= 0: in-process loopback communicator (testing transport), no RCCL */
+  /* peer-mapped transport (ext_mpi_amd_comm_init_ipc) */
+  int ipc;
+  ext_mpi_amd_allgather_fn ag;
+  void *ag_ctx;
+  void *sync;                      /* this rank's emac_sync block (uncached device memory) */
+  void *peer_sync[EMAC_MAX_RANKS]; /* every rank's block as mapped here (own at [rank]) */
+  void *peer_sync_base[EMAC_MAX_RANKS]; /* the mappings (hipIpcCloseMemHandle takes the base) */
+  void **d_peer_sync;              /* the same table in device memory */
+  int *err;                        /* pinned host word the barrier kernels report into */
+  unsigned xcc_mask;
+  long timeout_ticks;
+  int next_slot;
+  ipc_map *maps;
+  int nmaps;
 } emac_comm;
 
 /* Loopback groups: every rank of the communicator lives in this process; the i-th handle a
@@ -87,6 +110,11 @@ typedef struct {
   int started;
   int loop_index; /* position in the loopback group's per-rank handle list */
   int own_stream; /* 0 once the caller supplied the stream (ext_mpi_amd_set_stream) */
+  /* IPC form */
+  int slot;                /* synchronisation slot on the communicator */
+  unsigned long epoch[2];  /* barriers run per phase (before / after the fold) */
+  void *mapped[2 * EMAC_MAX_RANKS];
+  int nmapped;
 } emac_handle;
 
 static emac_handle *handles[MAX_HANDLES];
@@ -98,6 +126,8 @@ static int new_handle_slot(void) {
     if (!handles[i]) return i;
   return -1;
 }
+
+static void ipc_unmap(emac_comm *cm, void *base);
 
 static void release(emac_handle *h) {
   int r;
@@ -116,6 +146,7 @@ static void release(emac_handle *h) {
     if (h->send_reg[r]) emac_gpu_host_unregister(h->user_send[r]);
     if (h->recv_reg[r]) emac_gpu_host_unregister(h->user_recv[r]);
   }
+  for (r = 0; r < h->nmapped; r++) ipc_unmap(&comms[h->comm], h->mapped[r]);
   free(h->ops);
   emac_plan_free(&h->plan);
   free(h);
@@ -335,8 +366,206 @@ int ext_mpi_amd_comm_init_loopback(int size, int *comm_of_rank) {
   return 0;
 }
 
+/* ------------------------- peer-mapped form (IPC over xGMI), the reference's GPU path -------
+ * cuda_shmem.c:218-299 maps every node peer's device send/recv buffer with cudaIpc and
+ * cuda_core.cu:50-86 then loads the partners' chunks directly; ext_mpi_native_exec.c:21-84
+ * synchronises the ranks with flags in shared memory. Here: hipIpc (dmabuf) mappings, exchanged
+ * through the caller's allgather (the MPI layer passes PMPI_Allgather, as the reference does),
+ * and stream-ordered barrier kernels over a per-communicator block of uncached device flags
+ * (ipc.hip). Start = barrier -> fold of this rank's owner chunks over the peers' send buffers
+ * with the fan-out stored straight into every peer's receive buffer -> barrier. */
+
+static int ipc_agree(emac_comm *cm, int ok_local) {
+  int all[EMAC_MAX_RANKS], r;
+  if (cm->ag(cm->ag_ctx, &ok_local, all, (long)sizeof(int))) return EMAC_ERR_TRANSPORT;
+  for (r = 0; r < cm->size; r++)
+    if (!all[r]) return EMAC_ERR_TRANSPORT;
+  return 0;
+}
+
+static void *ipc_map_peer(emac_comm *cm, int peer, const unsigned char *handle) {
+  int i;
+  void *base;
+  for (i = 0; i < cm->nmaps; i++)
+    if (cm->maps[i].refs > 0 && cm->maps[i].peer == peer && !memcmp(cm->maps[i].handle, handle, EMAC_IPC_HANDLE_BYTES)) {
+      cm->maps[i].refs++;
+      return cm->maps[i].base;
+    }
+  if (emac_gpu_ipc_open(handle, &base)) return NULL;
+  for (i = 0; i < cm->nmaps && cm->maps[i].refs > 0; i++);
+  if (i == cm->nmaps) {
+    ipc_map *m = (ipc_map *)realloc(cm->maps, sizeof(ipc_map) * (size_t)(cm->nmaps + 1));
+    if (!m) {
+      emac_gpu_ipc_close(base);
+      return NULL;
+    }
+    cm->maps = m;
+    cm->nmaps++;
+  }
+  cm->maps[i].peer = peer;
+  memcpy(cm->maps[i].handle, handle, EMAC_IPC_HANDLE_BYTES);
+  cm->maps[i].base = base;
+  cm->maps[i].refs = 1;
+  return base;
+}
+
+static void ipc_unmap(emac_comm *cm, void *base) {
+  int i;
+  for (i = 0; i < cm->nmaps; i++)
+    if (cm->maps[i].refs > 0 && cm->maps[i].base == base) {
+      if (--cm->maps[i].refs == 0) emac_gpu_ipc_close(base);
+      return;
+    }
+}
+
+static void ipc_comm_release(emac_comm *cm) {
+  int r;
+  for (r = 0; r < cm->size; r++)
+    if (r != cm->rank && cm->peer_sync_base[r]) emac_gpu_ipc_close(cm->peer_sync_base[r]);
+  for (r = 0; r < cm->nmaps; r++)
+    if (cm->maps[r].refs > 0) emac_gpu_ipc_close(cm->maps[r].base);
+  free(cm->maps);
+  emac_gpu_free(cm->d_peer_sync);
+  emac_gpu_free(cm->sync);
+  emac_gpu_host_free(cm->err);
+  memset(cm, 0, sizeof(*cm));
+}
+
+typedef struct {
+  unsigned char handle[EMAC_IPC_HANDLE_BYTES];
+  long offset;
+  int status;
+} ipc_export;
+
+int ext_mpi_amd_comm_init_ipc(int rank, int size, ext_mpi_amd_allgather_fn allgather, void *ctx, int device,
+                              int *comm) {
+  emac_comm *cm;
+  ipc_export mine, *all = NULL;
+  const char *tmo;
+  int i, r, rc;
+  if (!comm || !allgather || size < 1 || size > EMAC_MAX_RANKS || rank < 0 || rank >= size) return EMAC_ERR_ARG;
+  *comm = -1;
+  for (i = 0; i < MAX_COMMS && comms[i].used; i++);
+  if (i == MAX_COMMS) return EMAC_ERR_MALLOC;
+  cm = &comms[i];
+  memset(cm, 0, sizeof(*cm));
+  cm->rank = rank;
+  cm->size = size;
+  cm->loop_group = -1;
+  cm->ipc = 1;
+  cm->ag = allgather;
+  cm->ag_ctx = ctx;
+  /* every rank takes part in every allgather below, whatever failed locally, so that all ranks
+     reach the same verdict */
+  memset(&mine, 0, sizeof(mine));
+  rc = emac_gpu_device_count() > 0 ? 0 : EMAC_ERR_DEVICE;
+  if (!rc && device >= 0) rc = emac_gpu_set_device(device);
+  if (!rc) rc = emac_gpu_get_device(&cm->device);
+  if (!rc) rc = emac_gpu_malloc_uncached(&cm->sync, sizeof(emac_sync));
+  if (!rc) rc = emac_gpu_host_alloc_mapped((void **)&cm->err, sizeof(int));
+  if (!rc) rc = emac_gpu_xcc_census(&cm->xcc_mask);
+  if (!rc) rc = emac_gpu_ipc_export(cm->sync, mine.handle, &mine.offset);
+  mine.status = rc == 0;
+  all = (ipc_export *)calloc((size_t)size, sizeof(ipc_export));
+  if (!all) return EMAC_ERR_MALLOC;
+  if (allgather(ctx, &mine, all, (long)sizeof(ipc_export))) {
+    rc = EMAC_ERR_TRANSPORT;
+  } else {
+    for (r = 0; r < size; r++)
+      if (!all[r].status) rc = rc ? rc : EMAC_ERR_TRANSPORT;
+  }
+  for (r = 0; !rc && r < size; r++) {
+    if (r == rank) {
+      cm->peer_sync[r] = cm->sync;
+    } else {
+      rc = emac_gpu_ipc_open(all[r].handle, &cm->peer_sync_base[r]);
+      if (!rc) cm->peer_sync[r] = (char *)cm->peer_sync_base[r] + all[r].offset;
+    }
+  }
+  free(all);
+  if (!rc && (rc = emac_gpu_malloc((void **)&cm->d_peer_sync, sizeof(void *) * (size_t)size)) == 0)
+    rc = emac_gpu_memcpy(cm->d_peer_sync, cm->peer_sync, sizeof(void *) * (size_t)size);
+  {
+    const int agreed = ipc_agree(cm, rc == 0); /* every rank mapped every block */
+    if (!rc) rc = agreed;
+  }
+  if (rc) {
+    ipc_comm_release(cm);
+    return rc;
+  }
+  /* a rank that never arrives is reported after this many seconds (default 30) */
+  tmo = getenv("EXT_MPI_AMD_BARRIER_TIMEOUT");
+  cm->timeout_ticks = (long)((tmo ? atof(tmo) : 30.0) * (double)emac_gpu_wallclock_hz());
+  cm->used = 1;
+  *comm = i;
+  return 0;
+}
+
+/* Collective: every rank runs the same two exchanges (exports, then the verdict) whatever
+   failed locally before (`rc`), so that a local failure cannot unmatch the sequence. */
+static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf, void *recvbuf, int rc) {
+  ipc_export mine[2], all[2 * EMAC_MAX_RANKS];
+  void *psend[EMAC_MAX_RANKS], *precv[EMAC_MAX_RANKS];
+  emac_bucket *b = NULL;
+  int R = cm->size, r, t, pc, nb = 0, c, agreed;
+  const int empty = h->bytes == 0; /* same count on every rank: nothing to map or fold */
+  memset(mine, 0, sizeof(mine));
+  if (!rc && !empty) rc = map_buffers(h, 0, sendbuf, recvbuf);
+  if (!rc && !empty) rc = emac_gpu_ipc_export(h->dsend[0], mine[0].handle, &mine[0].offset);
+  if (!rc && !empty) rc = emac_gpu_ipc_export(h->drecv[0], mine[1].handle, &mine[1].offset);
+  if (!rc && cm->next_slot >= EMAC_SYNC_SLOTS) rc = EMAC_ERR_MALLOC;
+  mine[0].status = rc == 0;
+  if (cm->ag(cm->ag_ctx, mine, all, (long)sizeof(mine))) return EMAC_ERR_TRANSPORT;
+  for (r = 0; r < R; r++)
+    if (!all[2 * r].status && !rc) rc = EMAC_ERR_TRANSPORT;
+  for (r = 0; !rc && !empty && r < R; r++) {
+    if (r == cm->rank) {
+      psend[r] = h->dsend[0];
+      precv[r] = h->drecv[0];
+      continue;
+    }
+    for (t = 0; t < 2 && !rc; t++) {
+      void *base = ipc_map_peer(cm, r, all[2 * r + t].handle);
+      if (!base) {
+        rc = EMAC_ERR_TRANSPORT;
+        break;
+      }
+      h->mapped[h->nmapped++] = base;
+      (t ? precv : psend)[r] = (char *)base + all[2 * r + t].offset;
+    }
+  }
+  /* every rank opened every mapping before anyone proceeds */
+  agreed = ipc_agree(cm, rc == 0);
+  if (rc || agreed) return rc ? rc : agreed;
+  h->slot = cm->next_slot++;
+  /* this rank's owner chunks: leaves from the peers' send buffers in the plan's fold order,
+     results into every rank's receive buffer (the fused reduce_copyout push) */
+  c = h->me_pos;
+  b = (emac_bucket *)calloc((size_t)h->plan.npieces, sizeof(emac_bucket));
+  if (!b) return EMAC_ERR_MALLOC;
+  for (pc = 0; pc < h->plan.npieces; pc++) {
+    long off = h->plan.chunk_off[(size_t)pc * R + c], len = h->plan.chunk_len[(size_t)pc * R + c];
+    emac_bucket *bk = &b[nb];
+    if (len <= 0) continue;
+    for (t = 0; t < R; t++) bk->src[t] = psend[h->plan.leaf_rank[c][t]];
+    for (r = 0; r < R; r++) bk->dst[r] = precv[r];
+    bk->ndst = R;
+    place_bucket(bk, R, off, len, h->plan.tsize);
+    nb++;
+  }
+  h->nsrc = R;
+  h->fan = R > 1;
+  rc = upload_buckets(h, b, nb);
+  free(b);
+  return rc;
+}
+
 int ext_mpi_amd_comm_free(int comm) {
   if (comm < 0 || comm >= MAX_COMMS || !comms[comm].used) return EMAC_ERR_ARG;
+  if (comms[comm].ipc) {
+    ipc_comm_release(&comms[comm]);
+    return 0;
+  }
   if (comms[comm].loop_group >= 0) {
     loop_group *g = &loops[comms[comm].loop_group];
     g->nh[comms[comm].rank] = -1; /* this rank left */
@@ -367,15 +596,24 @@ int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, i
   if (emac_gpu_set_device(cm->device)) return EMAC_ERR_DEVICE;
   h = (emac_handle *)calloc(1, sizeof(emac_handle));
   if (!h) return EMAC_ERR_MALLOC;
-  h->kind = KIND_COMM;
+  h->kind = cm->ipc ? KIND_IPC : KIND_COMM;
   h->comm = comm;
   h->device = cm->device;
-  if ((rc = emac_plan_build(&h->plan, R, count, dtype, op, &cfg))) goto fail;
-  h->me = cm->rank;
-  h->me_pos = h->plan.rank_pos[h->me];
-  h->bytes = (size_t)count * (size_t)h->plan.tsize;
+  rc = emac_plan_build(&h->plan, R, count, dtype, op, &cfg);
+  if (!rc) {
+    h->me = cm->rank;
+    h->me_pos = h->plan.rank_pos[h->me];
+    h->bytes = (size_t)count * (size_t)h->plan.tsize;
+  }
   h->nbuf = 1;
   h->nsrc = R;
+  if (cm->ipc) {
+    if ((rc = ipc_allreduce_init(h, cm, sendbuf, recvbuf, rc))) goto fail;
+    if ((rc = emac_gpu_stream_create(&h->stream))) goto fail;
+    if ((rc = finish_init(h, handle))) goto fail;
+    return 0;
+  }
+  if (rc) goto fail;
   if ((rc = map_buffers(h, 0, sendbuf, recvbuf))) goto fail;
   {
     emac_fold *folds = NULL;
@@ -503,6 +741,20 @@ static emac_handle *get(int handle) {
   return handles[handle];
 }
 
+/* IPC form: node barrier `phase` (0 before the fold: every rank's send buffer is ready and its
+   receive buffer free; 1 after it: every fan-out store has landed) on the handle's stream */
+static int ipc_barrier(emac_handle *h, int phase) {
+  emac_comm *cm = &comms[h->comm];
+  return emac_gpu_node_barrier(cm->sync, (void *const *)cm->d_peer_sync, h->slot, phase, ++h->epoch[phase], cm->size,
+                               cm->rank, cm->xcc_mask, cm->err, cm->timeout_ticks, h->stream);
+}
+
+/* barrier errors are reported through the communicator's pinned word (timeout: 1, XCC coverage: 2) */
+static int ipc_status(const emac_handle *h) {
+  if (h->kind != KIND_IPC) return 0;
+  return *(volatile int *)comms[h->comm].err ? EMAC_ERR_TRANSPORT : 0;
+}
+
 int ext_mpi_amd_start_legs(int handle, int legs) {
   emac_handle *h = get(handle);
   int rc, multi;
@@ -510,12 +762,17 @@ int ext_mpi_amd_start_legs(int handle, int legs) {
   multi = h->kind == KIND_COMM && h->plan.nranks > 1;
   if (emac_gpu_set_device(h->device)) return EMAC_ERR_DEVICE;
   if ((legs & EXT_MPI_AMD_LEG_STAGE_IN) && (rc = stage_in(h))) return rc;
+  if ((legs & EXT_MPI_AMD_LEG_REDUCE_SCATTER) && h->kind == KIND_IPC && h->plan.nranks > 1 &&
+      (rc = ipc_barrier(h, 0)))
+    return rc;
   if ((legs & EXT_MPI_AMD_LEG_REDUCE_SCATTER) && multi && (rc = run_leg(h, EMAC_LEG_RS))) return rc;
   if ((legs & EXT_MPI_AMD_LEG_FOLD) &&
       (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, h->fan, h->unroll, &h->plan.codes, h->d_buckets, h->nb, h->ntiles,
                           h->tiles_per_bucket, h->all_full, h->d_edges, h->nedges, h->stream)))
     return rc;
   if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && multi && (rc = run_leg(h, EMAC_LEG_AG))) return rc;
+  if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && h->kind == KIND_IPC && h->plan.nranks > 1 && (rc = ipc_barrier(h, 1)))
+    return rc;
   if ((legs & EXT_MPI_AMD_LEG_STAGE_OUT) && (rc = stage_out(h))) return rc;
   h->started = 1;
   return 0;
@@ -539,7 +796,10 @@ int ext_mpi_amd_test(int handle) {
   if (!h) return EMAC_ERR_ARG;
   if (!h->started) return 1;
   rc = emac_gpu_stream_query(h->stream);
-  if (rc == 1) h->started = 0;
+  if (rc == 1) {
+    h->started = 0;
+    if (ipc_status(h)) return EMAC_ERR_TRANSPORT;
+  }
   return rc;
 }
 
@@ -549,7 +809,7 @@ int ext_mpi_amd_wait(int handle) {
   if (!h) return EMAC_ERR_ARG;
   rc = emac_gpu_stream_sync(h->stream);
   h->started = 0;
-  return rc;
+  return rc ? rc : ipc_status(h);
 }
 
 int ext_mpi_amd_done(int handle) {

@@ -59,6 +59,31 @@ int emac_gpu_stream_sync(void *stream);
 int emac_gpu_stream_query(void *stream); /* 1 idle, 0 busy, <0 error */
 int emac_gpu_device_sync(void);
 
+/* ---- peer-mapped (IPC) form, ipc.hip ----
+   Per-communicator synchronisation block, in uncached device memory and mapped by every peer:
+   flags[slot][phase][q] = last epoch rank q signalled to this rank for that handle slot and
+   barrier phase (0: before the fold, 1: after it); arrive / xcc are this rank's own barrier
+   bookkeeping (workgroup arrivals, XCC coverage by epoch parity). */
+#define EMAC_SYNC_SLOTS 1024
+#define EMAC_SYNC_WG 64 /* barrier workgroups: enough to land on every XCD */
+#define EMAC_IPC_HANDLE_BYTES 64
+typedef struct {
+  unsigned long flags[EMAC_SYNC_SLOTS][2][EMAC_MAX_RANKS];
+  unsigned long arrive[EMAC_SYNC_SLOTS][2];
+  unsigned int xcc[EMAC_SYNC_SLOTS][2][2];
+} emac_sync;
+
+int emac_gpu_ipc_export(const void *p, void *handle, long *offset); /* handle of p's allocation + offset */
+int emac_gpu_ipc_open(const void *handle, void **base);
+int emac_gpu_ipc_close(void *base);
+int emac_gpu_malloc_uncached(void **p, size_t bytes); /* zeroed */
+int emac_gpu_host_alloc_mapped(void **p, size_t bytes); /* pinned, device-visible, zeroed */
+int emac_gpu_host_free(void *p);
+int emac_gpu_xcc_census(unsigned *mask); /* XCCs a wide launch lands on */
+long emac_gpu_wallclock_hz(void);
+int emac_gpu_node_barrier(void *self, void *const *d_peers, int slot, int phase, unsigned long epoch, int nranks,
+                          int me, unsigned xcc_expect, int *err, long timeout_ticks, void *stream);
+
 /* Unroll (16-byte vectors per lane per leaf) of a launch: a tile covers EMAC_BLOCK * unroll
    vectors. fan: the fan-out width equals nsrc (node form) instead of 1. */
 int emac_gpu_pick_unroll(int nsrc, int tree, int fan, long total_vectors);

@@ -1,0 +1,168 @@
+// ipc.hip -- peer-mapped execution form (one rank per GPU, buffers shared over xGMI) for gfx950.
+//
+// The reference's GPU path maps every node peer's device send/recv buffer into each process
+// with CUDA IPC (src/gpu/cuda_shmem.c:218-299) and its copy-reduce kernel then loads the
+// partners' chunks directly (src/gpu/cuda_core.cu:50-86); ranks synchronise through flags in
+// shared memory spun on by the CPU (src/mpi/ext_mpi_native_exec.c:21-84,513-528) around a
+// cudaDeviceSynchronize before every barrier. Here the same mapping is made with hipIpc
+// (dmabuf) and the node barrier is a small stream-ordered kernel, so a whole Allreduce is three
+// launches on the rank's own stream and never returns to the host:
+//
+//   node_barrier(in)  -> fold over peer-mapped leaves, fan-out into every peer's recv -> node_barrier(out)
+//
+// Visibility across GPUs: every XCD of a gfx950 has its own L2, and the L2 is neither written
+// back nor invalidated for other agents by plain stores/loads. A barrier workgroup therefore
+// runs a system-scope release (L2 write-back of its XCD) before it arrives and a system-scope
+// acquire (L2 invalidate) after the wait, and the barrier is launched wide enough to cover
+// every XCD: the workgroups OR their XCC id into a mask, and the rank's last arriver checks the
+// mask against the census taken at communicator set-up before it signals the peers (a missed
+// XCD is reported as a transport error instead of silently risking stale lines). Flags live in
+// uncached device memory and are written with system-scope atomics: one 8-byte word per
+// (handle slot, phase, peer), holding the last epoch that peer signalled. Every wait is bounded
+// by a wall-clock timeout that sets an error word in pinned host memory and lets the kernel end.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "gpu.h"
+
+namespace {
+
+inline int ok(hipError_t e) { return e == hipSuccess ? 0 : EMAC_ERR_DEVICE; }
+
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
+  return v;
+}
+
+__global__ void xcc_census_kernel(unsigned *mask) {
+  if (threadIdx.x == 0) atomicOr(mask, 1u << xcc_id());
+}
+
+// One lane per workgroup does the protocol; the workgroup count is EMAC_SYNC_WG.
+__global__ __launch_bounds__(64) void node_barrier_kernel(emac_sync *self, emac_sync *const *peers, int slot,
+                                                          int phase, unsigned long epoch, int nranks, int me,
+                                                          unsigned xcc_expect, int *err, long timeout) {
+  if (threadIdx.x != 0) return;
+  // release: every store this GPU made before the barrier (the fold's fan-out into the peers'
+  // receive buffers, the application's writes into the send buffer) leaves this XCD's L2
+  __threadfence_system();
+  atomicOr(&self->xcc[slot][phase][epoch & 1], 1u << xcc_id());
+  const unsigned long arrived =
+      __hip_atomic_fetch_add(&self->arrive[slot][phase], 1ul, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (arrived == epoch * gridDim.x - 1) {  // last workgroup of this rank: every XCD has released
+    const unsigned seen = __hip_atomic_load(&self->xcc[slot][phase][epoch & 1], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+    if ((seen & xcc_expect) != xcc_expect) __hip_atomic_fetch_or(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // next epoch's mask (the barrier of a slot and phase runs on one stream: no overlap)
+    __hip_atomic_store(&self->xcc[slot][phase][(epoch + 1) & 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence_system();
+    for (int q = 0; q < nranks; ++q)
+      if (q != me)
+        __hip_atomic_store(&peers[q]->flags[slot][phase][me], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  const long t0 = wall_clock64();
+  for (int q = 0; q < nranks; ++q) {
+    if (q == me) continue;
+    while (__hip_atomic_load(&self->flags[slot][phase][q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+      __builtin_amdgcn_s_sleep(4);
+      if (wall_clock64() - t0 > timeout) {
+        __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+      }
+    }
+  }
+  // acquire: lines of this XCD's L2 that the peers have since rewritten (their fan-out into
+  // this rank's receive buffer, their send buffers) are dropped
+  __threadfence_system();
+}
+
+}  // namespace
+
+extern "C" {
+
+int emac_gpu_ipc_export(const void *p, void *handle, long *offset) {
+  void *base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, const_cast<void *>(p)) != hipSuccess) {
+    (void)hipGetLastError();
+    return EMAC_ERR_ARG;
+  }
+  hipIpcMemHandle_t h;
+  if (hipIpcGetMemHandle(&h, base) != hipSuccess) {
+    (void)hipGetLastError();
+    return EMAC_ERR_TRANSPORT;
+  }
+  memcpy(handle, &h, sizeof(h));
+  *offset = (long)((const char *)p - (const char *)base);
+  return 0;
+}
+
+int emac_gpu_ipc_open(const void *handle, void **base) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  if (hipIpcOpenMemHandle(base, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+    (void)hipGetLastError();
+    *base = nullptr;
+    return EMAC_ERR_TRANSPORT;
+  }
+  return 0;
+}
+
+int emac_gpu_ipc_close(void *base) { return base ? ok(hipIpcCloseMemHandle(base)) : 0; }
+
+int emac_gpu_malloc_uncached(void **p, size_t bytes) {
+  *p = nullptr;
+  if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached) != hipSuccess) {
+    (void)hipGetLastError();
+    return EMAC_ERR_MALLOC;
+  }
+  if (hipMemset(*p, 0, bytes) != hipSuccess) return EMAC_ERR_DEVICE;
+  return 0;
+}
+
+int emac_gpu_host_alloc_mapped(void **p, size_t bytes) {
+  *p = nullptr;
+  if (hipHostMalloc(p, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    (void)hipGetLastError();
+    return EMAC_ERR_MALLOC;
+  }
+  memset(*p, 0, bytes);
+  return 0;
+}
+
+int emac_gpu_host_free(void *p) { return p ? ok(hipHostFree(p)) : 0; }
+
+int emac_gpu_xcc_census(unsigned *mask) {
+  unsigned *d = nullptr;
+  int rc;
+  *mask = 0;
+  if (hipMalloc(&d, sizeof(unsigned)) != hipSuccess) return EMAC_ERR_MALLOC;
+  rc = ok(hipMemset(d, 0, sizeof(unsigned)));
+  if (!rc) {
+    hipLaunchKernelGGL(xcc_census_kernel, dim3(4096), dim3(64), 0, 0, d);
+    rc = ok(hipGetLastError());
+  }
+  if (!rc) rc = ok(hipMemcpy(mask, d, sizeof(unsigned), hipMemcpyDeviceToHost));
+  (void)hipFree(d);
+  return rc;
+}
+
+long emac_gpu_wallclock_hz(void) {
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+    return 100000000L;  // gfx9 s_memrealtime runs at 100 MHz
+  return (long)khz * 1000L;
+}
+
+int emac_gpu_node_barrier(void *self, void *const *d_peers, int slot, int phase, unsigned long epoch, int nranks,
+                          int me, unsigned xcc_expect, int *err, long timeout_ticks, void *stream) {
+  hipLaunchKernelGGL(node_barrier_kernel, dim3(EMAC_SYNC_WG), dim3(64), 0, static_cast<hipStream_t>(stream),
+                     static_cast<emac_sync *>(self), reinterpret_cast<emac_sync *const *>(d_peers), slot, phase, epoch,
+                     nranks, me, xcc_expect, err, timeout_ticks);
+  return ok(hipGetLastError());
+}
+
+}  // extern "C"

@@ -78,6 +78,16 @@ int ext_mpi_amd_comm_free(int comm);
  * device; point-to-point ops become device copies executed by the receiving rank. Run each leg
  * on every rank before the next one (ext_mpi_amd_start_legs). Not for production. */
 int ext_mpi_amd_comm_init_loopback(int size, int *comm_of_rank);
+/* Peer-mapped communicator: one rank per GPU, every rank's device send/recv buffers mapped into
+ * every other rank with hipIpc (the reference's src/gpu/cuda_shmem.c:218-299 cudaIpc mapping),
+ * the fold reading the peers' chunks over xGMI and storing the result into every peer's receive
+ * buffer, node barriers as stream-ordered kernels. `allgather` is called collectively (same
+ * order on every rank) at communicator and handle set-up only: it must gather `bytes` bytes from
+ * every rank into `recv` in rank order (as PMPI_Allgather(send, bytes, MPI_BYTE, recv, bytes,
+ * MPI_BYTE, comm)) and return 0; it must stay callable while the communicator lives. */
+typedef int (*ext_mpi_amd_allgather_fn)(void *ctx, const void *send, void *recv, long bytes);
+int ext_mpi_amd_comm_init_ipc(int rank, int size, ext_mpi_amd_allgather_fn allgather, void *ctx, int device,
+                              int *comm);
 int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, int dtype, int op, int comm,
                                const char *copyin, int *handle);
 

@@ -1,0 +1,95 @@
+"""One rank of the peer-mapped (IPC) form, run as its own process by test_gpu_ipc.py.
+
+Every rank runs the same cases in the same order; for each it regenerates every rank's input
+(seeded per rank), checks its own receive buffer bit for bit against the CPU oracle and prints
+one line per case. Several ranks may share one GPU: the hipIpc mappings, the barrier kernels and
+the fan-out stores are then the same code the 8-GPU node runs, over the one device's memory.
+Exit status 0 iff every case matched.
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import ext_mpi_collectives_amd as emac  # noqa: E402
+from helpers import xorshift_inputs  # noqa: E402
+from oracle import oracle  # noqa: E402
+
+TORCH = {emac.FLOAT: torch.float32, emac.DOUBLE: torch.float64, emac.INT: torch.int32, emac.LONG: torch.int64}
+
+
+def cases(R):
+    full = f"6;1 -{R} {R}"
+    out = [(emac.FLOAT, 40961, full, False, False, 3), (emac.DOUBLE, 1000003, full, False, False, 2),
+           (emac.INT, 65536 * R + 5, full, False, False, 1), (emac.LONG, 777, full, False, False, 1),
+           (emac.FLOAT, 1, full, False, False, 1), (emac.FLOAT, 0, full, False, False, 1),
+           (emac.FLOAT, 100000, full, True, False, 2), (emac.DOUBLE, 33333, full, False, True, 2),
+           (emac.FLOAT, 5000, f"6;-64 -{R} {R}", False, False, 1), (emac.FLOAT, 70001, f"6;3 -{R} {R}", False, False, 1)]
+    if R == 4:
+        out += [(emac.FLOAT, 123457, "6;1 -2 -2 2 2", False, False, 2), (emac.DOUBLE, 54321, "6;1 -2 2 1 2 1 -2 2", False, False, 1)]
+    return out
+
+
+def main():
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dev = int(os.environ.get("IPC_DEVICE", "0"))
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo")
+    comm = emac.comm_init_ipc(rank, world, emac.torch_allgather(), dev)
+    failures = 0
+    for k, (code, count, copyin, in_place, host, repeats) in enumerate(cases(world)):
+        sends = xorshift_inputs(world, count, code, seed_base=0x1C0000 + 97 * k)
+        want = oracle.allreduce(sends, copyin, in_place=in_place)[rank]
+        if host:
+            hsend = sends[rank].copy()
+            hrecv = np.full_like(hsend, -1)
+            h = emac.allreduce_init(hsend.ctypes.data, hrecv.ctypes.data, count, code, comm, copyin)
+        else:
+            send = torch.from_numpy(sends[rank].copy()).cuda()
+            recv = send if in_place else torch.full((count,), -1, dtype=TORCH[code], device="cuda")
+            h = emac.allreduce_init(send.data_ptr(), recv.data_ptr(), count, code, comm, copyin)
+        ok = True
+        for _ in range(repeats):
+            if in_place:
+                send.copy_(torch.from_numpy(sends[rank]))
+            torch.cuda.synchronize()
+            emac.start(h)
+            emac.wait(h)
+            got = hrecv if host else recv.cpu().numpy()
+            ok &= bool(np.array_equal(got.view(np.uint8), want.view(np.uint8)))
+        emac.done(h)
+        failures += not ok
+        print(f"IPC rank {rank}/{world} case {k} code {code} count {count} '{copyin}' in_place={in_place} "
+              f"host={host} x{repeats}: {'ok' if ok else 'MISMATCH'}", flush=True)
+    # several handles in flight on separate streams, started in the same order on every rank
+    hs, bufs = [], []
+    for j in range(3):
+        s = torch.full((4099,), float(rank + 1 + j), device="cuda")
+        r = torch.empty_like(s)
+        bufs.append((s, r))
+        hs.append(emac.allreduce_init(s.data_ptr(), r.data_ptr(), 4099, emac.FLOAT, comm))
+    for _ in range(5):
+        for h in hs:
+            emac.start(h)
+    for h in hs:
+        emac.wait(h)
+    tri = world * (world + 1) / 2
+    ok = all(bool(torch.all(r == tri + world * j).item()) for j, (_, r) in enumerate(bufs))
+    for h in hs:
+        emac.done(h)
+    failures += not ok
+    print(f"IPC rank {rank}/{world} concurrent handles: {'ok' if ok else 'MISMATCH'}", flush=True)
+    emac.comm_free(comm)
+    dist.barrier()
+    dist.destroy_process_group()
+    sys.exit(1 if failures else 0)
+
+
+if __name__ == "__main__":
+    main()
