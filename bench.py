@@ -8,8 +8,11 @@ EXT_MPI_COPYIN '6;1 -R R' (copy-in method 6), device-resident synthetic buffers.
          (the reference's XPMEM / IPC-mapped node, ext_mpi_xpmem.c:68-133), one fused
          copy-in + copy-out fold launch per step. Buffer sets are rotated so the working set
          between re-uses (1 GiB) exceeds the 256 MiB Infinity Cache.
-  N > 1  (torchrun, one rank per GPU): each GPU holds one rank's 16 MiB; reduce-scatter and
-         allgather legs over RCCL/xGMI, the fold on the owner GPU.
+  N > 1  (torchrun, one rank per GPU): each GPU holds one rank's 16 MiB. Default transport: the
+         peer-mapped form (hipIpc over xGMI, the reference's cudaIpc design): barrier kernel, fold
+         of the owned chunk reading the peers' send buffers, fan-out stored into every peer's
+         receive buffer, barrier kernel. --transport rccl: reduce-scatter and allgather legs as
+         RCCL point-to-point rounds; the other transport is also timed as an extra.
 
 A step is one full Allreduce. value = bytes folded by all ranks (R x 16 MiB per step at N = 1,
 N x 16 MiB at N > 1) / wall time of K steps (max over ranks), inputs already in HBM.
@@ -51,6 +54,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the 256 MiB and host-buffer points")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU baseline sample")
+    ap.add_argument("--transport", default="ipc", choices=["ipc", "rccl"],
+                    help="N > 1: peer-mapped hipIpc form (default) or RCCL point-to-point legs")
     ap.add_argument("--alloc", default="hip", choices=["hip", "torch"],
                     help="device buffers from hipMalloc (library device ABI, like the reference's "
                          "tests/benchmark_gpu.c cudaMalloc) or torch's caching allocator")
@@ -414,6 +419,56 @@ def single_gpu(args):
     print(json.dumps(out), flush=True)
 
 
+def _comm_run(emac, comm, count, tdtype, code, dname, copyin, steps, warmup, rank, world, dist, torch, check=True):
+    """Persistent Allreduce of `count` elements per rank on communicator `comm`; returns the max-over-ranks
+    wall time of `steps` Starts (one stream), the handle's fold time alone, and the check."""
+    tsize = torch.empty((), dtype=tdtype).element_size()
+    np_dtype = {torch.float32: np.float32, torch.float64: np.float64, torch.int32: np.int32,
+                torch.int64: np.int64}[tdtype]
+    send, recv = DevBuf(max(1, count * tsize)), DevBuf(max(1, count * tsize))
+    mine = host_random(count, np_dtype, 0x5EED0000 + rank)
+    send.upload(mine)
+    h = emac.allreduce_init(send.data_ptr(), recv.data_ptr(), count, code, comm, copyin)
+    stream = torch.cuda.Stream()
+    emac.set_stream(h, stream.cuda_stream)
+    for _ in range(warmup):
+        emac.start(h)
+    emac.wait(h)
+    checked = True
+    if check:
+        got = np.empty(count, np_dtype)
+        recv.download(got)
+        idx = np.arange(0, count, max(1, count // (1 << 20)))  # <= 1 Mi samples spread over every chunk
+        allin = [None] * world
+        dist.all_gather_object(allin, mine[idx])
+        got = got[idx]
+        ref = np.sum(np.stack([a.astype(np.float64) for a in allin]), axis=0)
+        tol = 1e-5 * world if np.dtype(np_dtype).kind == "f" else 0.0
+        ok = torch.tensor([int(np.allclose(got.astype(np.float64), ref, rtol=0, atol=tol))])
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        checked = bool(ok.item())
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        emac.start(h)
+    emac.wait(h)
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    return h, send, recv, stream, el.item(), checked
+
+
+def _fold_only(emac, h, stream, steps, torch):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        emac.start_legs(h, emac.LEG_FOLD)
+    e1.record(stream)
+    stream.synchronize()
+    return e0.elapsed_time(e1) * 1e-3 / steps
+
+
 def multi_gpu(args):
     import torch
     import torch.distributed as dist
@@ -423,121 +478,107 @@ def multi_gpu(args):
     import signal
     signal.signal(signal.SIGALRM, lambda *_: (log(f"rank {rank}: watchdog expired"), os._exit(3)))
     signal.alarm(900)  # a rank stuck in a collective must not hang the job
-    torch.cuda.set_device(local)
+    ndev = torch.cuda.device_count()
+    dev = local % ndev  # one rank per GPU; ranks share a GPU only when there are fewer GPUs (rehearsal)
+    torch.cuda.set_device(dev)
     dist.init_process_group("gloo")
     tdtype, code, dname, tsize = dtype_info(args.dtype)
     count = int(args.size_mib * MIB) // tsize
     S = count * tsize
     copyin = args.copyin or f"6;1 -{world} {world}"
-    uid = [emac.get_unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(uid, src=0)
-    comm = emac.comm_init(rank, world, uid[0], local)
-    send = torch.empty(count, dtype=tdtype, device="cuda")
-    recv = torch.empty(count, dtype=tdtype, device="cuda")
-    fill(send, 0x5EED0000 + rank)
-    h = emac.allreduce_init(send.data_ptr(), recv.data_ptr(), count, code, comm, copyin)
-    stream = torch.cuda.Stream()
-    emac.set_stream(h, stream.cuda_stream)
-    for _ in range(args.warmup):
-        emac.start(h)
-    stream.synchronize()
-    # sanity against torch's own sum of the gathered inputs (parity proper: tests/)
-    allin = [torch.empty_like(send).cpu() for _ in range(world)]
-    dist.all_gather(allin, send.cpu())
-    ref = torch.stack([t.double() for t in allin]).sum(0).to("cuda")
-    checked = torch.tensor([int(torch.allclose(recv.double(), ref, rtol=0, atol=1e-5 * world))])
-    dist.all_reduce(checked, op=dist.ReduceOp.MIN)
+
+    def make_comm(transport):
+        if transport == "ipc":
+            return emac.comm_init_ipc(rank, world, emac.torch_allgather(), dev)
+        uid = [emac.get_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        return emac.comm_init(rank, world, uid[0], dev)
+
+    comm = make_comm(args.transport)
+    h, send, recv, stream, wall, checked = _comm_run(emac, comm, count, tdtype, code, dname, copyin, args.steps,
+                                                     args.warmup, rank, world, dist, torch)
+    # the fold leg alone on every GPU at once, then on rank 0's GPU while the others idle
     dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        emac.start(h)
-    stream.synchronize()
-    dist.barrier()
-    t1 = time.perf_counter()
-    el = torch.tensor([t1 - t0], dtype=torch.float64)
-    dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    # the fold kernel alone, on each GPU, inside the N-GPU job (staging holds real slices)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    dist.barrier()
-    e0.record(stream)
-    for _ in range(args.steps):
-        emac.start_legs(h, emac.LEG_FOLD)
-    e1.record(stream)
-    stream.synchronize()
-    fold_s = torch.tensor([e0.elapsed_time(e1) * 1e-3 / args.steps], dtype=torch.float64)
+    fold_s = torch.tensor([_fold_only(emac, h, stream, args.steps, torch)], dtype=torch.float64)
     dist.all_reduce(fold_s, op=dist.ReduceOp.MAX)
-    # the same fold on rank 0's GPU while every other GPU idles: the 1-GPU reference at equal C
     dist.barrier()
     alone_s = torch.zeros(1, dtype=torch.float64)
     if rank == 0:
-        e0.record(stream)
-        for _ in range(args.steps):
-            emac.start_legs(h, emac.LEG_FOLD)
-        e1.record(stream)
-        stream.synchronize()
-        alone_s[0] = e0.elapsed_time(e1) * 1e-3 / args.steps
+        alone_s[0] = _fold_only(emac, h, stream, args.steps, torch)
     dist.barrier()
+    dist.broadcast(alone_s, src=0)
     emac.done(h)
+    send.free()
+    recv.free()
+    extras = {"transport": args.transport, "gpus_visible": ndev}
     # BASELINE configs[3] (double, 256 MiB per rank) and a configs[4]-style size sweep, bounded
-    extra_points = []
-    points = [(args.dtype, n) for n in (8, 64 << 10, 1 << 20, 64 << 20, 256 << 20)] + [("double", 256 << 20)]
+    points = [(args.dtype, n) for n in (8, 64 << 10, 1 << 20, 16 << 20, 64 << 20, 256 << 20)] + [("double", 256 << 20)]
+    sweep = []
     for dname_p, nbytes in points:
         tdt, cde, _, tsz = dtype_info(dname_p)
         cnt = max(1, nbytes // tsz)
+        st = 100 if nbytes <= (1 << 20) else 10
         try:
-            sb = torch.empty(cnt, dtype=tdt, device="cuda")
-            rb = torch.empty(cnt, dtype=tdt, device="cuda")
-            fill(sb, 0x5EED0000 + rank)
-            hp = emac.allreduce_init(sb.data_ptr(), rb.data_ptr(), cnt, cde, comm, copyin)
-            emac.set_stream(hp, stream.cuda_stream)
-            st = 50 if nbytes <= (1 << 20) else 10
-            for _ in range(3):
-                emac.start(hp)
-            stream.synchronize()
-            dist.barrier()
-            t0 = time.perf_counter()
-            for _ in range(st):
-                emac.start(hp)
-            stream.synchronize()
-            dist.barrier()
-            el_p = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-            dist.all_reduce(el_p, op=dist.ReduceOp.MAX)
+            hp, sb, rb, _, el_p, ok_p = _comm_run(emac, comm, cnt, tdt, cde, dname_p, copyin, st, 3, rank, world, dist,
+                                                  torch)
             emac.done(hp)
-            extra_points.append({"dtype": dname_p, "bytes_per_rank": cnt * tsz,
-                                 "us_per_allreduce": round(el_p.item() * 1e6 / st, 2),
-                                 "algbw_gbps": round(cnt * tsz * st / el_p.item() / 1e9, 2)})
-            del sb, rb
+            sb.free()
+            rb.free()
+            sweep.append({"dtype": dname_p, "bytes_per_rank": cnt * tsz, "us_per_allreduce": round(el_p * 1e6 / st, 2),
+                          "algbw_gbps": round(cnt * tsz * st / el_p / 1e9, 2), "checked": ok_p})
         except Exception as e:  # a failing extra point must not lose the headline line
-            extra_points.append({"dtype": dname_p, "bytes_per_rank": nbytes, "error": str(e)})
+            sweep.append({"dtype": dname_p, "bytes_per_rank": nbytes, "error": str(e)})
+    extras["sweep"] = sweep
     emac.comm_free(comm)
+    # the other transport on the same workload, for comparison (RCCL refuses ranks sharing a GPU)
+    other = "rccl" if args.transport == "ipc" else "ipc"
+    try:
+        c2 = make_comm(other)
+        h2, s2, r2, _, wall2, ok2 = _comm_run(emac, c2, count, tdtype, code, dname, copyin, args.steps, args.warmup,
+                                              rank, world, dist, torch)
+        emac.done(h2)
+        s2.free()
+        r2.free()
+        emac.comm_free(c2)
+        extras[f"{other}_transport"] = {"ms_per_step": round(wall2 * 1e3 / args.steps, 4),
+                                        "value": round(world * S * args.steps / wall2 / 1e9, 2), "checked": ok2}
+    except Exception as e:  # noqa: BLE001
+        extras[f"{other}_transport"] = {"error": str(e)}
     if rank == 0:
-        wall = el.item()
         kf = fold_s.item()
         chunk = S / world
-        algo = (world + 1) * chunk  # R leaf reads + 1 write of the owned chunk
+        if args.transport == "ipc":
+            algo = 2 * world * chunk  # R leaf reads (R-1 over xGMI) + R fan-out writes (R-1 over xGMI)
+            remote = 2 * (world - 1) * chunk
+        else:
+            algo = (world + 1) * chunk  # R leaf reads from staging + 1 write of the owned chunk
+            remote = 0
         achieved = algo / kf / 1e9
+        extras.update({
+            "fold_us_all_gpus": round(kf * 1e6, 2), "fold_us_rank0_alone": round(alone_s.item() * 1e6, 2),
+            "per_gpu_fold_rate_retained": round(alone_s.item() / kf, 3),
+            "fold_xgmi_gbps_per_gpu": round(remote / kf / 1e9, 1) if remote else None,
+            "end_to_end_algbw_gbps_per_gpu": round(S * args.steps / wall / 1e9, 2),
+            "xgmi_bound_us": round(2 * (world - 1) / world * S / (min(world - 1, 7) * 153e9) * 1e6, 1)})
+        form = ("peer-mapped (hipIpc over xGMI): barrier kernel, fold of the owned chunk over the peers' send "
+                "buffers with the fan-out stored into every peer's receive buffer, barrier kernel"
+                if args.transport == "ipc" else
+                "reduce-scatter + allgather legs over RCCL/xGMI, fold on the owner GPU")
         out = {
             "metric": "device-resident GB/s reduced (float32 MPI_SUM) per GPU; % HBM3E roofline",
             "value": round(world * S * args.steps / wall / 1e9, 2),
             "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(wall * 1e3 / args.steps, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": dname,
-            "data": "synthetic: uniform [-1,1) per rank (seeded), device-resident",
+            "data": "synthetic: uniform [-1,1) per rank (seeded), device-resident (hipMalloc)",
             "config": {"workload": f"persistent Allreduce {args.dtype} MPI_SUM, {S // MIB} MiB per rank, one rank per "
-                                   f"GPU, EXT_MPI_COPYIN '{copyin}': reduce-scatter + allgather legs over RCCL/xGMI, "
-                                   f"fold on the owner GPU",
+                                   f"GPU, EXT_MPI_COPYIN '{copyin}': {form}",
                        "ranks": world, "message_bytes_per_rank": S, "copyin": copyin, "layout": "rank-per-gpu",
-                       "checked_vs_fp64_sum": bool(checked.item())},
+                       "transport": args.transport, "checked_vs_fp64_sum": checked},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None, "kernel": "fold_kernel",
                          "algorithmic_bytes_per_launch": int(algo), "avg_launch_us": round(kf * 1e6, 2)},
-            "extras": {"fold_gbps_reduced_per_gpu": round(S / kf / 1e9, 1),
-                       "fold_alone_on_one_gpu_us": round(alone_s.item() * 1e6, 2),
-                       "per_gpu_fold_rate_retained": round(alone_s.item() / kf, 3),
-                       "end_to_end_algbw_gbps_per_gpu": round(S * args.steps / wall / 1e9, 2),
-                       "xgmi_bound_us": round(2 * (world - 1) / world * S / (min(world - 1, 7) * 153e9) * 1e6, 1),
-                       "sweep_comm_form": extra_points},
+            "extras": extras,
         }
         print(json.dumps(out), flush=True)
     dist.barrier()

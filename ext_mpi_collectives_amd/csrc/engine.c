@@ -64,7 +64,8 @@ typedef struct {
   int *err;                        /* pinned host word the barrier kernels report into */
   unsigned xcc_mask;
   long timeout_ticks;
-  int next_slot;
+  unsigned char slot_used[EMAC_SYNC_SLOTS];
+  unsigned long slot_epoch[EMAC_SYNC_SLOTS][2]; /* a slot's epochs continue across its handles */
   ipc_map *maps;
   int nmaps;
 } emac_comm;
@@ -112,6 +113,7 @@ typedef struct {
   int own_stream; /* 0 once the caller supplied the stream (ext_mpi_amd_set_stream) */
   /* IPC form */
   int slot;                /* synchronisation slot on the communicator */
+  int slot_held;
   unsigned long epoch[2];  /* barriers run per phase (before / after the fold) */
   void *mapped[2 * EMAC_MAX_RANKS];
   int nmapped;
@@ -147,6 +149,12 @@ static void release(emac_handle *h) {
     if (h->recv_reg[r]) emac_gpu_host_unregister(h->user_recv[r]);
   }
   for (r = 0; r < h->nmapped; r++) ipc_unmap(&comms[h->comm], h->mapped[r]);
+  if (h->kind == KIND_IPC && h->slot_held) {
+    emac_comm *cm = &comms[h->comm];
+    cm->slot_used[h->slot] = 0;
+    cm->slot_epoch[h->slot][0] = h->epoch[0];
+    cm->slot_epoch[h->slot][1] = h->epoch[1];
+  }
   free(h->ops);
   emac_plan_free(&h->plan);
   free(h);
@@ -435,6 +443,7 @@ typedef struct {
   unsigned char handle[EMAC_IPC_HANDLE_BYTES];
   long offset;
   int status;
+  unsigned char free_slots[EMAC_SYNC_SLOTS / 8]; /* handle set-up: slots this rank can use */
 } ipc_export;
 
 int ext_mpi_amd_comm_init_ipc(int rank, int size, ext_mpi_amd_allgather_fn allgather, void *ctx, int device,
@@ -507,17 +516,25 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
   ipc_export mine[2], all[2 * EMAC_MAX_RANKS];
   void *psend[EMAC_MAX_RANKS], *precv[EMAC_MAX_RANKS];
   emac_bucket *b = NULL;
-  int R = cm->size, r, t, pc, nb = 0, c, agreed;
+  int R = cm->size, r, t, pc, nb = 0, c, agreed, slot;
   const int empty = h->bytes == 0; /* same count on every rank: nothing to map or fold */
   memset(mine, 0, sizeof(mine));
   if (!rc && !empty) rc = map_buffers(h, 0, sendbuf, recvbuf);
   if (!rc && !empty) rc = emac_gpu_ipc_export(h->dsend[0], mine[0].handle, &mine[0].offset);
   if (!rc && !empty) rc = emac_gpu_ipc_export(h->drecv[0], mine[1].handle, &mine[1].offset);
-  if (!rc && cm->next_slot >= EMAC_SYNC_SLOTS) rc = EMAC_ERR_MALLOC;
+  for (r = 0; r < EMAC_SYNC_SLOTS; r++)
+    if (!cm->slot_used[r]) mine[0].free_slots[r >> 3] |= (unsigned char)(1u << (r & 7));
   mine[0].status = rc == 0;
   if (cm->ag(cm->ag_ctx, mine, all, (long)sizeof(mine))) return EMAC_ERR_TRANSPORT;
   for (r = 0; r < R; r++)
     if (!all[2 * r].status && !rc) rc = EMAC_ERR_TRANSPORT;
+  /* the synchronisation slot: the lowest one free on every rank (ranks may have released
+     their handles in different orders) */
+  for (slot = 0; slot < EMAC_SYNC_SLOTS; slot++) {
+    for (r = 0; r < R && (all[2 * r].free_slots[slot >> 3] >> (slot & 7)) & 1; r++);
+    if (r == R) break;
+  }
+  if (slot == EMAC_SYNC_SLOTS && !rc) rc = EMAC_ERR_MALLOC;
   for (r = 0; !rc && !empty && r < R; r++) {
     if (r == cm->rank) {
       psend[r] = h->dsend[0];
@@ -537,7 +554,11 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
   /* every rank opened every mapping before anyone proceeds */
   agreed = ipc_agree(cm, rc == 0);
   if (rc || agreed) return rc ? rc : agreed;
-  h->slot = cm->next_slot++;
+  h->slot = slot;
+  cm->slot_used[slot] = 1;
+  h->slot_held = 1;
+  h->epoch[0] = cm->slot_epoch[slot][0];
+  h->epoch[1] = cm->slot_epoch[slot][1];
   /* this rank's owner chunks: leaves from the peers' send buffers in the plan's fold order,
      results into every rank's receive buffer (the fused reduce_copyout push) */
   c = h->me_pos;

@@ -27,9 +27,12 @@
  * ext_mpi_allreduce_blocking_<nodes>_<cores>.txt (/dev/shm first, then the working directory):
  * one row per message-size threshold, host rows then device rows (README "blocking").
  *
- * Transport: one RCCL communicator per MPI communicator, cached as an MPI attribute and
- * destroyed with it; bootstrapped with PMPI_Bcast of the unique id. The communicator must lie
- * within one node (the reference's inter-node legs are out of this path's scope).
+ * Transport (EXT_MPI_AMD_TRANSPORT): "ipc" (default) maps every rank's device buffers into every
+ * other rank with hipIpc, as the reference maps them with cudaIpc (src/gpu/cuda_shmem.c:218-299),
+ * bootstrapped with PMPI_Allgather; "rccl" runs the legs as RCCL point-to-point rounds,
+ * bootstrapped with PMPI_Bcast of the unique id. One engine communicator per MPI communicator,
+ * cached as an MPI attribute and destroyed with it. The communicator must lie within one node
+ * (the reference's inter-node legs are out of this path's scope).
  */
 #include <mpi.h>
 #include <stdio.h>
@@ -49,6 +52,7 @@ static int cfg_verbose = 0;
 static int cfg_debug = 1;
 static int cfg_num_sockets = -1;
 static int cfg_blocking = 0;
+static int cfg_rccl = 0; /* EXT_MPI_AMD_TRANSPORT=rccl: legs over RCCL instead of hipIpc mappings */
 static int initialised = 0;
 static int comm_keyval = MPI_KEYVAL_INVALID;
 static int blocking_keyval = MPI_KEYVAL_INVALID;
@@ -72,6 +76,7 @@ static void read_env(void) {
     cfg_blocking = getenv("EXT_MPI_BLOCKING") != NULL; /* ext_mpi_interface.c:46-51 */
     env_int("EXT_MPI_DEBUG", &cfg_debug);
     env_int("EXT_MPI_NUM_SOCKETS_PER_NODE", &cfg_num_sockets);
+    cfg_rccl = getenv("EXT_MPI_AMD_TRANSPORT") && !strcmp(getenv("EXT_MPI_AMD_TRANSPORT"), "rccl");
     if (c) {
       strncpy(cfg_copyin, c, sizeof(cfg_copyin) - 1);
       len = (int)strlen(cfg_copyin) + 1;
@@ -81,6 +86,7 @@ static void read_env(void) {
   PMPI_Bcast(&cfg_blocking, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_debug, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_num_sockets, 1, MPI_INT, 0, MPI_COMM_WORLD);
+  PMPI_Bcast(&cfg_rccl, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&len, 1, MPI_INT, 0, MPI_COMM_WORLD);
   if (len > 0) PMPI_Bcast(cfg_copyin, len, MPI_CHAR, 0, MPI_COMM_WORLD);
   cfg_has_copyin = len > 0;
@@ -150,11 +156,22 @@ static int request_handle(const MPI_Request *r) {
   return s < 0 ? -1 : rmap[s].handle;
 }
 
-/* ----------------------------------------------- communicator -> RCCL communicator */
+/* ------------------------------------------ communicator -> node communicator of the engine */
 
+/* Default: the peer-mapped form (every rank's device buffers mapped into every other rank with
+   hipIpc, exchanged with PMPI_Allgather as ext_mpi_sendrecvbuf_init_gpu does with cudaIpc,
+   cuda_shmem.c:218-299). EXT_MPI_AMD_TRANSPORT=rccl: an RCCL communicator bootstrapped with
+   PMPI_Bcast of the unique id. Either is cached as an attribute of the MPI communicator and
+   destroyed with it. The communicator must lie within one node. */
 typedef struct {
   int ext_comm;
+  MPI_Comm boot; /* private duplicate the IPC bootstrap exchanges run on */
 } comm_attr;
+
+static int mpi_allgather_cb(void *ctx, const void *send, void *recv, long bytes) {
+  comm_attr *a = (comm_attr *)ctx;
+  return PMPI_Allgather((void *)send, (int)bytes, MPI_BYTE, recv, (int)bytes, MPI_BYTE, a->boot) == MPI_SUCCESS ? 0 : -1;
+}
 
 static int comm_attr_delete(MPI_Comm comm, int keyval, void *attr, void *extra) {
   comm_attr *a = (comm_attr *)attr;
@@ -163,6 +180,7 @@ static int comm_attr_delete(MPI_Comm comm, int keyval, void *attr, void *extra) 
   (void)extra;
   if (a) {
     ext_mpi_amd_comm_free(a->ext_comm);
+    if (a->boot != MPI_COMM_NULL) PMPI_Comm_free(&a->boot);
     free(a);
   }
   return MPI_SUCCESS;
@@ -191,16 +209,30 @@ static int node_comm(MPI_Comm comm, const void *devbuf, int *ext_comm) {
   ndev = ext_mpi_amd_gpu_device_count();
   device = ext_mpi_amd_gpu_device_of(devbuf);
   if (device < 0) device = ndev > 0 ? nrank % ndev : -1;
-  if (rank == 0 && (rc = ext_mpi_amd_get_unique_id(id))) memset(id, 0, sizeof(id));
-  PMPI_Bcast(id, EXT_MPI_AMD_UNIQUE_ID_BYTES, MPI_BYTE, 0, comm);
-  rc = ndev > 0 ? ext_mpi_amd_comm_init(rank, size, id, device, ext_comm) : EXT_MPI_AMD_ERROR_DEVICE;
-  flag = rc == 0;
-  PMPI_Allreduce(MPI_IN_PLACE, &flag, 1, MPI_INT, MPI_MIN, comm);
-  if (!flag) {
-    if (rc == 0) ext_mpi_amd_comm_free(*ext_comm);
-    return rc ? rc : EXT_MPI_AMD_ERROR_TRANSPORT;
+  a = (comm_attr *)calloc(1, sizeof(comm_attr));
+  if (!a) return EXT_MPI_AMD_ERROR_MALLOC;
+  a->boot = MPI_COMM_NULL;
+  if (!cfg_rccl) {
+    PMPI_Comm_dup(comm, &a->boot);
+    /* collective even without a device: every rank reaches the same verdict */
+    rc = ext_mpi_amd_comm_init_ipc(rank, size, mpi_allgather_cb, a, ndev > 0 ? device : -1, ext_comm);
+    if (rc) {
+      PMPI_Comm_free(&a->boot);
+      free(a);
+      return rc;
+    }
+  } else {
+    if (rank == 0 && (rc = ext_mpi_amd_get_unique_id(id))) memset(id, 0, sizeof(id));
+    PMPI_Bcast(id, EXT_MPI_AMD_UNIQUE_ID_BYTES, MPI_BYTE, 0, comm);
+    rc = ndev > 0 ? ext_mpi_amd_comm_init(rank, size, id, device, ext_comm) : EXT_MPI_AMD_ERROR_DEVICE;
+    flag = rc == 0;
+    PMPI_Allreduce(MPI_IN_PLACE, &flag, 1, MPI_INT, MPI_MIN, comm);
+    if (!flag) {
+      if (rc == 0) ext_mpi_amd_comm_free(*ext_comm);
+      free(a);
+      return rc ? rc : EXT_MPI_AMD_ERROR_TRANSPORT;
+    }
   }
-  a = (comm_attr *)malloc(sizeof(comm_attr));
   a->ext_comm = *ext_comm;
   PMPI_Comm_set_attr(comm, comm_keyval, a);
   return 0;
@@ -289,6 +321,7 @@ typedef struct {
   void *recv;
   int count, dtype, side, row, handle;
   unsigned long used;
+  long serial; /* creation number: equal on every rank for the same collective creation */
 } bentry;
 
 /* Per-communicator state of the blocking path (comm_comm_blocking, ext_mpi_native_blocking.c). */
@@ -299,6 +332,7 @@ typedef struct {
   brow row[2][BROWS];
   bentry cache[BCACHE];
   unsigned long clock;
+  long serial;
   void *scratch;
   size_t scratch_bytes;
 } bcomm;
@@ -443,6 +477,18 @@ static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int
       break;
     }
   }
+  if (!cfg_rccl) {
+    /* a peer-mapped handle embeds every rank's buffers: it is reused only if every rank found
+       the same one (same creation); otherwise every rank creates a new one, in step */
+    long v[2];
+    v[0] = slot >= 0 ? b->cache[slot].serial : -1;
+    v[1] = slot >= 0 ? -b->cache[slot].serial : 1;
+    PMPI_Allreduce(MPI_IN_PLACE, v, 2, MPI_LONG, MPI_MIN, comm);
+    if (v[0] < 0 || v[0] != -v[1]) {
+      if (slot >= 0) bcomm_drop(b, slot); /* keep keys unique: the new handle replaces it */
+      slot = -1;
+    }
+  }
   if (slot < 0) {
     slot = 0;
     for (i = 0; i < BCACHE; i++) {
@@ -460,6 +506,7 @@ static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int
     }
     e->send = s;
     e->recv = r;
+    e->serial = ++b->serial;
     e->count = count;
     e->dtype = dtype;
     e->side = side;

@@ -85,6 +85,22 @@ def main():
         emac.done(h)
     failures += not ok
     print(f"IPC rank {rank}/{world} concurrent handles: {'ok' if ok else 'MISMATCH'}", flush=True)
+    # synchronisation slots are recycled: more handle lifetimes than slots, released in a
+    # rank-dependent order, each still synchronising correctly (epochs continue per slot)
+    ok = True
+    x = torch.full((64,), float(rank + 1), device="cuda")
+    y = torch.empty_like(x)
+    for it in range(600):
+        pair = [emac.allreduce_init(x.data_ptr(), y.data_ptr(), 64, emac.FLOAT, comm) for _ in range(2)]
+        for h in pair:
+            emac.start(h)
+            emac.wait(h)
+        if it % 50 == 0:
+            ok &= bool(torch.all(y == world * (world + 1) / 2).item())
+        for h in (pair if rank % 2 else pair[::-1]):
+            emac.done(h)
+    failures += not ok
+    print(f"IPC rank {rank}/{world} slot recycling (1200 handles): {'ok' if ok else 'MISMATCH'}", flush=True)
     emac.comm_free(comm)
     dist.barrier()
     dist.destroy_process_group()

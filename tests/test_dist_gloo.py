@@ -102,3 +102,41 @@ def test_comm_program_shape():
     assert all(b == emac.BUF_STAGE for b, _ in folds[0][2][1:])
     assert all(off % 16 == 0 for b, off in folds[0][2][1:])
     assert stage >= 7 * 4000
+
+
+def _ipc_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = []
+
+    def ag(payload):
+        calls.append(len(payload))
+        return emac.torch_allgather()(payload)
+    try:
+        emac.comm_init_ipc(rank, world, ag, -1)
+        q.put((rank, "no error", calls))
+    except emac.ExtMpiError as e:
+        q.put((rank, e.code, calls))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ipc_bootstrap_over_gloo_without_gpu(world):
+    """The peer-mapped communicator's set-up is collective: without a device every rank still
+    takes part in the same bootstrap exchanges (no rank left waiting) and all fail loudly with
+    ERROR_DEVICE instead of falling back to the CPU."""
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: tests/test_gpu_ipc.py covers the working path")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + world * 7 + os.getpid() % 200
+    procs = [ctx.Process(target=_ipc_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert [r[1] for r in results] == [-5] * world
+    assert len({tuple(r[2]) for r in results}) == 1 and results[0][2]  # same exchanges on every rank

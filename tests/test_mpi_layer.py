@@ -95,3 +95,22 @@ def test_mpi_blocking_single_rank_gpu(tmp_path, args, copyin):
     assert res and res[0].startswith("RESULT ok"), out
     chosen = [l for l in out.splitlines() if l.startswith("# EXT_MPI blocking allreduce")]
     assert chosen and all(l.endswith("copyin " + copyin) for l in chosen), out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,args,extra", [
+    (2, [100003, "f", "dev"], {}), (4, [4099, "d", "dev", "inplace"], {}), (3, [100000, "i", "host"], {}),
+    (4, [777, "l", "host", "inplace"], {}), (2, [0, "f", "dev"], {}),
+    (4, [100003, "f", "dev", "blocking"], {"EXT_MPI_BLOCKING": "1"}),
+    (2, [4099, "d", "host", "inplace", "blocking"], {"EXT_MPI_BLOCKING": "1"}),
+    (4, [65536, "f", "dev"], {"EXT_MPI_COPYIN": "6;1 -2 -2 2 2"}),
+])
+def test_mpi_layer_multi_rank_one_gpu(tmp_path, n, args, extra):
+    """n MPI ranks sharing the box's one GPU over the default peer-mapped transport: the
+    application's MPI_Allreduce_init / MPI_Start / MPI_Wait (with the known-answer self-test) or
+    blocking MPI_Allreduce, checked against PMPI_Allreduce on every rank."""
+    exe = _build(tmp_path)
+    env = {"EXT_MPI_DEBUG": "1", "EXT_MPI_AMD_BARRIER_TIMEOUT": "20"}
+    env.update(extra)
+    res, out = _run(exe, n, args, env=env, timeout=180)
+    assert res and res[0].startswith("RESULT ok"), out
