@@ -487,6 +487,11 @@ def multi_gpu(args):
     S = count * tsize
     copyin = args.copyin or f"6;1 -{world} {world}"
 
+    def everyone(ok):
+        t = torch.tensor([int(bool(ok))])
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
     def make_comm(transport):
         if transport == "ipc":
             return emac.comm_init_ipc(rank, world, emac.torch_allgather(), dev)
@@ -494,60 +499,85 @@ def multi_gpu(args):
         dist.broadcast_object_list(uid, src=0)
         return emac.comm_init(rank, world, uid[0], dev)
 
-    comm = make_comm(args.transport)
-    h, send, recv, stream, wall, checked = _comm_run(emac, comm, count, tdtype, code, dname, copyin, args.steps,
-                                                     args.warmup, rank, world, dist, torch)
-    # the fold leg alone on every GPU at once, then on rank 0's GPU while the others idle
-    dist.barrier()
-    fold_s = torch.tensor([_fold_only(emac, h, stream, args.steps, torch)], dtype=torch.float64)
-    dist.all_reduce(fold_s, op=dist.ReduceOp.MAX)
-    dist.barrier()
-    alone_s = torch.zeros(1, dtype=torch.float64)
-    if rank == 0:
-        alone_s[0] = _fold_only(emac, h, stream, args.steps, torch)
-    dist.barrier()
-    dist.broadcast(alone_s, src=0)
-    emac.done(h)
-    send.free()
-    recv.free()
-    extras = {"transport": args.transport, "gpus_visible": ndev}
-    # BASELINE configs[3] (double, 256 MiB per rank) and a configs[4]-style size sweep, bounded
-    points = [(args.dtype, n) for n in (8, 64 << 10, 1 << 20, 16 << 20, 64 << 20, 256 << 20)] + [("double", 256 << 20)]
-    sweep = []
-    for dname_p, nbytes in points:
-        tdt, cde, _, tsz = dtype_info(dname_p)
-        cnt = max(1, nbytes // tsz)
-        st = 100 if nbytes <= (1 << 20) else 10
+    def run_transport(transport, full):
+        """The headline workload on one transport (+ fold timings and the sweep when `full`)."""
+        res = {}
+        comm = make_comm(transport)
         try:
-            hp, sb, rb, _, el_p, ok_p = _comm_run(emac, comm, cnt, tdt, cde, dname_p, copyin, st, 3, rank, world, dist,
-                                                  torch)
-            emac.done(hp)
-            sb.free()
-            rb.free()
-            sweep.append({"dtype": dname_p, "bytes_per_rank": cnt * tsz, "us_per_allreduce": round(el_p * 1e6 / st, 2),
-                          "algbw_gbps": round(cnt * tsz * st / el_p / 1e9, 2), "checked": ok_p})
-        except Exception as e:  # a failing extra point must not lose the headline line
-            sweep.append({"dtype": dname_p, "bytes_per_rank": nbytes, "error": str(e)})
-    extras["sweep"] = sweep
-    emac.comm_free(comm)
-    # the other transport on the same workload, for comparison (RCCL refuses ranks sharing a GPU)
-    other = "rccl" if args.transport == "ipc" else "ipc"
-    try:
-        c2 = make_comm(other)
-        h2, s2, r2, _, wall2, ok2 = _comm_run(emac, c2, count, tdtype, code, dname, copyin, args.steps, args.warmup,
-                                              rank, world, dist, torch)
-        emac.done(h2)
-        s2.free()
-        r2.free()
-        emac.comm_free(c2)
-        extras[f"{other}_transport"] = {"ms_per_step": round(wall2 * 1e3 / args.steps, 4),
-                                        "value": round(world * S * args.steps / wall2 / 1e9, 2), "checked": ok2}
-    except Exception as e:  # noqa: BLE001
-        extras[f"{other}_transport"] = {"error": str(e)}
-    if rank == 0:
-        kf = fold_s.item()
+            h, send, recv, stream, wall, checked = _comm_run(emac, comm, count, tdtype, code, dname, copyin,
+                                                             args.steps, args.warmup, rank, world, dist, torch)
+            res.update(wall=wall, checked=checked)
+            if full:
+                # the fold leg alone on every GPU at once, then on rank 0's GPU while the others idle
+                dist.barrier()
+                fold_s = torch.tensor([_fold_only(emac, h, stream, args.steps, torch)], dtype=torch.float64)
+                dist.all_reduce(fold_s, op=dist.ReduceOp.MAX)
+                dist.barrier()
+                alone_s = torch.zeros(1, dtype=torch.float64)
+                if rank == 0:
+                    alone_s[0] = _fold_only(emac, h, stream, args.steps, torch)
+                dist.barrier()
+                dist.broadcast(alone_s, src=0)
+                res.update(fold_s=fold_s.item(), alone_s=alone_s.item())
+            emac.done(h)
+            send.free()
+            recv.free()
+            if full:
+                # BASELINE configs[3] (double, 256 MiB per rank) and a configs[4]-style size sweep
+                points = [(args.dtype, n) for n in (8, 64 << 10, 1 << 20, 16 << 20, 64 << 20, 256 << 20)]
+                points.append(("double", 256 << 20))
+                sweep = []
+                for dname_p, nbytes in points:
+                    tdt, cde, _, tsz = dtype_info(dname_p)
+                    cnt = max(1, nbytes // tsz)
+                    st = 100 if nbytes <= (1 << 20) else 10
+                    hp, sb, rb, _, el_p, ok_p = _comm_run(emac, comm, cnt, tdt, cde, dname_p, copyin, st, 3, rank,
+                                                          world, dist, torch)
+                    emac.done(hp)
+                    sb.free()
+                    rb.free()
+                    sweep.append({"dtype": dname_p, "bytes_per_rank": cnt * tsz,
+                                  "us_per_allreduce": round(el_p * 1e6 / st, 2),
+                                  "algbw_gbps": round(cnt * tsz * st / el_p / 1e9, 2), "checked": ok_p})
+                res["sweep"] = sweep
+        finally:
+            emac.comm_free(comm)
+        return res
+
+    # the requested transport first; if it fails on any rank (every rank agrees before moving
+    # on, so no rank is left inside a collective), the other one produces the headline
+    order = [args.transport, "rccl" if args.transport == "ipc" else "ipc"]
+    results = {}
+    for i, transport in enumerate(order):
+        full = not any("wall" in r for r in results.values())
+        try:
+            r = run_transport(transport, full)
+            err = None if r.get("checked") else "result check failed"
+        except Exception as e:  # noqa: BLE001
+            r, err = {}, f"{type(e).__name__}: {e}"
+        if not everyone(err is None):
+            r = {"error": err or "failed on another rank"}
+        results[transport] = r
+    primary = next((t for t in order if "wall" in results[t] and "fold_s" in results[t]), None)
+    extras = {"gpus_visible": ndev}
+    for t in order:
+        if t != primary:
+            r = results[t]
+            extras[f"{t}_transport"] = r if "wall" not in r else {
+                "ms_per_step": round(r["wall"] * 1e3 / args.steps, 4),
+                "value": round(world * S * args.steps / r["wall"] / 1e9, 2), "checked": r["checked"]}
+    if rank == 0 and primary is None:
+        print(json.dumps({"metric": "device-resident GB/s reduced (float32 MPI_SUM) per GPU; % HBM3E roofline",
+                          "value": 0.0, "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dname,
+                          "error": "no transport completed", "extras": extras}), flush=True)
+    if rank == 0 and primary is not None:
+        r = results[primary]
+        wall, checked, kf = r["wall"], r["checked"], r["fold_s"]
+        extras["transport"] = primary
+        extras["sweep"] = r["sweep"]
         chunk = S / world
-        if args.transport == "ipc":
+        if primary == "ipc":
             algo = 2 * world * chunk  # R leaf reads (R-1 over xGMI) + R fan-out writes (R-1 over xGMI)
             remote = 2 * (world - 1) * chunk
         else:
@@ -555,14 +585,14 @@ def multi_gpu(args):
             remote = 0
         achieved = algo / kf / 1e9
         extras.update({
-            "fold_us_all_gpus": round(kf * 1e6, 2), "fold_us_rank0_alone": round(alone_s.item() * 1e6, 2),
-            "per_gpu_fold_rate_retained": round(alone_s.item() / kf, 3),
+            "fold_us_all_gpus": round(kf * 1e6, 2), "fold_us_rank0_alone": round(r["alone_s"] * 1e6, 2),
+            "per_gpu_fold_rate_retained": round(r["alone_s"] / kf, 3),
             "fold_xgmi_gbps_per_gpu": round(remote / kf / 1e9, 1) if remote else None,
             "end_to_end_algbw_gbps_per_gpu": round(S * args.steps / wall / 1e9, 2),
             "xgmi_bound_us": round(2 * (world - 1) / world * S / (min(world - 1, 7) * 153e9) * 1e6, 1)})
         form = ("peer-mapped (hipIpc over xGMI): barrier kernel, fold of the owned chunk over the peers' send "
                 "buffers with the fan-out stored into every peer's receive buffer, barrier kernel"
-                if args.transport == "ipc" else
+                if primary == "ipc" else
                 "reduce-scatter + allgather legs over RCCL/xGMI, fold on the owner GPU")
         out = {
             "metric": "device-resident GB/s reduced (float32 MPI_SUM) per GPU; % HBM3E roofline",
@@ -574,7 +604,7 @@ def multi_gpu(args):
             "config": {"workload": f"persistent Allreduce {args.dtype} MPI_SUM, {S // MIB} MiB per rank, one rank per "
                                    f"GPU, EXT_MPI_COPYIN '{copyin}': {form}",
                        "ranks": world, "message_bytes_per_rank": S, "copyin": copyin, "layout": "rank-per-gpu",
-                       "transport": args.transport, "checked_vs_fp64_sum": checked},
+                       "transport": primary, "checked_vs_fp64_sum": checked},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None, "kernel": "fold_kernel",
                          "algorithmic_bytes_per_launch": int(algo), "avg_launch_us": round(kf * 1e6, 2)},
