@@ -41,14 +41,22 @@ inline int ok(hipError_t e) { return e == hipSuccess ? 0 : EMAC_ERR_DEVICE; }
 extern "C" {
 
 int emac_gpu_pick_unroll(int nsrc, int tree, int fan, long total_vectors) {
-  // instantiation policy of fold_kernel.hpp; among the instantiated unrolls take the deeper one
-  // once the launch has enough tiles to fill the chip several times over (measured:
-  // tools/foldbench.hip, U = 4 wins at 256 MiB x 8 ranks, U = 2 at 16 MiB x 8 ranks)
-  if (nsrc == 1) return total_vectors >= 2048L * EMAC_BLOCK * 2 ? 2 : 1;
-  if (tree) return nsrc <= 4 ? 4 : (nsrc <= 8 ? 2 : 1);
-  if (nsrc > 8) return 1;
-  if (fan) return total_vectors >= 8192L * EMAC_BLOCK * 2 ? 4 : 2;
-  return total_vectors >= 2048L * EMAC_BLOCK * 2 ? 2 : 1;
+  // returns U | ISSUE << 4 (fold_kernel.hpp, instantiation policy). Measured on MI355X with the
+  // production template, R = 8 float, node form (tools/ldsbench.hip, profiles/r01_ldsbench_issue_*):
+  // a back-to-back burst of every load of a tile wins at <= 2 MiB and >= 64 MiB per rank;
+  // between them U = 4 with an s_sleep after every 4 loads is 4-8 % faster (16 MiB: 41.9 vs
+  // 45.2-45.4 us); 64 MiB per rank prefers U = 2 (183 vs 194 us), >= 128 MiB U = 4.
+  using emac::sched;
+  if (nsrc == 1) return total_vectors >= 2048L * EMAC_BLOCK * 2 ? sched(2, 1) : sched(1, 1);
+  if (tree) return sched(nsrc <= 4 ? 4 : (nsrc <= 8 ? 2 : 1), 1);
+  if (nsrc > 8) return sched(1, 1);
+  if (fan) {
+    if (total_vectors < (192L << 10)) return sched(2, 1);
+    if (total_vectors < (3L << 20)) return sched(4, 5);
+    if (total_vectors < (6L << 20)) return sched(2, 1);
+    return sched(4, 1);
+  }
+  return total_vectors >= 2048L * EMAC_BLOCK * 2 ? sched(2, 1) : sched(1, 1);
 }
 
 int emac_gpu_fold(int dtype, int op, int nsrc, int fan, int unroll, const emac_codes *codes,

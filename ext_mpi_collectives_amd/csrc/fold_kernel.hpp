@@ -101,21 +101,29 @@ __device__ __forceinline__ void fold_scalar_element(const emac_bucket *b, long e
 // any load is issued, and used as global (address space 1) bases: the loads become
 // `global_load_dwordx4 v, v_off, s_base nt` issued back to back, instead of flat loads each
 // waiting on its own descriptor read.
-template <typename T, int N, int U, bool TREE, int D, bool FULL>
+// ISSUE (load issue schedule, measured in tools/ldsbench.hip): bit 0 = source-major order
+// (every vector of leaf 0, then leaf 1, ...) instead of vector-major; bits 1.. = s_sleep after
+// every 4 loads (0 = back-to-back burst).
+template <typename T, int N, int U, bool TREE, int D, bool FULL, int ISSUE = 1>
 __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_base, long nvec, const emac_codes &c) {
   typedef typename Lane<T>::V V;
   typedef __attribute__((address_space(1))) V GV;
+  constexpr bool SRC_MAJOR = ISSUE & 1;
+  constexpr int SLEEP = ISSUE >> 1;
   // vectors of this tile still inside the bucket (wave-uniform); lane offsets are 32-bit so
   // every access is `global_*_dwordx4 v, v_off, s_base` with the tile base in SGPRs
   const long left = nvec - tile_base;
   V x[U][N];
+  const GV *src[N];
 #pragma unroll
-  for (int s = 0; s < N; ++s) {
-    const GV *src = (const GV *)b->src[s] + tile_base;
+  for (int s = 0; s < N; ++s) src[s] = (const GV *)b->src[s] + tile_base;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const unsigned v = threadIdx.x + (unsigned)(u * EMAC_BLOCK);
-      if (FULL || (long)v < left) x[u][s] = __builtin_nontemporal_load(src + v);
+  for (int k = 0; k < N * U; ++k) {
+    const int s = SRC_MAJOR ? k / U : k % N, u = SRC_MAJOR ? k % U : k / N;
+    const unsigned v = threadIdx.x + (unsigned)(u * EMAC_BLOCK);
+    if (FULL || (long)v < left) x[u][s] = __builtin_nontemporal_load(src[s] + v);
+    if constexpr (SLEEP > 0) {
+      if ((k & 3) == 3 && k + 1 < N * U) __builtin_amdgcn_s_sleep(SLEEP);
     }
   }
   V r[U];
@@ -135,7 +143,7 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
 
 // Streaming body: one workgroup per tile (grid-stride); a tile is EMAC_BLOCK*U consecutive
 // 16-byte vectors of one bucket. Nothing element-granular runs here (see fold_edge_kernel).
-template <typename T, int N, int U, bool TREE, int D>
+template <typename T, int N, int U, bool TREE, int D, int ISSUE = 1>
 __global__ __launch_bounds__(EMAC_BLOCK) void fold_kernel(const emac_bucket *__restrict__ bk, int nb,
                                                           long ntiles, long tiles_per_bucket, int all_full,
                                                           emac_codes codes) {
@@ -166,9 +174,9 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_kernel(const emac_bucket *__r
     // all_full (host-known: every bucket a whole number of tiles) skips the dependent read of
     // nvec before the first load of the tile
     if (all_full || (t + 1) * TILE <= b->nvec)
-      fold_vectors<T, N, U, TREE, D, true>(b, t * TILE, 0, codes);
+      fold_vectors<T, N, U, TREE, D, true, ISSUE>(b, t * TILE, 0, codes);
     else
-      fold_vectors<T, N, U, TREE, D, false>(b, t * TILE, b->nvec, codes);
+      fold_vectors<T, N, U, TREE, D, false, ISSUE>(b, t * TILE, b->nvec, codes);
   }
 }
 
@@ -193,10 +201,14 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_edge_kernel(const emac_bucket
 }
 
 // ---- instantiation policy (keep in sync with emac_gpu_pick_unroll in fold.hip) ----
-// linear, fan-out N (node form):  N <= 8 -> U in {2, 4};  N > 8 -> U = 1
-// linear, fan-out 1 (comm form):  N <= 8 -> U in {1, 2};  N > 8 -> U = 1
-// tree (composite N), either fan-out: U = 4 / 2 / 1 for N <= 4 / <= 8 / > 8
+// A launch schedule is encoded as U | ISSUE << 4 (EMAC_SCHED).
+// linear, fan-out N (node / IPC form):  N <= 8 -> (U 2, burst), (U 4, burst), (U 4, s_sleep 2
+//                                        every 4 loads);  N > 8 -> (U 1, burst)
+// linear, fan-out 1 (comm form):        N <= 8 -> U in {1, 2}, burst;  N > 8 -> U = 1
+// tree (composite N), either fan-out:   U = 4 / 2 / 1 for N <= 4 / <= 8 / > 8, burst
+// (burst = ISSUE 1: every load of a tile back to back, source-major)
 constexpr int tree_unroll(int n) { return n <= 4 ? 4 : (n <= 8 ? 2 : 1); }
+constexpr int sched(int u, int issue) { return u | issue << 4; }
 
 struct Launch {
   const emac_codes *c;
@@ -209,12 +221,12 @@ struct Launch {
   hipStream_t s;
 };
 
-template <typename T, int N, int U, bool TREE, int D>
+template <typename T, int N, int U, bool TREE, int D, int ISSUE = 1>
 int launch_one(const Launch &L) {
   const long grid = L.ntiles < 8192 ? L.ntiles : 8192;
   if (grid > 0)
-    hipLaunchKernelGGL((fold_kernel<T, N, U, TREE, D>), dim3((unsigned)grid), dim3(EMAC_BLOCK), 0, L.s, L.b, L.nb,
-                       L.ntiles, L.tpb, L.all_full, *L.c);
+    hipLaunchKernelGGL((fold_kernel<T, N, U, TREE, D, ISSUE>), dim3((unsigned)grid), dim3(EMAC_BLOCK), 0, L.s, L.b,
+                       L.nb, L.ntiles, L.tpb, L.all_full, *L.c);
   if (L.nedges > 0)
     hipLaunchKernelGGL((fold_edge_kernel<T, N, TREE, D>), dim3((unsigned)L.nedges), dim3(EMAC_BLOCK), 0, L.s, L.b,
                        L.edges, *L.c);
@@ -225,18 +237,19 @@ template <typename T, int N, bool FAN>
 int launch_nf(bool tree, int unroll, const Launch &L) {
   constexpr int D = FAN ? N : 1;
   if constexpr (can_tree(N)) {
-    if (tree) return unroll == tree_unroll(N) ? launch_one<T, N, tree_unroll(N), true, D>(L)
-                                              : EMAC_ERR_UNSUPPORTED;
+    if (tree) return unroll == sched(tree_unroll(N), 1) ? launch_one<T, N, tree_unroll(N), true, D>(L)
+                                                        : EMAC_ERR_UNSUPPORTED;
   }
   if (tree) return EMAC_ERR_UNSUPPORTED;
   if constexpr (N > 8) {
-    return unroll == 1 ? launch_one<T, N, 1, false, D>(L) : EMAC_ERR_UNSUPPORTED;
+    return unroll == sched(1, 1) ? launch_one<T, N, 1, false, D>(L) : EMAC_ERR_UNSUPPORTED;
   } else if constexpr (FAN) {
-    if (unroll == 4) return launch_one<T, N, 4, false, D>(L);
-    if (unroll == 2) return launch_one<T, N, 2, false, D>(L);
+    if (unroll == sched(4, 5)) return launch_one<T, N, 4, false, D, 5>(L);
+    if (unroll == sched(4, 1)) return launch_one<T, N, 4, false, D, 1>(L);
+    if (unroll == sched(2, 1)) return launch_one<T, N, 2, false, D, 1>(L);
   } else {
-    if (unroll == 2) return launch_one<T, N, 2, false, D>(L);
-    if (unroll == 1) return launch_one<T, N, 1, false, D>(L);
+    if (unroll == sched(2, 1)) return launch_one<T, N, 2, false, D>(L);
+    if (unroll == sched(1, 1)) return launch_one<T, N, 1, false, D>(L);
   }
   return EMAC_ERR_UNSUPPORTED;
 }

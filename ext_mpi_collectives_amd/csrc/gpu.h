@@ -84,8 +84,9 @@ long emac_gpu_wallclock_hz(void);
 int emac_gpu_node_barrier(void *self, void *const *d_peers, int slot, int phase, unsigned long epoch, int nranks,
                           int me, unsigned xcc_expect, int *err, long timeout_ticks, void *stream);
 
-/* Unroll (16-byte vectors per lane per leaf) of a launch: a tile covers EMAC_BLOCK * unroll
-   vectors. fan: the fan-out width equals nsrc (node form) instead of 1. */
+/* Launch schedule: unroll U (16-byte vectors per lane per leaf; a tile covers EMAC_BLOCK * U
+   vectors) in the low 4 bits, load-issue schedule above (fold_kernel.hpp). fan: the fan-out
+   width equals nsrc (node / IPC form) instead of 1. */
 int emac_gpu_pick_unroll(int nsrc, int tree, int fan, long total_vectors);
 
 /* Launch the fold over nb device-resident buckets (ntiles tiles in total) on `stream`.

@@ -44,8 +44,8 @@ int emac_layout(emac_bucket *b, int nb, int nsrc, int tree, int fan, emac_edge *
   int i, ne = 0, unroll, all_full = 1;
   emac_edge *edges;
   for (i = 0; i < nb; i++) total += b[i].nvec;
-  unroll = emac_gpu_pick_unroll(nsrc, tree, fan, total);
-  tv = (long)EMAC_BLOCK * unroll;
+  unroll = emac_gpu_pick_unroll(nsrc, tree, fan, total); /* U | ISSUE << 4 */
+  tv = (long)EMAC_BLOCK * (unroll & 15);
   for (i = 0; i < nb; i++) {
     long t = (b[i].nvec + tv - 1) / tv;
     b[i].tile0 = tiles;

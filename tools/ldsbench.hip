@@ -247,9 +247,17 @@ int main(int argc, char **argv) {
     int kind;
     std::vector<float> us;
   };
-  std::vector<V> vs = {{"prod_u2", 0, {}},   {"prod_u4", 1, {}},   {"read_nt", 2, {}},  {"read_glds", 3, {}},
+  const bool quick = getenv("LDSBENCH_QUICK") != nullptr;
+  std::vector<V> vs = {{"u2_vec_burst", 20, {}}, {"u2_src_burst", 21, {}}, {"u2_vec_sleep1", 22, {}},
+                       {"u2_src_sleep1", 23, {}}, {"u2_vec_sleep2", 24, {}}, {"u2_src_sleep2", 25, {}},
+                       {"u2_vec_sleep3", 26, {}}, {"u2_src_sleep3", 27, {}}, {"u4_src_burst", 31, {}},
+                       {"u4_src_sleep1", 33, {}}, {"u4_src_sleep2", 35, {}},
+                       {"prod_u2", 0, {}},   {"prod_u4", 1, {}},   {"read_nt", 2, {}},  {"read_glds", 3, {}},
                        {"glds_u1", 4, {}},   {"glds_u2", 5, {}},   {"glds_pipe", 6, {}}, {"glds_pipe_g512", 7, {}},
                        {"copy_nt", 8, {}},   {"copy_glds", 9, {}}, {"fold_plainst_u2", 10, {}}};
+  if (quick) vs = {{"u2_src_burst", 21, {}}, {"u2_src_sleep1", 23, {}}, {"u2_src_sleep2", 25, {}},
+                   {"u2_src_sleep3", 27, {}}, {"u4_src_burst", 31, {}}, {"u4_src_sleep1", 33, {}},
+                   {"u4_src_sleep2", 35, {}}, {"u4_src_sleep3", 37, {}}, {"copy_nt", 8, {}}};
   auto run = [&](int kind, int set, int i) {
     switch (kind) {
     case 0:
@@ -257,11 +265,28 @@ int main(int argc, char **argv) {
       const int U = kind == 0 ? 2 : 4;
       const long tpb = C / (256 * U);
       emac::Launch L = {&codes, ebk[set], R, tpb * R, tpb, 1, nullptr, 0, s};
-      for (int c = 0; c < 0; ++c);
       if (U == 2)
         emac::launch_one<float, R, 2, false, R>(L);
       else
         emac::launch_one<float, R, 4, false, R>(L);
+      break;
+    }
+    case 20: case 21: case 22: case 23: case 24: case 25: case 26: case 27: {
+      // production template, U = 2, load issue schedule ISSUE = kind - 20
+      const long tpb = C / 512;
+      const dim3 g((unsigned)std::min<long>(tpb * R, 8192));
+#define ISS(i) case 20 + i: hipLaunchKernelGGL((emac::fold_kernel<float, R, 2, false, R, i>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, codes); break;
+      switch (kind) { ISS(0) ISS(1) ISS(2) ISS(3) ISS(4) ISS(5) ISS(6) ISS(7) }
+#undef ISS
+      break;
+    }
+    case 31: case 33: case 35: case 37: {
+      const long tpb = C / 1024;
+      const dim3 g((unsigned)std::min<long>(tpb * R, 8192));
+      if (kind == 31) hipLaunchKernelGGL((emac::fold_kernel<float, R, 4, false, R, 1>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, codes);
+      if (kind == 33) hipLaunchKernelGGL((emac::fold_kernel<float, R, 4, false, R, 3>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, codes);
+      if (kind == 35) hipLaunchKernelGGL((emac::fold_kernel<float, R, 4, false, R, 5>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, codes);
+      if (kind == 37) hipLaunchKernelGGL((emac::fold_kernel<float, R, 4, false, R, 7>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, codes);
       break;
     }
     case 2: hipLaunchKernelGGL(read_nt, dim3(8192), dim3(256), 0, s, ca + (i & 1) * cn, cn, dummy); break;
@@ -296,7 +321,7 @@ int main(int argc, char **argv) {
     std::vector<char> ref(C * 16), got(C * 16);
     Bucket hb;
     CHECK(hipMemcpy(&hb, dbk[0] + 3, sizeof(hb), hipMemcpyDeviceToHost));
-    for (int kind : {0, 1, 4, 5, 6, 7, 10}) {
+    for (int kind : {0, 1, 4, 5, 6, 7, 10, 20, 21, 22, 23, 24, 25, 26, 27, 31, 33, 35, 37}) {
       CHECK(hipMemset(hb.dst[5], 0, C * 16));
       run(kind, 0, 0);
       CHECK(hipStreamSynchronize(s));
