@@ -48,7 +48,12 @@ int emac_gpu_pick_unroll(int nsrc, int tree, int fan, long total_vectors) {
   // 45.2-45.4 us); 64 MiB per rank prefers U = 2 (183 vs 194 us), >= 128 MiB U = 4.
   using emac::sched;
   if (nsrc == 1) return total_vectors >= 2048L * EMAC_BLOCK * 2 ? sched(2, 1) : sched(1, 1);
-  if (tree) return sched(nsrc <= 4 ? 4 : (nsrc <= 8 ? 2 : 1), 1);
+  if (tree) {
+    // radix-chain trees at U = 2 (5 <= leaves <= 8): the same staggered issue wins in the
+    // middle range (16 MiB x 8, '-2 -2 -2': 44.2 vs 47.4 us), bursts at the ends
+    if (nsrc > 4 && nsrc <= 8 && total_vectors >= (192L << 10) && total_vectors < (3L << 20)) return sched(2, 5);
+    return sched(nsrc <= 4 ? 4 : (nsrc <= 8 ? 2 : 1), 1);
+  }
   if (nsrc > 8) return sched(1, 1);
   if (fan) {
     if (total_vectors < (192L << 10)) return sched(2, 1);

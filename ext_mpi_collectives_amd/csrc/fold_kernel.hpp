@@ -205,7 +205,8 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_edge_kernel(const emac_bucket
 // linear, fan-out N (node / IPC form):  N <= 8 -> (U 2, burst), (U 4, burst), (U 4, s_sleep 2
 //                                        every 4 loads);  N > 8 -> (U 1, burst)
 // linear, fan-out 1 (comm form):        N <= 8 -> U in {1, 2}, burst;  N > 8 -> U = 1
-// tree (composite N), either fan-out:   U = 4 / 2 / 1 for N <= 4 / <= 8 / > 8, burst
+// tree (composite N), either fan-out:   U = 4 / 2 / 1 for N <= 4 / <= 8 / > 8, burst; U = 2 also
+//                                        with s_sleep 2 every 4 loads
 // (burst = ISSUE 1: every load of a tile back to back, source-major)
 constexpr int tree_unroll(int n) { return n <= 4 ? 4 : (n <= 8 ? 2 : 1); }
 constexpr int sched(int u, int issue) { return u | issue << 4; }
@@ -237,8 +238,11 @@ template <typename T, int N, bool FAN>
 int launch_nf(bool tree, int unroll, const Launch &L) {
   constexpr int D = FAN ? N : 1;
   if constexpr (can_tree(N)) {
-    if (tree) return unroll == sched(tree_unroll(N), 1) ? launch_one<T, N, tree_unroll(N), true, D>(L)
-                                                        : EMAC_ERR_UNSUPPORTED;
+    if (tree && unroll == sched(tree_unroll(N), 1)) return launch_one<T, N, tree_unroll(N), true, D>(L);
+    if constexpr (tree_unroll(N) == 2) {
+      if (tree && unroll == sched(2, 5)) return launch_one<T, N, 2, true, D, 5>(L);
+    }
+    if (tree) return EMAC_ERR_UNSUPPORTED;
   }
   if (tree) return EMAC_ERR_UNSUPPORTED;
   if constexpr (N > 8) {

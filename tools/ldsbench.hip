@@ -234,6 +234,15 @@ int main(int argc, char **argv) {
   memset(&codes, 0, sizeof(codes));
   codes.nlev = 1;
   codes.nleaf = R;
+  emac_codes tcodes;
+  memset(&tcodes, 0, sizeof(tcodes));
+  tcodes.nlev = 3;
+  tcodes.nleaf = R;
+  for (int t = 0; t < R; t++) {
+    for (int l = 0; l < 3; l++)
+      if (t % (2 << l) == 0) tcodes.first[t] |= (unsigned char)(1 << l);
+    tcodes.close[t] = t % 8 == 7 ? 3 : t % 4 == 3 ? 2 : t % 2 == 1 ? 1 : 0;
+  }
   f4 *ca;
   long cn = 2 * R * S / 16;  // same bytes as one fold launch moves
   CHECK(hipMalloc(&ca, 2 * cn * 16));
@@ -255,7 +264,11 @@ int main(int argc, char **argv) {
                        {"prod_u2", 0, {}},   {"prod_u4", 1, {}},   {"read_nt", 2, {}},  {"read_glds", 3, {}},
                        {"glds_u1", 4, {}},   {"glds_u2", 5, {}},   {"glds_pipe", 6, {}}, {"glds_pipe_g512", 7, {}},
                        {"copy_nt", 8, {}},   {"copy_glds", 9, {}}, {"fold_plainst_u2", 10, {}}};
-  if (quick) vs = {{"u2_src_burst", 21, {}}, {"u2_src_sleep1", 23, {}}, {"u2_src_sleep2", 25, {}},
+  if (getenv("LDSBENCH_TREE"))
+    vs = {{"tree_u2_burst", 41, {}}, {"tree_u2_sleep1", 43, {}}, {"tree_u2_sleep2", 45, {}},
+          {"tree_u2_sleep3", 47, {}}, {"tree_u4_burst", 51, {}}, {"tree_u4_sleep2", 55, {}},
+          {"u4_src_sleep2", 35, {}}, {"u2_src_burst", 21, {}}};
+  else if (quick) vs = {{"u2_src_burst", 21, {}}, {"u2_src_sleep1", 23, {}}, {"u2_src_sleep2", 25, {}},
                    {"u2_src_sleep3", 27, {}}, {"u4_src_burst", 31, {}}, {"u4_src_sleep1", 33, {}},
                    {"u4_src_sleep2", 35, {}}, {"u4_src_sleep3", 37, {}}, {"copy_nt", 8, {}}};
   auto run = [&](int kind, int set, int i) {
@@ -278,6 +291,21 @@ int main(int argc, char **argv) {
 #define ISS(i) case 20 + i: hipLaunchKernelGGL((emac::fold_kernel<float, R, 2, false, R, i>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, codes); break;
       switch (kind) { ISS(0) ISS(1) ISS(2) ISS(3) ISS(4) ISS(5) ISS(6) ISS(7) }
 #undef ISS
+      break;
+    }
+    case 41: case 43: case 45: case 47: case 51: case 55: {
+      // binary-tree codes (radix chain -2 -2 -2): the production TREE template, U = 2 or 4
+      const int U = kind >= 51 ? 4 : 2;
+      const long tpb = C / (256 * U);
+      const dim3 g((unsigned)std::min<long>(tpb * R, 8192));
+      switch (kind) {
+      case 41: hipLaunchKernelGGL((emac::fold_kernel<float, R, 2, true, R, 1>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, tcodes); break;
+      case 43: hipLaunchKernelGGL((emac::fold_kernel<float, R, 2, true, R, 3>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, tcodes); break;
+      case 45: hipLaunchKernelGGL((emac::fold_kernel<float, R, 2, true, R, 5>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, tcodes); break;
+      case 47: hipLaunchKernelGGL((emac::fold_kernel<float, R, 2, true, R, 7>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, tcodes); break;
+      case 51: hipLaunchKernelGGL((emac::fold_kernel<float, R, 4, true, R, 1>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, tcodes); break;
+      case 55: hipLaunchKernelGGL((emac::fold_kernel<float, R, 4, true, R, 5>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, tcodes); break;
+      }
       break;
     }
     case 31: case 33: case 35: case 37: {
@@ -327,6 +355,18 @@ int main(int argc, char **argv) {
       CHECK(hipStreamSynchronize(s));
       CHECK(hipMemcpy(kind ? got.data() : ref.data(), hb.dst[5], C * 16, hipMemcpyDeviceToHost));
       if (kind && memcmp(ref.data(), got.data(), C * 16)) printf("MISMATCH kind %d\n", kind);
+    }
+  }
+  {
+    std::vector<char> ref(C * 16), got(C * 16);
+    Bucket hb;
+    CHECK(hipMemcpy(&hb, dbk[0] + 3, sizeof(hb), hipMemcpyDeviceToHost));
+    for (int kind : {41, 43, 45, 47, 51, 55}) {
+      CHECK(hipMemset(hb.dst[5], 0, C * 16));
+      run(kind, 0, 0);
+      CHECK(hipStreamSynchronize(s));
+      CHECK(hipMemcpy(kind == 41 ? ref.data() : got.data(), hb.dst[5], C * 16, hipMemcpyDeviceToHost));
+      if (kind != 41 && memcmp(ref.data(), got.data(), C * 16)) printf("MISMATCH tree kind %d\n", kind);
     }
   }
   hipEvent_t e0, e1;
