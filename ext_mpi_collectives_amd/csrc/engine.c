@@ -575,7 +575,7 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
     nb++;
   }
   h->nsrc = R;
-  h->fan = R > 1;
+  h->fan = R > 1 ? 2 : 0; /* peer-mapped fan-out: system-coherent launch */
   rc = upload_buckets(h, b, nb);
   free(b);
   return rc;

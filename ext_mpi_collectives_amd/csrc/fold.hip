@@ -24,7 +24,7 @@
 #include "gpu.h"
 
 extern "C" {
-#define EMAC_DECL(n) int emac_fold_launch_##n(int nsrc, bool tree, bool fan, int unroll, const emac::Launch *L);
+#define EMAC_DECL(n) int emac_fold_launch_##n(int nsrc, bool tree, int fan, int unroll, const emac::Launch *L);
 EMAC_DECL(f32)
 EMAC_DECL(f64)
 EMAC_DECL(i32)
@@ -47,6 +47,10 @@ int emac_gpu_pick_unroll(int nsrc, int tree, int fan, long total_vectors) {
   // between them U = 4 with an s_sleep after every 4 loads is 4-8 % faster (16 MiB: 41.9 vs
   // 45.2-45.4 us); 64 MiB per rank prefers U = 2 (183 vs 194 us), >= 128 MiB U = 4.
   using emac::sched;
+  if (fan == 2) {  // peer-mapped (IPC) form: one system-coherent schedule per shape
+    if (tree && nsrc > 1) return sched(nsrc <= 4 ? 4 : (nsrc <= 8 ? 2 : 1), 1 | emac::kRemote);
+    return sched(nsrc > 8 ? 1 : 2, 1 | emac::kRemote);
+  }
   if (nsrc == 1) return total_vectors >= 2048L * EMAC_BLOCK * 2 ? sched(2, 1) : sched(1, 1);
   if (tree) {
     // radix-chain trees at U = 2 (5 <= leaves <= 8): the same staggered issue wins in the
@@ -67,7 +71,7 @@ int emac_gpu_pick_unroll(int nsrc, int tree, int fan, long total_vectors) {
 int emac_gpu_fold(int dtype, int op, int nsrc, int fan, int unroll, const emac_codes *codes,
                   const emac_bucket *d_buckets, int nb, long ntiles, long tiles_per_bucket, int all_full,
                   const emac_edge *d_edges, int nedges, void *stream) {
-  const bool tree = codes->nlev > 1;
+  const bool tree = codes->nlev > 1;  /* fan: 0 one destination, 1 node fan-out, 2 peer-mapped fan-out */
   const emac::Launch L = {codes, d_buckets, nb, ntiles, tiles_per_bucket, all_full, d_edges, nedges,
                           static_cast<hipStream_t>(stream)};
   if (op != EMAC_SUM) return EMAC_ERR_UNSUPPORTED;

@@ -2,6 +2,6 @@
 // that the kernel set compiles in parallel). See fold_kernel.hpp.
 #include "fold_kernel.hpp"
 
-extern "C" int emac_fold_launch_f64(int nsrc, bool tree, bool fan, int unroll, const emac::Launch *L) {
+extern "C" int emac_fold_launch_f64(int nsrc, bool tree, int fan, int unroll, const emac::Launch *L) {
   return emac::launch_t<double>(nsrc, tree, fan, unroll, *L);
 }

@@ -44,6 +44,26 @@ template <> struct Lane<long> {
 
 constexpr int kMaxLevels = 4;  // 16 leaves with radix >= 2
 
+// ISSUE bit 8: peer-mapped (IPC) launch. Leaves may live in another GPU's HBM and results are
+// stored into other GPUs' receive buffers, so every access is system-coherent: 16-byte buffer
+// loads / stores with sc0 sc1 (cache policy 17: no stale L2 line is ever returned, stores
+// write through to the owner's memory). This is what lets the node barriers around the fold
+// get away with a single fence each (ipc.hip).
+constexpr int kRemote = 256;
+constexpr int kSysCoherent = 17;  // sc0 | sc1
+typedef unsigned int U32x4 __attribute__((ext_vector_type(4)));
+
+template <typename V>
+__device__ __forceinline__ V sys_load16(const void *tile_base, unsigned byte_off) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(tile_base), 0, 0x7FFFFFF0, 0x00020000);
+  return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kSysCoherent));
+}
+template <typename V>
+__device__ __forceinline__ void sys_store16(void *tile_base, unsigned byte_off, V v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(tile_base, 0, 0x7FFFFFF0, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U32x4, v), r, byte_off, 0, kSysCoherent);
+}
+
 // a multi-level tree needs a composite leaf count (every radix >= 2)
 constexpr bool can_tree(int n) {
   for (int d = 2; d < n; ++d)
@@ -82,16 +102,28 @@ __device__ __forceinline__ X fold_leaves(const X (&x)[N], const emac_codes &c) {
 
 // D = fan-out width, a compile-time constant: N for the node form (every rank's receive
 // buffer), 1 for the communicator form. All destination pointers are then loaded up front.
-template <typename T, int N, bool TREE, int D>
+template <typename T, int N, bool TREE, int D, bool REMOTE = false>
 __device__ __forceinline__ void fold_scalar_element(const emac_bucket *b, long e, const emac_codes &c) {
   typedef typename Lane<T>::S S;
   const long k = e - b->head;  // bucket pointers sit at element `head`
   S x[N];
 #pragma unroll
-  for (int s = 0; s < N; ++s) x[s] = static_cast<const S *>(b->src[s])[k];
+  for (int s = 0; s < N; ++s) {
+    const S *p = static_cast<const S *>(b->src[s]) + k;
+    if constexpr (REMOTE)
+      x[s] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else
+      x[s] = *p;
+  }
   const S r = fold_leaves<N, TREE>(x, c);
 #pragma unroll
-  for (int d = 0; d < D; ++d) static_cast<S *>(b->dst[d])[k] = r;
+  for (int d = 0; d < D; ++d) {
+    S *p = static_cast<S *>(b->dst[d]) + k;
+    if constexpr (REMOTE)
+      __hip_atomic_store(p, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else
+      *p = r;
+  }
 }
 
 // Loads are nontemporal (each leaf byte is read exactly once; keeping it out of L2/MALL leaves
@@ -109,7 +141,8 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
   typedef typename Lane<T>::V V;
   typedef __attribute__((address_space(1))) V GV;
   constexpr bool SRC_MAJOR = ISSUE & 1;
-  constexpr int SLEEP = ISSUE >> 1;
+  constexpr int SLEEP = (ISSUE >> 1) & 127;
+  constexpr bool REMOTE = ISSUE & kRemote;
   // vectors of this tile still inside the bucket (wave-uniform); lane offsets are 32-bit so
   // every access is `global_*_dwordx4 v, v_off, s_base` with the tile base in SGPRs
   const long left = nvec - tile_base;
@@ -121,7 +154,11 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
   for (int k = 0; k < N * U; ++k) {
     const int s = SRC_MAJOR ? k / U : k % N, u = SRC_MAJOR ? k % U : k / N;
     const unsigned v = threadIdx.x + (unsigned)(u * EMAC_BLOCK);
-    if (FULL || (long)v < left) x[u][s] = __builtin_nontemporal_load(src[s] + v);
+    if constexpr (REMOTE) {
+      if (FULL || (long)v < left) x[u][s] = sys_load16<V>((const void *)src[s], v * 16u);
+    } else {
+      if (FULL || (long)v < left) x[u][s] = __builtin_nontemporal_load(src[s] + v);
+    }
     if constexpr (SLEEP > 0) {
       if ((k & 3) == 3 && k + 1 < N * U) __builtin_amdgcn_s_sleep(SLEEP);
     }
@@ -136,9 +173,16 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const unsigned v = threadIdx.x + (unsigned)(u * EMAC_BLOCK);
-      if (FULL || (long)v < left) __builtin_nontemporal_store(r[u], dst + v);
+      if constexpr (REMOTE) {
+        if (FULL || (long)v < left) sys_store16<V>((void *)dst, v * 16u, r[u]);
+      } else {
+        if (FULL || (long)v < left) __builtin_nontemporal_store(r[u], dst + v);
+      }
     }
   }
+  // a peer-mapped launch's stores are acknowledged by the owners' memory before the wave ends,
+  // so the barrier launch after it can signal without a release fence
+  if constexpr (REMOTE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // Streaming body: one workgroup per tile (grid-stride); a tile is EMAC_BLOCK*U consecutive
@@ -181,7 +225,7 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_kernel(const emac_bucket *__r
 }
 
 // Element-granular work: unaligned heads/tails and misaligned buckets, one workgroup per item.
-template <typename T, int N, bool TREE, int D>
+template <typename T, int N, bool TREE, int D, bool REMOTE = false>
 __global__ __launch_bounds__(EMAC_BLOCK) void fold_edge_kernel(const emac_bucket *__restrict__ bk,
                                                                const emac_edge *__restrict__ items,
                                                                emac_codes codes) {
@@ -190,14 +234,15 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_edge_kernel(const emac_bucket
   const emac_bucket *b = bk + it.bucket;
   if (it.mode == 1) {
     for (long e = it.start + threadIdx.x; e < it.start + it.count; e += EMAC_BLOCK)
-      fold_scalar_element<T, N, TREE, D>(b, e, codes);
+      fold_scalar_element<T, N, TREE, D, REMOTE>(b, e, codes);
   } else {
     const long nsc = b->head + b->tail;
     for (long i = threadIdx.x; i < nsc; i += EMAC_BLOCK) {
       const long e = i < b->head ? i : b->head + b->nvec * EPV + (i - b->head);
-      fold_scalar_element<T, N, TREE, D>(b, e, codes);
+      fold_scalar_element<T, N, TREE, D, REMOTE>(b, e, codes);
     }
   }
+  if constexpr (REMOTE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ---- instantiation policy (keep in sync with emac_gpu_pick_unroll in fold.hip) ----
@@ -210,6 +255,8 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_edge_kernel(const emac_bucket
 // (burst = ISSUE 1: every load of a tile back to back, source-major)
 constexpr int tree_unroll(int n) { return n <= 4 ? 4 : (n <= 8 ? 2 : 1); }
 constexpr int sched(int u, int issue) { return u | issue << 4; }
+// peer-mapped (IPC) launches: (U 2, burst) linear <= 8 leaves, (U 1) above, the tree's U for
+// composite trees -- all with system-coherent accesses (ISSUE | kRemote)
 
 struct Launch {
   const emac_codes *c;
@@ -229,14 +276,25 @@ int launch_one(const Launch &L) {
     hipLaunchKernelGGL((fold_kernel<T, N, U, TREE, D, ISSUE>), dim3((unsigned)grid), dim3(EMAC_BLOCK), 0, L.s, L.b,
                        L.nb, L.ntiles, L.tpb, L.all_full, *L.c);
   if (L.nedges > 0)
-    hipLaunchKernelGGL((fold_edge_kernel<T, N, TREE, D>), dim3((unsigned)L.nedges), dim3(EMAC_BLOCK), 0, L.s, L.b,
-                       L.edges, *L.c);
+    hipLaunchKernelGGL((fold_edge_kernel<T, N, TREE, D, (ISSUE & kRemote) != 0>), dim3((unsigned)L.nedges),
+                       dim3(EMAC_BLOCK), 0, L.s, L.b, L.edges, *L.c);
   return hipGetLastError() == hipSuccess ? 0 : EMAC_ERR_DEVICE;
 }
 
-template <typename T, int N, bool FAN>
+template <typename T, int N, bool FAN, bool REMOTE = false>
 int launch_nf(bool tree, int unroll, const Launch &L) {
   constexpr int D = FAN ? N : 1;
+  if constexpr (REMOTE) {
+    // peer-mapped launches: one schedule per shape (U = 2 linear up to 8 leaves, else the tree's
+    // or 1), system-coherent accesses
+    constexpr int UR = N > 8 ? 1 : 2;
+    if constexpr (can_tree(N)) {
+      if (tree) return unroll == sched(tree_unroll(N), 1 | kRemote) ? launch_one<T, N, tree_unroll(N), true, D, 1 | kRemote>(L)
+                                                                    : EMAC_ERR_UNSUPPORTED;
+    }
+    if (tree) return EMAC_ERR_UNSUPPORTED;
+    return unroll == sched(UR, 1 | kRemote) ? launch_one<T, N, UR, false, D, 1 | kRemote>(L) : EMAC_ERR_UNSUPPORTED;
+  }
   if constexpr (can_tree(N)) {
     if (tree && unroll == sched(tree_unroll(N), 1)) return launch_one<T, N, tree_unroll(N), true, D>(L);
     if constexpr (tree_unroll(N) == 2) {
@@ -258,18 +316,19 @@ int launch_nf(bool tree, int unroll, const Launch &L) {
   return EMAC_ERR_UNSUPPORTED;
 }
 
+// fan: 0 fan-out 1 (comm form), 1 fan-out N (node form), 2 fan-out N peer-mapped (IPC form)
 template <typename T, int N>
-int launch_n(bool tree, bool fan, int unroll, const Launch &L) {
+int launch_n(bool tree, int fan, int unroll, const Launch &L) {
   if constexpr (N == 1) {
-    return launch_nf<T, 1, false>(false, unroll, L);
+    return fan == 2 ? launch_nf<T, 1, false, true>(false, unroll, L) : launch_nf<T, 1, false>(false, unroll, L);
   } else {
-    return fan ? launch_nf<T, N, true>(tree, unroll, L)
-               : launch_nf<T, N, false>(tree, unroll, L);
+    return fan == 2 ? launch_nf<T, N, true, true>(tree, unroll, L)
+                    : fan ? launch_nf<T, N, true>(tree, unroll, L) : launch_nf<T, N, false>(tree, unroll, L);
   }
 }
 
 template <typename T>
-int launch_t(int nsrc, bool tree, bool fan, int unroll, const Launch &L) {
+int launch_t(int nsrc, bool tree, int fan, int unroll, const Launch &L) {
   switch (nsrc) {
 #define EMAC_CASE(n) \
   case n: return launch_n<T, n>(tree, fan, unroll, L);

@@ -65,7 +65,7 @@ int emac_gpu_device_sync(void);
    barrier phase (0: before the fold, 1: after it); arrive / xcc are this rank's own barrier
    bookkeeping (workgroup arrivals, XCC coverage by epoch parity). */
 #define EMAC_SYNC_SLOTS 1024
-#define EMAC_SYNC_WG 64 /* barrier workgroups: enough to land on every XCD */
+#define EMAC_SYNC_WG 16 /* barrier workgroups: dealt round-robin over the 8 XCDs (coverage is checked) */
 #define EMAC_IPC_HANDLE_BYTES 64
 typedef struct {
   unsigned long flags[EMAC_SYNC_SLOTS][2][EMAC_MAX_RANKS];

@@ -11,10 +11,12 @@
 //   node_barrier(in)  -> fold over peer-mapped leaves, fan-out into every peer's recv -> node_barrier(out)
 //
 // Visibility across GPUs: every XCD of a gfx950 has its own L2, and the L2 is neither written
-// back nor invalidated for other agents by plain stores/loads. A barrier workgroup therefore
-// runs a system-scope release (L2 write-back of its XCD) before it arrives and a system-scope
-// acquire (L2 invalidate) after the wait, and the barrier is launched wide enough to cover
-// every XCD: the workgroups OR their XCC id into a mask, and the rank's last arriver checks the
+// back nor invalidated for other agents by plain stores/loads. The fold between the barriers
+// is system-coherent by itself (sc0 sc1 loads and write-through stores), so what remains is
+// the application's side: before the fold a barrier workgroup runs a system-scope release
+// (L2 write-back of its XCD: the send buffer the peers will read), after it a system-scope
+// acquire (L2 invalidate: the receive buffer the peers have written), and the barrier is
+// launched wide enough to cover every XCD: the workgroups OR their XCC id into a mask, and the rank's last arriver checks the
 // mask against the census taken at communicator set-up before it signals the peers (a missed
 // XCD is reported as a transport error instead of silently risking stale lines). Flags live in
 // uncached device memory and are written with system-scope atomics: one 8-byte word per
@@ -41,23 +43,33 @@ __global__ void xcc_census_kernel(unsigned *mask) {
 }
 
 // One lane per workgroup does the protocol; the workgroup count is EMAC_SYNC_WG.
+// Fences by phase. Before the fold (phase 0) only a release is needed: the application's
+// stores into this rank's send buffer may sit dirty in any XCD's L2, and the peers read that
+// buffer from memory. After the fold (phase 1) only an acquire: the peers' fan-out stores have
+// landed in this rank's receive buffer behind its L2s. The fold itself needs neither: its
+// accesses are system-coherent (sc0 sc1 loads, write-through stores drained before each wave
+// ends; fold_kernel.hpp kRemote).
 __global__ __launch_bounds__(64) void node_barrier_kernel(emac_sync *self, emac_sync *const *peers, int slot,
                                                           int phase, unsigned long epoch, int nranks, int me,
                                                           unsigned xcc_expect, int *err, long timeout) {
   if (threadIdx.x != 0) return;
-  // release: every store this GPU made before the barrier (the fold's fan-out into the peers'
-  // receive buffers, the application's writes into the send buffer) leaves this XCD's L2
-  __threadfence_system();
+  if (phase == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: L2 write-back
+    // hipcc drops the wait behind buffer_wbl2 when nothing else is outstanding
+    // (MI355X_MICROARCH.md, compiler hazard): the arrival below must follow the write-back
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   atomicOr(&self->xcc[slot][phase][epoch & 1], 1u << xcc_id());
   const unsigned long arrived =
-      __hip_atomic_fetch_add(&self->arrive[slot][phase], 1ul, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&self->arrive[slot][phase], 1ul, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // (relaxed: the release above has already drained -- s_waitcnt after buffer_wbl2 -- before
+  // this add issues, so the last arriver's signal follows every workgroup's write-back)
   if (arrived == epoch * gridDim.x - 1) {  // last workgroup of this rank: every XCD has released
     const unsigned seen = __hip_atomic_load(&self->xcc[slot][phase][epoch & 1], __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
     if ((seen & xcc_expect) != xcc_expect) __hip_atomic_fetch_or(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // next epoch's mask (the barrier of a slot and phase runs on one stream: no overlap)
     __hip_atomic_store(&self->xcc[slot][phase][(epoch + 1) & 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __threadfence_system();
     for (int q = 0; q < nranks; ++q)
       if (q != me)
         __hip_atomic_store(&peers[q]->flags[slot][phase][me], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -74,8 +86,11 @@ __global__ __launch_bounds__(64) void node_barrier_kernel(emac_sync *self, emac_
     }
   }
   // acquire: lines of this XCD's L2 that the peers have since rewritten (their fan-out into
-  // this rank's receive buffer, their send buffers) are dropped
-  __threadfence_system();
+  // this rank's receive buffer) are dropped
+  if (phase == 1) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: L2 invalidate
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // completed before the launch ends
+  }
 }
 
 }  // namespace
