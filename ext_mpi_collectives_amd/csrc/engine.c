@@ -39,14 +39,29 @@
 
 enum { KIND_NODE = 1, KIND_COMM = 2, KIND_IPC = 3 };
 
-/* one peer allocation mapped into this process (hipIpcOpenMemHandle), shared by the handles
-   that reference it */
+/* one peer allocation mapped into this process (hipIpcOpenMemHandle), shared by the handles that
+   reference the same allocation (the exporter's allocation id and size) and closed when the last
+   of them is done, as the reference closes its cudaIpc mappings in EXT_MPI_Done
+   (src/gpu/cuda_shmem.c:301-314). */
 typedef struct {
   int peer;
+  unsigned long long buf_id;
+  long extent;
   unsigned char handle[EMAC_IPC_HANDLE_BYTES];
   void *base;
   int refs;
 } ipc_map;
+
+/* device mirrors of host buffers in the IPC form: exported to the peers, so they are never
+   freed while a peer may still map them -- they return to this per-communicator pool at handle
+   done and are released only by the (collective) communicator free. Freeing an exported
+   allocation before every importer has closed it is undefined behaviour in HIP and was
+   measured to corrupt the exporter's later allocations (8 ranks on one GPU). */
+typedef struct {
+  void *p;
+  size_t bytes;
+  int busy;
+} ipc_mirror;
 
 typedef struct {
   int used;
@@ -68,6 +83,8 @@ typedef struct {
   unsigned long slot_epoch[EMAC_SYNC_SLOTS][2]; /* a slot's epochs continue across its handles */
   ipc_map *maps;
   int nmaps;
+  ipc_mirror *mirrors;
+  int nmirrors;
 } emac_comm;
 
 /* Loopback groups: every rank of the communicator lives in this process; the i-th handle a
@@ -130,6 +147,7 @@ static int new_handle_slot(void) {
 }
 
 static void ipc_unmap(emac_comm *cm, void *base);
+static void mirror_free(emac_handle *h, void *p);
 
 static void release(emac_handle *h) {
   int r;
@@ -143,8 +161,8 @@ static void release(emac_handle *h) {
   emac_gpu_free(h->staging);
   for (r = 0; r < h->nbuf; r++) {
     int same = h->dsend[r] == h->drecv[r];
-    if (h->send_mirror[r]) emac_gpu_free(h->dsend[r]);
-    if (h->recv_mirror[r] && !(same && h->send_mirror[r])) emac_gpu_free(h->drecv[r]);
+    if (h->send_mirror[r]) mirror_free(h, h->dsend[r]);
+    if (h->recv_mirror[r] && !(same && h->send_mirror[r])) mirror_free(h, h->drecv[r]);
     if (h->send_reg[r]) emac_gpu_host_unregister(h->user_send[r]);
     if (h->recv_reg[r]) emac_gpu_host_unregister(h->user_recv[r]);
   }
@@ -160,27 +178,59 @@ static void release(emac_handle *h) {
   free(h);
 }
 
-/* Device view of rank r's buffers: user device pointers are used in place; host buffers get
-   a device mirror (in place stays in place) and are page-locked for async DMA. */
+static int ipc_mirror_get(emac_comm *cm, void **p, size_t bytes);
+static void ipc_mirror_put(emac_comm *cm, void *p);
+
+static int mirror_alloc(emac_handle *h, void **p) {
+  if (h->kind == KIND_IPC) return ipc_mirror_get(&comms[h->comm], p, h->bytes);
+  return emac_gpu_malloc(p, h->bytes);
+}
+
+static void mirror_free(emac_handle *h, void *p) {
+  if (h->kind == KIND_IPC)
+    ipc_mirror_put(&comms[h->comm], p);
+  else
+    emac_gpu_free(p);
+}
+
+/* A buffer the handle can use in place: device memory, and in the IPC form also exportable as a
+   whole allocation (emac_gpu_ipc_exportable). Anything else gets a device mirror. */
+static int in_place_ok(const emac_handle *h, const void *p) {
+  if (!emac_gpu_is_device_pointer(p)) return 0;
+  return h->kind != KIND_IPC || emac_gpu_ipc_exportable(p);
+}
+
+/* Page-lock a host buffer for async DMA, except in the IPC form: a process that has imported
+   its peers' memory (dmabuf) and also holds registered user pages was measured to receive an
+   asynchronous illegal-address error a few handles after the registration was dropped (8
+   processes on one MI355X, every transfer already complete); unregistered buffers are staged by
+   the runtime instead. EXT_MPI_AMD_NO_HOST_REGISTER turns registration off everywhere. */
+static int host_register(const emac_handle *h, const void *p) {
+  if (h->kind == KIND_IPC || emac_gpu_is_device_pointer(p)) return 0;
+  return emac_gpu_host_register((void *)p, h->bytes) == 0;
+}
+
+/* Device view of rank r's buffers: usable user device pointers are used in place; other buffers
+   get a device mirror (in place stays in place), staged in and out on the handle's stream. */
 static int map_buffers(emac_handle *h, int r, const void *send, void *recv) {
   int rc;
   h->user_send[r] = (void *)send;
   h->user_recv[r] = recv;
-  if (emac_gpu_is_device_pointer(recv)) {
+  if (in_place_ok(h, recv)) {
     h->drecv[r] = recv;
   } else {
-    if ((rc = emac_gpu_malloc(&h->drecv[r], h->bytes))) return rc;
+    if ((rc = mirror_alloc(h, &h->drecv[r]))) return rc;
     h->recv_mirror[r] = 1;
-    h->recv_reg[r] = emac_gpu_host_register(recv, h->bytes) == 0;
+    h->recv_reg[r] = host_register(h, recv);
   }
   if (send == recv) {
     h->dsend[r] = h->drecv[r];
-  } else if (emac_gpu_is_device_pointer(send)) {
+  } else if (in_place_ok(h, send)) {
     h->dsend[r] = (void *)send;
   } else {
-    if ((rc = emac_gpu_malloc(&h->dsend[r], h->bytes))) return rc;
+    if ((rc = mirror_alloc(h, &h->dsend[r]))) return rc;
     h->send_mirror[r] = 1;
-    h->send_reg[r] = emac_gpu_host_register((void *)send, h->bytes) == 0;
+    h->send_reg[r] = host_register(h, send);
   }
   return 0;
 }
@@ -391,16 +441,20 @@ static int ipc_agree(emac_comm *cm, int ok_local) {
   return 0;
 }
 
-static void *ipc_map_peer(emac_comm *cm, int peer, const unsigned char *handle) {
+static void *ipc_map_peer(emac_comm *cm, int peer, const unsigned char *handle, unsigned long long buf_id,
+                          long extent) {
   int i;
   void *base;
-  for (i = 0; i < cm->nmaps; i++)
-    if (cm->maps[i].refs > 0 && cm->maps[i].peer == peer && !memcmp(cm->maps[i].handle, handle, EMAC_IPC_HANDLE_BYTES)) {
-      cm->maps[i].refs++;
-      return cm->maps[i].base;
+  for (i = 0; i < cm->nmaps; i++) {
+    ipc_map *m = &cm->maps[i];
+    if (m->base && m->peer == peer && m->extent == extent &&
+        (buf_id ? m->buf_id == buf_id : !memcmp(m->handle, handle, EMAC_IPC_HANDLE_BYTES))) {
+      m->refs++;
+      return m->base;
     }
+  }
   if (emac_gpu_ipc_open(handle, &base)) return NULL;
-  for (i = 0; i < cm->nmaps && cm->maps[i].refs > 0; i++);
+  for (i = 0; i < cm->nmaps && cm->maps[i].base; i++);
   if (i == cm->nmaps) {
     ipc_map *m = (ipc_map *)realloc(cm->maps, sizeof(ipc_map) * (size_t)(cm->nmaps + 1));
     if (!m) {
@@ -411,6 +465,8 @@ static void *ipc_map_peer(emac_comm *cm, int peer, const unsigned char *handle) 
     cm->nmaps++;
   }
   cm->maps[i].peer = peer;
+  cm->maps[i].buf_id = buf_id;
+  cm->maps[i].extent = extent;
   memcpy(cm->maps[i].handle, handle, EMAC_IPC_HANDLE_BYTES);
   cm->maps[i].base = base;
   cm->maps[i].refs = 1;
@@ -421,18 +477,55 @@ static void ipc_unmap(emac_comm *cm, void *base) {
   int i;
   for (i = 0; i < cm->nmaps; i++)
     if (cm->maps[i].refs > 0 && cm->maps[i].base == base) {
-      if (--cm->maps[i].refs == 0) emac_gpu_ipc_close(base);
+      if (--cm->maps[i].refs == 0) {
+        emac_gpu_ipc_close(base);
+        cm->maps[i].base = NULL;
+      }
       return;
     }
 }
 
+static int ipc_mirror_get(emac_comm *cm, void **p, size_t bytes) {
+  int i, best = -1, rc;
+  for (i = 0; i < cm->nmirrors; i++)
+    if (!cm->mirrors[i].busy && cm->mirrors[i].bytes >= bytes &&
+        (best < 0 || cm->mirrors[i].bytes < cm->mirrors[best].bytes))
+      best = i;
+  if (best < 0) {
+    ipc_mirror *m = (ipc_mirror *)realloc(cm->mirrors, sizeof(ipc_mirror) * (size_t)(cm->nmirrors + 1));
+    if (!m) return EMAC_ERR_MALLOC;
+    cm->mirrors = m;
+    best = cm->nmirrors;
+    bytes = (bytes + EMAC_IPC_GRANULE - 1) / EMAC_IPC_GRANULE * EMAC_IPC_GRANULE; /* never sub-allocated */
+    if ((rc = emac_gpu_malloc(&m[best].p, bytes))) return rc;
+    m[best].bytes = bytes;
+    cm->nmirrors++;
+  }
+  cm->mirrors[best].busy = 1;
+  *p = cm->mirrors[best].p;
+  return 0;
+}
+
+static void ipc_mirror_put(emac_comm *cm, void *p) {
+  int i;
+  for (i = 0; i < cm->nmirrors; i++)
+    if (cm->mirrors[i].p == p) cm->mirrors[i].busy = 0;
+}
+
+static int ipc_agree(emac_comm *cm, int ok_local);
+
+/* Collective: every rank first closes its mappings of the others' memory, then all agree, and
+   only then is this rank's exported memory (synchronisation block, mirror pool) freed. */
 static void ipc_comm_release(emac_comm *cm) {
   int r;
   for (r = 0; r < cm->size; r++)
     if (r != cm->rank && cm->peer_sync_base[r]) emac_gpu_ipc_close(cm->peer_sync_base[r]);
   for (r = 0; r < cm->nmaps; r++)
-    if (cm->maps[r].refs > 0) emac_gpu_ipc_close(cm->maps[r].base);
+    if (cm->maps[r].base) emac_gpu_ipc_close(cm->maps[r].base);
   free(cm->maps);
+  if (cm->ag && cm->size > 1) ipc_agree(cm, 1);
+  for (r = 0; r < cm->nmirrors; r++) emac_gpu_free(cm->mirrors[r].p);
+  free(cm->mirrors);
   emac_gpu_free(cm->d_peer_sync);
   emac_gpu_free(cm->sync);
   emac_gpu_host_free(cm->err);
@@ -442,6 +535,8 @@ static void ipc_comm_release(emac_comm *cm) {
 typedef struct {
   unsigned char handle[EMAC_IPC_HANDLE_BYTES];
   long offset;
+  long extent; /* bytes of the exported allocation: the importer's mapping must match */
+  unsigned long long buf_id; /* the exporter's allocation id (0: unknown) */
   int status;
   unsigned char free_slots[EMAC_SYNC_SLOTS / 8]; /* handle set-up: slots this rank can use */
 } ipc_export;
@@ -522,6 +617,13 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
   if (!rc && !empty) rc = map_buffers(h, 0, sendbuf, recvbuf);
   if (!rc && !empty) rc = emac_gpu_ipc_export(h->dsend[0], mine[0].handle, &mine[0].offset);
   if (!rc && !empty) rc = emac_gpu_ipc_export(h->drecv[0], mine[1].handle, &mine[1].offset);
+  if (!rc && !empty) {
+    void *b0, *b1;
+    mine[0].extent = emac_gpu_alloc_extent(h->dsend[0], &b0);
+    mine[1].extent = emac_gpu_alloc_extent(h->drecv[0], &b1);
+    mine[0].buf_id = emac_gpu_buffer_id(b0);
+    mine[1].buf_id = emac_gpu_buffer_id(b1);
+  }
   for (r = 0; r < EMAC_SYNC_SLOTS; r++)
     if (!cm->slot_used[r]) mine[0].free_slots[r >> 3] |= (unsigned char)(1u << (r & 7));
   mine[0].status = rc == 0;
@@ -542,13 +644,28 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
       continue;
     }
     for (t = 0; t < 2 && !rc; t++) {
-      void *base = ipc_map_peer(cm, r, all[2 * r + t].handle);
+      void *base = ipc_map_peer(cm, r, all[2 * r + t].handle, all[2 * r + t].buf_id, all[2 * r + t].extent), *ext_base;
+      long extent;
       if (!base) {
         rc = EMAC_ERR_TRANSPORT;
         break;
       }
       h->mapped[h->nmapped++] = base;
       (t ? precv : psend)[r] = (char *)base + all[2 * r + t].offset;
+      /* the mapping must hold the peer's whole buffer: never launch over a short mapping */
+      extent = emac_gpu_alloc_extent(base, &ext_base);
+      if (extent < 0 || ext_base != base || extent != all[2 * r + t].extent || all[2 * r + t].offset < 0 ||
+          all[2 * r + t].offset + (long)h->bytes > extent)
+        rc = EMAC_ERR_TRANSPORT;
+      if (getenv("EXT_MPI_AMD_DEBUG_IPC")) {
+        const unsigned char *hb = all[2 * r + t].handle;
+        fprintf(stderr,
+                "ipc rank %d: peer %d %s handle %02x%02x%02x%02x%02x%02x%02x%02x.. id %llu base %p extent %ld "
+                "(exported %ld) offset %ld bytes %zu -> %s\n",
+                cm->rank, r, t ? "recv" : "send", hb[0], hb[1], hb[2], hb[3], hb[4], hb[5], hb[6], hb[7],
+                all[2 * r + t].buf_id, base, extent, all[2 * r + t].extent, all[2 * r + t].offset, h->bytes,
+                rc ? "REJECTED" : "ok");
+      }
     }
   }
   /* every rank opened every mapping before anyone proceeds */
@@ -576,6 +693,9 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
   }
   h->nsrc = R;
   h->fan = R > 1 ? 2 : 0; /* peer-mapped fan-out: system-coherent launch */
+  if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
+    fprintf(stderr, "ipc rank %d: own send %p recv %p bytes %zu, %d buckets, slot %d\n", cm->rank, h->dsend[0],
+            h->drecv[0], h->bytes, nb, slot);
   rc = upload_buckets(h, b, nb);
   free(b);
   return rc;

@@ -17,6 +17,8 @@
 // bit-identical to the reference's x86 behaviour without signed-overflow UB); float/double
 // keep IEEE round-to-nearest with denormals (no fast-math, no FTZ flags at build time).
 #include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -34,7 +36,19 @@ EMAC_DECL(i64)
 
 namespace {
 
-inline int ok(hipError_t e) { return e == hipSuccess ? 0 : EMAC_ERR_DEVICE; }
+/* EXT_MPI_AMD_DEBUG_HIP=1: report every failing HIP call (and every error cleared after a
+   failed probe) on stderr */
+inline int ok_at(hipError_t e, const char *what) {
+  if (e == hipSuccess) return 0;
+  if (getenv("EXT_MPI_AMD_DEBUG_HIP")) fprintf(stderr, "ext_mpi_amd: %s -> %s\n", what, hipGetErrorString(e));
+  return EMAC_ERR_DEVICE;
+}
+#define ok(e) ok_at((e), #e)
+inline void clear_error(const char *what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess && getenv("EXT_MPI_AMD_DEBUG_HIP"))
+    fprintf(stderr, "ext_mpi_amd: %s: cleared %s\n", what, hipGetErrorString(e));
+}
 
 }  // namespace
 
@@ -112,22 +126,23 @@ int emac_gpu_is_device_pointer(const void *p) {
   hipPointerAttribute_t a;
   if (!p) return 0;
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-    (void)hipGetLastError();  // unregistered host memory: clear the sticky error
+    clear_error("emac_gpu_is_device_pointer");  // unregistered host memory: clear the sticky error
     return 0;
   }
   return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 int emac_gpu_host_register(void *p, size_t bytes) {
   if (!bytes) return 0;
+  if (getenv("EXT_MPI_AMD_NO_HOST_REGISTER")) return EMAC_ERR_DEVICE;
   if (hipHostRegister(p, bytes, hipHostRegisterDefault) != hipSuccess) {
-    (void)hipGetLastError();
+    clear_error("emac_gpu_host_register");
     return EMAC_ERR_DEVICE;
   }
   return 0;
 }
 int emac_gpu_host_unregister(void *p) {
   if (hipHostUnregister(p) != hipSuccess) {
-    (void)hipGetLastError();
+    clear_error("emac_gpu_host_unregister");
     return EMAC_ERR_DEVICE;
   }
   return 0;
@@ -144,7 +159,7 @@ int emac_gpu_stream_query(void *stream) {
   hipError_t e = hipStreamQuery(static_cast<hipStream_t>(stream));
   if (e == hipSuccess) return 1;
   if (e == hipErrorNotReady) {
-    (void)hipGetLastError();
+    clear_error("emac_gpu_stream_query");
     return 0;
   }
   return EMAC_ERR_DEVICE;
@@ -170,7 +185,7 @@ int ext_mpi_amd_gpu_device_count(void) { return emac_gpu_device_count(); }
 int ext_mpi_amd_gpu_device_of(const void *p) {
   hipPointerAttribute_t a;
   if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
-    (void)hipGetLastError();
+    clear_error("ext_mpi_amd_gpu_device_of");
     return -1;
   }
   return (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) ? a.device : -1;

@@ -76,7 +76,11 @@ typedef struct {
 int emac_gpu_ipc_export(const void *p, void *handle, long *offset); /* handle of p's allocation + offset */
 int emac_gpu_ipc_open(const void *handle, void **base);
 int emac_gpu_ipc_close(void *base);
-int emac_gpu_malloc_uncached(void **p, size_t bytes); /* zeroed */
+long emac_gpu_alloc_extent(const void *p, void **base); /* bytes of the allocation holding p, or -1 */
+unsigned long long emac_gpu_buffer_id(const void *p);   /* unique id of the allocation, 0 if unknown */
+#define EMAC_IPC_GRANULE (2ul << 20) /* exported allocations: 2 MiB aligned, 2 MiB multiples */
+int emac_gpu_ipc_exportable(const void *p); /* p lies in an allocation of IPC granularity */
+int emac_gpu_malloc_uncached(void **p, size_t bytes); /* zeroed, rounded up to EMAC_IPC_GRANULE */
 int emac_gpu_host_alloc_mapped(void **p, size_t bytes); /* pinned, device-visible, zeroed */
 int emac_gpu_host_free(void *p);
 int emac_gpu_xcc_census(unsigned *mask); /* XCCs a wide launch lands on */

@@ -23,6 +23,8 @@
 // (handle slot, phase, peer), holding the last epoch that peer signalled. Every wait is bounded
 // by a wall-clock timeout that sets an error word in pinned host memory and lets the kernel end.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -30,7 +32,19 @@
 
 namespace {
 
-inline int ok(hipError_t e) { return e == hipSuccess ? 0 : EMAC_ERR_DEVICE; }
+/* EXT_MPI_AMD_DEBUG_HIP=1: report every failing HIP call (and every error cleared after a
+   failed probe) on stderr */
+inline int ok_at(hipError_t e, const char *what) {
+  if (e == hipSuccess) return 0;
+  if (getenv("EXT_MPI_AMD_DEBUG_HIP")) fprintf(stderr, "ext_mpi_amd: %s -> %s\n", what, hipGetErrorString(e));
+  return EMAC_ERR_DEVICE;
+}
+#define ok(e) ok_at((e), #e)
+inline void clear_error(const char *what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess && getenv("EXT_MPI_AMD_DEBUG_HIP"))
+    fprintf(stderr, "ext_mpi_amd: %s: cleared %s\n", what, hipGetErrorString(e));
+}
 
 __device__ __forceinline__ unsigned xcc_id() {
   unsigned v;
@@ -101,12 +115,12 @@ int emac_gpu_ipc_export(const void *p, void *handle, long *offset) {
   void *base = nullptr;
   size_t size = 0;
   if (hipMemGetAddressRange(&base, &size, const_cast<void *>(p)) != hipSuccess) {
-    (void)hipGetLastError();
+    clear_error("emac_gpu_ipc_export");
     return EMAC_ERR_ARG;
   }
   hipIpcMemHandle_t h;
   if (hipIpcGetMemHandle(&h, base) != hipSuccess) {
-    (void)hipGetLastError();
+    clear_error("emac_gpu_ipc_export");
     return EMAC_ERR_TRANSPORT;
   }
   memcpy(handle, &h, sizeof(h));
@@ -118,7 +132,7 @@ int emac_gpu_ipc_open(const void *handle, void **base) {
   hipIpcMemHandle_t h;
   memcpy(&h, handle, sizeof(h));
   if (hipIpcOpenMemHandle(base, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
-    (void)hipGetLastError();
+    clear_error("emac_gpu_ipc_open");
     *base = nullptr;
     return EMAC_ERR_TRANSPORT;
   }
@@ -127,10 +141,45 @@ int emac_gpu_ipc_open(const void *handle, void **base) {
 
 int emac_gpu_ipc_close(void *base) { return base ? ok(hipIpcCloseMemHandle(base)) : 0; }
 
+unsigned long long emac_gpu_buffer_id(const void *p) {
+  unsigned long long id = 0;
+  if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)p) != hipSuccess) {
+    clear_error("emac_gpu_buffer_id");
+    return 0;
+  }
+  return id;
+}
+
+long emac_gpu_alloc_extent(const void *p, void **base) {
+  size_t size = 0;
+  *base = nullptr;
+  if (hipMemGetAddressRange(base, &size, const_cast<void *>(p)) != hipSuccess) {
+    clear_error("emac_gpu_alloc_extent");
+    return -1;
+  }
+  return (long)size;
+}
+
+/* Only a whole allocation of IPC granularity is exported: the runtime sub-allocates small
+   hipMallocs out of a shared 2 MiB chunk, and importing such a buffer maps the exporter's whole
+   chunk into the peers; on one MI355X shared by 8 processes that was followed by illegal-address
+   faults in importers a few handles later. A buffer that is not the start of a 2 MiB-aligned
+   allocation of a 2 MiB multiple goes through a pooled mirror instead (engine.c). */
+int emac_gpu_ipc_exportable(const void *p) {
+  void *base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, const_cast<void *>(p)) != hipSuccess) {
+    clear_error("emac_gpu_ipc_exportable");
+    return 0;
+  }
+  return ((uintptr_t)base & (EMAC_IPC_GRANULE - 1)) == 0 && size % EMAC_IPC_GRANULE == 0;
+}
+
 int emac_gpu_malloc_uncached(void **p, size_t bytes) {
   *p = nullptr;
+  bytes = (bytes + EMAC_IPC_GRANULE - 1) / EMAC_IPC_GRANULE * EMAC_IPC_GRANULE; /* exported whole */
   if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached) != hipSuccess) {
-    (void)hipGetLastError();
+    clear_error("emac_gpu_malloc_uncached");
     return EMAC_ERR_MALLOC;
   }
   if (hipMemset(*p, 0, bytes) != hipSuccess) return EMAC_ERR_DEVICE;
@@ -140,7 +189,7 @@ int emac_gpu_malloc_uncached(void **p, size_t bytes) {
 int emac_gpu_host_alloc_mapped(void **p, size_t bytes) {
   *p = nullptr;
   if (hipHostMalloc(p, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
-    (void)hipGetLastError();
+    clear_error("emac_gpu_host_alloc_mapped");
     return EMAC_ERR_MALLOC;
   }
   memset(*p, 0, bytes);

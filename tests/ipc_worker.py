@@ -6,6 +6,7 @@ one line per case. Several ranks may share one GPU: the hipIpc mappings, the bar
 the fan-out stores are then the same code the 8-GPU node runs, over the one device's memory.
 Exit status 0 iff every case matched.
 """
+import ctypes
 import os
 import sys
 
@@ -30,9 +31,16 @@ def cases(R):
            (emac.INT, 65536 * R + 5, full, False, False, 1), (emac.LONG, 777, full, False, False, 1),
            (emac.FLOAT, 1, full, False, False, 1), (emac.FLOAT, 0, full, False, False, 1),
            (emac.FLOAT, 100000, full, True, False, 2), (emac.DOUBLE, 33333, full, False, True, 2),
-           (emac.FLOAT, 5000, f"6;-64 -{R} {R}", False, False, 1), (emac.FLOAT, 70001, f"6;3 -{R} {R}", False, False, 1)]
+           (emac.FLOAT, 5000, f"6;-64 -{R} {R}", False, False, 1), (emac.FLOAT, 70001, f"6;3 -{R} {R}", False, False, 1),
+           # small raw hipMalloc buffers (sub-allocated by the runtime: not exported, staged through mirrors)
+           (emac.INT, 12345, full, False, "raw", 2), (emac.FLOAT, 3001, full, True, "raw", 1)]
     if R == 4:
         out += [(emac.FLOAT, 123457, "6;1 -2 -2 2 2", False, False, 2), (emac.DOUBLE, 54321, "6;1 -2 2 1 2 1 -2 2", False, False, 1)]
+    if R == 8:
+        out += [(emac.FLOAT, 262147, "6;1 -2 -2 -2 2 2 2", False, False, 2), (emac.DOUBLE, 100001, "6;1 -4 -2 2 4", False, False, 1),
+                (emac.LONG, 65539, "6;1 -4 4 1 4 1 -2 2", False, False, 1), (emac.FLOAT, 4 << 20, full, False, False, 1)]
+    if R == 3:
+        out += [(emac.DOUBLE, 99999, "6;2 -3 3", True, False, 2)]
     return out
 
 
@@ -43,10 +51,23 @@ def main():
     dist.init_process_group("gloo")
     comm = emac.comm_init_ipc(rank, world, emac.torch_allgather(), dev)
     failures = 0
-    for k, (code, count, copyin, in_place, host, repeats) in enumerate(cases(world)):
+    only = os.environ.get("IPC_CASES")  # diagnosis: comma-separated case indices, in order, repeats allowed
+    order = [int(x) for x in only.split(",")] if only else list(range(len(cases(world))))
+    for k in order:
+        code, count, copyin, in_place, host, repeats = cases(world)[k]
         sends = xorshift_inputs(world, count, code, seed_base=0x1C0000 + 97 * k)
         want = oracle.allreduce(sends, copyin, in_place=in_place)[rank]
-        if host:
+        raw = host == "raw"
+        if raw:
+            L, nbytes = emac.lib(), sends[rank].nbytes
+            dsend, drecv = ctypes.c_void_p(), ctypes.c_void_p()
+            assert L.ext_mpi_amd_gpu_malloc(ctypes.byref(dsend), nbytes) == 0
+            if in_place:
+                drecv = dsend
+            else:
+                assert L.ext_mpi_amd_gpu_malloc(ctypes.byref(drecv), nbytes) == 0
+            h = emac.allreduce_init(dsend.value, drecv.value, count, code, comm, copyin)
+        elif host:
             hsend = sends[rank].copy()
             hrecv = np.full_like(hsend, -1)
             h = emac.allreduce_init(hsend.ctypes.data, hrecv.ctypes.data, count, code, comm, copyin)
@@ -56,17 +77,35 @@ def main():
             h = emac.allreduce_init(send.data_ptr(), recv.data_ptr(), count, code, comm, copyin)
         ok = True
         for _ in range(repeats):
-            if in_place:
+            if raw:
+                src = np.ascontiguousarray(sends[rank])
+                assert L.ext_mpi_amd_gpu_memcpy_hd(dsend, src.ctypes.data, nbytes) == 0
+            elif in_place:
                 send.copy_(torch.from_numpy(sends[rank]))
             torch.cuda.synchronize()
             emac.start(h)
             emac.wait(h)
-            got = hrecv if host else recv.cpu().numpy()
+            if raw:
+                got = np.empty_like(want)
+                assert L.ext_mpi_amd_gpu_memcpy_dh(got.ctypes.data, drecv, nbytes) == 0
+            else:
+                got = hrecv if host else recv.cpu().numpy()
             ok &= bool(np.array_equal(got.view(np.uint8), want.view(np.uint8)))
         emac.done(h)
+        if os.environ.get("IPC_SYNC_AFTER_DONE"):  # diagnosis: surface an asynchronous fault at its case
+            torch.cuda.synchronize()
+        if raw:
+            L.ext_mpi_amd_gpu_free(dsend)
+            if not in_place:
+                L.ext_mpi_amd_gpu_free(drecv)
         failures += not ok
         print(f"IPC rank {rank}/{world} case {k} code {code} count {count} '{copyin}' in_place={in_place} "
               f"host={host} x{repeats}: {'ok' if ok else 'MISMATCH'}", flush=True)
+    if os.environ.get("IPC_CASES_ONLY"):
+        emac.comm_free(comm)
+        dist.barrier()
+        dist.destroy_process_group()
+        sys.exit(1 if failures else 0)
     # several handles in flight on separate streams, started in the same order on every rank
     hs, bufs = [], []
     for j in range(3):

@@ -33,7 +33,7 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_ipc_ranks_share_one_gpu(world):
     port = _port()
     procs = []
@@ -45,7 +45,7 @@ def test_ipc_ranks_share_one_gpu(world):
     outs, codes = [], []
     for p in procs:
         try:
-            out, _ = p.communicate(timeout=100)
+            out, _ = p.communicate(timeout=150)
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
