@@ -444,7 +444,13 @@ def _comm_run(emac, comm, count, tdtype, code, dname, copyin, steps, warmup, ran
         got = got[idx]
         ref = np.sum(np.stack([a.astype(np.float64) for a in allin]), axis=0)
         tol = 1e-5 * world if np.dtype(np_dtype).kind == "f" else 0.0
-        ok = torch.tensor([int(np.allclose(got.astype(np.float64), ref, rtol=0, atol=tol))])
+        good = np.isclose(got.astype(np.float64), ref, rtol=0, atol=tol)
+        if not good.all():
+            bad = np.flatnonzero(~good)
+            log(f"rank {rank}: {dname} {count} elements: {bad.size}/{idx.size} samples differ, first at element "
+                f"{idx[bad[0]]} (chunk {idx[bad[0]] * world // count}), last at {idx[bad[-1]]}: got {got[bad[0]]} "
+                f"want {ref[bad[0]]}")
+        ok = torch.tensor([int(good.all())])
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         checked = bool(ok.item())
     dist.barrier()

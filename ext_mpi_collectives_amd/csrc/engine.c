@@ -194,10 +194,11 @@ static void mirror_free(emac_handle *h, void *p) {
 }
 
 /* A buffer the handle can use in place: device memory, and in the IPC form also exportable as a
-   whole allocation (emac_gpu_ipc_exportable). Anything else gets a device mirror. */
+   whole allocation (emac_gpu_ipc_exportable) and long enough for the set-up probe (R bytes).
+   Anything else gets a device mirror. */
 static int in_place_ok(const emac_handle *h, const void *p) {
   if (!emac_gpu_is_device_pointer(p)) return 0;
-  return h->kind != KIND_IPC || emac_gpu_ipc_exportable(p);
+  return h->kind != KIND_IPC || (h->bytes >= EMAC_MAX_RANKS && emac_gpu_ipc_exportable(p));
 }
 
 /* Page-lock a host buffer for async DMA, except in the IPC form: a process that has imported
@@ -538,6 +539,9 @@ typedef struct {
   long extent; /* bytes of the exported allocation: the importer's mapping must match */
   unsigned long long buf_id; /* the exporter's allocation id (0: unknown) */
   int status;
+  int in_place;  /* [0]: the receive buffer is the send buffer */
+  int refused;   /* [0]: the runtime refused to export one of this rank's buffers */
+  unsigned char probe[EMAC_MAX_RANKS]; /* original first R bytes of the buffer (ipc_exchange) */
   unsigned char free_slots[EMAC_SYNC_SLOTS / 8]; /* handle set-up: slots this rank can use */
 } ipc_export;
 
@@ -605,77 +609,188 @@ int ext_mpi_amd_comm_init_ipc(int rank, int size, ext_mpi_amd_allgather_fn allga
   return 0;
 }
 
-/* Collective: every rank runs the same two exchanges (exports, then the verdict) whatever
-   failed locally before (`rc`), so that a local failure cannot unmatch the sequence. */
-static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf, void *recvbuf, int rc) {
-  ipc_export mine[2], all[2 * EMAC_MAX_RANKS];
-  void *psend[EMAC_MAX_RANKS], *precv[EMAC_MAX_RANKS];
-  emac_bucket *b = NULL;
-  int R = cm->size, r, t, pc, nb = 0, c, agreed, slot;
-  const int empty = h->bytes == 0; /* same count on every rank: nothing to map or fold */
+/* The runtime's IPC handle of an allocation is a function of the exporter's address and size,
+   and an export can resolve to OLD memory: when a buffer is freed while a peer still maps it and
+   a new one is allocated at the same address, the new handle equals the old one and importing it
+   maps the old (still referenced) memory -- or the export is refused. Measured with 4 processes
+   (stale leaves read, fan-out stores lost); nothing in the handle tells the cases apart. So every
+   mapping is validated with a write probe before it is used: each importer q flips byte q of
+   every peer buffer through its mapping, and each exporter checks that its own buffers show the
+   flips (then restores them). A buffer some peer failed to reach is re-placed in a fresh pooled
+   mirror (new address, staged in and out on the handle's stream) and the exchange repeats.
+   The probe touches the first R bytes of each buffer during set-up only: the buffers must not be
+   written by the device while the set-up runs. */
+#define EMAC_PROBE_FLIP 0x5A
+#define EMAC_IPC_ATTEMPTS 4
+
+static void ipc_mirror_poison(emac_comm *cm, void *p) {
+  int i;
+  for (i = 0; i < cm->nmirrors; i++)
+    if (cm->mirrors[i].p == p) cm->mirrors[i].busy = 2; /* kept, never handed out again */
+}
+
+/* re-place this rank's send (recv_side 0) or receive buffer in a fresh mirror (in place: both) */
+static int ipc_remirror(emac_handle *h, int recv_side) {
+  emac_comm *cm = &comms[h->comm];
+  const int same = h->dsend[0] == h->drecv[0];
+  unsigned char *flag;
+  void **d, *p;
+  int rc;
+  if (same) recv_side = 1; /* in place: one buffer, held as the receive side (stage_in / stage_out) */
+  flag = recv_side ? &h->recv_mirror[0] : &h->send_mirror[0];
+  d = recv_side ? &h->drecv[0] : &h->dsend[0];
+  if (*flag) ipc_mirror_poison(cm, *d);
+  if ((rc = ipc_mirror_get(cm, &p, h->bytes))) return rc;
+  *d = p;
+  *flag = 1;
+  if (same) h->dsend[0] = p;
+  return 0;
+}
+
+/* own probe bytes: the first R bytes of the send buffer, then of the receive buffer */
+static int ipc_probe_own(emac_handle *h, int R, int in_place, unsigned char *vals, int store) {
+  void *p[EMAC_PROBE_MAX];
+  int t, q, n = 0;
+  for (t = 0; t < (in_place ? 1 : 2); t++)
+    for (q = 0; q < R; q++) p[n++] = (char *)(t ? h->drecv[0] : h->dsend[0]) + q;
+  return store ? emac_gpu_poke(p, vals, n, h->stream) : emac_gpu_peek((const void *const *)p, vals, n, h->stream);
+}
+
+/* One exchange of the IPC set-up (collective whatever failed locally before: `rc`). On return
+   psend/precv hold the validated peer mappings, all[] the exports, and stale[t] tells that this
+   rank's buffer t (0 send, 1 receive) was refused for export or missed by some peer. */
+static int ipc_exchange(emac_handle *h, emac_comm *cm, int rc, int empty, ipc_export *all, void **psend, void **precv,
+                        int *stale) {
+  ipc_export mine[2];
+  unsigned char orig[2 * EMAC_MAX_RANKS], seen[2 * EMAC_MAX_RANKS];
+  int R = cm->size, r, t, q, any_refused = 0, agreed;
+  const int in_place = h->dsend[0] == h->drecv[0];
   memset(mine, 0, sizeof(mine));
-  if (!rc && !empty) rc = map_buffers(h, 0, sendbuf, recvbuf);
-  if (!rc && !empty) rc = emac_gpu_ipc_export(h->dsend[0], mine[0].handle, &mine[0].offset);
-  if (!rc && !empty) rc = emac_gpu_ipc_export(h->drecv[0], mine[1].handle, &mine[1].offset);
-  if (!rc && !empty) {
-    void *b0, *b1;
-    mine[0].extent = emac_gpu_alloc_extent(h->dsend[0], &b0);
-    mine[1].extent = emac_gpu_alloc_extent(h->drecv[0], &b1);
-    mine[0].buf_id = emac_gpu_buffer_id(b0);
-    mine[1].buf_id = emac_gpu_buffer_id(b1);
+  stale[0] = stale[1] = 0;
+  if (!rc && !empty) rc = ipc_probe_own(h, R, in_place, orig, 0);
+  for (t = 0; t < 2 && !rc && !empty; t++) {
+    void *d = t ? h->drecv[0] : h->dsend[0], *b0;
+    const int er = emac_gpu_ipc_export(d, mine[t].handle, &mine[t].offset);
+    if (er == EMAC_ERR_TRANSPORT)
+      stale[t] = 1; /* refused by the runtime: re-place it */
+    else
+      rc = er;
+    mine[t].extent = emac_gpu_alloc_extent(d, &b0);
+    mine[t].buf_id = emac_gpu_buffer_id(b0);
+    memcpy(mine[t].probe, orig + (in_place ? 0 : t) * R, (size_t)R);
   }
+  if (in_place) stale[0] = stale[1] = stale[0] | stale[1];
+  mine[0].in_place = in_place;
+  mine[0].refused = stale[0] | stale[1];
   for (r = 0; r < EMAC_SYNC_SLOTS; r++)
     if (!cm->slot_used[r]) mine[0].free_slots[r >> 3] |= (unsigned char)(1u << (r & 7));
   mine[0].status = rc == 0;
   if (cm->ag(cm->ag_ctx, mine, all, (long)sizeof(mine))) return EMAC_ERR_TRANSPORT;
-  for (r = 0; r < R; r++)
+  for (r = 0; r < R; r++) {
     if (!all[2 * r].status && !rc) rc = EMAC_ERR_TRANSPORT;
+    any_refused |= all[2 * r].refused;
+  }
+  if (empty || any_refused) return rc; /* nothing to map, or this attempt is void on every rank */
+  /* map every peer buffer; one that cannot be mapped whole is left unprobed, so that its
+     exporter sees the miss and re-places it */
+  {
+    void *pk[EMAC_PROBE_MAX];
+    unsigned char vals[EMAC_PROBE_MAX];
+    int n = 0;
+    for (r = 0; r < R; r++) {
+      psend[r] = precv[r] = NULL;
+      if (r == cm->rank) {
+        psend[r] = h->dsend[0];
+        precv[r] = h->drecv[0];
+        continue;
+      }
+      for (t = 0; t < 2 && !rc; t++) {
+        const ipc_export *e = &all[2 * r + t];
+        void *base, *ext_base;
+        long extent;
+        if (t == 1 && all[2 * r].in_place) {
+          precv[r] = psend[r];
+          continue;
+        }
+        base = ipc_map_peer(cm, r, e->handle, e->buf_id, e->extent);
+        if (!base) continue;
+        h->mapped[h->nmapped++] = base;
+        extent = emac_gpu_alloc_extent(base, &ext_base);
+        if (extent < 0 || ext_base != base || extent != e->extent || e->offset < 0 ||
+            e->offset + (long)h->bytes > extent || e->offset + R > extent)
+          continue; /* short mapping: never launched over */
+        (t ? precv : psend)[r] = (char *)base + e->offset;
+        pk[n] = (char *)base + e->offset + cm->rank;
+        vals[n++] = e->probe[cm->rank] ^ EMAC_PROBE_FLIP;
+        if (getenv("EXT_MPI_AMD_DEBUG_IPC")) {
+          char hex[2 * EMAC_IPC_HANDLE_BYTES + 1];
+          for (q = 0; q < EMAC_IPC_HANDLE_BYTES; q++) sprintf(hex + 2 * q, "%02x", e->handle[q]);
+          fprintf(stderr, "ipc rank %d: peer %d %s handle %s id %llu base %p extent %ld offset %ld bytes %zu\n",
+                  cm->rank, r, t ? "recv" : "send", hex, e->buf_id, base, extent, e->offset, h->bytes);
+        }
+      }
+    }
+    if (!rc) rc = emac_gpu_poke(pk, vals, n, h->stream);
+  }
+  /* every rank's flips have landed */
+  agreed = ipc_agree(cm, rc == 0);
+  if (!rc) rc = agreed;
+  if (rc) return rc;
+  if ((rc = ipc_probe_own(h, R, in_place, seen, 0))) return rc;
+  for (t = 0; t < (in_place ? 1 : 2); t++)
+    for (q = 0; q < R; q++)
+      if (q != cm->rank && seen[t * R + q] != (orig[t * R + q] ^ EMAC_PROBE_FLIP)) {
+        stale[t] = 1;
+        if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
+          fprintf(stderr, "ipc rank %d: peer %d does not reach my %s buffer\n", cm->rank, q, t ? "recv" : "send");
+      }
+  if (in_place) stale[1] = stale[0];
+  return ipc_probe_own(h, R, in_place, orig, 1); /* restore */
+}
+
+/* Collective: every rank runs the same exchanges whatever failed locally before (`rc`), so that
+   a local failure cannot unmatch the sequence. */
+static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf, void *recvbuf, int rc) {
+  ipc_export all[2 * EMAC_MAX_RANKS];
+  void *psend[EMAC_MAX_RANKS], *precv[EMAC_MAX_RANKS];
+  emac_bucket *b = NULL;
+  int R = cm->size, r, t, pc, nb = 0, c, slot, attempt;
+  const int empty = h->bytes == 0; /* same count on every rank: nothing to map or fold */
+  if (!rc && !empty) rc = map_buffers(h, 0, sendbuf, recvbuf);
+  for (attempt = 0;; attempt++) {
+    int stale[2], v[3], allv[3 * EMAC_MAX_RANKS], again = 0;
+    rc = ipc_exchange(h, cm, rc, empty, all, psend, precv, stale);
+    v[0] = rc == 0;
+    v[1] = stale[0];
+    v[2] = stale[1];
+    if (cm->ag(cm->ag_ctx, v, allv, (long)sizeof(v))) return EMAC_ERR_TRANSPORT;
+    for (r = 0; r < R; r++) {
+      if (!allv[3 * r]) return rc ? rc : EMAC_ERR_TRANSPORT;
+      again |= allv[3 * r + 1] | allv[3 * r + 2];
+    }
+    if (!again) break;
+    if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
+      fprintf(stderr, "ipc rank %d: attempt %d: re-placing%s%s\n", cm->rank, attempt, stale[0] ? " send" : "",
+              stale[1] ? " recv" : "");
+    if (attempt == EMAC_IPC_ATTEMPTS - 1) return EMAC_ERR_TRANSPORT;
+    for (r = 0; r < h->nmapped; r++) ipc_unmap(cm, h->mapped[r]);
+    h->nmapped = 0;
+    if (stale[0]) rc = ipc_remirror(h, 0);
+    if (!rc && stale[1] && h->dsend[0] != h->drecv[0]) rc = ipc_remirror(h, 1);
+  }
   /* the synchronisation slot: the lowest one free on every rank (ranks may have released
      their handles in different orders) */
   for (slot = 0; slot < EMAC_SYNC_SLOTS; slot++) {
     for (r = 0; r < R && (all[2 * r].free_slots[slot >> 3] >> (slot & 7)) & 1; r++);
     if (r == R) break;
   }
-  if (slot == EMAC_SYNC_SLOTS && !rc) rc = EMAC_ERR_MALLOC;
-  for (r = 0; !rc && !empty && r < R; r++) {
-    if (r == cm->rank) {
-      psend[r] = h->dsend[0];
-      precv[r] = h->drecv[0];
-      continue;
-    }
-    for (t = 0; t < 2 && !rc; t++) {
-      void *base = ipc_map_peer(cm, r, all[2 * r + t].handle, all[2 * r + t].buf_id, all[2 * r + t].extent), *ext_base;
-      long extent;
-      if (!base) {
-        rc = EMAC_ERR_TRANSPORT;
-        break;
-      }
-      h->mapped[h->nmapped++] = base;
-      (t ? precv : psend)[r] = (char *)base + all[2 * r + t].offset;
-      /* the mapping must hold the peer's whole buffer: never launch over a short mapping */
-      extent = emac_gpu_alloc_extent(base, &ext_base);
-      if (extent < 0 || ext_base != base || extent != all[2 * r + t].extent || all[2 * r + t].offset < 0 ||
-          all[2 * r + t].offset + (long)h->bytes > extent)
-        rc = EMAC_ERR_TRANSPORT;
-      if (getenv("EXT_MPI_AMD_DEBUG_IPC")) {
-        const unsigned char *hb = all[2 * r + t].handle;
-        fprintf(stderr,
-                "ipc rank %d: peer %d %s handle %02x%02x%02x%02x%02x%02x%02x%02x.. id %llu base %p extent %ld "
-                "(exported %ld) offset %ld bytes %zu -> %s\n",
-                cm->rank, r, t ? "recv" : "send", hb[0], hb[1], hb[2], hb[3], hb[4], hb[5], hb[6], hb[7],
-                all[2 * r + t].buf_id, base, extent, all[2 * r + t].extent, all[2 * r + t].offset, h->bytes,
-                rc ? "REJECTED" : "ok");
-      }
-    }
-  }
-  /* every rank opened every mapping before anyone proceeds */
-  agreed = ipc_agree(cm, rc == 0);
-  if (rc || agreed) return rc ? rc : agreed;
+  if (slot == EMAC_SYNC_SLOTS) return EMAC_ERR_MALLOC; /* same verdict on every rank */
   h->slot = slot;
   cm->slot_used[slot] = 1;
   h->slot_held = 1;
   h->epoch[0] = cm->slot_epoch[slot][0];
   h->epoch[1] = cm->slot_epoch[slot][1];
+  if (empty) return 0;
   /* this rank's owner chunks: leaves from the peers' send buffers in the plan's fold order,
      results into every rank's receive buffer (the fused reduce_copyout push) */
   c = h->me_pos;
@@ -694,8 +809,8 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
   h->nsrc = R;
   h->fan = R > 1 ? 2 : 0; /* peer-mapped fan-out: system-coherent launch */
   if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
-    fprintf(stderr, "ipc rank %d: own send %p recv %p bytes %zu, %d buckets, slot %d\n", cm->rank, h->dsend[0],
-            h->drecv[0], h->bytes, nb, slot);
+    fprintf(stderr, "ipc rank %d: own send %p recv %p bytes %zu, %d buckets, slot %d, %d attempt(s)\n", cm->rank,
+            h->dsend[0], h->drecv[0], h->bytes, nb, slot, attempt + 1);
   rc = upload_buckets(h, b, nb);
   free(b);
   return rc;
@@ -749,8 +864,8 @@ int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, i
   h->nbuf = 1;
   h->nsrc = R;
   if (cm->ipc) {
+    if (!rc) rc = emac_gpu_stream_create(&h->stream);
     if ((rc = ipc_allreduce_init(h, cm, sendbuf, recvbuf, rc))) goto fail;
-    if ((rc = emac_gpu_stream_create(&h->stream))) goto fail;
     if ((rc = finish_init(h, handle))) goto fail;
     return 0;
   }

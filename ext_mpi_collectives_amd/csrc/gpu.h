@@ -81,6 +81,11 @@ unsigned long long emac_gpu_buffer_id(const void *p);   /* unique id of the allo
 #define EMAC_IPC_GRANULE (2ul << 20) /* exported allocations: 2 MiB aligned, 2 MiB multiples */
 int emac_gpu_ipc_exportable(const void *p); /* p lies in an allocation of IPC granularity */
 int emac_gpu_malloc_uncached(void **p, size_t bytes); /* zeroed, rounded up to EMAC_IPC_GRANULE */
+/* byte probes (IPC set-up): store vals[i] at ptrs[i] / load ptrs[i] into vals[i], system-coherent,
+   complete on return */
+#define EMAC_PROBE_MAX (2 * EMAC_MAX_RANKS)
+int emac_gpu_poke(void *const *ptrs, const unsigned char *vals, int n, void *stream);
+int emac_gpu_peek(const void *const *ptrs, unsigned char *vals, int n, void *stream);
 int emac_gpu_host_alloc_mapped(void **p, size_t bytes); /* pinned, device-visible, zeroed */
 int emac_gpu_host_free(void *p);
 int emac_gpu_xcc_census(unsigned *mask); /* XCCs a wide launch lands on */

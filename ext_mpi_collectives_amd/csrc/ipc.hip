@@ -57,12 +57,13 @@ __global__ void xcc_census_kernel(unsigned *mask) {
 }
 
 // One lane per workgroup does the protocol; the workgroup count is EMAC_SYNC_WG.
-// Fences by phase. Before the fold (phase 0) only a release is needed: the application's
-// stores into this rank's send buffer may sit dirty in any XCD's L2, and the peers read that
-// buffer from memory. After the fold (phase 1) only an acquire: the peers' fan-out stores have
-// landed in this rank's receive buffer behind its L2s. The fold itself needs neither: its
-// accesses are system-coherent (sc0 sc1 loads, write-through stores drained before each wave
-// ends; fold_kernel.hpp kRemote).
+// Fences by phase. Before the fold (phase 0) a release: the application's stores into this
+// rank's send buffer may sit dirty in any XCD's L2, and the peers read that buffer from memory;
+// and, once every peer has signalled, an acquire, so that no line of a peer's buffer that an
+// earlier kernel of this process left valid in an L2 is returned to the fold. After the fold
+// (phase 1) only the acquire: the peers' fan-out stores have landed in this rank's receive
+// buffer behind its L2s. The fold's own accesses are system-coherent (sc0 sc1 loads,
+// write-through stores drained before each wave ends; fold_kernel.hpp kRemote).
 __global__ __launch_bounds__(64) void node_barrier_kernel(emac_sync *self, emac_sync *const *peers, int slot,
                                                           int phase, unsigned long epoch, int nranks, int me,
                                                           unsigned xcc_expect, int *err, long timeout) {
@@ -99,28 +100,88 @@ __global__ __launch_bounds__(64) void node_barrier_kernel(emac_sync *self, emac_
       }
     }
   }
-  // acquire: lines of this XCD's L2 that the peers have since rewritten (their fan-out into
-  // this rank's receive buffer) are dropped
-  if (phase == 1) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: L2 invalidate
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // completed before the launch ends
-  }
+  // acquire: lines of this XCD's L2 that the peers have since rewritten are dropped -- after
+  // the fold (phase 1) their fan-out into this rank's receive buffer; before it (phase 0) their
+  // send buffers, which the fold is about to load (a line this process's earlier kernels left
+  // valid would otherwise be returned even to the fold's sc0 sc1 loads)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: L2 invalidate
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // completed before the launch ends
+}
+
+// Byte probes of the IPC set-up (engine.c ipc_exchange): one lane per byte. Stores are
+// published with a system-scope release (L2 write-back of this XCD); loads follow a system-scope
+// acquire (L2 invalidate), so both see memory as the other processes left it.
+struct ProbeSet {
+  unsigned char *p[EMAC_PROBE_MAX];
+  unsigned char v[EMAC_PROBE_MAX];
+  int n;
+};
+
+__global__ __launch_bounds__(64) void poke_kernel(ProbeSet a) {
+  const int i = threadIdx.x;
+  if (i < a.n) *reinterpret_cast<volatile unsigned char *>(a.p[i]) = a.v[i];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // and drop the lines: a valid copy of a peer's line left in this XCD's L2 would be returned
+  // to later loads after the peer has restored the byte (measured: 8 processes on one GPU)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__global__ __launch_bounds__(64) void peek_kernel(ProbeSet a, unsigned char *out) {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const int i = threadIdx.x;
+  if (i < a.n) out[i] = *reinterpret_cast<volatile const unsigned char *>(a.p[i]);
 }
 
 }  // namespace
 
 extern "C" {
 
+int emac_gpu_poke(void *const *ptrs, const unsigned char *vals, int n, void *stream) {
+  ProbeSet a;
+  if (n < 0 || n > EMAC_PROBE_MAX) return EMAC_ERR_ARG;
+  if (!n) return 0;
+  memset(&a, 0, sizeof(a));
+  for (int i = 0; i < n; ++i) {
+    a.p[i] = static_cast<unsigned char *>(ptrs[i]);
+    a.v[i] = vals[i];
+  }
+  a.n = n;
+  hipLaunchKernelGGL(poke_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+  int rc = ok(hipGetLastError());
+  return rc ? rc : ok(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+}
+
+int emac_gpu_peek(const void *const *ptrs, unsigned char *vals, int n, void *stream) {
+  ProbeSet a;
+  unsigned char *d = nullptr;
+  if (n < 0 || n > EMAC_PROBE_MAX) return EMAC_ERR_ARG;
+  if (!n) return 0;
+  memset(&a, 0, sizeof(a));
+  for (int i = 0; i < n; ++i) a.p[i] = static_cast<unsigned char *>(const_cast<void *>(ptrs[i]));
+  a.n = n;
+  if (hipMalloc(&d, EMAC_PROBE_MAX) != hipSuccess) return EMAC_ERR_MALLOC;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(peek_kernel, dim3(1), dim3(64), 0, s, a, d);
+  int rc = ok(hipGetLastError());
+  if (!rc) rc = ok(hipMemcpyAsync(vals, d, (size_t)n, hipMemcpyDeviceToHost, s));
+  if (!rc) rc = ok(hipStreamSynchronize(s));
+  (void)hipFree(d);
+  return rc;
+}
+
 int emac_gpu_ipc_export(const void *p, void *handle, long *offset) {
   void *base = nullptr;
   size_t size = 0;
   if (hipMemGetAddressRange(&base, &size, const_cast<void *>(p)) != hipSuccess) {
-    clear_error("emac_gpu_ipc_export");
+    clear_error("emac_gpu_ipc_export: hipMemGetAddressRange");
     return EMAC_ERR_ARG;
   }
   hipIpcMemHandle_t h;
   if (hipIpcGetMemHandle(&h, base) != hipSuccess) {
-    clear_error("emac_gpu_ipc_export");
+    clear_error("emac_gpu_ipc_export: hipIpcGetMemHandle");
+    if (getenv("EXT_MPI_AMD_DEBUG_HIP")) fprintf(stderr, "ext_mpi_amd: export of %p (base %p, %zu bytes) refused\n", p, base, size);
     return EMAC_ERR_TRANSPORT;
   }
   memcpy(handle, &h, sizeof(h));

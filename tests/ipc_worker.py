@@ -9,6 +9,7 @@ Exit status 0 iff every case matched.
 import ctypes
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -39,6 +40,9 @@ def cases(R):
     if R == 8:
         out += [(emac.FLOAT, 262147, "6;1 -2 -2 -2 2 2 2", False, False, 2), (emac.DOUBLE, 100001, "6;1 -4 -2 2 4", False, False, 1),
                 (emac.LONG, 65539, "6;1 -4 4 1 4 1 -2 2", False, False, 1), (emac.FLOAT, 4 << 20, full, False, False, 1)]
+    if R == 2 and os.environ.get("IPC_BIG"):  # 256 MiB per rank, float then double (same bytes: reused addresses)
+        out += [(emac.FLOAT, 64 << 20, full, False, False, 1), (emac.DOUBLE, 32 << 20, full, False, False, 1),
+                (emac.FLOAT, 64 << 20, full, False, False, 1)]
     if R == 3:
         out += [(emac.DOUBLE, 99999, "6;2 -3 3", True, False, 2)]
     return out
@@ -106,6 +110,53 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
         sys.exit(1 if failures else 0)
+    # Freed and re-allocated user buffers: the same 64 MiB hipMalloc address comes back with
+    # new memory while a slower rank still maps the old one. The runtime's IPC handle of the new
+    # allocation can then equal the old one's, so a handle exported before every peer has
+    # dropped its old mapping would import the old memory (stale leaves, lost fan-out).
+    L, n = emac.lib(), 16 << 20
+    ok = True
+    for it in range(4):
+        bufs = []
+        for _ in range(2):
+            p = ctypes.c_void_p()
+            assert L.ext_mpi_amd_gpu_malloc(ctypes.byref(p), 4 * n) == 0
+            bufs.append(p)
+        fill = np.full(n, float((rank + 1) * (it + 1)), np.float32)
+        assert L.ext_mpi_amd_gpu_memcpy_hd(bufs[0], fill.ctypes.data, 4 * n) == 0
+        h = emac.allreduce_init(bufs[0].value, bufs[1].value, n, emac.FLOAT, comm)
+        emac.start(h)
+        emac.wait(h)
+        got = np.empty(n, np.float32)
+        assert L.ext_mpi_amd_gpu_memcpy_dh(got.ctypes.data, bufs[1], 4 * n) == 0
+        ok &= bool(np.all(got == (it + 1) * world * (world + 1) / 2))
+        if os.environ.get("EXT_MPI_AMD_DEBUG_IPC"):
+            q = [got[j * n // world: (j + 1) * n // world] for j in range(world)]
+            print(f"rank {rank} re-allocation {it}: {ok}; per chunk first/last/n_bad: "
+                  f"{[(float(c[0]), float(c[-1]), int(np.sum(c != (it + 1) * world * (world + 1) / 2))) for c in q]}",
+                  file=sys.stderr, flush=True)
+        if rank == 0:
+            time.sleep(0.3)  # the others free, re-allocate and export first
+        emac.done(h)
+        for p in bufs:
+            L.ext_mpi_amd_gpu_free(p)
+    failures += not ok
+    print(f"IPC rank {rank}/{world} re-allocated buffers: {'ok' if ok else 'MISMATCH'}", flush=True)
+    # new send data before every Start (the fold must never see a previous iteration's lines)
+    ok = True
+    for in_place in (False, True):
+        x = torch.empty(100003, device="cuda")
+        y = x if in_place else torch.empty_like(x)
+        h = emac.allreduce_init(x.data_ptr(), y.data_ptr(), x.numel(), emac.FLOAT, comm)
+        for it in range(5):
+            x.fill_(float((rank + 1) * (it + 1)))
+            torch.cuda.synchronize()
+            emac.start(h)
+            emac.wait(h)
+            ok &= bool(torch.all(y == (it + 1) * world * (world + 1) / 2).item())
+        emac.done(h)
+    failures += not ok
+    print(f"IPC rank {rank}/{world} new data every Start: {'ok' if ok else 'MISMATCH'}", flush=True)
     # several handles in flight on separate streams, started in the same order on every rank
     hs, bufs = [], []
     for j in range(3):
@@ -135,7 +186,10 @@ def main():
             emac.start(h)
             emac.wait(h)
         if it % 50 == 0:
-            ok &= bool(torch.all(y == world * (world + 1) / 2).item())
+            good = bool(torch.all(y == world * (world + 1) / 2).item())
+            if not good and ok:
+                print(f"rank {rank}: slot recycling iteration {it}: y[:4] = {y[:4].tolist()}", file=sys.stderr, flush=True)
+            ok &= good
         for h in (pair if rank % 2 else pair[::-1]):
             emac.done(h)
     failures += not ok
