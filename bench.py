@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU baseline sample")
     ap.add_argument("--transport", default="ipc", choices=["ipc", "rccl"],
                     help="N > 1: peer-mapped hipIpc form (default) or RCCL point-to-point legs")
+    ap.add_argument("--child-transport", default=None, choices=["ipc", "rccl"], help=argparse.SUPPRESS)
+    ap.add_argument("--child-full", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--child-result", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--alloc", default="hip", choices=["hip", "torch"],
                     help="device buffers from hipMalloc (library device ABI, like the reference's "
                          "tests/benchmark_gpu.c cudaMalloc) or torch's caching allocator")
@@ -429,8 +432,9 @@ def _comm_run(emac, comm, count, tdtype, code, dname, copyin, steps, warmup, ran
     mine = host_random(count, np_dtype, 0x5EED0000 + rank)
     send.upload(mine)
     h = emac.allreduce_init(send.data_ptr(), recv.data_ptr(), count, code, comm, copyin)
-    stream = torch.cuda.Stream()
-    emac.set_stream(h, stream.cuda_stream)
+    # the handle's own HIP stream (on the 1-GPU rehearsal box the first handle put on a torch
+    # pool stream ran its barriers ~8x slower, tools/ipc_latency.py IPC_LAT_OWN_STREAM)
+    stream = torch.cuda.ExternalStream(emac.stream(h))
     for _ in range(warmup):
         emac.start(h)
     emac.wait(h)
@@ -475,7 +479,9 @@ def _fold_only(emac, h, stream, steps, torch):
     return e0.elapsed_time(e1) * 1e-3 / steps
 
 
-def multi_gpu(args):
+def transport_child(args):
+    """One transport's N > 1 measurement in a process of its own (spawned by multi_gpu): its own
+    gloo group, its own HIP context. Writes this rank's results as JSON to --child-result."""
     import torch
     import torch.distributed as dist
     import ext_mpi_collectives_amd as emac
@@ -483,89 +489,125 @@ def multi_gpu(args):
     local = int(os.environ.get("LOCAL_RANK", rank))
     import signal
     signal.signal(signal.SIGALRM, lambda *_: (log(f"rank {rank}: watchdog expired"), os._exit(3)))
-    signal.alarm(900)  # a rank stuck in a collective must not hang the job
+    signal.alarm(600)  # a rank stuck in a collective must not hang the job
     ndev = torch.cuda.device_count()
     dev = local % ndev  # one rank per GPU; ranks share a GPU only when there are fewer GPUs (rehearsal)
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo")
     tdtype, code, dname, tsize = dtype_info(args.dtype)
     count = int(args.size_mib * MIB) // tsize
+    copyin = args.copyin or f"6;1 -{world} {world}"
+    transport, full = args.child_transport, args.child_full
+    res = {}
+    log(f"rank {rank}: {transport} child on GPU {dev}: communicator set-up")
+    if transport == "ipc":
+        comm = emac.comm_init_ipc(rank, world, emac.torch_allgather(), dev)
+    else:
+        uid = [emac.get_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = emac.comm_init(rank, world, uid[0], dev)
+    log(f"rank {rank}: {transport} child: communicator ready")
+    try:
+        h, send, recv, stream, wall, checked = _comm_run(emac, comm, count, tdtype, code, dname, copyin,
+                                                         args.steps, args.warmup, rank, world, dist, torch)
+        res.update(wall=wall, checked=checked)
+        log(f"rank {rank}: {transport}: {args.steps} steps in {wall * 1e3:.3f} ms, checked {checked}")
+        if full:
+            # the fold leg alone on every GPU at once, then on rank 0's GPU while the others idle
+            dist.barrier()
+            fold_s = torch.tensor([_fold_only(emac, h, stream, args.steps, torch)], dtype=torch.float64)
+            dist.all_reduce(fold_s, op=dist.ReduceOp.MAX)
+            dist.barrier()
+            alone_s = torch.zeros(1, dtype=torch.float64)
+            if rank == 0:
+                alone_s[0] = _fold_only(emac, h, stream, args.steps, torch)
+            dist.barrier()
+            dist.broadcast(alone_s, src=0)
+            res.update(fold_s=fold_s.item(), alone_s=alone_s.item())
+        emac.done(h)
+        send.free()
+        recv.free()
+        if full:
+            # BASELINE configs[3] (double, 256 MiB per rank) and a configs[4]-style size sweep
+            points = [(args.dtype, n) for n in (8, 64 << 10, 1 << 20, 16 << 20, 64 << 20, 256 << 20)]
+            points.append(("double", 256 << 20))
+            sweep = []
+            for dname_p, nbytes in points:
+                tdt, cde, _, tsz = dtype_info(dname_p)
+                cnt = max(1, nbytes // tsz)
+                st = 100 if nbytes <= (1 << 20) else 10
+                hp, sb, rb, _, el_p, ok_p = _comm_run(emac, comm, cnt, tdt, cde, dname_p, copyin, st, 3, rank,
+                                                      world, dist, torch)
+                emac.done(hp)
+                sb.free()
+                rb.free()
+                sweep.append({"dtype": dname_p, "bytes_per_rank": cnt * tsz,
+                              "us_per_allreduce": round(el_p * 1e6 / st, 2),
+                              "algbw_gbps": round(cnt * tsz * st / el_p / 1e9, 2), "checked": ok_p})
+                log(f"rank {rank}: {transport}: sweep {dname_p} {cnt * tsz} B: {el_p * 1e6 / st:.2f} us, checked {ok_p}")
+            res["sweep"] = sweep
+    finally:
+        emac.comm_free(comm)
+    with open(args.child_result, "w") as f:
+        json.dump(res, f)
+    dist.barrier()
+    dist.destroy_process_group()
+    signal.alarm(0)
+
+
+def multi_gpu(args):
+    """N > 1 driver rank. It never touches the GPU itself: each transport runs in a child process
+    per rank (own gloo group, own HIP context), so a transport that fails -- even by a GPU fault
+    that ends its processes -- leaves these ranks alive to agree on it and try the other one."""
+    import subprocess
+    import torch
+    import torch.distributed as dist
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo")
+    tdtype, code, dname, tsize = dtype_info(args.dtype)
+    count = int(args.size_mib * MIB) // tsize
     S = count * tsize
     copyin = args.copyin or f"6;1 -{world} {world}"
+    base_port = int(os.environ.get("MASTER_PORT", "29500"))
 
     def everyone(ok):
         t = torch.tensor([int(bool(ok))])
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return bool(t.item())
 
-    def make_comm(transport):
-        if transport == "ipc":
-            return emac.comm_init_ipc(rank, world, emac.torch_allgather(), dev)
-        uid = [emac.get_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        return emac.comm_init(rank, world, uid[0], dev)
-
-    def run_transport(transport, full):
-        """The headline workload on one transport (+ fold timings and the sweep when `full`)."""
-        res = {}
-        comm = make_comm(transport)
+    def run_child(i, transport, full):
+        out = os.path.join("/tmp", f"emac_bench_{base_port}_{i}_{rank}.json")
+        if os.path.exists(out):
+            os.remove(out)
+        cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(args.gpus), "--steps", str(args.steps),
+               "--warmup", str(args.warmup), "--size-mib", str(args.size_mib), "--dtype", args.dtype,
+               "--child-transport", transport, "--child-result", out] + (["--child-full"] if full else []) + \
+              (["--copyin", args.copyin] if args.copyin else [])
+        env = dict(os.environ, MASTER_PORT=str(base_port + 101 + i))
+        env.pop("TORCHELASTIC_USE_AGENT_STORE", None)  # the children's rank 0 hosts their own store
         try:
-            h, send, recv, stream, wall, checked = _comm_run(emac, comm, count, tdtype, code, dname, copyin,
-                                                             args.steps, args.warmup, rank, world, dist, torch)
-            res.update(wall=wall, checked=checked)
-            if full:
-                # the fold leg alone on every GPU at once, then on rank 0's GPU while the others idle
-                dist.barrier()
-                fold_s = torch.tensor([_fold_only(emac, h, stream, args.steps, torch)], dtype=torch.float64)
-                dist.all_reduce(fold_s, op=dist.ReduceOp.MAX)
-                dist.barrier()
-                alone_s = torch.zeros(1, dtype=torch.float64)
-                if rank == 0:
-                    alone_s[0] = _fold_only(emac, h, stream, args.steps, torch)
-                dist.barrier()
-                dist.broadcast(alone_s, src=0)
-                res.update(fold_s=fold_s.item(), alone_s=alone_s.item())
-            emac.done(h)
-            send.free()
-            recv.free()
-            if full:
-                # BASELINE configs[3] (double, 256 MiB per rank) and a configs[4]-style size sweep
-                points = [(args.dtype, n) for n in (8, 64 << 10, 1 << 20, 16 << 20, 64 << 20, 256 << 20)]
-                points.append(("double", 256 << 20))
-                sweep = []
-                for dname_p, nbytes in points:
-                    tdt, cde, _, tsz = dtype_info(dname_p)
-                    cnt = max(1, nbytes // tsz)
-                    st = 100 if nbytes <= (1 << 20) else 10
-                    hp, sb, rb, _, el_p, ok_p = _comm_run(emac, comm, cnt, tdt, cde, dname_p, copyin, st, 3, rank,
-                                                          world, dist, torch)
-                    emac.done(hp)
-                    sb.free()
-                    rb.free()
-                    sweep.append({"dtype": dname_p, "bytes_per_rank": cnt * tsz,
-                                  "us_per_allreduce": round(el_p * 1e6 / st, 2),
-                                  "algbw_gbps": round(cnt * tsz * st / el_p / 1e9, 2), "checked": ok_p})
-                res["sweep"] = sweep
-        finally:
-            emac.comm_free(comm)
-        return res
+            rc = subprocess.run(cmd, env=env, timeout=700).returncode
+        except subprocess.TimeoutExpired:
+            rc = "timeout"
+        if rc == 0 and os.path.exists(out):
+            with open(out) as f:
+                r = json.load(f)
+            os.remove(out)
+            return r, (None if r.get("checked") else "result check failed")
+        return {}, f"{transport} child exited with {rc}"
 
     # the requested transport first; if it fails on any rank (every rank agrees before moving
-    # on, so no rank is left inside a collective), the other one produces the headline
+    # on), the other one produces the headline
     order = [args.transport, "rccl" if args.transport == "ipc" else "ipc"]
     results = {}
     for i, transport in enumerate(order):
         full = not any("wall" in r for r in results.values())
-        try:
-            r = run_transport(transport, full)
-            err = None if r.get("checked") else "result check failed"
-        except Exception as e:  # noqa: BLE001
-            r, err = {}, f"{type(e).__name__}: {e}"
+        r, err = run_child(i, transport, full)
         if not everyone(err is None):
             r = {"error": err or "failed on another rank"}
         results[transport] = r
     primary = next((t for t in order if "wall" in results[t] and "fold_s" in results[t]), None)
-    extras = {"gpus_visible": ndev}
+    extras = {"gpus_visible": torch.cuda.device_count(), "process_per_transport": True}
     for t in order:
         if t != primary:
             r = results[t]
@@ -619,12 +661,13 @@ def multi_gpu(args):
         print(json.dumps(out), flush=True)
     dist.barrier()
     dist.destroy_process_group()
-    signal.alarm(0)
 
 
 def main():
     args = parse()
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    if args.child_transport:
+        transport_child(args)
+    elif int(os.environ.get("WORLD_SIZE", "1")) > 1:
         multi_gpu(args)
     else:
         single_gpu(args)

@@ -198,7 +198,7 @@ static void mirror_free(emac_handle *h, void *p) {
    Anything else gets a device mirror. */
 static int in_place_ok(const emac_handle *h, const void *p) {
   if (!emac_gpu_is_device_pointer(p)) return 0;
-  return h->kind != KIND_IPC || (h->bytes >= EMAC_MAX_RANKS && emac_gpu_ipc_exportable(p));
+  return h->kind != KIND_IPC || (h->bytes >= (size_t)comms[h->comm].size && emac_gpu_ipc_exportable(p));
 }
 
 /* Page-lock a host buffer for async DMA, except in the IPC form: a process that has imported

@@ -37,14 +37,23 @@ def main():
     dist.init_process_group("gloo")
     comm = emac.comm_init_ipc(rank, world, emac.torch_allgather(), dev)
     out = {"world": world, "gpus": torch.cuda.device_count(), "points": []}
-    for nbytes in (8, 65536, 1 << 20):
+    sizes = [int(v) for v in os.environ.get("IPC_LAT_SIZES", "8,65536,1048576").split(",")]
+    for nbytes in sizes:
         n = max(1, nbytes // 4)
         x = torch.ones(n, device="cuda")
         y = torch.empty_like(x)
         h = emac.allreduce_init(x.data_ptr(), y.data_ptr(), n, emac.FLOAT, comm)
-        s = torch.cuda.Stream()
-        emac.set_stream(h, s.cuda_stream)
+        if os.environ.get("IPC_LAT_OWN_STREAM"):  # diagnosis: the handle's own HIP stream
+            s = torch.cuda.ExternalStream(emac.lib().ext_mpi_amd_stream(h))
+        else:
+            for _ in range(int(os.environ.get("IPC_LAT_SKIP_STREAMS", "0"))):  # diagnosis: pool position
+                torch.cuda.Stream()
+            s = torch.cuda.Stream()
+            emac.set_stream(h, s.cuda_stream)
         full = timed(h, emac.LEG_ALL, 200, s)
+        if os.environ.get("IPC_LAT_TWICE"):  # diagnosis: the same handle and stream timed again
+            out.setdefault("first_timing_us", []).append(round(full, 2))
+            full = timed(h, emac.LEG_ALL, 2000, s)
         bars = timed(h, emac.LEG_REDUCE_SCATTER | emac.LEG_ALLGATHER, 200, s)
         fold = timed(h, emac.LEG_FOLD, 200, s)
         emac.wait(h)
