@@ -85,6 +85,7 @@ typedef struct {
   int nmaps;
   ipc_mirror *mirrors;
   int nmirrors;
+  int err_reported;
 } emac_comm;
 
 /* Loopback groups: every rank of the communicator lives in this process; the i-th handle a
@@ -248,7 +249,7 @@ static void place_bucket(emac_bucket *b, int nsrc, long off, long len, int tsize
 static int upload_buckets(emac_handle *h, emac_bucket *b, int nb) {
   emac_edge *edges = NULL;
   int rc;
-  if ((rc = emac_layout(b, nb, h->nsrc, h->plan.codes.nlev > 1, h->fan, &edges, &h->nedges, &h->ntiles,
+  if ((rc = emac_layout(b, nb, h->plan.op, h->nsrc, h->plan.codes.nlev > 1, h->fan, &edges, &h->nedges, &h->ntiles,
                         &h->tiles_per_bucket, &h->all_full, &h->unroll)))
     return rc;
   h->nb = nb;
@@ -1007,8 +1008,17 @@ static int ipc_barrier(emac_handle *h, int phase) {
 
 /* barrier errors are reported through the communicator's pinned word (timeout: 1, XCC coverage: 2) */
 static int ipc_status(const emac_handle *h) {
+  int e;
   if (h->kind != KIND_IPC) return 0;
-  return *(volatile int *)comms[h->comm].err ? EMAC_ERR_TRANSPORT : 0;
+  e = *(volatile int *)comms[h->comm].err;
+  if (!e) return 0;
+  if (!comms[h->comm].err_reported) {
+    comms[h->comm].err_reported = 1;
+    fprintf(stderr, "ext_mpi_amd: rank %d: node barrier failed:%s%s\n", comms[h->comm].rank,
+            (e & 1) ? " a peer did not arrive within EXT_MPI_AMD_BARRIER_TIMEOUT" : "",
+            (e & 2) ? " the barrier launch missed an XCD" : "");
+  }
+  return EMAC_ERR_TRANSPORT;
 }
 
 int ext_mpi_amd_start_legs(int handle, int legs) {

@@ -26,7 +26,9 @@
 #include "gpu.h"
 
 extern "C" {
-#define EMAC_DECL(n) int emac_fold_launch_##n(int nsrc, bool tree, int fan, int unroll, const emac::Launch *L);
+#define EMAC_DECL(n)                                                                       \
+  int emac_fold_launch_##n(int nsrc, bool tree, int fan, int unroll, const emac::Launch *L); \
+  int emac_fold_launch_##n##_mm(int op, int nsrc, bool tree, int fan, int unroll, const emac::Launch *L);
 EMAC_DECL(f32)
 EMAC_DECL(f64)
 EMAC_DECL(i32)
@@ -54,13 +56,17 @@ inline void clear_error(const char *what) {
 
 extern "C" {
 
-int emac_gpu_pick_unroll(int nsrc, int tree, int fan, long total_vectors) {
+int emac_gpu_pick_unroll(int op, int nsrc, int tree, int fan, long total_vectors) {
   // returns U | ISSUE << 4 (fold_kernel.hpp, instantiation policy). Measured on MI355X with the
   // production template, R = 8 float, node form (tools/ldsbench.hip, profiles/r01_ldsbench_issue_*):
   // a back-to-back burst of every load of a tile wins at <= 2 MiB and >= 64 MiB per rank;
   // between them U = 4 with an s_sleep after every 4 loads is 4-8 % faster (16 MiB: 41.9 vs
   // 45.2-45.4 us); 64 MiB per rank prefers U = 2 (183 vs 194 us), >= 128 MiB U = 4.
   using emac::sched;
+  if (op != EMAC_SUM && fan != 2) {  // MIN / MAX: the burst schedule of the shape (fold_kernel.hpp)
+    if (tree && nsrc > 1) return sched(emac::tree_unroll(nsrc), 1);
+    return sched(nsrc > 8 ? 1 : 2, 1);
+  }
   if (fan == 2) {  // peer-mapped (IPC) form: one system-coherent schedule per shape
     if (tree && nsrc > 1) return sched(nsrc <= 4 ? 4 : (nsrc <= 8 ? 2 : 1), 1 | emac::kRemote);
     return sched(nsrc > 8 ? 1 : 2, 1 | emac::kRemote);
@@ -88,14 +94,18 @@ int emac_gpu_fold(int dtype, int op, int nsrc, int fan, int unroll, const emac_c
   const bool tree = codes->nlev > 1;  /* fan: 0 one destination, 1 node fan-out, 2 peer-mapped fan-out */
   const emac::Launch L = {codes, d_buckets, nb, ntiles, tiles_per_bucket, all_full, d_edges, nedges,
                           static_cast<hipStream_t>(stream)};
-  if (op != EMAC_SUM) return EMAC_ERR_UNSUPPORTED;
+  if (op < EMAC_SUM || op > EMAC_MAX) return EMAC_ERR_UNSUPPORTED;
   if (nb <= 0 || (ntiles <= 0 && nedges <= 0)) return 0;
   if (codes->nlev > emac::kMaxLevels) return EMAC_ERR_UNSUPPORTED;
   switch (dtype) {
-  case EMAC_FLOAT: return emac_fold_launch_f32(nsrc, tree, fan, unroll, &L);
-  case EMAC_DOUBLE: return emac_fold_launch_f64(nsrc, tree, fan, unroll, &L);
-  case EMAC_INT: return emac_fold_launch_i32(nsrc, tree, fan, unroll, &L);
-  case EMAC_LONG: return emac_fold_launch_i64(nsrc, tree, fan, unroll, &L);
+  case EMAC_FLOAT:
+    return op == EMAC_SUM ? emac_fold_launch_f32(nsrc, tree, fan, unroll, &L) : emac_fold_launch_f32_mm(op, nsrc, tree, fan, unroll, &L);
+  case EMAC_DOUBLE:
+    return op == EMAC_SUM ? emac_fold_launch_f64(nsrc, tree, fan, unroll, &L) : emac_fold_launch_f64_mm(op, nsrc, tree, fan, unroll, &L);
+  case EMAC_INT:
+    return op == EMAC_SUM ? emac_fold_launch_i32(nsrc, tree, fan, unroll, &L) : emac_fold_launch_i32_mm(op, nsrc, tree, fan, unroll, &L);
+  case EMAC_LONG:
+    return op == EMAC_SUM ? emac_fold_launch_i64(nsrc, tree, fan, unroll, &L) : emac_fold_launch_i64_mm(op, nsrc, tree, fan, unroll, &L);
   }
   return EMAC_ERR_ARG;
 }
@@ -217,7 +227,7 @@ int ext_mpi_amd_gpu_copy_reduce(int dtype, int op, int nsrc, const void *const *
   long ntiles = 0, tpb = 0;
   const int fan = ndst > 1;
   if (ndst > 1 && ndst != nsrc) return EMAC_ERR_UNSUPPORTED; /* fan-out width is 1 or nsrc */
-  if ((rc = emac_layout(&b, 1, nsrc, 0, fan, &edges, &nedges, &ntiles, &tpb, &all_full, &unroll))) return rc;
+  if ((rc = emac_layout(&b, 1, op, nsrc, 0, fan, &edges, &nedges, &ntiles, &tpb, &all_full, &unroll))) return rc;
   hipStream_t s = static_cast<hipStream_t>(hip_stream);
   if (hipMallocAsync((void **)&d, sizeof(b) + sizeof(emac_edge) * (nedges + 1), s) != hipSuccess) {
     free(edges);

@@ -3,5 +3,5 @@
 #include "fold_kernel.hpp"
 
 extern "C" int emac_fold_launch_f32(int nsrc, bool tree, int fan, int unroll, const emac::Launch *L) {
-  return emac::launch_t<float>(nsrc, tree, fan, unroll, *L);
+  return emac::launch_t<float, EMAC_SUM>(nsrc, tree, fan, unroll, *L);
 }

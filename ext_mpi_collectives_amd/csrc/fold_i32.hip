@@ -3,5 +3,5 @@
 #include "fold_kernel.hpp"
 
 extern "C" int emac_fold_launch_i32(int nsrc, bool tree, int fan, int unroll, const emac::Launch *L) {
-  return emac::launch_t<int>(nsrc, tree, fan, unroll, *L);
+  return emac::launch_t<int, EMAC_SUM>(nsrc, tree, fan, unroll, *L);
 }

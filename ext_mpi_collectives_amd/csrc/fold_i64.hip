@@ -3,5 +3,5 @@
 #include "fold_kernel.hpp"
 
 extern "C" int emac_fold_launch_i64(int nsrc, bool tree, int fan, int unroll, const emac::Launch *L) {
-  return emac::launch_t<long>(nsrc, tree, fan, unroll, *L);
+  return emac::launch_t<long, EMAC_SUM>(nsrc, tree, fan, unroll, *L);
 }

@@ -1,0 +1,8 @@
+// fold_i64_mm.hip -- long MIN / MAX instantiations of the fold kernels (burst schedule only; see
+// fold_kernel.hpp). The reference's CPU reduction supports both (ext_mpi_native_exec.c:240-318).
+#include "fold_kernel.hpp"
+
+extern "C" int emac_fold_launch_i64_mm(int op, int nsrc, bool tree, int fan, int unroll, const emac::Launch *L) {
+  return op == EMAC_MIN ? emac::launch_t<long, EMAC_MIN>(nsrc, tree, fan, unroll, *L)
+                        : emac::launch_t<long, EMAC_MAX>(nsrc, tree, fan, unroll, *L);
+}

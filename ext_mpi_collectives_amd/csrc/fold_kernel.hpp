@@ -64,6 +64,32 @@ __device__ __forceinline__ void sys_store16(void *tile_base, unsigned byte_off, 
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U32x4, v), r, byte_off, 0, kSysCoherent);
 }
 
+// The element operation. SUM: a + b (integers in unsigned arithmetic). MIN / MAX as the
+// reference's CPU reduction (src/mpi/ext_mpi_native_exec.c:240-318): the accumulator p1 takes
+// the incoming p2 iff p2 < p1 (MIN) / p2 > p1 (MAX), compared in the element's own signed /
+// IEEE type -- a compare and select, not v_min/v_max, so NaN and signed-zero outcomes follow
+// the same order-dependent rule. X is a scalar or a 16-byte vector of T's lane type.
+template <int OP, typename T, typename X>
+__device__ __forceinline__ X combine(X acc, X x) {
+  if constexpr (OP == EMAC_SUM) {
+    return acc + x;
+  } else {
+    constexpr int L = sizeof(X) / sizeof(typename Lane<T>::S);
+    if constexpr (L == 1) {
+      const T a = (T)acc, b = (T)x;
+      return (OP == EMAC_MIN ? b < a : b > a) ? x : acc;
+    } else {
+      X r = acc;
+#pragma unroll
+      for (int i = 0; i < L; ++i) {
+        const T a = (T)acc[i], b = (T)x[i];
+        if (OP == EMAC_MIN ? b < a : b > a) r[i] = x[i];
+      }
+      return r;
+    }
+  }
+}
+
 // a multi-level tree needs a composite leaf count (every radix >= 2)
 constexpr bool can_tree(int n) {
   for (int d = 2; d < n; ++d)
@@ -74,12 +100,12 @@ constexpr bool can_tree(int n) {
 // Replay the fold tree over the leaf values x[0..N) (leaf order of plan.c).
 // Linear form (one reduce-scatter radix): ((x0 + x1) + x2) + ...
 // Tree form: nested left folds, level l accumulates the completed level-(l-1) partials.
-template <int N, bool TREE, typename X>
+template <int OP, typename T, int N, bool TREE, typename X>
 __device__ __forceinline__ X fold_leaves(const X (&x)[N], const emac_codes &c) {
   if constexpr (!TREE) {
     X acc = x[0];
 #pragma unroll
-    for (int t = 1; t < N; ++t) acc = acc + x[t];
+    for (int t = 1; t < N; ++t) acc = combine<OP, T>(acc, x[t]);
     return acc;
   } else {
     X cur = x[0];
@@ -91,7 +117,7 @@ __device__ __forceinline__ X fold_leaves(const X (&x)[N], const emac_codes &c) {
       for (int l = 0; l < kMaxLevels; ++l) {
         if (l < c.nlev) {  // wave-uniform
           // level l takes a value at leaf t iff levels 0..l-1 all completed at t
-          if (l == 0 || c.close[t] >= l) acc[l] = ((c.first[t] >> l) & 1) ? cur : acc[l] + cur;
+          if (l == 0 || c.close[t] >= l) acc[l] = ((c.first[t] >> l) & 1) ? cur : combine<OP, T>(acc[l], cur);
           cur = acc[l];
         }
       }
@@ -102,7 +128,7 @@ __device__ __forceinline__ X fold_leaves(const X (&x)[N], const emac_codes &c) {
 
 // D = fan-out width, a compile-time constant: N for the node form (every rank's receive
 // buffer), 1 for the communicator form. All destination pointers are then loaded up front.
-template <typename T, int N, bool TREE, int D, bool REMOTE = false>
+template <typename T, int OP, int N, bool TREE, int D, bool REMOTE = false>
 __device__ __forceinline__ void fold_scalar_element(const emac_bucket *b, long e, const emac_codes &c) {
   typedef typename Lane<T>::S S;
   const long k = e - b->head;  // bucket pointers sit at element `head`
@@ -115,7 +141,7 @@ __device__ __forceinline__ void fold_scalar_element(const emac_bucket *b, long e
     else
       x[s] = *p;
   }
-  const S r = fold_leaves<N, TREE>(x, c);
+  const S r = fold_leaves<OP, T, N, TREE>(x, c);
 #pragma unroll
   for (int d = 0; d < D; ++d) {
     S *p = static_cast<S *>(b->dst[d]) + k;
@@ -136,7 +162,7 @@ __device__ __forceinline__ void fold_scalar_element(const emac_bucket *b, long e
 // ISSUE (load issue schedule, measured in tools/ldsbench.hip): bit 0 = source-major order
 // (every vector of leaf 0, then leaf 1, ...) instead of vector-major; bits 1.. = s_sleep after
 // every 4 loads (0 = back-to-back burst).
-template <typename T, int N, int U, bool TREE, int D, bool FULL, int ISSUE = 1>
+template <typename T, int OP, int N, int U, bool TREE, int D, bool FULL, int ISSUE = 1>
 __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_base, long nvec, const emac_codes &c) {
   typedef typename Lane<T>::V V;
   typedef __attribute__((address_space(1))) V GV;
@@ -165,7 +191,7 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
   }
   V r[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u) r[u] = fold_leaves<N, TREE>(x[u], c);
+  for (int u = 0; u < U; ++u) r[u] = fold_leaves<OP, T, N, TREE>(x[u], c);
   // destination pointers are only needed now: their descriptor read overlaps the loads
 #pragma unroll
   for (int d = 0; d < D; ++d) {
@@ -187,7 +213,7 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
 
 // Streaming body: one workgroup per tile (grid-stride); a tile is EMAC_BLOCK*U consecutive
 // 16-byte vectors of one bucket. Nothing element-granular runs here (see fold_edge_kernel).
-template <typename T, int N, int U, bool TREE, int D, int ISSUE = 1>
+template <typename T, int OP, int N, int U, bool TREE, int D, int ISSUE = 1>
 __global__ __launch_bounds__(EMAC_BLOCK) void fold_kernel(const emac_bucket *__restrict__ bk, int nb,
                                                           long ntiles, long tiles_per_bucket, int all_full,
                                                           emac_codes codes) {
@@ -218,14 +244,14 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_kernel(const emac_bucket *__r
     // all_full (host-known: every bucket a whole number of tiles) skips the dependent read of
     // nvec before the first load of the tile
     if (all_full || (t + 1) * TILE <= b->nvec)
-      fold_vectors<T, N, U, TREE, D, true, ISSUE>(b, t * TILE, 0, codes);
+      fold_vectors<T, OP, N, U, TREE, D, true, ISSUE>(b, t * TILE, 0, codes);
     else
-      fold_vectors<T, N, U, TREE, D, false, ISSUE>(b, t * TILE, b->nvec, codes);
+      fold_vectors<T, OP, N, U, TREE, D, false, ISSUE>(b, t * TILE, b->nvec, codes);
   }
 }
 
 // Element-granular work: unaligned heads/tails and misaligned buckets, one workgroup per item.
-template <typename T, int N, bool TREE, int D, bool REMOTE = false>
+template <typename T, int OP, int N, bool TREE, int D, bool REMOTE = false>
 __global__ __launch_bounds__(EMAC_BLOCK) void fold_edge_kernel(const emac_bucket *__restrict__ bk,
                                                                const emac_edge *__restrict__ items,
                                                                emac_codes codes) {
@@ -234,12 +260,12 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_edge_kernel(const emac_bucket
   const emac_bucket *b = bk + it.bucket;
   if (it.mode == 1) {
     for (long e = it.start + threadIdx.x; e < it.start + it.count; e += EMAC_BLOCK)
-      fold_scalar_element<T, N, TREE, D, REMOTE>(b, e, codes);
+      fold_scalar_element<T, OP, N, TREE, D, REMOTE>(b, e, codes);
   } else {
     const long nsc = b->head + b->tail;
     for (long i = threadIdx.x; i < nsc; i += EMAC_BLOCK) {
       const long e = i < b->head ? i : b->head + b->nvec * EPV + (i - b->head);
-      fold_scalar_element<T, N, TREE, D, REMOTE>(b, e, codes);
+      fold_scalar_element<T, OP, N, TREE, D, REMOTE>(b, e, codes);
     }
   }
   if constexpr (REMOTE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -253,6 +279,8 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_edge_kernel(const emac_bucket
 // tree (composite N), either fan-out:   U = 4 / 2 / 1 for N <= 4 / <= 8 / > 8, burst; U = 2 also
 //                                        with s_sleep 2 every 4 loads
 // (burst = ISSUE 1: every load of a tile back to back, source-major)
+// MIN / MAX (any fan-out, not peer-mapped): the burst schedule only -- U = tree_unroll(N) for
+// trees, else U = 2 (N <= 8) / 1 -- so the two extra operations add two kernels per shape.
 constexpr int tree_unroll(int n) { return n <= 4 ? 4 : (n <= 8 ? 2 : 1); }
 constexpr int sched(int u, int issue) { return u | issue << 4; }
 // peer-mapped (IPC) launches: (U 2, burst) linear <= 8 leaves, (U 1) above, the tree's U for
@@ -269,19 +297,19 @@ struct Launch {
   hipStream_t s;
 };
 
-template <typename T, int N, int U, bool TREE, int D, int ISSUE = 1>
+template <typename T, int OP, int N, int U, bool TREE, int D, int ISSUE = 1>
 int launch_one(const Launch &L) {
   const long grid = L.ntiles < 8192 ? L.ntiles : 8192;
   if (grid > 0)
-    hipLaunchKernelGGL((fold_kernel<T, N, U, TREE, D, ISSUE>), dim3((unsigned)grid), dim3(EMAC_BLOCK), 0, L.s, L.b,
+    hipLaunchKernelGGL((fold_kernel<T, OP, N, U, TREE, D, ISSUE>), dim3((unsigned)grid), dim3(EMAC_BLOCK), 0, L.s, L.b,
                        L.nb, L.ntiles, L.tpb, L.all_full, *L.c);
   if (L.nedges > 0)
-    hipLaunchKernelGGL((fold_edge_kernel<T, N, TREE, D, (ISSUE & kRemote) != 0>), dim3((unsigned)L.nedges),
+    hipLaunchKernelGGL((fold_edge_kernel<T, OP, N, TREE, D, (ISSUE & kRemote) != 0>), dim3((unsigned)L.nedges),
                        dim3(EMAC_BLOCK), 0, L.s, L.b, L.edges, *L.c);
   return hipGetLastError() == hipSuccess ? 0 : EMAC_ERR_DEVICE;
 }
 
-template <typename T, int N, bool FAN, bool REMOTE = false>
+template <typename T, int OP, int N, bool FAN, bool REMOTE = false>
 int launch_nf(bool tree, int unroll, const Launch &L) {
   constexpr int D = FAN ? N : 1;
   if constexpr (REMOTE) {
@@ -289,49 +317,58 @@ int launch_nf(bool tree, int unroll, const Launch &L) {
     // or 1), system-coherent accesses
     constexpr int UR = N > 8 ? 1 : 2;
     if constexpr (can_tree(N)) {
-      if (tree) return unroll == sched(tree_unroll(N), 1 | kRemote) ? launch_one<T, N, tree_unroll(N), true, D, 1 | kRemote>(L)
+      if (tree) return unroll == sched(tree_unroll(N), 1 | kRemote) ? launch_one<T, OP, N, tree_unroll(N), true, D, 1 | kRemote>(L)
                                                                     : EMAC_ERR_UNSUPPORTED;
     }
     if (tree) return EMAC_ERR_UNSUPPORTED;
-    return unroll == sched(UR, 1 | kRemote) ? launch_one<T, N, UR, false, D, 1 | kRemote>(L) : EMAC_ERR_UNSUPPORTED;
-  }
-  if constexpr (can_tree(N)) {
-    if (tree && unroll == sched(tree_unroll(N), 1)) return launch_one<T, N, tree_unroll(N), true, D>(L);
-    if constexpr (tree_unroll(N) == 2) {
-      if (tree && unroll == sched(2, 5)) return launch_one<T, N, 2, true, D, 5>(L);
+    return unroll == sched(UR, 1 | kRemote) ? launch_one<T, OP, N, UR, false, D, 1 | kRemote>(L) : EMAC_ERR_UNSUPPORTED;
+  } else if constexpr (OP != EMAC_SUM) {
+    // MIN / MAX: one burst schedule per shape (canonical_sched)
+    if constexpr (can_tree(N)) {
+      if (tree) return unroll == sched(tree_unroll(N), 1) ? launch_one<T, OP, N, tree_unroll(N), true, D>(L) : EMAC_ERR_UNSUPPORTED;
     }
     if (tree) return EMAC_ERR_UNSUPPORTED;
-  }
-  if (tree) return EMAC_ERR_UNSUPPORTED;
-  if constexpr (N > 8) {
-    return unroll == sched(1, 1) ? launch_one<T, N, 1, false, D>(L) : EMAC_ERR_UNSUPPORTED;
-  } else if constexpr (FAN) {
-    if (unroll == sched(4, 5)) return launch_one<T, N, 4, false, D, 5>(L);
-    if (unroll == sched(4, 1)) return launch_one<T, N, 4, false, D, 1>(L);
-    if (unroll == sched(2, 1)) return launch_one<T, N, 2, false, D, 1>(L);
+    constexpr int UL = N > 8 ? 1 : 2;
+    return unroll == sched(UL, 1) ? launch_one<T, OP, N, UL, false, D>(L) : EMAC_ERR_UNSUPPORTED;
   } else {
-    if (unroll == sched(2, 1)) return launch_one<T, N, 2, false, D>(L);
-    if (unroll == sched(1, 1)) return launch_one<T, N, 1, false, D>(L);
+    if constexpr (can_tree(N)) {
+      if (tree && unroll == sched(tree_unroll(N), 1)) return launch_one<T, OP, N, tree_unroll(N), true, D>(L);
+      if constexpr (tree_unroll(N) == 2) {
+        if (tree && unroll == sched(2, 5)) return launch_one<T, OP, N, 2, true, D, 5>(L);
+      }
+      if (tree) return EMAC_ERR_UNSUPPORTED;
+    }
+    if (tree) return EMAC_ERR_UNSUPPORTED;
+    if constexpr (N > 8) {
+      return unroll == sched(1, 1) ? launch_one<T, OP, N, 1, false, D>(L) : EMAC_ERR_UNSUPPORTED;
+    } else if constexpr (FAN) {
+      if (unroll == sched(4, 5)) return launch_one<T, OP, N, 4, false, D, 5>(L);
+      if (unroll == sched(4, 1)) return launch_one<T, OP, N, 4, false, D, 1>(L);
+      if (unroll == sched(2, 1)) return launch_one<T, OP, N, 2, false, D, 1>(L);
+    } else {
+      if (unroll == sched(2, 1)) return launch_one<T, OP, N, 2, false, D>(L);
+      if (unroll == sched(1, 1)) return launch_one<T, OP, N, 1, false, D>(L);
+    }
+    return EMAC_ERR_UNSUPPORTED;
   }
-  return EMAC_ERR_UNSUPPORTED;
 }
 
 // fan: 0 fan-out 1 (comm form), 1 fan-out N (node form), 2 fan-out N peer-mapped (IPC form)
-template <typename T, int N>
+template <typename T, int OP, int N>
 int launch_n(bool tree, int fan, int unroll, const Launch &L) {
   if constexpr (N == 1) {
-    return fan == 2 ? launch_nf<T, 1, false, true>(false, unroll, L) : launch_nf<T, 1, false>(false, unroll, L);
+    return fan == 2 ? launch_nf<T, OP, 1, false, true>(false, unroll, L) : launch_nf<T, OP, 1, false>(false, unroll, L);
   } else {
-    return fan == 2 ? launch_nf<T, N, true, true>(tree, unroll, L)
-                    : fan ? launch_nf<T, N, true>(tree, unroll, L) : launch_nf<T, N, false>(tree, unroll, L);
+    return fan == 2 ? launch_nf<T, OP, N, true, true>(tree, unroll, L)
+                    : fan ? launch_nf<T, OP, N, true>(tree, unroll, L) : launch_nf<T, OP, N, false>(tree, unroll, L);
   }
 }
 
-template <typename T>
+template <typename T, int OP>
 int launch_t(int nsrc, bool tree, int fan, int unroll, const Launch &L) {
   switch (nsrc) {
 #define EMAC_CASE(n) \
-  case n: return launch_n<T, n>(tree, fan, unroll, L);
+  case n: return launch_n<T, OP, n>(tree, fan, unroll, L);
     EMAC_CASE(1) EMAC_CASE(2) EMAC_CASE(3) EMAC_CASE(4) EMAC_CASE(5) EMAC_CASE(6) EMAC_CASE(7) EMAC_CASE(8)
     EMAC_CASE(9) EMAC_CASE(10) EMAC_CASE(11) EMAC_CASE(12) EMAC_CASE(13) EMAC_CASE(14) EMAC_CASE(15) EMAC_CASE(16)
 #undef EMAC_CASE

@@ -96,7 +96,7 @@ int emac_gpu_node_barrier(void *self, void *const *d_peers, int slot, int phase,
 /* Launch schedule: unroll U (16-byte vectors per lane per leaf; a tile covers EMAC_BLOCK * U
    vectors) in the low 4 bits, load-issue schedule above (fold_kernel.hpp). fan: the fan-out
    width equals nsrc (node / IPC form) instead of 1. */
-int emac_gpu_pick_unroll(int nsrc, int tree, int fan, long total_vectors);
+int emac_gpu_pick_unroll(int op, int nsrc, int tree, int fan, long total_vectors);
 
 /* Launch the fold over nb device-resident buckets (ntiles tiles in total) on `stream`.
    tiles_per_bucket > 0 declares that every bucket spans exactly that many tiles. */
@@ -107,7 +107,7 @@ int emac_gpu_fold(int dtype, int op, int nsrc, int fan, int unroll, const emac_c
 /* layout.c: alignment split of a bucket whose pointers sit at its first element, and the
    launch layout (tiles, uniform tiles per bucket, unroll, edge items; caller frees edges). */
 void emac_split_alignment(emac_bucket *b, int nsrc, long len, int tsize);
-int emac_layout(emac_bucket *b, int nb, int nsrc, int tree, int fan, emac_edge **edges, int *nedges,
+int emac_layout(emac_bucket *b, int nb, int op, int nsrc, int tree, int fan, emac_edge **edges, int *nedges,
                 long *ntiles, long *tiles_per_bucket, int *all_full, int *unroll);
 
 #ifdef __cplusplus

@@ -38,13 +38,13 @@ void emac_split_alignment(emac_bucket *b, int nsrc, long len, int tsize) {
   for (i = 0; i < b->ndst; i++) b->dst[i] = (char *)b->dst[i] + head * tsize;
 }
 
-int emac_layout(emac_bucket *b, int nb, int nsrc, int tree, int fan, emac_edge **edges_out, int *nedges,
+int emac_layout(emac_bucket *b, int nb, int op, int nsrc, int tree, int fan, emac_edge **edges_out, int *nedges,
                 long *ntiles_out, long *tpb_out, int *all_full_out, int *unroll_out) {
   long total = 0, tv, tiles = 0, uniform = -1;
   int i, ne = 0, unroll, all_full = 1;
   emac_edge *edges;
   for (i = 0; i < nb; i++) total += b[i].nvec;
-  unroll = emac_gpu_pick_unroll(nsrc, tree, fan, total); /* U | ISSUE << 4 */
+  unroll = emac_gpu_pick_unroll(op, nsrc, tree, fan, total); /* U | ISSUE << 4 */
   tv = (long)EMAC_BLOCK * (unroll & 15);
   for (i = 0; i < nb; i++) {
     long t = (b[i].nvec + tv - 1) / tv;

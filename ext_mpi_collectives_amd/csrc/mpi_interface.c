@@ -248,6 +248,14 @@ static int map_type(MPI_Datatype t) {
   return -1;
 }
 
+/* get_reduction_op (include/mpi/ext_mpi_native.h:77-140): SUM, MIN and MAX; user ops -> PMPI */
+static int map_op(MPI_Op op) {
+  if (op == MPI_SUM) return EXT_MPI_AMD_SUM;
+  if (op == MPI_MIN) return EXT_MPI_AMD_MIN;
+  if (op == MPI_MAX) return EXT_MPI_AMD_MAX;
+  return -1;
+}
+
 /* ------------------------------------------- known-answer self-test (debug_persistent.c) */
 
 static void kat_fill(void *buf, long count, int tsize, int world_rank, long add) {
@@ -319,7 +327,7 @@ typedef struct {
 typedef struct {
   const void *send;
   void *recv;
-  int count, dtype, side, row, handle;
+  int count, dtype, op, side, row, handle;
   unsigned long used;
   long serial; /* creation number: equal on every rank for the same collective creation */
 } bentry;
@@ -419,7 +427,7 @@ static int blocking_select_row(const bcomm *b, int side, long bytes) {
 }
 
 /* 0: done, 1: not for this path (caller uses PMPI_Allreduce), <0: engine error. */
-static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int dtype, int tsize, bcomm *b,
+static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int dtype, int op, int tsize, bcomm *b,
                               MPI_Comm comm) {
   size_t bytes = (size_t)count * (size_t)tsize, need, stride;
   int on_dev, side, row, i, rc, slot = -1, in_place, rank;
@@ -471,7 +479,8 @@ static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int
   }
   for (i = 0; i < BCACHE; i++) {
     e = &b->cache[i];
-    if (e->handle >= 0 && e->send == s && e->recv == r && e->count == count && e->dtype == dtype && e->side == side &&
+    if (e->handle >= 0 && e->send == s && e->recv == r && e->count == count && e->dtype == dtype && e->op == op &&
+        e->side == side &&
         e->row == row) {
       slot = i;
       break;
@@ -500,7 +509,7 @@ static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int
     }
     bcomm_drop(b, slot);
     e = &b->cache[slot];
-    if ((rc = ext_mpi_amd_allreduce_init(s, r, count, dtype, EXT_MPI_AMD_SUM, b->ext_comm, copyin, &e->handle))) {
+    if ((rc = ext_mpi_amd_allreduce_init(s, r, count, dtype, op, b->ext_comm, copyin, &e->handle))) {
       e->handle = -1;
       return rc;
     }
@@ -509,6 +518,7 @@ static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int
     e->serial = ++b->serial;
     e->count = count;
     e->dtype = dtype;
+    e->op = op;
     e->side = side;
     e->row = row;
     if (cfg_verbose) {
@@ -560,12 +570,12 @@ int EXT_MPI_Finalize(void) {
 
 int EXT_MPI_Allreduce_init(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
                            MPI_Comm comm, MPI_Info info, int *handle) {
-  int dtype = map_type(datatype), ext_comm, rc, flag = 0, rank, tsize;
+  int dtype = map_type(datatype), eop = map_op(op), ext_comm, rc, flag = 0, rank, tsize;
   const char *copyin = NULL;
   char info_copyin[1024];
   *handle = -1;
   if (!initialised) EXT_MPI_Init();
-  if (dtype < 0 || op != MPI_SUM || count < 0) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
+  if (dtype < 0 || eop < 0 || count < 0) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
   if (sendbuf == MPI_IN_PLACE) sendbuf = recvbuf; /* ext_mpi.c:651-653 */
   /* sockets only change the reference's partner encoding, not the arithmetic (plan.h) */
   if (cfg_num_sockets > 1) {
@@ -583,7 +593,7 @@ int EXT_MPI_Allreduce_init(const void *sendbuf, void *recvbuf, int count, MPI_Da
   PMPI_Type_size(datatype, &tsize);
   if (cfg_debug && (rc = known_answer_test(recvbuf, sendbuf == recvbuf, count, tsize, comm, ext_comm, copyin)))
     return rc;
-  rc = ext_mpi_amd_allreduce_init(sendbuf, recvbuf, count, dtype, EXT_MPI_AMD_SUM, ext_comm, copyin, handle);
+  rc = ext_mpi_amd_allreduce_init(sendbuf, recvbuf, count, dtype, eop, ext_comm, copyin, handle);
   if (cfg_verbose) {
     PMPI_Comm_rank(comm, &rank);
     if (rank == 0) printf("# EXT_MPI allreduce parameters copyin %s\n", copyin ? copyin : "(default 6;1 -R R)");
@@ -748,17 +758,17 @@ int MPI_Testsome(int incount, MPI_Request array_of_requests[], int *outcount, in
   return ret;
 }
 
-/* Blocking MPI_Allreduce (ext_mpi_interface.c:507-535): SUM over the four types below 100 MB on
+/* Blocking MPI_Allreduce (ext_mpi_interface.c:507-535): SUM / MIN / MAX over the four types below 100 MB on
    a registered communicator; anything else goes to PMPI_Allreduce. */
 int MPI_Allreduce(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op, MPI_Comm comm) {
-  int dtype = map_type(datatype), tsize, flag = 0, rc, rank;
+  int dtype = map_type(datatype), eop = map_op(op), tsize, flag = 0, rc, rank;
   bcomm *b = NULL;
-  if (cfg_blocking && initialised && dtype >= 0 && op == MPI_SUM && count >= 0) {
+  if (cfg_blocking && initialised && dtype >= 0 && eop >= 0 && count >= 0) {
     PMPI_Type_size(datatype, &tsize);
     if ((long)count * tsize < BLOCKING_MAX_BYTES) {
       PMPI_Comm_get_attr(comm, blocking_keyval, &b, &flag);
       if (flag && b) {
-        rc = blocking_allreduce(sendbuf, recvbuf, count, dtype, tsize, b, comm);
+        rc = blocking_allreduce(sendbuf, recvbuf, count, dtype, eop, tsize, b, comm);
         if (rc == 0) return MPI_SUCCESS;
         if (rc < 0) {
           PMPI_Comm_rank(comm, &rank);

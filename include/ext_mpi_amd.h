@@ -45,8 +45,12 @@ extern "C" {
 #define EXT_MPI_AMD_LONG 1
 #define EXT_MPI_AMD_FLOAT 2
 #define EXT_MPI_AMD_INT 3
-/* operations (only SUM is on the hot path) */
+/* element operations: SUM is the hot path; MIN / MAX follow the reference's CPU reduction
+   (src/mpi/ext_mpi_native_exec.c:240-318: the accumulator takes the incoming element iff it
+   compares less / greater), which its GPU kernel (src/gpu/cuda_core.cu:88-106) does not cover */
 #define EXT_MPI_AMD_SUM 0
+#define EXT_MPI_AMD_MIN 1
+#define EXT_MPI_AMD_MAX 2
 
 #define EXT_MPI_AMD_SUCCESS 0
 #define EXT_MPI_AMD_ERROR_MALLOC (-1)

@@ -17,6 +17,7 @@ _LIB_PATH = os.path.join(_HERE, "liboracle.so")
 
 # element type codes (ref_oracle.h)
 DOUBLE, LONG, FLOAT, INT, CHAR = 0, 1, 2, 3, 4
+SUM, MIN, MAX = 0, 1, 2  # element operations (ref_oracle.h REF_RED_*)
 NP_DTYPE = {DOUBLE: np.float64, LONG: np.int64, FLOAT: np.float32, INT: np.int32, CHAR: np.int8}
 BY_NAME = {"double": DOUBLE, "f64": DOUBLE, "long": LONG, "int64": LONG, "float": FLOAT,
            "f32": FLOAT, "int": INT, "int32": INT}
@@ -53,6 +54,10 @@ def lib():
         _lib.ref_emulate.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_char_p,
                                      ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                                      ctypes.POINTER(ctypes.c_void_p)]
+        _lib.ref_emulate_op.restype = ctypes.c_int
+        _lib.ref_emulate_op.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                                        ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                        ctypes.POINTER(ctypes.c_void_p)]
         _lib.ref_sizes_displs.restype = None
         _lib.ref_sizes_displs.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_long,
                                           ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_long)]
@@ -113,8 +118,8 @@ def _ptrs(arrays):
     return (ctypes.c_void_p * len(arrays))(*[a.ctypes.data for a in arrays])
 
 
-def allreduce(sends, copyin, in_place=False):
-    """Reference result of an R-rank Allreduce(SUM) of the host arrays ``sends``.
+def allreduce(sends, copyin, in_place=False, op=SUM):
+    """Reference result of an R-rank Allreduce(op: SUM, MIN or MAX) of the host arrays ``sends``.
 
     Returns the list of R receive arrays (all equal for a correct schedule).
     """
@@ -127,7 +132,7 @@ def allreduce(sends, copyin, in_place=False):
         recvs = [s.copy() for s in sends]
     else:
         recvs = [np.full_like(s, -1) for s in sends]
-    rc = lib().ref_emulate(R, a0.size, code, copyin.encode(), int(in_place), _ptrs(sends), _ptrs(recvs))
+    rc = lib().ref_emulate_op(R, a0.size, code, op, copyin.encode(), int(in_place), _ptrs(sends), _ptrs(recvs))
     if rc != 0:
         raise ValueError(f"oracle rejected copyin {copyin!r} for R={R}")
     return recvs

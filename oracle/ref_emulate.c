@@ -43,18 +43,23 @@ static int build_programs(int R, long count, int dtype, const char *copyin, int 
   return 0;
 }
 
-static void exec_op(int R, int r, const ref_op *o, int dtype, void *const *send, void *const *recv) {
+static void exec_op(int R, int r, const ref_op *o, int dtype, int red, void *const *send, void *const *recv) {
   char *dst = (char *)(o->dbuf == REF_BUF_RECV ? recv : send)[(r + o->drel) % R] + o->doff;
   const char *src = (const char *)(o->sbuf == REF_BUF_RECV ? recv : send)[(r + o->srel) % R] + o->soff;
   if (o->op == REF_OP_COPY) {
     if (dst != src) memmove(dst, src, (size_t)o->bytes);
   } else if (o->op == REF_OP_SUM) {
-    ref_reduction(dtype, dst, src, o->bytes / ref_type_size(dtype));
+    ref_reduction_op(red, dtype, dst, src, o->bytes / ref_type_size(dtype));
   }
 }
 
 int ref_emulate(int R, long count, int dtype, const char *copyin, int in_place,
                 void *const *sendbufs, void *const *recvbufs) {
+  return ref_emulate_op(R, count, dtype, REF_RED_SUM, copyin, in_place, sendbufs, recvbufs);
+}
+
+int ref_emulate_op(int R, long count, int dtype, int red, const char *copyin, int in_place,
+                   void *const *sendbufs, void *const *recvbufs) {
   rank_prog *progs;
   void *const *send = in_place ? recvbufs : sendbufs;
   int r, active, rc = 0;
@@ -72,7 +77,7 @@ int ref_emulate(int R, long count, int dtype, const char *copyin, int in_place,
     active = 0;
     for (r = 0; r < R; r++) {
       rank_prog *p = &progs[r];
-      while (p->pc < p->n && p->ops[p->pc].op != REF_OP_PHASE) exec_op(R, r, &p->ops[p->pc++], dtype, send, recvbufs);
+      while (p->pc < p->n && p->ops[p->pc].op != REF_OP_PHASE) exec_op(R, r, &p->ops[p->pc++], dtype, red, send, recvbufs);
       if (p->pc < p->n) p->pc++; /* step over the phase marker */
       if (p->pc < p->n) active = 1;
     }

@@ -6,7 +6,7 @@
  * hook and bench.py's cpu_baseline leg may load this library.
  *
  * Reference files restated (paths relative to the reference checkout):
- *   src/mpi/ext_mpi_native_exec.c:207-234    reduction(), SUM cases        -> ref_reduction.c
+ *   src/mpi/ext_mpi_native_exec.c:207-318    reduction(), SUM/MIN/MAX      -> ref_reduction.c
  *   src/core/reduce_copyin.c:396-427         ext_mpi_sizes_displs          -> ref_schedule.c
  *   src/core/reduce_copyin.c:375-394         ext_mpi_rank_order            -> ref_schedule.c
  *   src/core/reduce_copyin.c:482-486         get_rank_cyclic (1 socket)    -> ref_schedule.c
@@ -50,6 +50,11 @@ int ref_type_size(int dtype);
 /* ext_mpi_native_exec.c:207-234: p1[i] += p2[i] for i < n elements */
 void ref_reduction(int dtype, void *p1, const void *p2, long n);
 
+/* element operations (get_reduction_op, include/mpi/ext_mpi_native.h:77-140) */
+enum { REF_RED_SUM = 0, REF_RED_MIN = 1, REF_RED_MAX = 2 };
+/* ext_mpi_native_exec.c:207-318: SUM as above; MIN / MAX: p1[i] takes p2[i] iff p2[i] < / > p1[i] */
+void ref_reduction_op(int op, int dtype, void *p1, const void *p2, long n);
+
 /* reduce_copyin.c:396-427. sizes/displs in bytes; displs has R+1 entries. */
 void ref_sizes_displs(int R, long bytes, int tsize, long size_l, long *sizes, long *displs);
 
@@ -76,6 +81,9 @@ int ref_schedule(int R, int node_rank, long bytes, int dtype, const int *factors
  */
 int ref_emulate(int R, long count, int dtype, const char *copyin, int in_place,
                 void *const *sendbufs, void *const *recvbufs);
+/* the same with element operation `op` (REF_RED_*) on every SREDUCE line */
+int ref_emulate_op(int R, long count, int dtype, int op, const char *copyin, int in_place,
+                   void *const *sendbufs, void *const *recvbufs);
 
 /* Known-answer input pattern of debug_persistent.c:491-497 (CPU: add=73, GPU: add=0). */
 void ref_kat_fill(void *buf, long count, int tsize, int world_rank, long add);

@@ -34,7 +34,10 @@ def cases(R):
            (emac.FLOAT, 100000, full, True, False, 2), (emac.DOUBLE, 33333, full, False, True, 2),
            (emac.FLOAT, 5000, f"6;-64 -{R} {R}", False, False, 1), (emac.FLOAT, 70001, f"6;3 -{R} {R}", False, False, 1),
            # small raw hipMalloc buffers (sub-allocated by the runtime: not exported, staged through mirrors)
-           (emac.INT, 12345, full, False, "raw", 2), (emac.FLOAT, 3001, full, True, "raw", 1)]
+           (emac.INT, 12345, full, False, "raw", 2), (emac.FLOAT, 3001, full, True, "raw", 1),
+           # MIN / MAX (the reference's CPU reduction, ext_mpi_native_exec.c:240-318)
+           (emac.FLOAT, 100003, full, False, False, 2, emac.MIN), (emac.LONG, 77777, full, False, False, 1, emac.MAX),
+           (emac.DOUBLE, 4099, f"6;-64 -{R} {R}", True, False, 1, emac.MAX)]
     if R == 4:
         out += [(emac.FLOAT, 123457, "6;1 -2 -2 2 2", False, False, 2), (emac.DOUBLE, 54321, "6;1 -2 2 1 2 1 -2 2", False, False, 1)]
     if R == 8:
@@ -58,9 +61,10 @@ def main():
     only = os.environ.get("IPC_CASES")  # diagnosis: comma-separated case indices, in order, repeats allowed
     order = [int(x) for x in only.split(",")] if only else list(range(len(cases(world))))
     for k in order:
-        code, count, copyin, in_place, host, repeats = cases(world)[k]
+        code, count, copyin, in_place, host, repeats = cases(world)[k][:6]
+        op = cases(world)[k][6] if len(cases(world)[k]) > 6 else emac.SUM
         sends = xorshift_inputs(world, count, code, seed_base=0x1C0000 + 97 * k)
-        want = oracle.allreduce(sends, copyin, in_place=in_place)[rank]
+        want = oracle.allreduce(sends, copyin, in_place=in_place, op=op)[rank]
         raw = host == "raw"
         if raw:
             L, nbytes = emac.lib(), sends[rank].nbytes
@@ -70,15 +74,15 @@ def main():
                 drecv = dsend
             else:
                 assert L.ext_mpi_amd_gpu_malloc(ctypes.byref(drecv), nbytes) == 0
-            h = emac.allreduce_init(dsend.value, drecv.value, count, code, comm, copyin)
+            h = emac.allreduce_init(dsend.value, drecv.value, count, code, comm, copyin, op=op)
         elif host:
             hsend = sends[rank].copy()
             hrecv = np.full_like(hsend, -1)
-            h = emac.allreduce_init(hsend.ctypes.data, hrecv.ctypes.data, count, code, comm, copyin)
+            h = emac.allreduce_init(hsend.ctypes.data, hrecv.ctypes.data, count, code, comm, copyin, op=op)
         else:
             send = torch.from_numpy(sends[rank].copy()).cuda()
             recv = send if in_place else torch.full((count,), -1, dtype=TORCH[code], device="cuda")
-            h = emac.allreduce_init(send.data_ptr(), recv.data_ptr(), count, code, comm, copyin)
+            h = emac.allreduce_init(send.data_ptr(), recv.data_ptr(), count, code, comm, copyin, op=op)
         ok = True
         for _ in range(repeats):
             if raw:
@@ -103,7 +107,7 @@ def main():
             if not in_place:
                 L.ext_mpi_amd_gpu_free(drecv)
         failures += not ok
-        print(f"IPC rank {rank}/{world} case {k} code {code} count {count} '{copyin}' in_place={in_place} "
+        print(f"IPC rank {rank}/{world} case {k} code {code} op {op} count {count} '{copyin}' in_place={in_place} "
               f"host={host} x{repeats}: {'ok' if ok else 'MISMATCH'}", flush=True)
     if os.environ.get("IPC_CASES_ONLY"):
         emac.comm_free(comm)

@@ -1,6 +1,6 @@
 /* Drop-in check of libext_mpi_collectives.so, written like an application of the reference
  * (tests/benchmark.c shape): only MPI calls plus the MPI-4 prototype from ext_mpi_interface.h.
- * argv: count dtype(f|d|i|l) mem(dev|host) [inplace] [blocking]. "blocking" drives MPI_Allreduce
+ * argv: count dtype(f|d|i|l) mem(dev|host) [inplace] [blocking] [min|max]. "blocking" drives MPI_Allreduce
  * (run with EXT_MPI_BLOCKING set) instead of MPI_Allreduce_init. Prints "RESULT ok" / "RESULT no-device"
  * / "RESULT fail ...". Integer inputs are checked exactly against PMPI_Allreduce; float inputs
  * are integer-valued (exact in any order) so the same comparison applies. */
@@ -20,9 +20,12 @@ int main(int argc, char **argv) {
   size_t bytes = (size_t)count * ts;
   void *hs, *hr, *ref, *s = NULL, *r = NULL;
   MPI_Request req, p2p[2];
+  MPI_Op op = MPI_SUM;
   for (i = 4; i < argc; i++) {
     inplace |= !strcmp(argv[i], "inplace");
     blocking |= !strcmp(argv[i], "blocking");
+    if (!strcmp(argv[i], "min")) op = MPI_MIN;
+    if (!strcmp(argv[i], "max")) op = MPI_MAX;
   }
   MPI_Init(&argc, &argv);
   MPI_Comm_rank(MPI_COMM_WORLD, &rank);
@@ -37,7 +40,7 @@ int main(int argc, char **argv) {
     else if (t == 'i') ((int *)hs)[i] = (int)v;
     else ((long *)hs)[i] = v;
   }
-  PMPI_Allreduce(hs, ref, count, dt, MPI_SUM, MPI_COMM_WORLD);
+  PMPI_Allreduce(hs, ref, count, dt, op, MPI_COMM_WORLD);
   /* requests we do not own fall through to PMPI (ext_mpi_interface.c:257-265) */
   {
     int a = rank, b = -1, peer = (rank + 1) % size, from = (rank + size - 1) % size;
@@ -50,8 +53,8 @@ int main(int argc, char **argv) {
     if (b != from) bad |= 1;
   }
   if (ext_mpi_amd_gpu_device_count() <= 0) {
-    if (blocking) rc = MPI_Allreduce(hs, hr, count, dt, MPI_SUM, MPI_COMM_WORLD) == MPI_SUCCESS ? 0 : -5;
-    else rc = MPI_Allreduce_init(hs, hr, count, dt, MPI_SUM, MPI_COMM_WORLD, MPI_INFO_NULL, &req);
+    if (blocking) rc = MPI_Allreduce(hs, hr, count, dt, op, MPI_COMM_WORLD) == MPI_SUCCESS ? 0 : -5;
+    else rc = MPI_Allreduce_init(hs, hr, count, dt, op, MPI_COMM_WORLD, MPI_INFO_NULL, &req);
     if (rank == 0) printf("RESULT %s rc=%d\n", (rc == -5 && !bad) ? "no-device" : "fail", rc);
     MPI_Finalize();
     return 0;
@@ -87,7 +90,7 @@ int main(int argc, char **argv) {
         if (dev) ext_mpi_amd_gpu_memcpy_hd(rr, hs, bytes);
         else memcpy(rr, hs, bytes);
       }
-      rc = MPI_Allreduce(inplace ? MPI_IN_PLACE : ss, rr, count, dt, MPI_SUM, c);
+      rc = MPI_Allreduce(inplace ? MPI_IN_PLACE : ss, rr, count, dt, op, c);
       if (rc != MPI_SUCCESS) {
         printf("RESULT fail blocking rc=%d\n", rc);
         MPI_Abort(MPI_COMM_WORLD, 1);
@@ -106,7 +109,7 @@ int main(int argc, char **argv) {
     }
     goto report;
   }
-  rc = MPI_Allreduce_init(inplace ? MPI_IN_PLACE : s, r, count, dt, MPI_SUM, MPI_COMM_WORLD, MPI_INFO_NULL, &req);
+  rc = MPI_Allreduce_init(inplace ? MPI_IN_PLACE : s, r, count, dt, op, MPI_COMM_WORLD, MPI_INFO_NULL, &req);
   if (rc) {
     printf("RESULT fail init rc=%d\n", rc);
     MPI_Abort(MPI_COMM_WORLD, 1);
@@ -128,8 +131,9 @@ int main(int argc, char **argv) {
   MPI_Request_free(&req);
 report:
   MPI_Allreduce(MPI_IN_PLACE, &bad, 1, MPI_INT, MPI_BOR, MPI_COMM_WORLD);
-  if (rank == 0) printf("RESULT %s (size=%d count=%d type=%c mem=%s%s%s) bad=%d\n", bad ? "fail" : "ok", size, count, t,
-                        dev ? "dev" : "host", inplace ? " inplace" : "", blocking ? " blocking" : "", bad);
+  if (rank == 0) printf("RESULT %s (size=%d count=%d type=%c mem=%s%s%s%s) bad=%d\n", bad ? "fail" : "ok", size, count, t,
+                        dev ? "dev" : "host", inplace ? " inplace" : "", blocking ? " blocking" : "",
+                        op == MPI_MIN ? " min" : op == MPI_MAX ? " max" : "", bad);
   if (dev) {
     ext_mpi_amd_gpu_free(r);
     ext_mpi_amd_gpu_free(s);

@@ -29,13 +29,14 @@ def _dev(a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
-def run_node(sends, code, copyin, in_place=False, repeats=1):
+def run_node(sends, code, copyin, in_place=False, repeats=1, op=emac.SUM):
     """Node-form Allreduce of host arrays `sends` on device buffers; returns host results."""
     R = len(sends)
     count = sends[0].size
     dsend = [_dev(s) for s in sends]
     drecv = dsend if in_place else [torch.full((count,), -1, dtype=TORCH[code], device="cuda") for _ in range(R)]
-    h = emac.node_allreduce_init([t.data_ptr() for t in dsend], [t.data_ptr() for t in drecv], count, code, copyin)
+    h = emac.node_allreduce_init([t.data_ptr() for t in dsend], [t.data_ptr() for t in drecv], count, code, copyin,
+                                 op=op)
     try:
         for _ in range(repeats):
             if in_place:
@@ -228,7 +229,7 @@ def test_fold_handle_and_copy_reduce(code, nsrc, ndst):
             assert np.array_equal(d.cpu().numpy().view(np.uint8), want.view(np.uint8)), (how, nsrc, ndst)
 
 
-def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=None):
+def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=None, op=emac.SUM):
     """COMM form (one rank per communicator) on the in-process loopback transport: the legs run
     on every rank in lock-step -- stage-in, reduce-scatter, fold, all-gather, stage-out -- so
     the staging slots, fold buckets and leg programs of the multi-GPU path execute on one GPU."""
@@ -252,7 +253,7 @@ def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=Non
     hs = []
     try:
         for r in range(R):
-            hs.append(emac.allreduce_init(ptrs[r][0], ptrs[r][1], count, code, comms[r], copyin))
+            hs.append(emac.allreduce_init(ptrs[r][0], ptrs[r][1], count, code, comms[r], copyin, op=op))
         torch.cuda.synchronize()
         for leg in (emac.LEG_STAGE_IN, emac.LEG_REDUCE_SCATTER, emac.LEG_FOLD, emac.LEG_ALLGATHER, emac.LEG_STAGE_OUT):
             for h in hs:
@@ -289,3 +290,51 @@ def test_comm_form_loopback_host_and_in_place(oracle, in_place):
     for host in (False, True):
         got = run_comm_loopback(sends, emac.DOUBLE, "6;1 -4 4", host=host, in_place=in_place)
         assert_bitwise(got, want, f"comm host={host} in_place={in_place}")
+
+
+# ---- MIN / MAX: the reference's CPU reduction (ext_mpi_native_exec.c:240-318), not its GPU kernel
+
+def special_inputs(R, count, code, seed):
+    """xorshift inputs with NaN, signed zeros and infinities planted on some ranks (floating
+    point), so that the order-dependent compare-and-select rule is exercised, not only min()."""
+    sends = xorshift_inputs(R, count, code, seed_base=seed)
+    if code in (emac.FLOAT, emac.DOUBLE) and count:
+        idx = np.arange(count)
+        for r, x in enumerate(sends):
+            x[(idx % 7 == 0) & (idx % R == r)] = np.nan
+            x[(idx % 11 == 3)] = -0.0 if r % 2 else 0.0
+            x[(idx % 13 == 5) & (idx % R == (r + 1) % R)] = np.inf
+            x[(idx % 17 == 6) & (idx % R == (r + 2) % R)] = -np.inf
+    return sends
+
+
+MINMAX_CONFIGS = [(2, "6;1 -2 2"), (3, "6;1 -3 3"), (4, "6;1 -2 -2 2 2"), (8, "6;1 -8 8"), (8, "6;1 -2 -2 -2 2 2 2"),
+                  (8, "6;-64 -8 8"), (8, "6;1 -4 4 1 4 1 -2 2"), (16, "6;1 -16 16")]
+
+
+@pytest.mark.parametrize("op", [emac.MIN, emac.MAX])
+@pytest.mark.parametrize("R,copyin", MINMAX_CONFIGS)
+@pytest.mark.parametrize("code", CODES)
+def test_node_min_max_vs_oracle(oracle, op, R, copyin, code):
+    for count in (1, 1031, 65536 + 3):
+        sends = special_inputs(R, count, code, 0x313A0000 + count)
+        want = oracle.allreduce(sends, copyin, op=op)
+        got = run_node(sends, code, copyin, op=op)
+        assert_bitwise(got, want, f"op={op} R={R} {copyin} code={code} n={count}")
+
+
+@pytest.mark.parametrize("op", [emac.MIN, emac.MAX])
+@pytest.mark.parametrize("code", CODES)
+def test_comm_loopback_min_max_vs_oracle(oracle, op, code):
+    for R, copyin in [(4, "6;1 -2 -2 2 2"), (8, "6;1 -8 8")]:
+        sends = special_inputs(R, 65536 + 5, code, 0x313B0000 + R)
+        want = oracle.allreduce(sends, copyin, op=op)
+        got = run_comm_loopback(sends, code, copyin, phase=[(r * 3) % 4 for r in range(R)], op=op)
+        assert_bitwise(got, want, f"comm op={op} R={R} {copyin} code={code}")
+
+
+@pytest.mark.parametrize("op", [emac.MIN, emac.MAX])
+def test_node_min_max_in_place_and_full_size(oracle, op):
+    sends = special_inputs(8, (16 << 20) // 4, emac.FLOAT, 0x313C0000)
+    want = oracle.allreduce(sends, "6;1 -8 8", in_place=True, op=op)
+    assert_bitwise(run_node(sends, emac.FLOAT, "6;1 -8 8", in_place=True, repeats=2, op=op), want, "in place")

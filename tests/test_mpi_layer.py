@@ -104,6 +104,9 @@ def test_mpi_blocking_single_rank_gpu(tmp_path, args, copyin):
     (4, [100003, "f", "dev", "blocking"], {"EXT_MPI_BLOCKING": "1"}),
     (2, [4099, "d", "host", "inplace", "blocking"], {"EXT_MPI_BLOCKING": "1"}),
     (4, [65536, "f", "dev"], {"EXT_MPI_COPYIN": "6;1 -2 -2 2 2"}),
+    # MPI_MIN / MPI_MAX (get_reduction_op, ext_mpi_native.h:77-140): persistent and blocking
+    (4, [100003, "d", "dev", "min"], {}), (2, [4099, "i", "host", "inplace", "max"], {}),
+    (4, [65536, "l", "dev", "blocking", "max"], {"EXT_MPI_BLOCKING": "1"}),
 ])
 def test_mpi_layer_multi_rank_one_gpu(tmp_path, n, args, extra):
     """n MPI ranks sharing the box's one GPU over the default peer-mapped transport: the

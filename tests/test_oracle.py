@@ -117,3 +117,29 @@ def test_cpu_threads_baseline_matches_emulator(oracle):
     want = oracle.allreduce(sends, "6;1 -4 4")
     for r in range(4):
         assert np.array_equal(recvs[r], want[r])
+
+
+@pytest.mark.parametrize("copyin", ["6;1 -4 4", "6;1 -2 -2 2 2", "6;-64 -4 4", "6;3 -4 4"])
+@pytest.mark.parametrize("dt", [np.float32, np.float64, np.int32, np.int64])
+def test_min_max_finite_inputs_are_elementwise_extrema(oracle, copyin, dt):
+    # ext_mpi_native_exec.c:240-318 on finite values: any fold order yields the extremum
+    rng = np.random.default_rng(11)
+    sends = [(rng.integers(-1000, 1000, 3001)).astype(dt) for _ in range(4)]
+    for op, ref in ((oracle.MIN, np.minimum.reduce), (oracle.MAX, np.maximum.reduce)):
+        want = ref(sends)
+        for out in oracle.allreduce(sends, copyin, op=op):
+            assert np.array_equal(out, want)
+
+
+def test_min_max_nan_follows_the_accumulator_rule(oracle):
+    # p1 (the owner's accumulator, its own leaf first) takes p2 only if p2 < p1 (MIN) / p2 > p1
+    # (MAX); every comparison with NaN is false. So the owner's NaN survives, a partner's NaN
+    # never enters: the two owner halves of a 2-rank Allreduce differ.
+    sends = [np.full(8, np.nan, np.float32), np.full(8, 1.0, np.float32)]
+    for op in (oracle.MIN, oracle.MAX):
+        for out in oracle.allreduce(sends, "6;1 -2 2", op=op):
+            assert np.isnan(out[:4]).all() and (out[4:] == 1.0).all()
+    # signed zeros: -0.0 < +0.0 is false, so the accumulator keeps its own zero
+    z = [np.array([0.0, -0.0], np.float64), np.array([-0.0, 0.0], np.float64)]
+    out = oracle.allreduce(z, "6;1 -2 2", op=oracle.MIN)[0]
+    assert np.signbit(out).tolist() == [False, False]
