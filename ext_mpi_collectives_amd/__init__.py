@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(HERE, "libext_mpi_amd.so")
 MPI_LIB_PATH = os.path.join(HERE, "libext_mpi_collectives.so")
 
 DOUBLE, LONG, FLOAT, INT = 0, 1, 2, 3
-SUM = 0
+SUM, MIN, MAX = 0, 1, 2  # element operations (include/ext_mpi_amd.h EXT_MPI_AMD_SUM / _MIN / _MAX)
 UNIQUE_ID_BYTES = 128
 MAX_RANKS = 16
 ERRORS = {-1: "ERROR_MALLOC", -2: "ERROR_SHMEM", -3: "ERROR_ARG", -4: "ERROR_UNSUPPORTED",
