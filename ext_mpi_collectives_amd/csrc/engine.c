@@ -194,9 +194,9 @@ static void mirror_free(emac_handle *h, void *p) {
     emac_gpu_free(p);
 }
 
-/* A buffer the handle can use in place: device memory, and in the IPC form also exportable as a
-   whole allocation (emac_gpu_ipc_exportable) and long enough for the set-up probe (R bytes).
-   Anything else gets a device mirror. */
+/* A buffer the handle can use in place: device memory, and in the IPC form also exportable
+   (emac_gpu_ipc_exportable) and long enough for the set-up probe (R bytes). Anything else gets
+   a device mirror. */
 static int in_place_ok(const emac_handle *h, const void *p) {
   if (!emac_gpu_is_device_pointer(p)) return 0;
   return h->kind != KIND_IPC || (h->bytes >= (size_t)comms[h->comm].size && emac_gpu_ipc_exportable(p));

@@ -78,8 +78,8 @@ int emac_gpu_ipc_open(const void *handle, void **base);
 int emac_gpu_ipc_close(void *base);
 long emac_gpu_alloc_extent(const void *p, void **base); /* bytes of the allocation holding p, or -1 */
 unsigned long long emac_gpu_buffer_id(const void *p);   /* unique id of the allocation, 0 if unknown */
-#define EMAC_IPC_GRANULE (2ul << 20) /* exported allocations: 2 MiB aligned, 2 MiB multiples */
-int emac_gpu_ipc_exportable(const void *p); /* p lies in an allocation of IPC granularity */
+#define EMAC_IPC_GRANULE (2ul << 20) /* library-owned exported allocations: 2 MiB multiples */
+int emac_gpu_ipc_exportable(const void *p); /* p lies in a device allocation the runtime can export */
 int emac_gpu_malloc_uncached(void **p, size_t bytes); /* zeroed, rounded up to EMAC_IPC_GRANULE */
 /* byte probes (IPC set-up): store vals[i] at ptrs[i] / load ptrs[i] into vals[i], system-coherent,
    complete on return */

@@ -221,11 +221,10 @@ long emac_gpu_alloc_extent(const void *p, void **base) {
   return (long)size;
 }
 
-/* Only a whole allocation of IPC granularity is exported: the runtime sub-allocates small
-   hipMallocs out of a shared 2 MiB chunk, and importing such a buffer maps the exporter's whole
-   chunk into the peers; on one MI355X shared by 8 processes that was followed by illegal-address
-   faults in importers a few handles later. A buffer that is not the start of a 2 MiB-aligned
-   allocation of a 2 MiB multiple goes through a pooled mirror instead (engine.c). */
+/* A device buffer is exported in place when the runtime knows its allocation (hipMemGetAddressRange):
+   small hipMallocs are sub-allocated out of a shared chunk and their handle maps that chunk into
+   the peers, which is harmless (the kernels touch only the message range) and every mapping is
+   validated by the set-up probe anyway (engine.c ipc_exchange). */
 int emac_gpu_ipc_exportable(const void *p) {
   void *base = nullptr;
   size_t size = 0;
@@ -233,7 +232,7 @@ int emac_gpu_ipc_exportable(const void *p) {
     clear_error("emac_gpu_ipc_exportable");
     return 0;
   }
-  return ((uintptr_t)base & (EMAC_IPC_GRANULE - 1)) == 0 && size % EMAC_IPC_GRANULE == 0;
+  return size > 0;
 }
 
 int emac_gpu_malloc_uncached(void **p, size_t bytes) {
