@@ -135,6 +135,7 @@ typedef struct {
   unsigned long epoch[2];  /* barriers run per phase (before / after the fold) */
   void *mapped[2 * EMAC_MAX_RANKS];
   int nmapped;
+  int fused; /* whole Allreduce in one launch (emac_gpu_fold_fused) */
 } emac_handle;
 
 static emac_handle *handles[MAX_HANDLES];
@@ -809,6 +810,13 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
   }
   h->nsrc = R;
   h->fan = R > 1 ? 2 : 0; /* peer-mapped fan-out: system-coherent launch */
+  {
+    /* small messages: barrier, fold and barrier in one launch (EXT_MPI_AMD_IPC_FUSED_MAX bytes
+       per rank, default 1 MiB; 0 disables) */
+    const char *fm = getenv("EXT_MPI_AMD_IPC_FUSED_MAX");
+    const long fused_max = fm ? atol(fm) : (1L << 20);
+    h->fused = R > 1 && h->plan.op == EMAC_SUM && (long)h->bytes <= fused_max;
+  }
   if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
     fprintf(stderr, "ipc rank %d: own send %p recv %p bytes %zu, %d buckets, slot %d, %d attempt(s)\n", cm->rank,
             h->dsend[0], h->drecv[0], h->bytes, nb, slot, attempt + 1);
@@ -1024,10 +1032,23 @@ static int ipc_status(const emac_handle *h) {
 int ext_mpi_amd_start_legs(int handle, int legs) {
   emac_handle *h = get(handle);
   int rc, multi;
+  const int core = EXT_MPI_AMD_LEG_REDUCE_SCATTER | EXT_MPI_AMD_LEG_FOLD | EXT_MPI_AMD_LEG_ALLGATHER;
   if (!h) return EMAC_ERR_ARG;
   multi = h->kind == KIND_COMM && h->plan.nranks > 1;
   if (emac_gpu_set_device(h->device)) return EMAC_ERR_DEVICE;
   if ((legs & EXT_MPI_AMD_LEG_STAGE_IN) && (rc = stage_in(h))) return rc;
+  if (h->kind == KIND_IPC && h->fused && (legs & core) == core) {
+    emac_comm *cm = &comms[h->comm];
+    const unsigned long e0 = ++h->epoch[0], e1 = ++h->epoch[1];
+    if ((rc = emac_gpu_fold_fused(h->plan.dtype, h->nsrc, h->unroll, &h->plan.codes, h->d_buckets, h->nb, h->ntiles,
+                                  h->tiles_per_bucket, h->all_full, h->d_edges, h->nedges, cm->sync,
+                                  (void *const *)cm->d_peer_sync, h->slot, cm->size, cm->rank, cm->xcc_mask, cm->err,
+                                  cm->timeout_ticks, e0, e1, h->stream)))
+      return rc;
+    if ((legs & EXT_MPI_AMD_LEG_STAGE_OUT) && (rc = stage_out(h))) return rc;
+    h->started = 1;
+    return 0;
+  }
   if ((legs & EXT_MPI_AMD_LEG_REDUCE_SCATTER) && h->kind == KIND_IPC && h->plan.nranks > 1 &&
       (rc = ipc_barrier(h, 0)))
     return rc;

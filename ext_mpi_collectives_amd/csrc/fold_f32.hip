@@ -5,3 +5,7 @@
 extern "C" int emac_fold_launch_f32(int nsrc, bool tree, int fan, int unroll, const emac::Launch *L) {
   return emac::launch_t<float, EMAC_SUM>(nsrc, tree, fan, unroll, *L);
 }
+
+extern "C" int emac_fold_fused_launch_f32(int nsrc, bool tree, const emac::Launch *L, const emac::FusedLaunch *F) {
+  return emac::launch_fused_t<float>(nsrc, tree, *L, *F);
+}

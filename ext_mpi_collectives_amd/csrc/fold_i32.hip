@@ -5,3 +5,7 @@
 extern "C" int emac_fold_launch_i32(int nsrc, bool tree, int fan, int unroll, const emac::Launch *L) {
   return emac::launch_t<int, EMAC_SUM>(nsrc, tree, fan, unroll, *L);
 }
+
+extern "C" int emac_fold_fused_launch_i32(int nsrc, bool tree, const emac::Launch *L, const emac::FusedLaunch *F) {
+  return emac::launch_fused_t<int>(nsrc, tree, *L, *F);
+}

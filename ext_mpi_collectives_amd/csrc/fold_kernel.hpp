@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include "gpu.h"
+#include "ipc_sync.hpp"
 
 namespace emac {
 
@@ -271,6 +272,66 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_edge_kernel(const emac_bucket
   if constexpr (REMOTE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// The whole peer-mapped Allreduce in ONE launch, for small messages where the two kernel
+// boundaries of barrier -> fold -> barrier cost as much as the fold (each ≈ 1.5-2 us): node
+// barrier phase 0 (ipc_sync.hpp, every workgroup takes part), the tiles and edge items of every
+// bucket grid-strided over the workgroups with system-coherent accesses (fold_vectors REMOTE),
+// node barrier phase 1. The grid never exceeds one workgroup per CU, so every workgroup is
+// resident while any of them waits.
+template <typename T, int OP, int N, int U, bool TREE>
+__global__ __launch_bounds__(EMAC_BLOCK) void ipc_fused_kernel(const emac_bucket *__restrict__ bk, int nb, long ntiles,
+                                                               long tiles_per_bucket, int all_full,
+                                                               const emac_edge *__restrict__ items, int nedges,
+                                                               emac_codes codes, NodeSync ns, unsigned long epoch0,
+                                                               unsigned long epoch1) {
+  constexpr int ISSUE = 1 | kRemote;
+  constexpr long TILE = (long)EMAC_BLOCK * U;
+  constexpr long EPV = 16 / sizeof(typename Lane<T>::S);
+  if (threadIdx.x == 0) node_barrier_lane(ns, 0, epoch0);
+  __syncthreads();
+  for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    int bi;
+    long t;
+    if (tiles_per_bucket > 0) {
+      bi = (int)((unsigned)tile / (unsigned)tiles_per_bucket);
+      t = tile - (long)bi * tiles_per_bucket;
+    } else {
+      int lo = 0, hi = nb - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (bk[mid].tile0 <= tile)
+          lo = mid;
+        else
+          hi = mid - 1;
+      }
+      bi = lo;
+      t = tile - bk[lo].tile0;
+    }
+    const emac_bucket *b = bk + bi;
+    if (all_full || (t + 1) * TILE <= b->nvec)
+      fold_vectors<T, OP, N, U, TREE, N, true, ISSUE>(b, t * TILE, 0, codes);
+    else
+      fold_vectors<T, OP, N, U, TREE, N, false, ISSUE>(b, t * TILE, b->nvec, codes);
+  }
+  for (int item = blockIdx.x; item < nedges; item += gridDim.x) {
+    const emac_edge it = items[item];
+    const emac_bucket *b = bk + it.bucket;
+    if (it.mode == 1) {
+      for (long e = it.start + threadIdx.x; e < it.start + it.count; e += EMAC_BLOCK)
+        fold_scalar_element<T, OP, N, TREE, N, true>(b, e, codes);
+    } else {
+      const long nsc = b->head + b->tail;
+      for (long i = threadIdx.x; i < nsc; i += EMAC_BLOCK) {
+        const long e = i < b->head ? i : b->head + b->nvec * EPV + (i - b->head);
+        fold_scalar_element<T, OP, N, TREE, N, true>(b, e, codes);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every fan-out store acknowledged
+  __syncthreads();
+  if (threadIdx.x == 0) node_barrier_lane(ns, 1, epoch1);
+}
+
 // ---- instantiation policy (keep in sync with emac_gpu_pick_unroll in fold.hip) ----
 // A launch schedule is encoded as U | ISSUE << 4 (EMAC_SCHED).
 // linear, fan-out N (node / IPC form):  N <= 8 -> (U 2, burst), (U 4, burst), (U 4, s_sleep 2
@@ -362,6 +423,42 @@ int launch_n(bool tree, int fan, int unroll, const Launch &L) {
     return fan == 2 ? launch_nf<T, OP, N, true, true>(tree, unroll, L)
                     : fan ? launch_nf<T, OP, N, true>(tree, unroll, L) : launch_nf<T, OP, N, false>(tree, unroll, L);
   }
+}
+
+struct FusedLaunch {
+  NodeSync ns;
+  unsigned long epoch0, epoch1;
+  int grid;
+};
+
+// fused peer-mapped launch: the IPC form's schedule of the shape (pick_unroll fan == 2)
+template <typename T, int N>
+int launch_fused_n(bool tree, const Launch &L, const FusedLaunch &F) {
+  constexpr int UR = N > 8 ? 1 : 2;
+  if constexpr (can_tree(N)) {
+    if (tree) {
+      hipLaunchKernelGGL((ipc_fused_kernel<T, EMAC_SUM, N, tree_unroll(N), true>), dim3((unsigned)F.grid),
+                         dim3(EMAC_BLOCK), 0, L.s, L.b, L.nb, L.ntiles, L.tpb, L.all_full, L.edges, L.nedges, *L.c, F.ns,
+                         F.epoch0, F.epoch1);
+      return hipGetLastError() == hipSuccess ? 0 : EMAC_ERR_DEVICE;
+    }
+  }
+  if (tree) return EMAC_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL((ipc_fused_kernel<T, EMAC_SUM, N, UR, false>), dim3((unsigned)F.grid), dim3(EMAC_BLOCK), 0, L.s,
+                     L.b, L.nb, L.ntiles, L.tpb, L.all_full, L.edges, L.nedges, *L.c, F.ns, F.epoch0, F.epoch1);
+  return hipGetLastError() == hipSuccess ? 0 : EMAC_ERR_DEVICE;
+}
+
+template <typename T>
+int launch_fused_t(int nsrc, bool tree, const Launch &L, const FusedLaunch &F) {
+  switch (nsrc) {
+#define EMAC_CASE(n) \
+  case n: return launch_fused_n<T, n>(tree, L, F);
+    EMAC_CASE(2) EMAC_CASE(3) EMAC_CASE(4) EMAC_CASE(5) EMAC_CASE(6) EMAC_CASE(7) EMAC_CASE(8)
+    EMAC_CASE(9) EMAC_CASE(10) EMAC_CASE(11) EMAC_CASE(12) EMAC_CASE(13) EMAC_CASE(14) EMAC_CASE(15) EMAC_CASE(16)
+#undef EMAC_CASE
+  }
+  return EMAC_ERR_UNSUPPORTED;
 }
 
 template <typename T, int OP>

@@ -63,13 +63,13 @@ int emac_gpu_device_sync(void);
    Per-communicator synchronisation block, in uncached device memory and mapped by every peer:
    flags[slot][phase][q] = last epoch rank q signalled to this rank for that handle slot and
    barrier phase (0: before the fold, 1: after it); arrive / xcc are this rank's own barrier
-   bookkeeping (workgroup arrivals, XCC coverage by epoch parity). */
+   bookkeeping (workgroup arrivals, XCC coverage by epoch parity; ipc_sync.hpp). */
 #define EMAC_SYNC_SLOTS 1024
 #define EMAC_SYNC_WG 16 /* barrier workgroups: dealt round-robin over the 8 XCDs (coverage is checked) */
 #define EMAC_IPC_HANDLE_BYTES 64
 typedef struct {
   unsigned long flags[EMAC_SYNC_SLOTS][2][EMAC_MAX_RANKS];
-  unsigned long arrive[EMAC_SYNC_SLOTS][2];
+  unsigned long arrive[EMAC_SYNC_SLOTS][2]; /* workgroups arrived in the running launch */
   unsigned int xcc[EMAC_SYNC_SLOTS][2][2];
 } emac_sync;
 
@@ -92,6 +92,13 @@ int emac_gpu_xcc_census(unsigned *mask); /* XCCs a wide launch lands on */
 long emac_gpu_wallclock_hz(void);
 int emac_gpu_node_barrier(void *self, void *const *d_peers, int slot, int phase, unsigned long epoch, int nranks,
                           int me, unsigned xcc_expect, int *err, long timeout_ticks, void *stream);
+/* the whole peer-mapped Allreduce (barrier, fold, barrier) in one launch: SUM, small messages */
+#define EMAC_FUSED_MIN_WG 64
+#define EMAC_FUSED_MAX_WG 256
+int emac_gpu_fold_fused(int dtype, int nsrc, int unroll, const emac_codes *codes, const emac_bucket *d_buckets, int nb,
+                        long ntiles, long tiles_per_bucket, int all_full, const emac_edge *d_edges, int nedges,
+                        void *self_sync, void *const *d_peers, int slot, int nranks, int me, unsigned xcc_expect,
+                        int *err, long timeout_ticks, unsigned long epoch0, unsigned long epoch1, void *stream);
 
 /* Launch schedule: unroll U (16-byte vectors per lane per leaf; a tile covers EMAC_BLOCK * U
    vectors) in the low 4 bits, load-issue schedule above (fold_kernel.hpp). fan: the fan-out

@@ -29,6 +29,7 @@
 #include <string.h>
 
 #include "gpu.h"
+#include "ipc_sync.hpp"
 
 namespace {
 
@@ -46,66 +47,13 @@ inline void clear_error(const char *what) {
     fprintf(stderr, "ext_mpi_amd: %s: cleared %s\n", what, hipGetErrorString(e));
 }
 
-__device__ __forceinline__ unsigned xcc_id() {
-  unsigned v;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
-  return v;
-}
-
 __global__ void xcc_census_kernel(unsigned *mask) {
-  if (threadIdx.x == 0) atomicOr(mask, 1u << xcc_id());
+  if (threadIdx.x == 0) atomicOr(mask, 1u << emac::xcc_id());
 }
 
-// One lane per workgroup does the protocol; the workgroup count is EMAC_SYNC_WG.
-// Fences by phase. Before the fold (phase 0) a release: the application's stores into this
-// rank's send buffer may sit dirty in any XCD's L2, and the peers read that buffer from memory;
-// and, once every peer has signalled, an acquire, so that no line of a peer's buffer that an
-// earlier kernel of this process left valid in an L2 is returned to the fold. After the fold
-// (phase 1) only the acquire: the peers' fan-out stores have landed in this rank's receive
-// buffer behind its L2s. The fold's own accesses are system-coherent (sc0 sc1 loads,
-// write-through stores drained before each wave ends; fold_kernel.hpp kRemote).
-__global__ __launch_bounds__(64) void node_barrier_kernel(emac_sync *self, emac_sync *const *peers, int slot,
-                                                          int phase, unsigned long epoch, int nranks, int me,
-                                                          unsigned xcc_expect, int *err, long timeout) {
-  if (threadIdx.x != 0) return;
-  if (phase == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: L2 write-back
-    // hipcc drops the wait behind buffer_wbl2 when nothing else is outstanding
-    // (MI355X_MICROARCH.md, compiler hazard): the arrival below must follow the write-back
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  atomicOr(&self->xcc[slot][phase][epoch & 1], 1u << xcc_id());
-  const unsigned long arrived =
-      __hip_atomic_fetch_add(&self->arrive[slot][phase], 1ul, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // (relaxed: the release above has already drained -- s_waitcnt after buffer_wbl2 -- before
-  // this add issues, so the last arriver's signal follows every workgroup's write-back)
-  if (arrived == epoch * gridDim.x - 1) {  // last workgroup of this rank: every XCD has released
-    const unsigned seen = __hip_atomic_load(&self->xcc[slot][phase][epoch & 1], __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-    if ((seen & xcc_expect) != xcc_expect) __hip_atomic_fetch_or(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    // next epoch's mask (the barrier of a slot and phase runs on one stream: no overlap)
-    __hip_atomic_store(&self->xcc[slot][phase][(epoch + 1) & 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int q = 0; q < nranks; ++q)
-      if (q != me)
-        __hip_atomic_store(&peers[q]->flags[slot][phase][me], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  const long t0 = wall_clock64();
-  for (int q = 0; q < nranks; ++q) {
-    if (q == me) continue;
-    while (__hip_atomic_load(&self->flags[slot][phase][q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-      __builtin_amdgcn_s_sleep(4);
-      if (wall_clock64() - t0 > timeout) {
-        __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return;
-      }
-    }
-  }
-  // acquire: lines of this XCD's L2 that the peers have since rewritten are dropped -- after
-  // the fold (phase 1) their fan-out into this rank's receive buffer; before it (phase 0) their
-  // send buffers, which the fold is about to load (a line this process's earlier kernels left
-  // valid would otherwise be returned even to the fold's sc0 sc1 loads)
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: L2 invalidate
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // completed before the launch ends
+// The stand-alone node barrier (ipc_sync.hpp): EMAC_SYNC_WG one-lane workgroups.
+__global__ __launch_bounds__(64) void node_barrier_kernel(emac::NodeSync ns, int phase, unsigned long epoch) {
+  if (threadIdx.x == 0) emac::node_barrier_lane(ns, phase, epoch);
 }
 
 // Byte probes of the IPC set-up (engine.c ipc_exchange): one lane per byte. Stores are
@@ -283,9 +231,10 @@ long emac_gpu_wallclock_hz(void) {
 
 int emac_gpu_node_barrier(void *self, void *const *d_peers, int slot, int phase, unsigned long epoch, int nranks,
                           int me, unsigned xcc_expect, int *err, long timeout_ticks, void *stream) {
-  hipLaunchKernelGGL(node_barrier_kernel, dim3(EMAC_SYNC_WG), dim3(64), 0, static_cast<hipStream_t>(stream),
-                     static_cast<emac_sync *>(self), reinterpret_cast<emac_sync *const *>(d_peers), slot, phase, epoch,
-                     nranks, me, xcc_expect, err, timeout_ticks);
+  const emac::NodeSync ns = {static_cast<emac_sync *>(self), reinterpret_cast<emac_sync *const *>(d_peers), slot,
+                             nranks, me, xcc_expect, err, timeout_ticks};
+  hipLaunchKernelGGL(node_barrier_kernel, dim3(EMAC_SYNC_WG), dim3(64), 0, static_cast<hipStream_t>(stream), ns, phase,
+                     epoch);
   return ok(hipGetLastError());
 }
 
