@@ -6,7 +6,8 @@
 // shared memory spun on by the CPU (src/mpi/ext_mpi_native_exec.c:21-84,513-528) around a
 // cudaDeviceSynchronize before every barrier. Here the same mapping is made with hipIpc
 // (dmabuf) and the node barrier is a small stream-ordered kernel, so a whole Allreduce is three
-// launches on the rank's own stream and never returns to the host:
+// launches on the rank's own stream and never returns to the host (one launch for small
+// messages: fold_kernel.hpp ipc_fused_kernel):
 //
 //   node_barrier(in)  -> fold over peer-mapped leaves, fan-out into every peer's recv -> node_barrier(out)
 //
@@ -14,8 +15,9 @@
 // back nor invalidated for other agents by plain stores/loads. The fold between the barriers
 // is system-coherent by itself (sc0 sc1 loads and write-through stores), so what remains is
 // the application's side: before the fold a barrier workgroup runs a system-scope release
-// (L2 write-back of its XCD: the send buffer the peers will read), after it a system-scope
-// acquire (L2 invalidate: the receive buffer the peers have written), and the barrier is
+// (L2 write-back of its XCD: the send buffer the peers will read), after each barrier a
+// system-scope acquire (L2 invalidate: the receive buffer the peers have written, and lines of
+// the peers' buffers left by earlier kernels of this process), and the barrier is
 // launched wide enough to cover every XCD: the workgroups OR their XCC id into a mask, and the rank's last arriver checks the
 // mask against the census taken at communicator set-up before it signals the peers (a missed
 // XCD is reported as a transport error instead of silently risking stale lines). Flags live in
