@@ -467,8 +467,12 @@ def _comm_run(emac, comm, count, tdtype, code, dname, copyin, steps, warmup, ran
     for _ in range(steps):
         emac.start(h)
     emac.wait(h)
-    dist.barrier()
+    torch.cuda.synchronize()
+    # each rank's own completion time (the barrier above aligned the starts); the slowest rank's
+    # is the job's. The trailing barrier stays outside the timed region: a gloo round trip is
+    # 100-300 us, as long as dozens of small Allreduces.
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.barrier()
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     return h, send, recv, stream, el.item(), checked
 
@@ -550,6 +554,23 @@ def transport_child(args):
                               "algbw_gbps": round(cnt * tsz * st / el_p / 1e9, 2), "checked": ok_p})
                 log(f"rank {rank}: {transport}: sweep {dname_p} {cnt * tsz} B: {el_p * 1e6 / st:.2f} us, checked {ok_p}")
             res["sweep"] = sweep
+            # BASELINE configs[4]: EXT_MPI_COPYIN radix variants of this node size (radix chains
+            # and the small-message -64 fraction) at a latency, a middle and a bandwidth point
+            variants = {8: ["6;1 -2 -2 -2 2 2 2", "6;1 -4 -2 2 4", "6;-64 -8 8"], 4: ["6;1 -2 -2 2 2", "6;-64 -4 4"],
+                        2: ["6;-64 -2 2"]}.get(world, [])
+            radix = []
+            for cp in variants:
+                for nbytes in (64 << 10, 1 << 20, 16 << 20):
+                    cnt, st = nbytes // tsize, 100 if nbytes <= (1 << 20) else 20
+                    hp, sb, rb, _, el_p, ok_p = _comm_run(emac, comm, cnt, tdtype, code, dname, cp, st, 3, rank, world,
+                                                          dist, torch)
+                    emac.done(hp)
+                    sb.free()
+                    rb.free()
+                    radix.append({"copyin": cp, "bytes_per_rank": nbytes, "us_per_allreduce": round(el_p * 1e6 / st, 2),
+                                  "algbw_gbps": round(nbytes * st / el_p / 1e9, 2), "checked": ok_p})
+                    log(f"rank {rank}: {transport}: '{cp}' {nbytes} B: {el_p * 1e6 / st:.2f} us, checked {ok_p}")
+            res["radix_sweep"] = radix
     finally:
         emac.comm_free(comm)
     with open(args.child_result, "w") as f:
@@ -628,6 +649,7 @@ def multi_gpu(args):
         wall, checked, kf = r["wall"], r["checked"], r["fold_s"]
         extras["transport"] = primary
         extras["sweep"] = r["sweep"]
+        extras["radix_sweep"] = r.get("radix_sweep", [])
         chunk = S / world
         if primary == "ipc":
             algo = 2 * world * chunk  # R leaf reads (R-1 over xGMI) + R fan-out writes (R-1 over xGMI)
