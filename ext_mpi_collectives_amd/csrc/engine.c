@@ -717,9 +717,15 @@ static int ipc_exchange(emac_handle *h, emac_comm *cm, int rc, int empty, ipc_ex
         base = ipc_map_peer(cm, r, e->handle, e->buf_id, e->extent);
         if (!base) continue;
         h->mapped[h->nmapped++] = base;
+        /* a mapping the runtime can describe must hold the peer's whole buffer (one it cannot
+           describe is taken at the exporter's word; the probe still checks it is reachable) */
         extent = emac_gpu_alloc_extent(base, &ext_base);
-        if (extent < 0 || ext_base != base || extent != e->extent || e->offset < 0 ||
-            e->offset + (long)h->bytes > extent || e->offset + R > extent)
+        if (extent < 0) {
+          extent = e->extent;
+          ext_base = base;
+        }
+        if (ext_base != base || extent != e->extent || e->offset < 0 || e->offset + (long)h->bytes > extent ||
+            e->offset + R > extent)
           continue; /* short mapping: never launched over */
         (t ? precv : psend)[r] = (char *)base + e->offset;
         pk[n] = (char *)base + e->offset + cm->rank;
