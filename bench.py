@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--copyin", default=None, help="EXT_MPI_COPYIN (default '6;1 -R R')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the 256 MiB and host-buffer points")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound of the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=30.0, help="bound of the CPU baseline sample")
     ap.add_argument("--transport", default="ipc", choices=["ipc", "rccl"],
                     help="N > 1: peer-mapped hipIpc form (default) or RCCL point-to-point legs")
     ap.add_argument("--child-transport", default=None, choices=["ipc", "rccl"], help=argparse.SUPPRESS)
@@ -315,11 +315,12 @@ def cpu_baseline(R, count, np_dtype, copyin, seconds):
     recvs = [np.empty_like(s) for s in sends]
     iters, t = 1, 0.0
     budget_left = seconds
-    # tests/benchmark.c:92-157: double the iteration count until a run takes >= 2 s
+    # tests/benchmark.c:92-157 doubles the iteration count until a run takes >= 2 s; here until
+    # >= 8 s (a 10-30 s sample of CPU work in all, bounded by `seconds`)
     while True:
         t = oracle.cpu_allreduce_threads(sends, recvs, copyin, iters)
         budget_left -= t
-        if t >= 2.0 or budget_left < 2.5 * t:
+        if t >= 8.0 or budget_left < 2.5 * t:
             break
         iters *= 2
     return {"value": round(iters * R * count * np.dtype(np_dtype).itemsize / t / 1e9, 3), "unit": "GB/s",
