@@ -48,6 +48,24 @@ def cases(R):
                 (emac.FLOAT, 64 << 20, full, False, False, 1)]
     if R == 3:
         out += [(emac.DOUBLE, 99999, "6;2 -3 3", True, False, 2)]
+    return out + fuzz_cases(R, int(os.environ.get("IPC_FUZZ", "0")))
+
+
+def fuzz_cases(R, n):
+    """n random cases (IPC_FUZZ=n), the same on every rank: sizes log-uniform up to 4 Mi elements,
+    every type and operation, copy-in variants of R, in place, host and raw device buffers."""
+    rng = np.random.default_rng(0xF022 + R)
+    variants = [f"6;1 -{R} {R}", f"6;-64 -{R} {R}", f"6;2 -{R} {R}", f"6;3 -{R} {R}"]
+    variants += {4: ["6;1 -2 -2 2 2"], 8: ["6;1 -2 -2 -2 2 2 2", "6;1 -4 -2 2 4"], 6: ["6;1 -2 -3 3 2"]}.get(R, [])
+    out = []
+    for _ in range(n):
+        count = int(min(4 << 20, np.exp(rng.uniform(0, np.log(4 << 20)))))
+        code = int(rng.choice([emac.FLOAT, emac.DOUBLE, emac.INT, emac.LONG]))
+        op = int(rng.choice([emac.SUM, emac.SUM, emac.MIN, emac.MAX]))
+        in_place = bool(rng.random() < 0.3)
+        host = [False, False, True, "raw"][int(rng.integers(4))]
+        in_place = in_place and host is not True  # the host branch below has no in-place form
+        out.append((code, count, variants[int(rng.integers(len(variants)))], in_place, host, int(rng.integers(1, 3)), op))
     return out
 
 
