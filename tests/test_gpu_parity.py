@@ -338,3 +338,31 @@ def test_node_min_max_in_place_and_full_size(oracle, op):
     sends = special_inputs(8, (16 << 20) // 4, emac.FLOAT, 0x313C0000)
     want = oracle.allreduce(sends, "6;1 -8 8", in_place=True, op=op)
     assert_bitwise(run_node(sends, emac.FLOAT, "6;1 -8 8", in_place=True, repeats=2, op=op), want, "in place")
+
+
+def _radix_chain(R):
+    fs, n = [], R
+    for p in (2, 3, 5, 7, 11, 13):
+        while n % p == 0:
+            fs.append(p)
+            n //= p
+    return "6;1 " + " ".join(f"-{f}" for f in fs) + " " + " ".join(str(f) for f in reversed(fs)) if len(fs) > 1 else None
+
+
+def test_node_random_cases_vs_oracle(oracle):
+    """Seeded random node-form cases: node size, size, type, operation, copy-in variant, in place."""
+    rng = np.random.default_rng(0x9A11)
+    for _ in range(40):
+        R = int(rng.integers(2, 17))
+        variants = [f"6;1 -{R} {R}", f"6;-64 -{R} {R}", f"6;{int(rng.integers(2, 5))} -{R} {R}"]
+        if _radix_chain(R):
+            variants.append(_radix_chain(R))
+        copyin = variants[int(rng.integers(len(variants)))]
+        count = int(min(1 << 21, np.exp(rng.uniform(0, np.log(1 << 21)))))
+        code = int(rng.choice(CODES))
+        op = int(rng.choice([emac.SUM, emac.SUM, emac.MIN, emac.MAX]))
+        in_place = bool(rng.random() < 0.3)
+        sends = special_inputs(R, count, code, int(rng.integers(1 << 30)))
+        want = oracle.allreduce(sends, copyin, in_place=in_place, op=op)
+        got = run_node(sends, code, copyin, in_place=in_place, op=op)
+        assert_bitwise(got, want, f"R={R} '{copyin}' code={code} op={op} n={count} in_place={in_place}")
