@@ -809,7 +809,9 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
     emac_bucket *bk = &b[nb];
     if (len <= 0) continue;
     for (t = 0; t < R; t++) bk->src[t] = psend[h->plan.leaf_rank[c][t]];
-    for (r = 0; r < R; r++) bk->dst[r] = precv[r];
+    /* fan-out order rotated by rank (next peer first, own buffer last), so that at any moment
+       the ranks' stores head for different GPUs' links rather than all for rank 0's */
+    for (r = 0; r < R; r++) bk->dst[r] = precv[(cm->rank + 1 + r) % R];
     bk->ndst = R;
     place_bucket(bk, R, off, len, h->plan.tsize);
     nb++;
