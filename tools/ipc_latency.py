@@ -35,6 +35,8 @@ def main():
     dev = int(os.environ.get("LOCAL_RANK", rank)) % torch.cuda.device_count()
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo")
+    if os.environ.get("IPC_LAT_EARLY_POOL"):  # diagnosis: torch's stream pool created before the communicator
+        torch.cuda.Stream()
     comm = emac.comm_init_ipc(rank, world, emac.torch_allgather(), dev)
     out = {"world": world, "gpus": torch.cuda.device_count(), "points": []}
     sizes = [int(v) for v in os.environ.get("IPC_LAT_SIZES", "8,65536,1048576").split(",")]
@@ -49,6 +51,10 @@ def main():
             for _ in range(int(os.environ.get("IPC_LAT_SKIP_STREAMS", "0"))):  # diagnosis: pool position
                 torch.cuda.Stream()
             s = torch.cuda.Stream()
+            if os.environ.get("IPC_LAT_WARM"):  # diagnosis: the stream used once before the handle gets it
+                with torch.cuda.stream(s):
+                    torch.zeros(1, device="cuda").add_(1)
+                s.synchronize()
             emac.set_stream(h, s.cuda_stream)
         full = timed(h, emac.LEG_ALL, 200, s)
         if os.environ.get("IPC_LAT_TWICE"):  # diagnosis: the same handle and stream timed again
