@@ -533,6 +533,22 @@ def transport_child(args):
             dist.barrier()
             dist.broadcast(alone_s, src=0)
             res.update(fold_s=fold_s.item(), alone_s=alone_s.item())
+            # SURVEY.md 8(d)'s 'per-GPU rate retained': the LOCAL fold kernel (R leaves of this
+            # run's chunk size -> 1 destination, all in this GPU's HBM) on every GPU at once
+            # inside the N-GPU job, against the same kernel on rank 0's GPU while the others idle
+            chunk = max(1, count // world)
+            dist.barrier()
+            lf = torch.tensor([comm_shape_fold(world, chunk, tdtype, code, 100)["avg_launch_us"]], dtype=torch.float64)
+            dist.all_reduce(lf, op=dist.ReduceOp.MAX)
+            dist.barrier()
+            lf_alone = torch.zeros(1, dtype=torch.float64)
+            if rank == 0:
+                lf_alone[0] = comm_shape_fold(world, chunk, tdtype, code, 100)["avg_launch_us"]
+            dist.barrier()
+            dist.broadcast(lf_alone, src=0)
+            res["local_fold"] = {"leaves": world, "chunk_bytes": chunk * tsize, "us_all_gpus": lf.item(),
+                                 "us_rank0_alone": lf_alone.item(),
+                                 "rate_retained": round(lf_alone.item() / lf.item(), 3)}
         emac.done(h)
         send.free()
         recv.free()
@@ -651,6 +667,7 @@ def multi_gpu(args):
         extras["transport"] = primary
         extras["sweep"] = r["sweep"]
         extras["radix_sweep"] = r.get("radix_sweep", [])
+        extras["local_fold_rate_retained"] = r.get("local_fold")
         chunk = S / world
         if primary == "ipc":
             algo = 2 * world * chunk  # R leaf reads (R-1 over xGMI) + R fan-out writes (R-1 over xGMI)
