@@ -124,8 +124,8 @@ int emac_gpu_fold_fused(int dtype, int nsrc, int unroll, const emac_codes *codes
           xcc_expect, err, timeout_ticks};
   F.epoch0 = epoch0;
   F.epoch1 = epoch1;
-  /* at least EMAC_SYNC_WG workgroups (XCD coverage of the fences), at most one per CU (every
-     workgroup resident while others wait) */
+  /* at least EMAC_SYNC_WG workgroups (XCD coverage of the fences), at most EMAC_FUSED_MAX_WG
+     (all resident while others wait; few CUs held from other streams while a peer is late) */
   F.grid = (int)(work < EMAC_FUSED_MIN_WG ? EMAC_FUSED_MIN_WG : work > EMAC_FUSED_MAX_WG ? EMAC_FUSED_MAX_WG : work);
   if (codes->nlev > emac::kMaxLevels || nsrc < 2) return EMAC_ERR_UNSUPPORTED;
   if (nb > 0 && unroll != emac_gpu_pick_unroll(EMAC_SUM, nsrc, tree, 2, 0)) return EMAC_ERR_UNSUPPORTED; /* layout's tiles */
