@@ -99,6 +99,31 @@ typedef struct {
 } loop_group;
 static loop_group loops[MAX_LOOP_GROUPS];
 
+/* one fold launch over a set of device-resident buckets (a handle's main launch, or one part of
+   a pipelined host-staged NODE handle) */
+typedef struct {
+  emac_bucket *d_buckets;
+  int nb;
+  long ntiles, tiles_per_bucket;
+  int all_full;
+  emac_edge *d_edges;
+  int nedges;
+  int unroll;
+} emac_launch;
+
+/* NODE form with host buffers: the message is staged in EMAC_PIPE_PARTS element ranges so that
+   the H2D copies of part p+1, the fold of part p and the D2H copies of part p-1 overlap
+   (three streams, events between them) */
+#define EMAC_PIPE_PARTS 8
+#define EMAC_PIPE_MIN_BYTES (4L << 20) /* per rank */
+typedef struct {
+  int nparts;
+  long off[EMAC_PIPE_PARTS + 1]; /* element ranges */
+  emac_launch part[EMAC_PIPE_PARTS];
+  void *s_in, *s_out;
+  void *ev_start, *ev_in[EMAC_PIPE_PARTS], *ev_fold[EMAC_PIPE_PARTS], *ev_done;
+} emac_pipe;
+
 typedef struct {
   int kind;
   emac_plan plan;
@@ -136,6 +161,7 @@ typedef struct {
   void *mapped[2 * EMAC_MAX_RANKS];
   int nmapped;
   int fused; /* whole Allreduce in one launch (emac_gpu_fold_fused) */
+  emac_pipe *pipe; /* pipelined host staging (NODE form), or NULL */
 } emac_handle;
 
 static emac_handle *handles[MAX_HANDLES];
@@ -151,6 +177,24 @@ static int new_handle_slot(void) {
 static void ipc_unmap(emac_comm *cm, void *base);
 static void mirror_free(emac_handle *h, void *p);
 
+static void pipe_free(emac_pipe *pp) {
+  int p;
+  if (!pp) return;
+  if (pp->s_in) emac_gpu_stream_sync(pp->s_in);
+  if (pp->s_out) emac_gpu_stream_sync(pp->s_out);
+  for (p = 0; p < pp->nparts; p++) {
+    emac_gpu_free(pp->part[p].d_buckets);
+    emac_gpu_free(pp->part[p].d_edges);
+    emac_gpu_event_destroy(pp->ev_in[p]);
+    emac_gpu_event_destroy(pp->ev_fold[p]);
+  }
+  emac_gpu_event_destroy(pp->ev_start);
+  emac_gpu_event_destroy(pp->ev_done);
+  if (pp->s_in) emac_gpu_stream_destroy(pp->s_in);
+  if (pp->s_out) emac_gpu_stream_destroy(pp->s_out);
+  free(pp);
+}
+
 static void release(emac_handle *h) {
   int r;
   if (!h) return;
@@ -158,6 +202,7 @@ static void release(emac_handle *h) {
     emac_gpu_stream_sync(h->stream);
     if (h->own_stream) emac_gpu_stream_destroy(h->stream);
   }
+  pipe_free(h->pipe);
   emac_gpu_free(h->d_buckets);
   emac_gpu_free(h->d_edges);
   emac_gpu_free(h->staging);
@@ -247,6 +292,21 @@ static void place_bucket(emac_bucket *b, int nsrc, long off, long len, int tsize
   emac_split_alignment(b, nsrc, len, tsize);
 }
 
+static int upload_launch(const emac_handle *h, emac_launch *L, emac_bucket *b, int nb) {
+  emac_edge *edges = NULL;
+  int rc;
+  if ((rc = emac_layout(b, nb, h->plan.op, h->nsrc, h->plan.codes.nlev > 1, h->fan, &edges, &L->nedges, &L->ntiles,
+                        &L->tiles_per_bucket, &L->all_full, &L->unroll)))
+    return rc;
+  L->nb = nb;
+  if (nb && (rc = emac_gpu_malloc((void **)&L->d_buckets, sizeof(emac_bucket) * (size_t)nb)) == 0)
+    rc = emac_gpu_memcpy(L->d_buckets, b, sizeof(emac_bucket) * (size_t)nb);
+  if (!rc && L->nedges && (rc = emac_gpu_malloc((void **)&L->d_edges, sizeof(emac_edge) * (size_t)L->nedges)) == 0)
+    rc = emac_gpu_memcpy(L->d_edges, edges, sizeof(emac_edge) * (size_t)L->nedges);
+  free(edges);
+  return rc;
+}
+
 static int upload_buckets(emac_handle *h, emac_bucket *b, int nb) {
   emac_edge *edges = NULL;
   int rc;
@@ -280,12 +340,75 @@ static int finish_init(emac_handle *h, int *handle) {
   return 0;
 }
 
+/* The NODE form's buckets restricted to message elements [lo, hi): every owner chunk (piece pc,
+   position c) clipped to the range; leaves in the plan's fold order, fan-out into every rank's
+   receive buffer. Returns the number written to b (capacity npieces * nranks). */
+static int node_buckets(const emac_handle *h, long lo, long hi, emac_bucket *b) {
+  const int R = h->plan.nranks;
+  int pc, c, t, r, nb = 0;
+  for (pc = 0; pc < h->plan.npieces; pc++) {
+    for (c = 0; c < R; c++) {
+      const long off = h->plan.chunk_off[(size_t)pc * R + c], len = h->plan.chunk_len[(size_t)pc * R + c];
+      const long a = off > lo ? off : lo, e = off + len < hi ? off + len : hi;
+      emac_bucket *bk = &b[nb];
+      if (len <= 0 || a >= e) continue;
+      memset(bk, 0, sizeof(*bk));
+      for (t = 0; t < R; t++) bk->src[t] = h->dsend[h->plan.leaf_rank[c][t]];
+      for (r = 0; r < R; r++) bk->dst[r] = h->drecv[r];
+      bk->ndst = R;
+      place_bucket(bk, R, a, e - a, h->plan.tsize);
+      nb++;
+    }
+  }
+  return nb;
+}
+
+/* Pipelined staging of a NODE handle whose buffers are mirrored host memory: the message in
+   EMAC_PIPE_PARTS element ranges, each its own fold launch between its copies (ext_mpi_amd_start). */
+static int node_pipe_init(emac_handle *h) {
+  emac_pipe *pp;
+  emac_bucket *pb;
+  const long count = (long)(h->bytes / (size_t)h->plan.tsize);
+  long step;
+  int r, p, any = 0, rc = 0;
+  for (r = 0; r < h->nbuf; r++) any |= h->send_mirror[r] | h->recv_mirror[r];
+  if (!any || (long)h->bytes < EMAC_PIPE_MIN_BYTES || getenv("EXT_MPI_AMD_NO_PIPELINE")) return 0;
+  pp = (emac_pipe *)calloc(1, sizeof(emac_pipe));
+  pb = (emac_bucket *)calloc((size_t)h->plan.npieces * (size_t)h->plan.nranks, sizeof(emac_bucket));
+  if (!pp || !pb) {
+    free(pp);
+    free(pb);
+    return EMAC_ERR_MALLOC;
+  }
+  h->pipe = pp;
+  {
+    const char *np = getenv("EXT_MPI_AMD_PIPE_PARTS");
+    pp->nparts = np ? atoi(np) : EMAC_PIPE_PARTS;
+    if (pp->nparts < 1 || pp->nparts > EMAC_PIPE_PARTS) pp->nparts = EMAC_PIPE_PARTS;
+  }
+  step = ((count + pp->nparts - 1) / pp->nparts + 4095) / 4096 * 4096; /* 16-byte aligned ranges, any type */
+  for (p = 0; p < pp->nparts; p++) pp->off[p] = (long)p * step < count ? (long)p * step : count;
+  pp->off[pp->nparts] = count;
+  for (p = 0; p < pp->nparts && !rc; p++) {
+    const int n = node_buckets(h, pp->off[p], pp->off[p + 1], pb);
+    rc = upload_launch(h, &pp->part[p], pb, n);
+    if (!rc) rc = emac_gpu_event_create(&pp->ev_in[p]);
+    if (!rc) rc = emac_gpu_event_create(&pp->ev_fold[p]);
+  }
+  free(pb);
+  if (!rc) rc = emac_gpu_event_create(&pp->ev_start);
+  if (!rc) rc = emac_gpu_event_create(&pp->ev_done);
+  if (!rc) rc = emac_gpu_stream_create(&pp->s_in);
+  if (!rc) rc = emac_gpu_stream_create(&pp->s_out);
+  return rc;
+}
+
 int ext_mpi_amd_node_allreduce_init(int nranks, const void *const *sendbufs, void *const *recvbufs, long count,
                                     int dtype, int op, const char *copyin, int *handle) {
   emac_handle *h;
   emac_copyin cfg;
   emac_bucket *b = NULL;
-  int rc, r, pc, c, t, nb = 0;
+  int rc, r, nb = 0;
   if (!handle || !sendbufs || !recvbufs || nranks < 1 || nranks > EMAC_MAX_RANKS || count < 0)
     return EMAC_ERR_ARG;
   *handle = -1;
@@ -307,19 +430,9 @@ int ext_mpi_amd_node_allreduce_init(int nranks, const void *const *sendbufs, voi
     rc = EMAC_ERR_MALLOC;
     goto fail;
   }
-  for (pc = 0; pc < h->plan.npieces; pc++) {
-    for (c = 0; c < nranks; c++) {
-      long off = h->plan.chunk_off[(size_t)pc * nranks + c], len = h->plan.chunk_len[(size_t)pc * nranks + c];
-      emac_bucket *bk = &b[nb];
-      if (len <= 0) continue;
-      for (t = 0; t < nranks; t++) bk->src[t] = h->dsend[h->plan.leaf_rank[c][t]];
-      for (r = 0; r < nranks; r++) bk->dst[r] = h->drecv[r];
-      bk->ndst = nranks;
-      place_bucket(bk, nranks, off, len, h->plan.tsize);
-      nb++;
-    }
-  }
+  nb = node_buckets(h, 0, count, b);
   if ((rc = upload_buckets(h, b, nb))) goto fail;
+  if ((rc = node_pipe_init(h))) goto fail;
   free(b);
   b = NULL;
   if ((rc = emac_gpu_stream_create(&h->stream))) goto fail;
@@ -1037,6 +1150,47 @@ static int ipc_status(const emac_handle *h) {
   return EMAC_ERR_TRANSPORT;
 }
 
+/* A pipelined NODE Start: H2D of every part on s_in, the part's fold on the handle's stream
+   after its copies, its D2H on s_out after its fold; the handle's stream then waits for the
+   last D2H, so Wait / Test and the next Start see the whole Allreduce. */
+static int pipe_start(emac_handle *h) {
+  emac_pipe *pp = h->pipe;
+  const size_t ts = (size_t)h->plan.tsize;
+  int p, r, rc;
+  /* the caller's earlier work on the handle's stream (and the previous Start) comes first */
+  if ((rc = emac_gpu_event_record(pp->ev_start, h->stream)) || (rc = emac_gpu_stream_wait(pp->s_in, pp->ev_start)))
+    return rc;
+  for (p = 0; p < pp->nparts; p++) {
+    const size_t o = (size_t)pp->off[p] * ts, n = (size_t)(pp->off[p + 1] - pp->off[p]) * ts;
+    for (r = 0; r < h->nbuf && n; r++) {
+      const void *src = h->send_mirror[r] ? h->user_send[r]
+                                          : (h->recv_mirror[r] && h->dsend[r] == h->drecv[r] ? h->user_recv[r] : NULL);
+      if (src && (rc = emac_gpu_memcpy_async((char *)h->dsend[r] + o, (const char *)src + o, n, pp->s_in))) return rc;
+    }
+    if ((rc = emac_gpu_event_record(pp->ev_in[p], pp->s_in))) return rc;
+  }
+  for (p = 0; p < pp->nparts; p++) {
+    const emac_launch *L = &pp->part[p];
+    if ((rc = emac_gpu_stream_wait(h->stream, pp->ev_in[p]))) return rc;
+    if ((rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, h->fan, L->unroll, &h->plan.codes, L->d_buckets, L->nb,
+                            L->ntiles, L->tiles_per_bucket, L->all_full, L->d_edges, L->nedges, h->stream)))
+      return rc;
+    if ((rc = emac_gpu_event_record(pp->ev_fold[p], h->stream))) return rc;
+  }
+  for (p = 0; p < pp->nparts; p++) {
+    const size_t o = (size_t)pp->off[p] * ts, n = (size_t)(pp->off[p + 1] - pp->off[p]) * ts;
+    if ((rc = emac_gpu_stream_wait(pp->s_out, pp->ev_fold[p]))) return rc;
+    for (r = 0; r < h->nbuf && n; r++)
+      if (h->recv_mirror[r] &&
+          (rc = emac_gpu_memcpy_async((char *)h->user_recv[r] + o, (const char *)h->drecv[r] + o, n, pp->s_out)))
+        return rc;
+  }
+  if ((rc = emac_gpu_event_record(pp->ev_done, pp->s_out)) || (rc = emac_gpu_stream_wait(h->stream, pp->ev_done)))
+    return rc;
+  h->started = 1;
+  return 0;
+}
+
 int ext_mpi_amd_start_legs(int handle, int legs) {
   emac_handle *h = get(handle);
   int rc, multi;
@@ -1044,6 +1198,7 @@ int ext_mpi_amd_start_legs(int handle, int legs) {
   if (!h) return EMAC_ERR_ARG;
   multi = h->kind == KIND_COMM && h->plan.nranks > 1;
   if (emac_gpu_set_device(h->device)) return EMAC_ERR_DEVICE;
+  if (h->pipe && (legs & EXT_MPI_AMD_LEG_ALL) == EXT_MPI_AMD_LEG_ALL) return pipe_start(h);
   if ((legs & EXT_MPI_AMD_LEG_STAGE_IN) && (rc = stage_in(h))) return rc;
   if (h->kind == KIND_IPC && h->fused && (legs & core) == core) {
     emac_comm *cm = &comms[h->comm];

@@ -207,6 +207,19 @@ int emac_gpu_stream_query(void *stream) {
   return EMAC_ERR_DEVICE;
 }
 int emac_gpu_device_sync(void) { return ok(hipDeviceSynchronize()); }
+int emac_gpu_event_create(void **ev) {
+  hipEvent_t e;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return EMAC_ERR_DEVICE;
+  *ev = e;
+  return 0;
+}
+int emac_gpu_event_destroy(void *ev) { return ev ? ok(hipEventDestroy(static_cast<hipEvent_t>(ev))) : 0; }
+int emac_gpu_event_record(void *ev, void *stream) {
+  return ok(hipEventRecord(static_cast<hipEvent_t>(ev), static_cast<hipStream_t>(stream)));
+}
+int emac_gpu_stream_wait(void *stream, void *ev) {
+  return ok(hipStreamWaitEvent(static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(ev), 0));
+}
 
 }  // extern "C"
 

@@ -58,6 +58,10 @@ int emac_gpu_stream_destroy(void *stream);
 int emac_gpu_stream_sync(void *stream);
 int emac_gpu_stream_query(void *stream); /* 1 idle, 0 busy, <0 error */
 int emac_gpu_device_sync(void);
+int emac_gpu_event_create(void **ev); /* timing disabled */
+int emac_gpu_event_destroy(void *ev);
+int emac_gpu_event_record(void *ev, void *stream);
+int emac_gpu_stream_wait(void *stream, void *ev); /* stream waits for ev */
 
 /* ---- peer-mapped (IPC) form, ipc.hip ----
    Per-communicator synchronisation block, in uncached device memory and mapped by every peer:

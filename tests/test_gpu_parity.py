@@ -114,6 +114,30 @@ def test_host_buffers_staged(oracle):
     assert_bitwise(recvs, oracle.allreduce(sends, "6;1 -4 4"), "host staged")
 
 
+@pytest.mark.parametrize("code,R,count,copyin,in_place", [
+    (emac.FLOAT, 8, (4 << 20) + 7, "6;1 -8 8", False),            # pipelined: 8 element ranges
+    (emac.DOUBLE, 4, (1 << 20) + 1001, "6;1 -2 -2 2 2", True),
+    (emac.INT, 3, 3 << 20, "6;3 -3 3", False),                    # pieces clipped by the ranges
+    (emac.LONG, 8, 1 << 20, "6;-64 -8 8", False)])
+def test_host_buffers_pipelined(oracle, code, R, count, copyin, in_place):
+    """Host buffers of >= 4 MiB per rank: H2D, fold and D2H overlap in element-range parts on
+    three streams; repeated Starts reuse the parts (the previous Start's copies come first)."""
+    sends = xorshift_inputs(R, count, code, seed_base=0x9191 + count)
+    recvs = [s.copy() for s in sends] if in_place else [np.full(count, -1, dtype=s.dtype) for s in sends]
+    h = emac.node_allreduce_init([(r if in_place else s).ctypes.data for s, r in zip(sends, recvs)],
+                                 [r.ctypes.data for r in recvs], count, code, copyin)
+    try:
+        for _ in range(3):
+            if in_place:
+                for r, s in zip(recvs, sends):
+                    r[:] = s
+            emac.start(h)
+            emac.wait(h)
+            assert_bitwise(recvs, oracle.allreduce(sends, copyin, in_place=in_place), "host pipelined")
+    finally:
+        emac.done(h)
+
+
 def test_misaligned_buffers_take_element_path(oracle):
     """Buffers whose 16-byte phases differ fall back to the element-granular kernel path."""
     R, count = 4, 50001
