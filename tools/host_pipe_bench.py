@@ -25,6 +25,9 @@ def main():
     for r, t in enumerate(sends):
         t.fill_(float(r + 1))
     h = emac.node_allreduce_init([t.data_ptr() for t in sends], [t.data_ptr() for t in recvs], count, emac.FLOAT)
+    if os.environ.get("HOST_TORCH_STREAM"):  # the caller's stream, as bench.py's node_run sets it
+        s = torch.cuda.Stream()
+        emac.set_stream(h, s.cuda_stream)
     for _ in range(2):
         emac.start(h)
     emac.wait(h)
