@@ -416,11 +416,15 @@ def single_gpu(args):
         extras["radix_chains_16MiB"] = chains
         extras["fold_comm_shape"] = comm_shape_fold(R, count // R, tdtype, code, 200)
         hst = node_run(R, count, tdtype, code, copyin, 10, 3, host=True)
+        os.environ["EXT_MPI_AMD_PIPELINE"] = "1"  # the opt-in pipelined staging, for comparison
+        hst1 = node_run(R, count, tdtype, code, copyin, 10, 3, host=True)
+        del os.environ["EXT_MPI_AMD_PIPELINE"]
         extras["host_buffers_pcie_inclusive"] = {
             "gbps_reduced": round(R * S * 10 / hst["wall_s"] / 1e9, 2),
-            "ms_per_step": round(hst["wall_s"] * 1e3 / 10, 3), "checked": hst["checked"],
-            "note": "pinned host send/recv buffers: H2D, fold and D2H pipelined over 8 element ranges "
-                    "on three streams (the handle's own copy streams are created lazily: 3 warm-up Starts)"}
+            "ms_per_step": round(hst["wall_s"] * 1e3 / 10, 3), "checked": hst["checked"] and hst1["checked"],
+            "pipelined_gbps_reduced": round(R * S * 10 / hst1["wall_s"] / 1e9, 2),
+            "note": "pinned host send/recv buffers, H2D -> fold -> D2H on one stream (default); pipelined: "
+                    "EXT_MPI_AMD_PIPELINE=1, 8 element ranges on three streams, 3 warm-up Starts"}
         out["extras"] = extras
     if not args.no_cpu_baseline:
         np_dtype = {"float": np.float32, "double": np.float64, "int": np.int32, "long": np.int64}[args.dtype]

@@ -372,7 +372,11 @@ static int node_pipe_init(emac_handle *h) {
   long step;
   int r, p, any = 0, rc = 0;
   for (r = 0; r < h->nbuf; r++) any |= h->send_mirror[r] | h->recv_mirror[r];
-  if (!any || (long)h->bytes < EMAC_PIPE_MIN_BYTES || getenv("EXT_MPI_AMD_NO_PIPELINE")) return 0;
+  /* opt-in (EXT_MPI_AMD_PIPELINE=1): +12-25 % in a process with few streams, but down to -8 % in
+     one that has made many (hardware-queue sharing) */
+  if (!any || (long)h->bytes < EMAC_PIPE_MIN_BYTES || !getenv("EXT_MPI_AMD_PIPELINE") ||
+      atoi(getenv("EXT_MPI_AMD_PIPELINE")) <= 0)
+    return 0;
   pp = (emac_pipe *)calloc(1, sizeof(emac_pipe));
   pb = (emac_bucket *)calloc((size_t)h->plan.npieces * (size_t)h->plan.nranks, sizeof(emac_bucket));
   if (!pp || !pb) {
@@ -398,8 +402,13 @@ static int node_pipe_init(emac_handle *h) {
   free(pb);
   if (!rc) rc = emac_gpu_event_create(&pp->ev_start);
   if (!rc) rc = emac_gpu_event_create(&pp->ev_done);
-  if (!rc) rc = emac_gpu_stream_create(&pp->s_in);
-  if (!rc) rc = emac_gpu_stream_create(&pp->s_out);
+  /* The copy streams get an explicit (least) priority: streams of the default priority share the
+     process's few hardware queues round-robin, and a copy stream that landed on the fold
+     stream's queue serialised the pipeline (8 x 16 MiB pinned: 20-22 GB/s reduced against 25-26
+     unpipelined, depending on how many streams the process had made before); on a priority's own
+     queues it ran at 29-31 GB/s whatever came before (profiles/r01_host_pipeline_priority.json). */
+  if (!rc) rc = emac_gpu_stream_create_priority(&pp->s_in, 0);
+  if (!rc) rc = emac_gpu_stream_create_priority(&pp->s_out, 0);
   return rc;
 }
 

@@ -54,6 +54,7 @@ int emac_gpu_is_device_pointer(const void *p);
 int emac_gpu_host_register(void *p, size_t bytes);
 int emac_gpu_host_unregister(void *p);
 int emac_gpu_stream_create(void **stream);
+int emac_gpu_stream_create_priority(void **stream, int high); /* non-blocking, greatest / least priority */
 int emac_gpu_stream_destroy(void *stream);
 int emac_gpu_stream_sync(void *stream);
 int emac_gpu_stream_query(void *stream); /* 1 idle, 0 busy, <0 error */

@@ -119,9 +119,11 @@ def test_host_buffers_staged(oracle):
     (emac.DOUBLE, 4, (1 << 20) + 1001, "6;1 -2 -2 2 2", True),
     (emac.INT, 3, 3 << 20, "6;3 -3 3", False),                    # pieces clipped by the ranges
     (emac.LONG, 8, 1 << 20, "6;-64 -8 8", False)])
-def test_host_buffers_pipelined(oracle, code, R, count, copyin, in_place):
-    """Host buffers of >= 4 MiB per rank: H2D, fold and D2H overlap in element-range parts on
-    three streams; repeated Starts reuse the parts (the previous Start's copies come first)."""
+def test_host_buffers_pipelined(oracle, monkeypatch, code, R, count, copyin, in_place):
+    """Host buffers of >= 4 MiB per rank with EXT_MPI_AMD_PIPELINE=1: H2D, fold and D2H overlap in
+    element-range parts on three streams; repeated Starts reuse the parts (the previous Start's
+    copies come first)."""
+    monkeypatch.setenv("EXT_MPI_AMD_PIPELINE", "1")
     sends = xorshift_inputs(R, count, code, seed_base=0x9191 + count)
     recvs = [s.copy() for s in sends] if in_place else [np.full(count, -1, dtype=s.dtype) for s in sends]
     h = emac.node_allreduce_init([(r if in_place else s).ctypes.data for s, r in zip(sends, recvs)],

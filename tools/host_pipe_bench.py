@@ -1,6 +1,6 @@
 """PCIe-inclusive NODE-form rate with host buffers (the path's real start and end): R ranks x S
 bytes of pinned (or pageable) host send/recv buffers, H2D + fold + D2H per Start. Prints one
-JSON line. EXT_MPI_AMD_NO_PIPELINE / EXT_MPI_AMD_PIPE_PARTS select the staging schedule."""
+JSON line. EXT_MPI_AMD_PIPELINE=1 / EXT_MPI_AMD_PIPE_PARTS select the staging schedule."""
 import json
 import os
 import sys
@@ -20,6 +20,13 @@ def main():
     count = (mib << 20) // 4
     mk = (lambda: torch.empty(count, dtype=torch.float32).pin_memory()) if pinned else \
         (lambda: torch.empty(count, dtype=torch.float32))
+    keep = []
+    for _ in range(int(os.environ.get("HOST_PRE_STREAMS", "0"))):  # diagnosis: shift the HW-queue mapping
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            keep.append(torch.zeros(1, device="cuda") + 1)
+        st.synchronize()
+        keep.append(st)
     sends = [mk() for _ in range(R)]
     recvs = [mk() for _ in range(R)]
     for r, t in enumerate(sends):
@@ -40,7 +47,7 @@ def main():
     emac.done(h)
     print(json.dumps({"ranks": R, "mib_per_rank": mib, "pinned": pinned, "ms_per_allreduce": round(dt * 1e3, 3),
                       "gbps_reduced": round(R * (mib << 20) / dt / 1e9, 2), "checked": ok,
-                      "pipeline": os.environ.get("EXT_MPI_AMD_NO_PIPELINE") is None,
+                      "pipeline": os.environ.get("EXT_MPI_AMD_PIPELINE", "0") != "0",
                       "parts": os.environ.get("EXT_MPI_AMD_PIPE_PARTS", "8")}), flush=True)
 
 
