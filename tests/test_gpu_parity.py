@@ -392,3 +392,22 @@ def test_node_random_cases_vs_oracle(oracle):
         want = oracle.allreduce(sends, copyin, in_place=in_place, op=op)
         got = run_node(sends, code, copyin, in_place=in_place, op=op)
         assert_bitwise(got, want, f"R={R} '{copyin}' code={code} op={op} n={count} in_place={in_place}")
+
+
+def test_comm_loopback_random_cases_vs_oracle(oracle):
+    """Seeded random COMM-form cases on the loopback transport (staging slots, leg programs and
+    the owner's fold): node size, size, type, operation, copy-in variant, buffer phase."""
+    rng = np.random.default_rng(0xC0BB)
+    for _ in range(16):
+        R = int(rng.integers(2, 9))
+        variants = [f"6;1 -{R} {R}", f"6;-64 -{R} {R}"]
+        if _radix_chain(R):
+            variants.append(_radix_chain(R))
+        copyin = variants[int(rng.integers(len(variants)))]
+        count = int(min(1 << 20, np.exp(rng.uniform(0, np.log(1 << 20)))))
+        code = int(rng.choice(CODES))
+        op = int(rng.choice([emac.SUM, emac.MIN, emac.MAX]))
+        sends = special_inputs(R, count, code, int(rng.integers(1 << 30)))
+        want = oracle.allreduce(sends, copyin, op=op)
+        got = run_comm_loopback(sends, code, copyin, phase=[int(x) for x in rng.integers(0, 4, R)], op=op)
+        assert_bitwise(got, want, f"comm R={R} '{copyin}' code={code} op={op} n={count}")
