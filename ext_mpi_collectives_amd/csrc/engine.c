@@ -248,13 +248,16 @@ static int in_place_ok(const emac_handle *h, const void *p) {
   return h->kind != KIND_IPC || (h->bytes >= (size_t)comms[h->comm].size && emac_gpu_ipc_exportable(p));
 }
 
-/* Page-lock a host buffer for async DMA, except in the IPC form: a process that has imported
-   its peers' memory (dmabuf) and also holds registered user pages was measured to receive an
-   asynchronous illegal-address error a few handles after the registration was dropped (8
-   processes on one MI355X, every transfer already complete); unregistered buffers are staged by
-   the runtime instead. EXT_MPI_AMD_NO_HOST_REGISTER turns registration off everywhere. */
+/* Page-locking a caller's host buffer is opt-in (EXT_MPI_AMD_HOST_REGISTER=1; never in the IPC
+   form). Registered user pages, unregistered at handle release and then freed and reused by the
+   application, were twice followed by an asynchronous illegal-address error in a later, unrelated
+   launch or copy of the same process (8 IPC processes on one MI355X; the single-process GPU suite
+   after the host-buffer tests), and both went away without registration. Unregistered buffers
+   are staged by the runtime; buffers the caller already pinned (hipHostMalloc, torch
+   pin_memory) are copied at full rate either way. */
 static int host_register(const emac_handle *h, const void *p) {
-  if (h->kind == KIND_IPC || emac_gpu_is_device_pointer(p)) return 0;
+  const char *e = getenv("EXT_MPI_AMD_HOST_REGISTER");
+  if (!e || atoi(e) <= 0 || h->kind == KIND_IPC || emac_gpu_is_device_pointer(p)) return 0;
   return emac_gpu_host_register((void *)p, h->bytes) == 0;
 }
 
@@ -1353,3 +1356,148 @@ out:
 }
 
 const char *ext_mpi_amd_version(void) { return "ext_mpi_collectives_amd 0.1 (gfx950)"; }
+
+/* ---- layout self-check (host only, no device): the NODE form's buckets and launch layout for
+   buffers at the given 16-byte phases, with every access the kernels would make replayed on the
+   host (fold_kernel tiles, fold_edge_kernel items; fold_kernel.hpp). Returns the number of
+   accesses outside a buffer's [0, count) elements or destination elements not written exactly
+   once per launch; -1 on a set-up error. Test infrastructure for the planner/layout pair. */
+typedef struct {
+  long count;
+  int tsize;
+  long bad;
+  unsigned char *hits; /* per destination rank and element: writes seen */
+} chk_state;
+
+static long chk_elem(const void *base, const void *p, int tsize) {
+  return (long)(((const char *)p - (const char *)base) / tsize);
+}
+
+static void chk_access(chk_state *st, long e, int r, int write) {
+  if (e < 0 || e >= st->count) {
+    if (st->bad++ < 3) fprintf(stderr, "layout check: %s of element %ld (count %ld) rank %d\n", write ? "store" : "load", e, st->count, r);
+    return;
+  }
+  if (write) st->hits[(size_t)r * (size_t)st->count + (size_t)e]++;
+}
+
+int ext_mpi_amd_check_node_layout(int nranks, long count, int dtype, int op, const char *copyin, const int *phase,
+                                  int fan) {
+  emac_handle hh, *h = &hh;
+  emac_copyin cfg;
+  emac_bucket *b = NULL;
+  emac_edge *edges = NULL;
+  emac_launch L;
+  chk_state st;
+  int rc, r, nb, i, t, d;
+  const long base_stride = 1L << 40;
+  if (nranks < 1 || nranks > EMAC_MAX_RANKS || count < 0) return -1;
+  memset(h, 0, sizeof(*h));
+  memset(&L, 0, sizeof(L));
+  if (parse_cfg(copyin, nranks, &cfg) || emac_plan_build(&h->plan, nranks, count, dtype, op, &cfg)) return -1;
+  h->kind = KIND_NODE;
+  h->bytes = (size_t)count * (size_t)h->plan.tsize;
+  h->nbuf = h->nsrc = nranks;
+  h->fan = fan ? nranks > 1 : 0;
+  for (r = 0; r < nranks; r++) { /* fake, disjoint buffers at the requested 16-byte phases */
+    h->dsend[r] = (void *)(base_stride * (2 * r + 1) + (phase ? phase[2 * r] : 0));
+    h->drecv[r] = (void *)(base_stride * (2 * r + 2) + (phase ? phase[2 * r + 1] : 0));
+  }
+  b = (emac_bucket *)calloc((size_t)h->plan.npieces * nranks + 1, sizeof(emac_bucket));
+  st.count = count;
+  st.tsize = h->plan.tsize;
+  st.bad = 0;
+  st.hits = (unsigned char *)calloc((size_t)nranks * (size_t)(count + 1), 1);
+  if (!b || !st.hits) {
+    rc = -1;
+    goto out;
+  }
+  nb = node_buckets(h, 0, count, b);
+  if (!h->fan)
+    for (i = 0; i < nb; i++) b[i].ndst = 1; /* COMM-like fan-out 1: only the first destination */
+  if ((rc = emac_layout(b, nb, op, h->nsrc, h->plan.codes.nlev > 1, h->fan, &edges, &L.nedges, &L.ntiles,
+                        &L.tiles_per_bucket, &L.all_full, &L.unroll))) {
+    rc = -1;
+    goto out;
+  }
+  {
+    const long EPV = 16 / h->plan.tsize, TILE = (long)EMAC_BLOCK * (L.unroll & 15);
+    long tile;
+    /* fold_kernel: each tile's vectors of its bucket */
+    for (tile = 0; tile < L.ntiles; tile++) {
+      int bi;
+      long tt, v, v0, v1;
+      if (L.tiles_per_bucket > 0) {
+        bi = (int)(tile / L.tiles_per_bucket);
+        tt = tile - (long)bi * L.tiles_per_bucket;
+      } else {
+        int lo = 0, hi = nb - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (b[mid].tile0 <= tile)
+            lo = mid;
+          else
+            hi = mid - 1;
+        }
+        bi = lo;
+        tt = tile - b[lo].tile0;
+      }
+      if (bi < 0 || bi >= nb) {
+        st.bad++;
+        continue;
+      }
+      v0 = tt * TILE;
+      v1 = (L.all_full || (tt + 1) * TILE <= b[bi].nvec) ? v0 + TILE : b[bi].nvec;
+      for (v = v0; v < v1; v++)
+        for (i = 0; i < (int)EPV; i++) {
+          for (t = 0; t < h->nsrc; t++) {
+            /* which rank's send buffer leaf t points into (the fake bases are 2^40 apart) */
+            const long bi_rank = ((long)((const char *)b[bi].src[t] - (const char *)0) / base_stride - 1) / 2;
+            chk_access(&st, chk_elem(h->dsend[bi_rank], b[bi].src[t], st.tsize) + v * EPV + i, (int)bi_rank, 0);
+          }
+          for (d = 0; d < b[bi].ndst; d++) {
+            const long dr = ((long)((const char *)b[bi].dst[d] - (const char *)0) / base_stride - 2) / 2;
+            chk_access(&st, chk_elem(h->drecv[dr], b[bi].dst[d], st.tsize) + v * EPV + i, (int)dr, 1);
+          }
+        }
+    }
+    /* fold_edge_kernel items */
+    for (i = 0; i < L.nedges; i++) {
+      const emac_edge it = edges[i];
+      const emac_bucket *bk = &b[it.bucket];
+      long k, e, n = it.mode == 1 ? it.count : bk->head + bk->tail;
+      for (k = 0; k < n; k++) {
+        if (it.mode == 1)
+          e = it.start + k;
+        else
+          e = k < bk->head ? k : bk->head + bk->nvec * EPV + (k - bk->head);
+        e -= bk->head; /* pointers sit at element head */
+        for (t = 0; t < h->nsrc; t++) {
+          const long sr = ((long)((const char *)bk->src[t] - (const char *)0) / base_stride - 1) / 2;
+          chk_access(&st, chk_elem(h->dsend[sr], bk->src[t], st.tsize) + e, (int)sr, 0);
+        }
+        for (d = 0; d < bk->ndst; d++) {
+          const long dr = ((long)((const char *)bk->dst[d] - (const char *)0) / base_stride - 2) / 2;
+          chk_access(&st, chk_elem(h->drecv[dr], bk->dst[d], st.tsize) + e, (int)dr, 1);
+        }
+      }
+    }
+  }
+  /* every destination element written exactly once (fan-out N) / the first destination (fan 1) */
+  for (r = 0; r < (h->fan ? nranks : 1); r++) {
+    long e;
+    for (e = 0; e < count; e++)
+      if (st.hits[(size_t)r * (size_t)count + (size_t)e] != (h->fan || r == 0 ? 1 : 0)) {
+        if (st.bad++ < 3)
+          fprintf(stderr, "layout check: rank %d element %ld written %d times\n", r, e,
+                  st.hits[(size_t)r * (size_t)count + (size_t)e]);
+      }
+  }
+  rc = st.bad > 0x7fffffff ? 0x7fffffff : (int)st.bad;
+out:
+  free(edges);
+  free(b);
+  free(st.hits);
+  emac_plan_free(&h->plan);
+  return rc;
+}

@@ -175,7 +175,6 @@ int emac_gpu_is_device_pointer(const void *p) {
 }
 int emac_gpu_host_register(void *p, size_t bytes) {
   if (!bytes) return 0;
-  if (getenv("EXT_MPI_AMD_NO_HOST_REGISTER")) return EMAC_ERR_DEVICE;
   if (hipHostRegister(p, bytes, hipHostRegisterDefault) != hipSuccess) {
     clear_error("emac_gpu_host_register");
     return EMAC_ERR_DEVICE;
