@@ -76,3 +76,39 @@ def test_subsplit_leaf_order():
     # position 3: outer member 1 of group {1,3,5,7}; inner member 1 of block {2,3}
     assert d["leaves"] == [3, 1, 5, 7, 2, 0, 4, 6]
     assert d["nlev"] == 2 and d["pieces"] == [(3000, 1000)]  # outer quarter [2000, 4000), inner half 1
+
+
+def _radix_chain_copyin(R):
+    fs, n = [], R
+    for p in (2, 3, 5, 7, 11, 13):
+        while n % p == 0:
+            fs.append(p)
+            n //= p
+    return "6;1 " + " ".join(f"-{f}" for f in fs) + " " + " ".join(str(f) for f in reversed(fs)) if len(fs) > 1 else None
+
+
+def test_layout_accesses_stay_in_bounds():
+    """Host replay of every access the fold kernels make (tiles and edge items) for the NODE
+    form's buckets: inside [0, count) of every buffer, each destination element written once.
+    Random node sizes 1-16, copy-in variants (pieces, -64 fractions, radix chains), element
+    counts, types, SUM/MIN/MAX, fan-out 1 or N, and 16-byte phases of every buffer."""
+    import ctypes
+    import numpy as np
+    import ext_mpi_collectives_amd as emac
+    f = emac.lib().ext_mpi_amd_check_node_layout
+    f.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                  ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+    rng = np.random.default_rng(0x1A70)
+    tsize = {emac.DOUBLE: 8, emac.LONG: 8, emac.FLOAT: 4, emac.INT: 4}
+    for _ in range(1500):
+        R = int(rng.integers(1, 17))
+        code = int(rng.choice(list(tsize)))
+        variants = [f"6;1 -{R} {R}", f"6;-64 -{R} {R}", f"6;{int(rng.integers(2, 6))} -{R} {R}"]
+        if _radix_chain_copyin(R):
+            variants.append(_radix_chain_copyin(R))
+        copyin = variants[int(rng.integers(len(variants)))]
+        count = int(min(1 << 17, np.exp(rng.uniform(0, np.log(1 << 17)))))
+        phase = (ctypes.c_int * (2 * R))(*[int(x) * tsize[code] for x in rng.integers(0, 16 // tsize[code], 2 * R)])
+        op = int(rng.choice([emac.SUM, emac.MIN, emac.MAX]))
+        fan = int(rng.integers(0, 2))
+        assert f(R, count, code, op, copyin.encode(), phase, fan) == 0, (R, count, code, copyin, list(phase), fan)
