@@ -948,7 +948,7 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
        per rank, default 1 MiB; 0 disables) */
     const char *fm = getenv("EXT_MPI_AMD_IPC_FUSED_MAX");
     const long fused_max = fm ? atol(fm) : (1L << 20);
-    h->fused = R > 1 && h->plan.op == EMAC_SUM && (long)h->bytes <= fused_max;
+    h->fused = R > 1 && (long)h->bytes <= fused_max;
   }
   if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
     fprintf(stderr, "ipc rank %d: own send %p recv %p bytes %zu, %d buckets, slot %d, %d attempt(s)\n", cm->rank,
@@ -1215,7 +1215,7 @@ int ext_mpi_amd_start_legs(int handle, int legs) {
   if (h->kind == KIND_IPC && h->fused && (legs & core) == core) {
     emac_comm *cm = &comms[h->comm];
     const unsigned long e0 = ++h->epoch[0], e1 = ++h->epoch[1];
-    if ((rc = emac_gpu_fold_fused(h->plan.dtype, h->nsrc, h->unroll, &h->plan.codes, h->d_buckets, h->nb, h->ntiles,
+    if ((rc = emac_gpu_fold_fused(h->plan.dtype, h->plan.op, h->nsrc, h->unroll, &h->plan.codes, h->d_buckets, h->nb, h->ntiles,
                                   h->tiles_per_bucket, h->all_full, h->d_edges, h->nedges, cm->sync,
                                   (void *const *)cm->d_peer_sync, h->slot, cm->size, cm->rank, cm->xcc_mask, cm->err,
                                   cm->timeout_ticks, e0, e1, h->stream)))

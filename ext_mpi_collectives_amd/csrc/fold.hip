@@ -29,7 +29,8 @@ extern "C" {
 #define EMAC_DECL(n)                                                                       \
   int emac_fold_launch_##n(int nsrc, bool tree, int fan, int unroll, const emac::Launch *L); \
   int emac_fold_launch_##n##_mm(int op, int nsrc, bool tree, int fan, int unroll, const emac::Launch *L); \
-  int emac_fold_fused_launch_##n(int nsrc, bool tree, const emac::Launch *L, const emac::FusedLaunch *F);
+  int emac_fold_fused_launch_##n(int nsrc, bool tree, const emac::Launch *L, const emac::FusedLaunch *F); \
+  int emac_fold_fused_launch_##n##_mm(int op, int nsrc, bool tree, const emac::Launch *L, const emac::FusedLaunch *F);
 EMAC_DECL(f32)
 EMAC_DECL(f64)
 EMAC_DECL(i32)
@@ -111,7 +112,7 @@ int emac_gpu_fold(int dtype, int op, int nsrc, int fan, int unroll, const emac_c
   return EMAC_ERR_ARG;
 }
 
-int emac_gpu_fold_fused(int dtype, int nsrc, int unroll, const emac_codes *codes, const emac_bucket *d_buckets, int nb,
+int emac_gpu_fold_fused(int dtype, int op, int nsrc, int unroll, const emac_codes *codes, const emac_bucket *d_buckets, int nb,
                         long ntiles, long tiles_per_bucket, int all_full, const emac_edge *d_edges, int nedges,
                         void *self_sync, void *const *d_peers, int slot, int nranks, int me, unsigned xcc_expect,
                         int *err, long timeout_ticks, unsigned long epoch0, unsigned long epoch1, void *stream) {
@@ -128,16 +129,21 @@ int emac_gpu_fold_fused(int dtype, int nsrc, int unroll, const emac_codes *codes
      (all resident while others wait; few CUs held from other streams while a peer is late) */
   F.grid = (int)(work < EMAC_FUSED_MIN_WG ? EMAC_FUSED_MIN_WG : work > EMAC_FUSED_MAX_WG ? EMAC_FUSED_MAX_WG : work);
   if (codes->nlev > emac::kMaxLevels || nsrc < 2) return EMAC_ERR_UNSUPPORTED;
-  if (nb > 0 && unroll != emac_gpu_pick_unroll(EMAC_SUM, nsrc, tree, 2, 0)) return EMAC_ERR_UNSUPPORTED; /* layout's tiles */
+  if (op < EMAC_SUM || op > EMAC_MAX) return EMAC_ERR_UNSUPPORTED;
+  if (nb > 0 && unroll != emac_gpu_pick_unroll(op, nsrc, tree, 2, 0)) return EMAC_ERR_UNSUPPORTED; /* layout's tiles */
   if (nb <= 0) {
     F.grid = EMAC_FUSED_MIN_WG;  /* nothing to fold here: the barriers only */
     return emac_fold_fused_launch_f32(nsrc, false, &L, &F);
   }
   switch (dtype) {
-  case EMAC_FLOAT: return emac_fold_fused_launch_f32(nsrc, tree, &L, &F);
-  case EMAC_DOUBLE: return emac_fold_fused_launch_f64(nsrc, tree, &L, &F);
-  case EMAC_INT: return emac_fold_fused_launch_i32(nsrc, tree, &L, &F);
-  case EMAC_LONG: return emac_fold_fused_launch_i64(nsrc, tree, &L, &F);
+  case EMAC_FLOAT:
+    return op == EMAC_SUM ? emac_fold_fused_launch_f32(nsrc, tree, &L, &F) : emac_fold_fused_launch_f32_mm(op, nsrc, tree, &L, &F);
+  case EMAC_DOUBLE:
+    return op == EMAC_SUM ? emac_fold_fused_launch_f64(nsrc, tree, &L, &F) : emac_fold_fused_launch_f64_mm(op, nsrc, tree, &L, &F);
+  case EMAC_INT:
+    return op == EMAC_SUM ? emac_fold_fused_launch_i32(nsrc, tree, &L, &F) : emac_fold_fused_launch_i32_mm(op, nsrc, tree, &L, &F);
+  case EMAC_LONG:
+    return op == EMAC_SUM ? emac_fold_fused_launch_i64(nsrc, tree, &L, &F) : emac_fold_fused_launch_i64_mm(op, nsrc, tree, &L, &F);
   }
   return EMAC_ERR_ARG;
 }

@@ -6,3 +6,9 @@ extern "C" int emac_fold_launch_f32_mm(int op, int nsrc, bool tree, int fan, int
   return op == EMAC_MIN ? emac::launch_t<float, EMAC_MIN>(nsrc, tree, fan, unroll, *L)
                         : emac::launch_t<float, EMAC_MAX>(nsrc, tree, fan, unroll, *L);
 }
+
+extern "C" int emac_fold_fused_launch_f32_mm(int op, int nsrc, bool tree, const emac::Launch *L,
+                                           const emac::FusedLaunch *F) {
+  return op == EMAC_MIN ? emac::launch_fused_t<float, EMAC_MIN>(nsrc, tree, *L, *F)
+                        : emac::launch_fused_t<float, EMAC_MAX>(nsrc, tree, *L, *F);
+}

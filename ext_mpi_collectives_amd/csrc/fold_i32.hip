@@ -7,5 +7,5 @@ extern "C" int emac_fold_launch_i32(int nsrc, bool tree, int fan, int unroll, co
 }
 
 extern "C" int emac_fold_fused_launch_i32(int nsrc, bool tree, const emac::Launch *L, const emac::FusedLaunch *F) {
-  return emac::launch_fused_t<int>(nsrc, tree, *L, *F);
+  return emac::launch_fused_t<int, EMAC_SUM>(nsrc, tree, *L, *F);
 }

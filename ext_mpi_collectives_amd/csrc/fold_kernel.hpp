@@ -432,28 +432,28 @@ struct FusedLaunch {
 };
 
 // fused peer-mapped launch: the IPC form's schedule of the shape (pick_unroll fan == 2)
-template <typename T, int N>
+template <typename T, int OP, int N>
 int launch_fused_n(bool tree, const Launch &L, const FusedLaunch &F) {
   constexpr int UR = N > 8 ? 1 : 2;
   if constexpr (can_tree(N)) {
     if (tree) {
-      hipLaunchKernelGGL((ipc_fused_kernel<T, EMAC_SUM, N, tree_unroll(N), true>), dim3((unsigned)F.grid),
+      hipLaunchKernelGGL((ipc_fused_kernel<T, OP, N, tree_unroll(N), true>), dim3((unsigned)F.grid),
                          dim3(EMAC_BLOCK), 0, L.s, L.b, L.nb, L.ntiles, L.tpb, L.all_full, L.edges, L.nedges, *L.c, F.ns,
                          F.epoch0, F.epoch1);
       return hipGetLastError() == hipSuccess ? 0 : EMAC_ERR_DEVICE;
     }
   }
   if (tree) return EMAC_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL((ipc_fused_kernel<T, EMAC_SUM, N, UR, false>), dim3((unsigned)F.grid), dim3(EMAC_BLOCK), 0, L.s,
+  hipLaunchKernelGGL((ipc_fused_kernel<T, OP, N, UR, false>), dim3((unsigned)F.grid), dim3(EMAC_BLOCK), 0, L.s,
                      L.b, L.nb, L.ntiles, L.tpb, L.all_full, L.edges, L.nedges, *L.c, F.ns, F.epoch0, F.epoch1);
   return hipGetLastError() == hipSuccess ? 0 : EMAC_ERR_DEVICE;
 }
 
-template <typename T>
+template <typename T, int OP>
 int launch_fused_t(int nsrc, bool tree, const Launch &L, const FusedLaunch &F) {
   switch (nsrc) {
 #define EMAC_CASE(n) \
-  case n: return launch_fused_n<T, n>(tree, L, F);
+  case n: return launch_fused_n<T, OP, n>(tree, L, F);
     EMAC_CASE(2) EMAC_CASE(3) EMAC_CASE(4) EMAC_CASE(5) EMAC_CASE(6) EMAC_CASE(7) EMAC_CASE(8)
     EMAC_CASE(9) EMAC_CASE(10) EMAC_CASE(11) EMAC_CASE(12) EMAC_CASE(13) EMAC_CASE(14) EMAC_CASE(15) EMAC_CASE(16)
 #undef EMAC_CASE

@@ -97,12 +97,12 @@ int emac_gpu_xcc_census(unsigned *mask); /* XCCs a wide launch lands on */
 long emac_gpu_wallclock_hz(void);
 int emac_gpu_node_barrier(void *self, void *const *d_peers, int slot, int phase, unsigned long epoch, int nranks,
                           int me, unsigned xcc_expect, int *err, long timeout_ticks, void *stream);
-/* the whole peer-mapped Allreduce (barrier, fold, barrier) in one launch: SUM, small messages.
+/* the whole peer-mapped Allreduce (barrier, fold, barrier) in one launch, small messages.
    The grid is kept small (as many workgroups as tiles, 16..64): every workgroup spins while a
    peer is late, and a wide grid would hold that many CUs from the rank's other streams. */
 #define EMAC_FUSED_MIN_WG EMAC_SYNC_WG
 #define EMAC_FUSED_MAX_WG 64
-int emac_gpu_fold_fused(int dtype, int nsrc, int unroll, const emac_codes *codes, const emac_bucket *d_buckets, int nb,
+int emac_gpu_fold_fused(int dtype, int op, int nsrc, int unroll, const emac_codes *codes, const emac_bucket *d_buckets, int nb,
                         long ntiles, long tiles_per_bucket, int all_full, const emac_edge *d_edges, int nedges,
                         void *self_sync, void *const *d_peers, int slot, int nranks, int me, unsigned xcc_expect,
                         int *err, long timeout_ticks, unsigned long epoch0, unsigned long epoch1, void *stream);
