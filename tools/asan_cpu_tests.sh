@@ -16,8 +16,7 @@ mkdir -p "$W/tree"
 (cd "$R" && git ls-files | tar -cf - -T -) | (cd "$W/tree" && tar -xf -)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -fsanitize=address,undefined \
   -o "$W/tree/ext_mpi_collectives_amd/libext_mpi_amd.so" "$W"/plan.o "$W"/layout.o "$W"/engine.o \
-  "$B"/fold.o "$B"/ipc.o "$B"/fold_f32.o "$B"/fold_f64.o "$B"/fold_i32.o "$B"/fold_i64.o \
-  "$B"/fold_f32_mm.o "$B"/fold_f64_mm.o "$B"/fold_i32_mm.o "$B"/fold_i64_mm.o -L/opt/rocm/lib -lrccl \
+  "$B"/ipc.o "$B"/fold*.o -L/opt/rocm/lib -lrccl \
   -Wl,-rpath,/opt/rocm/lib
 make -s -C "$R/oracle"
 cp "$R/oracle/liboracle.so" "$W/tree/oracle/"
