@@ -127,7 +127,8 @@ def host_random(count, np_dtype, seed):
     rng = np.random.Generator(np.random.PCG64(seed))
     if np.dtype(np_dtype).kind == "f":
         return (rng.random(count, dtype=np.float64) * 2 - 1).astype(np_dtype)
-    return rng.integers(-(1 << 20), 1 << 20, count).astype(np_dtype)
+    lim = 1 << (40 if np.dtype(np_dtype).itemsize == 8 else 20)  # sums cannot overflow
+    return rng.integers(-lim, lim, count).astype(np_dtype)
 
 
 def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * MIB, host=False, alloc="torch"):
@@ -331,6 +332,23 @@ def cpu_baseline(R, count, np_dtype, copyin, seconds):
                       f"host nproc={os.cpu_count()}"}
 
 
+def cpu_config0():
+    """BASELINE configs[0] on the host: the CPU restatement at tests/benchmark.c's shape (4 ranks,
+    64 KiB float, '6;1 -4 4'), iteration count doubled until a run takes >= 2 s (benchmark.c:150)."""
+    from oracle import oracle
+    rng = np.random.default_rng(0x5EED0000)
+    sends = [(rng.random(16384) * 2 - 1).astype(np.float32) for _ in range(4)]
+    recvs = [np.empty_like(s) for s in sends]
+    iters = 1
+    while True:
+        t = oracle.cpu_allreduce_threads(sends, recvs, "6;1 -4 4", iters)
+        if t >= 2.0 or iters >= (1 << 24):
+            break
+        iters *= 2
+    return {"us_per_allreduce": round(t * 1e6 / iters, 3), "gbps_reduced": round(iters * 4 * 65536 / t / 1e9, 3),
+            "cores": 4, "kind": "port", "sample": f"{iters} Allreduce(s) in {t:.2f} s"}
+
+
 def single_gpu(args):
     import torch
     import ext_mpi_collectives_amd as emac
@@ -425,10 +443,32 @@ def single_gpu(args):
             "pipelined_gbps_reduced": round(R * S * 10 / hst1["wall_s"] / 1e9, 2),
             "note": "pinned host send/recv buffers, H2D -> fold -> D2H on one stream (default); pipelined: "
                     "EXT_MPI_AMD_PIPELINE=1, 8 element ranges on three streams, 3 warm-up Starts"}
+        # BASELINE configs[2]: int and long, 4 MiB per rank, 8 ranks; integer sums are exact in any
+        # order, so the check against the float64 sum of the inputs is bit-exact (|values| <= 2^20
+        # int, 2^40 long: every partial sum is exact in float64)
+        ints = {}
+        for dn, td, cd in (("int", torch.int32, emac.INT), ("long", torch.int64, emac.LONG)):
+            ts = torch.empty((), dtype=td).element_size()
+            r = node_run(R, (4 * MIB) // ts, td, cd, copyin, 50, 5, alloc=args.alloc)
+            k = r["event_ms"] * 1e-3 / 50
+            ints[dn] = {"gbps_reduced": round(R * 4 * MIB / k / 1e9, 1), "avg_launch_us": round(k * 1e6, 2),
+                        "achieved_gbps": round(2 * R * 4 * MIB / k / 1e9, 1), "bitexact": r["checked"]}
+        extras["config3_int_long_4MiB"] = ints
+        # BASELINE configs[0] shape (tests/benchmark.c: 4 ranks, 64 KiB float, '6;1 -4 4') on this path
+        c0 = (64 << 10) // 4
+        d0 = node_run(4, c0, torch.float32, emac.FLOAT, "6;1 -4 4", 400, 20, min_set_bytes=0, alloc=args.alloc)
+        h0 = node_run(4, c0, torch.float32, emac.FLOAT, "6;1 -4 4", 200, 20, host=True)
+        extras["config0_64KiB_4ranks"] = {
+            "device_us_per_allreduce": round(d0["wall_s"] * 1e6 / 400, 2),
+            "host_buffers_us_per_allreduce": round(h0["wall_s"] * 1e6 / 200, 2),
+            "checked": d0["checked"] and h0["checked"],
+            "note": "4 node ranks in one MI355X; host_buffers = pinned host send/recv, H2D -> fold -> D2H"}
         out["extras"] = extras
     if not args.no_cpu_baseline:
         np_dtype = {"float": np.float32, "double": np.float64, "int": np.int32, "long": np.int64}[args.dtype]
         out["cpu_baseline"] = cpu_baseline(R, count, np_dtype, copyin, args.cpu_seconds)
+        if not args.no_extras:
+            out["cpu_baseline"]["config0_64KiB_4ranks"] = cpu_config0()
     print(json.dumps(out), flush=True)
 
 
