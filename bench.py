@@ -434,14 +434,19 @@ def single_gpu(args):
         extras["radix_chains_16MiB"] = chains
         extras["fold_comm_shape"] = comm_shape_fold(R, count // R, tdtype, code, 200)
         hst = node_run(R, count, tdtype, code, copyin, 10, 3, host=True)
-        os.environ["EXT_MPI_AMD_PIPELINE"] = "1"  # the opt-in pipelined staging, for comparison
+        os.environ["EXT_MPI_AMD_HOST_DIRECT"] = "0"  # staged through device mirrors, for comparison
+        hst0 = node_run(R, count, tdtype, code, copyin, 10, 3, host=True)
+        os.environ["EXT_MPI_AMD_PIPELINE"] = "1"  # the opt-in pipelined staging
         hst1 = node_run(R, count, tdtype, code, copyin, 10, 3, host=True)
-        del os.environ["EXT_MPI_AMD_PIPELINE"]
+        del os.environ["EXT_MPI_AMD_PIPELINE"], os.environ["EXT_MPI_AMD_HOST_DIRECT"]
         extras["host_buffers_pcie_inclusive"] = {
             "gbps_reduced": round(R * S * 10 / hst["wall_s"] / 1e9, 2),
-            "ms_per_step": round(hst["wall_s"] * 1e3 / 10, 3), "checked": hst["checked"] and hst1["checked"],
+            "ms_per_step": round(hst["wall_s"] * 1e3 / 10, 3),
+            "checked": hst["checked"] and hst0["checked"] and hst1["checked"],
+            "staged_gbps_reduced": round(R * S * 10 / hst0["wall_s"] / 1e9, 2),
             "pipelined_gbps_reduced": round(R * S * 10 / hst1["wall_s"] / 1e9, 2),
-            "note": "pinned host send/recv buffers, H2D -> fold -> D2H on one stream (default); pipelined: "
+            "note": "pinned host send/recv buffers read and written by the fold kernel over PCIe (default); "
+                    "staged: EXT_MPI_AMD_HOST_DIRECT=0, H2D -> fold -> D2H on one stream; pipelined: staged + "
                     "EXT_MPI_AMD_PIPELINE=1, 8 element ranges on three streams, 3 warm-up Starts"}
         # BASELINE configs[2]: int and long, 4 MiB per rank, 8 ranks; integer sums are exact in any
         # order, so the check against the float64 sum of the inputs is bit-exact (|values| <= 2^20
@@ -458,11 +463,16 @@ def single_gpu(args):
         c0 = (64 << 10) // 4
         d0 = node_run(4, c0, torch.float32, emac.FLOAT, "6;1 -4 4", 400, 20, min_set_bytes=0, alloc=args.alloc)
         h0 = node_run(4, c0, torch.float32, emac.FLOAT, "6;1 -4 4", 200, 20, host=True)
+        os.environ["EXT_MPI_AMD_HOST_DIRECT"] = "0"
+        h1 = node_run(4, c0, torch.float32, emac.FLOAT, "6;1 -4 4", 200, 20, host=True)
+        del os.environ["EXT_MPI_AMD_HOST_DIRECT"]
         extras["config0_64KiB_4ranks"] = {
             "device_us_per_allreduce": round(d0["wall_s"] * 1e6 / 400, 2),
             "host_buffers_us_per_allreduce": round(h0["wall_s"] * 1e6 / 200, 2),
-            "checked": d0["checked"] and h0["checked"],
-            "note": "4 node ranks in one MI355X; host_buffers = pinned host send/recv, H2D -> fold -> D2H"}
+            "host_buffers_staged_us_per_allreduce": round(h1["wall_s"] * 1e6 / 200, 2),
+            "checked": d0["checked"] and h0["checked"] and h1["checked"],
+            "note": "4 node ranks in one MI355X; host_buffers = pinned host send/recv read and written by the "
+                    "fold kernel over PCIe; staged = H2D -> fold -> D2H (EXT_MPI_AMD_HOST_DIRECT=0)"}
         out["extras"] = extras
     if not args.no_cpu_baseline:
         np_dtype = {"float": np.float32, "double": np.float64, "int": np.int32, "long": np.int64}[args.dtype]

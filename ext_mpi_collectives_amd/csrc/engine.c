@@ -261,14 +261,28 @@ static int host_register(const emac_handle *h, const void *p) {
   return emac_gpu_host_register((void *)p, h->bytes) == 0;
 }
 
-/* Device view of rank r's buffers: usable user device pointers are used in place; other buffers
-   get a device mirror (in place stays in place), staged in and out on the handle's stream. */
+/* NODE form: host memory the caller already page-locked (hipHostMalloc, torch pin_memory) is
+   read and written by the fold kernel itself over PCIe (EXT_MPI_AMD_HOST_DIRECT=0 turns this
+   off). One launch replaces R host-to-device copies, the fold and R device-to-host copies, and
+   the leaf reads overlap the fan-out writes on the link's two directions. */
+static int host_direct(const emac_handle *h, const void *p, void **dev) {
+  const char *e = getenv("EXT_MPI_AMD_HOST_DIRECT");
+  if (h->kind != KIND_NODE || (e && atoi(e) <= 0)) return 0;
+  return emac_gpu_pinned_view(p, dev) == 0;
+}
+
+/* Device view of rank r's buffers: usable user device pointers are used in place, page-locked
+   host memory in the NODE form through its device address; other buffers get a device mirror
+   (in place stays in place), staged in and out on the handle's stream. */
 static int map_buffers(emac_handle *h, int r, const void *send, void *recv) {
   int rc;
+  void *dv;
   h->user_send[r] = (void *)send;
   h->user_recv[r] = recv;
   if (in_place_ok(h, recv)) {
     h->drecv[r] = recv;
+  } else if (host_direct(h, recv, &dv)) {
+    h->drecv[r] = dv;
   } else {
     if ((rc = mirror_alloc(h, &h->drecv[r]))) return rc;
     h->recv_mirror[r] = 1;
@@ -278,6 +292,8 @@ static int map_buffers(emac_handle *h, int r, const void *send, void *recv) {
     h->dsend[r] = h->drecv[r];
   } else if (in_place_ok(h, send)) {
     h->dsend[r] = (void *)send;
+  } else if (host_direct(h, send, &dv)) {
+    h->dsend[r] = dv;
   } else {
     if ((rc = mirror_alloc(h, &h->dsend[r]))) return rc;
     h->send_mirror[r] = 1;

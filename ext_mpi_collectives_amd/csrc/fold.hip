@@ -179,6 +179,17 @@ int emac_gpu_is_device_pointer(const void *p) {
   }
   return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
+int emac_gpu_pinned_view(const void *p, void **dev) {
+  hipPointerAttribute_t a;
+  if (!p) return EMAC_ERR_ARG;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    clear_error("emac_gpu_pinned_view");  // pageable host memory
+    return EMAC_ERR_ARG;
+  }
+  if (a.type != hipMemoryTypeHost || !a.devicePointer) return EMAC_ERR_ARG;
+  *dev = a.devicePointer;  // the device address of p itself (offset into the pinned range kept)
+  return 0;
+}
 int emac_gpu_host_register(void *p, size_t bytes) {
   if (!bytes) return 0;
   if (hipHostRegister(p, bytes, hipHostRegisterDefault) != hipSuccess) {

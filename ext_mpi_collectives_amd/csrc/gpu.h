@@ -51,6 +51,7 @@ int emac_gpu_memcpy(void *dst, const void *src, size_t bytes); /* synchronous, a
 int emac_gpu_memcpy_async(void *dst, const void *src, size_t bytes, void *stream);
 int emac_gpu_memset_async(void *dst, int v, size_t bytes, void *stream);
 int emac_gpu_is_device_pointer(const void *p);
+int emac_gpu_pinned_view(const void *p, void **dev); /* page-locked host memory: its device address */
 int emac_gpu_host_register(void *p, size_t bytes);
 int emac_gpu_host_unregister(void *p);
 int emac_gpu_stream_create(void **stream);

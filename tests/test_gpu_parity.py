@@ -114,6 +114,42 @@ def test_host_buffers_staged(oracle):
     assert_bitwise(recvs, oracle.allreduce(sends, "6;1 -4 4"), "host staged")
 
 
+@pytest.mark.parametrize("direct", ["1", "0"])
+@pytest.mark.parametrize("code,R,count,copyin,in_place,elem_off", [
+    (emac.FLOAT, 4, 300007, "6;1 -4 4", False, 0),
+    (emac.FLOAT, 8, 16384, "6;1 -2 -2 -2 2 2 2", True, 0),
+    (emac.DOUBLE, 3, 100003, "6;3 -3 3", False, 1),                # views 8 bytes into the pinned block
+    (emac.INT, 4, 1 << 20, "6;-64 -4 4", False, 3),                # 12 bytes in: element-granular edges
+    (emac.LONG, 8, 5, "6;1 -8 8", True, 0)])
+def test_pinned_host_buffers(oracle, monkeypatch, direct, code, R, count, copyin, in_place, elem_off):
+    """Page-locked host buffers (torch pin_memory) in the NODE form: read and written by the fold
+    kernel over PCIe (default), or staged through device mirrors (EXT_MPI_AMD_HOST_DIRECT=0).
+    Views that start inside a pinned block check that the device address keeps the offset."""
+    monkeypatch.setenv("EXT_MPI_AMD_HOST_DIRECT", direct)
+    sends = xorshift_inputs(R, count, code, seed_base=0x7107 + count)
+    blocks_s = [torch.empty(count + elem_off, dtype=TORCH[code]).pin_memory() for _ in range(R)]
+    blocks_r = blocks_s if in_place else [torch.empty(count + elem_off, dtype=TORCH[code]).pin_memory()
+                                          for _ in range(R)]
+    ts = [b[elem_off:] for b in blocks_s]
+    tr = [b[elem_off:] for b in blocks_r]
+    h = emac.node_allreduce_init([t.data_ptr() for t in ts], [t.data_ptr() for t in tr], count, code, copyin)
+    try:
+        for _ in range(2):
+            for t, s in zip(ts, sends):
+                t.copy_(torch.from_numpy(s))
+            if not in_place:
+                for t in tr:
+                    t.fill_(-1)
+            emac.start(h)
+            emac.wait(h)
+            assert_bitwise([t.numpy() for t in tr], oracle.allreduce(sends, copyin, in_place=in_place),
+                           f"pinned host direct={direct}")
+            if not in_place:  # the send buffers are read only
+                assert_bitwise([t.numpy() for t in ts], sends, "pinned send buffers unchanged")
+    finally:
+        emac.done(h)
+
+
 @pytest.mark.parametrize("code,R,count,copyin,in_place", [
     (emac.FLOAT, 8, (4 << 20) + 7, "6;1 -8 8", False),            # pipelined: 8 element ranges
     (emac.DOUBLE, 4, (1 << 20) + 1001, "6;1 -2 -2 2 2", True),
