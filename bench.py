@@ -543,6 +543,37 @@ def _fold_only(emac, h, stream, steps, torch):
     return e0.elapsed_time(e1) * 1e-3 / steps
 
 
+def _rccl_allreduce_baseline(rank, world, dist, torch):
+    """RCCL's own float Allreduce at the sweep's sizes (the reference's tests/benchmark_nccl.c
+    comparison), through torch's RCCL process group; max over ranks. A reported
+    baseline: its summation order is RCCL's, not the reference's."""
+    try:
+        g = dist.new_group(backend="nccl")
+        pts = []
+        for nbytes in (8, 64 << 10, 1 << 20, 16 << 20, 64 << 20, 256 << 20):
+            n = max(1, nbytes // 4)
+            x = torch.ones(n, device="cuda")
+            st = 100 if nbytes <= (1 << 20) else 10
+            for _ in range(5):
+                dist.all_reduce(x, group=g)
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(st):
+                dist.all_reduce(x, group=g)
+            torch.cuda.synchronize()
+            el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+            pts.append({"bytes_per_rank": n * 4, "us_per_allreduce": round(el.item() * 1e6 / st, 2),
+                        "algbw_gbps": round(n * 4 * st / el.item() / 1e9, 2)})
+            del x
+        dist.destroy_process_group(g)
+        return pts
+    except Exception as e:  # noqa: BLE001 -- a baseline, never the measurement
+        log(f"rank {rank}: RCCL Allreduce baseline failed: {e}")
+        return {"error": str(e)[:200]}
+
+
 def transport_child(args):
     """One transport's N > 1 measurement in a process of its own (spawned by multi_gpu): its own
     gloo group, its own HIP context. Writes this rank's results as JSON to --child-result."""
@@ -607,6 +638,8 @@ def transport_child(args):
         emac.done(h)
         send.free()
         recv.free()
+        if transport == "rccl":
+            res["rccl_allreduce_baseline"] = _rccl_allreduce_baseline(rank, world, dist, torch)
         if full:
             # BASELINE configs[3] (double, 256 MiB per rank) and a configs[4]-style size sweep
             points = [(args.dtype, n) for n in (8, 64 << 10, 1 << 20, 16 << 20, 64 << 20, 256 << 20)]
@@ -711,6 +744,8 @@ def multi_gpu(args):
             extras[f"{t}_transport"] = r if "wall" not in r else {
                 "ms_per_step": round(r["wall"] * 1e3 / args.steps, 4),
                 "value": round(world * S * args.steps / r["wall"] / 1e9, 2), "checked": r["checked"]}
+        if "rccl_allreduce_baseline" in results[t]:  # whichever role RCCL had
+            extras["rccl_allreduce_baseline"] = results[t]["rccl_allreduce_baseline"]
     if rank == 0 and primary is None:
         print(json.dumps({"metric": "device-resident GB/s reduced (float32 MPI_SUM) per GPU; % HBM3E roofline",
                           "value": 0.0, "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
