@@ -772,6 +772,12 @@ def multi_gpu(args):
             "fold_xgmi_gbps_per_gpu": round(remote / kf / 1e9, 1) if remote else None,
             "end_to_end_algbw_gbps_per_gpu": round(S * args.steps / wall / 1e9, 2),
             "xgmi_bound_us": round(2 * (world - 1) / world * S / (min(world - 1, 7) * 153e9) * 1e6, 1)})
+        # the N > 1 Allreduce is bound by xGMI (each GPU moves 2(N-1)/N S over its links), not by
+        # HBM as the N = 1 kernel-only workload (8 node ranks in one HBM) is: its fraction of
+        # that bound, and what N = 1 measures instead
+        extras["end_to_end_frac_of_xgmi_bound"] = round(extras["xgmi_bound_us"] / (wall * 1e6 / args.steps), 3)
+        extras["note_vs_n1"] = ("N = 1 is BASELINE configs[1]: 8 node ranks resident in one GPU's HBM, HBM-bound; "
+                                "N > 1 is one rank per GPU, every rank's chunk crossing xGMI (bound: xgmi_bound_us)")
         form = ("peer-mapped (hipIpc over xGMI): barrier kernel, fold of the owned chunk over the peers' send "
                 "buffers with the fan-out stored into every peer's receive buffer, barrier kernel"
                 if primary == "ipc" else
