@@ -145,6 +145,7 @@ typedef struct {
   void *dsend[EMAC_MAX_RANKS], *drecv[EMAC_MAX_RANKS];
   unsigned char send_mirror[EMAC_MAX_RANKS], recv_mirror[EMAC_MAX_RANKS];
   unsigned char send_reg[EMAC_MAX_RANKS], recv_reg[EMAC_MAX_RANKS];
+  int host_direct; /* NODE form: some buffer is page-locked host memory the fold reads / writes */
   /* COMM form */
   int comm;
   int me, me_pos;
@@ -283,6 +284,7 @@ static int map_buffers(emac_handle *h, int r, const void *send, void *recv) {
     h->drecv[r] = recv;
   } else if (host_direct(h, recv, &dv)) {
     h->drecv[r] = dv;
+    h->host_direct = 1;
   } else {
     if ((rc = mirror_alloc(h, &h->drecv[r]))) return rc;
     h->recv_mirror[r] = 1;
@@ -294,6 +296,7 @@ static int map_buffers(emac_handle *h, int r, const void *send, void *recv) {
     h->dsend[r] = (void *)send;
   } else if (host_direct(h, send, &dv)) {
     h->dsend[r] = dv;
+    h->host_direct = 1;
   } else {
     if ((rc = mirror_alloc(h, &h->dsend[r]))) return rc;
     h->send_mirror[r] = 1;
@@ -329,8 +332,9 @@ static int upload_launch(const emac_handle *h, emac_launch *L, emac_bucket *b, i
 static int upload_buckets(emac_handle *h, emac_bucket *b, int nb) {
   emac_edge *edges = NULL;
   int rc;
-  if ((rc = emac_layout(b, nb, h->plan.op, h->nsrc, h->plan.codes.nlev > 1, h->fan, &edges, &h->nedges, &h->ntiles,
-                        &h->tiles_per_bucket, &h->all_full, &h->unroll)))
+  /* (fan | EMAC_FAN_HOST: the schedule for buffers across PCIe, emac_gpu_pick_unroll) */
+  if ((rc = emac_layout(b, nb, h->plan.op, h->nsrc, h->plan.codes.nlev > 1, h->fan | (h->host_direct ? EMAC_FAN_HOST : 0),
+                        &edges, &h->nedges, &h->ntiles, &h->tiles_per_bucket, &h->all_full, &h->unroll)))
     return rc;
   h->nb = nb;
   if (nb && (rc = emac_gpu_malloc((void **)&h->d_buckets, sizeof(emac_bucket) * (size_t)nb)) == 0)

@@ -65,6 +65,8 @@ int emac_gpu_pick_unroll(int op, int nsrc, int tree, int fan, long total_vectors
   // between them U = 4 with an s_sleep after every 4 loads is 4-8 % faster (16 MiB: 41.9 vs
   // 45.2-45.4 us); 64 MiB per rank prefers U = 2 (183 vs 194 us), >= 128 MiB U = 4.
   using emac::sched;
+  const int host = fan & EMAC_FAN_HOST;
+  fan &= ~EMAC_FAN_HOST;
   if (op != EMAC_SUM && fan != 2) {  // MIN / MAX: the burst schedule of the shape (fold_kernel.hpp)
     if (tree && nsrc > 1) return sched(emac::tree_unroll(nsrc), 1);
     return sched(nsrc > 8 ? 1 : 2, 1);
@@ -82,6 +84,9 @@ int emac_gpu_pick_unroll(int op, int nsrc, int tree, int fan, long total_vectors
   }
   if (nsrc > 8) return sched(1, 1);
   if (fan) {
+    // page-locked host buffers (NODE form): every access crosses PCIe, where a CU's own request
+    // rate, not HBM, binds -- the smallest tiles spread a small message over the most CUs
+    if (host) return sched(1, 1);
     if (total_vectors < (192L << 10)) return sched(2, 1);
     if (total_vectors < (3L << 20)) return sched(4, 5);
     if (total_vectors < (6L << 20)) return sched(2, 1);

@@ -335,7 +335,8 @@ __global__ __launch_bounds__(EMAC_BLOCK) void ipc_fused_kernel(const emac_bucket
 // ---- instantiation policy (keep in sync with emac_gpu_pick_unroll in fold.hip) ----
 // A launch schedule is encoded as U | ISSUE << 4 (EMAC_SCHED).
 // linear, fan-out N (node / IPC form):  N <= 8 -> (U 2, burst), (U 4, burst), (U 4, s_sleep 2
-//                                        every 4 loads);  N > 8 -> (U 1, burst)
+//                                        every 4 loads), (U 1, burst: page-locked host buffers);
+//                                        N > 8 -> (U 1, burst)
 // linear, fan-out 1 (comm form):        N <= 8 -> U in {1, 2}, burst;  N > 8 -> U = 1
 // tree (composite N), either fan-out:   U = 4 / 2 / 1 for N <= 4 / <= 8 / > 8, burst; U = 2 also
 //                                        with s_sleep 2 every 4 loads
@@ -403,6 +404,7 @@ int launch_nf(bool tree, int unroll, const Launch &L) {
     if constexpr (N > 8) {
       return unroll == sched(1, 1) ? launch_one<T, OP, N, 1, false, D>(L) : EMAC_ERR_UNSUPPORTED;
     } else if constexpr (FAN) {
+      if (unroll == sched(1, 1)) return launch_one<T, OP, N, 1, false, D, 1>(L);  // host buffers
       if (unroll == sched(4, 5)) return launch_one<T, OP, N, 4, false, D, 5>(L);
       if (unroll == sched(4, 1)) return launch_one<T, OP, N, 4, false, D, 1>(L);
       if (unroll == sched(2, 1)) return launch_one<T, OP, N, 2, false, D, 1>(L);

@@ -111,6 +111,7 @@ int emac_gpu_fold_fused(int dtype, int op, int nsrc, int unroll, const emac_code
 /* Launch schedule: unroll U (16-byte vectors per lane per leaf; a tile covers EMAC_BLOCK * U
    vectors) in the low 4 bits, load-issue schedule above (fold_kernel.hpp). fan: the fan-out
    width equals nsrc (node / IPC form) instead of 1. */
+#define EMAC_FAN_HOST 4 /* or-ed into pick_unroll's fan: node fan-out over page-locked host memory */
 int emac_gpu_pick_unroll(int op, int nsrc, int tree, int fan, long total_vectors);
 
 /* Launch the fold over nb device-resident buckets (ntiles tiles in total) on `stream`.
