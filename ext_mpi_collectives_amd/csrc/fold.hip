@@ -85,7 +85,8 @@ int emac_gpu_pick_unroll(int op, int nsrc, int tree, int fan, long total_vectors
   if (nsrc > 8) return sched(1, 1);
   if (fan) {
     // page-locked host buffers (NODE form): every access crosses PCIe, where a CU's own request
-    // rate, not HBM, binds -- the smallest tiles spread a small message over the most CUs
+    // rate, not HBM, binds -- the smallest tiles spread a message over the most CUs (better up
+    // to 16 MiB per rank, equal at 64 MiB: profiles/r01_host_direct_sweep.json)
     if (host) return sched(1, 1);
     if (total_vectors < (192L << 10)) return sched(2, 1);
     if (total_vectors < (3L << 20)) return sched(4, 5);
