@@ -123,6 +123,27 @@ class DevBuf:
             self.ptr = ctypes.c_void_p()
 
 
+class HostBuf:
+    """A page-locked host buffer (torch pin_memory) with DevBuf's interface: the path's real start
+    and end (the reference's XPMEM-mapped MPI buffers)."""
+
+    def __init__(self, nbytes):
+        import torch
+        self.t = torch.empty(max(1, nbytes), dtype=torch.uint8).pin_memory()
+
+    def data_ptr(self):
+        return self.t.data_ptr()
+
+    def upload(self, arr):
+        ctypes.memmove(self.t.data_ptr(), arr.ctypes.data, arr.nbytes)
+
+    def download(self, arr):
+        ctypes.memmove(arr.ctypes.data, self.t.data_ptr(), arr.nbytes)
+
+    def free(self):
+        self.t = None
+
+
 def host_random(count, np_dtype, seed):
     rng = np.random.Generator(np.random.PCG64(seed))
     if np.dtype(np_dtype).kind == "f":
@@ -482,13 +503,15 @@ def single_gpu(args):
     print(json.dumps(out), flush=True)
 
 
-def _comm_run(emac, comm, count, tdtype, code, dname, copyin, steps, warmup, rank, world, dist, torch, check=True):
+def _comm_run(emac, comm, count, tdtype, code, dname, copyin, steps, warmup, rank, world, dist, torch, check=True,
+              host=False):
     """Persistent Allreduce of `count` elements per rank on communicator `comm`; returns the max-over-ranks
     wall time of `steps` Starts (one stream), the handle's fold time alone, and the check."""
     tsize = torch.empty((), dtype=tdtype).element_size()
     np_dtype = {torch.float32: np.float32, torch.float64: np.float64, torch.int32: np.int32,
                 torch.int64: np.int64}[tdtype]
-    send, recv = DevBuf(max(1, count * tsize)), DevBuf(max(1, count * tsize))
+    Buf = HostBuf if host else DevBuf
+    send, recv = Buf(max(1, count * tsize)), Buf(max(1, count * tsize))
     mine = host_random(count, np_dtype, 0x5EED0000 + rank)
     send.upload(mine)
     h = emac.allreduce_init(send.data_ptr(), recv.data_ptr(), count, code, comm, copyin)
@@ -676,6 +699,17 @@ def transport_child(args):
                                   "algbw_gbps": round(nbytes * st / el_p / 1e9, 2), "checked": ok_p})
                     log(f"rank {rank}: {transport}: '{cp}' {nbytes} B: {el_p * 1e6 / st:.2f} us, checked {ok_p}")
             res["radix_sweep"] = radix
+            # the path's real start and end: page-locked host send / receive buffers, staged through
+            # device mirrors on each rank's own PCIe link (H2D, legs, D2H on the handle's stream)
+            hp, sb, rb, _, el_p, ok_p = _comm_run(emac, comm, count, tdtype, code, dname, copyin, 10, 3, rank, world,
+                                                  dist, torch, host=True)
+            emac.done(hp)
+            sb.free()
+            rb.free()
+            res["host_buffers"] = {"bytes_per_rank": count * tsize, "us_per_allreduce": round(el_p * 1e6 / 10, 2),
+                                   "gbps_reduced_job": round(world * count * tsize * 10 / el_p / 1e9, 2),
+                                   "checked": ok_p}
+            log(f"rank {rank}: {transport}: host buffers {count * tsize} B: {el_p * 1e5:.2f} us, checked {ok_p}")
     finally:
         emac.comm_free(comm)
     with open(args.child_result, "w") as f:
@@ -758,6 +792,7 @@ def multi_gpu(args):
         extras["sweep"] = r["sweep"]
         extras["radix_sweep"] = r.get("radix_sweep", [])
         extras["local_fold_rate_retained"] = r.get("local_fold")
+        extras["host_buffers_pcie_inclusive"] = r.get("host_buffers")
         chunk = S / world
         if primary == "ipc":
             algo = 2 * world * chunk  # R leaf reads (R-1 over xGMI) + R fan-out writes (R-1 over xGMI)
