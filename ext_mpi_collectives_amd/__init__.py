@@ -68,6 +68,14 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: run ext_mpi_collectives_amd.build() "
                               "(the HIP path has no CPU fallback)")
+        # One HIP runtime per process: torch's bundled runtime is needed as "libamdhip64.so", this
+        # library's as "libamdhip64.so.7" (the SONAME both carry). With torch loaded first the
+        # loader reuses its runtime for this library; the other order loads /opt/rocm's copy and
+        # torch then loads a second one (two runtimes corrupted the heap at exit on this image).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         c_int, c_long, c_void_p = ctypes.c_int, ctypes.c_long, ctypes.c_void_p
         P = ctypes.POINTER

@@ -43,3 +43,21 @@ def test_version_and_no_gpu_error():
     with pytest.raises(emac.ExtMpiError) as e:
         emac.node_allreduce_init([0, 0], [0, 0], 16, emac.FLOAT)
     assert e.value.code == -5
+
+
+def test_launch_schedule_policy():
+    """emac_gpu_pick_unroll (host code, no GPU): the HBM-tuned node schedule (U = 4, staggered, at
+    16 MiB x 8 float), the smallest tile for page-locked host buffers (EMAC_FAN_HOST = 4), and
+    MIN / MAX keeping their one burst schedule whatever the buffers."""
+    f = emac.lib().emac_gpu_pick_unroll
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]
+    sched = lambda u, issue: u | issue << 4  # noqa: E731
+    nvec = 8 * (2 << 20) // 16  # 8 buckets of 2 MiB
+    assert f(emac.SUM, 8, 0, 1, nvec) == sched(4, 5)
+    assert f(emac.SUM, 8, 0, 1 | 4, nvec) == sched(1, 1)
+    assert f(emac.SUM, 8, 0, 1 | 4, 64) == sched(1, 1)
+    assert f(emac.SUM, 8, 0, 1 | 4, 1 << 24) == sched(1, 1)
+    assert f(emac.SUM, 8, 1, 1 | 4, nvec) == f(emac.SUM, 8, 1, 1, nvec)  # trees: their own schedule
+    for op in (emac.MIN, emac.MAX):
+        assert f(op, 8, 0, 1 | 4, nvec) == f(op, 8, 0, 1, nvec) == sched(2, 1)
