@@ -810,7 +810,9 @@ def multi_gpu(args):
         # the N > 1 Allreduce is bound by xGMI (each GPU moves 2(N-1)/N S over its links), not by
         # HBM as the N = 1 kernel-only workload (8 node ranks in one HBM) is: its fraction of
         # that bound, and what N = 1 measures instead
-        extras["end_to_end_frac_of_xgmi_bound"] = round(extras["xgmi_bound_us"] / (wall * 1e6 / args.steps), 3)
+        extras["end_to_end_frac_of_xgmi_bound"] = (
+            round(extras["xgmi_bound_us"] / (wall * 1e6 / args.steps), 3)
+            if extras["gpus_visible"] >= world else None)  # ranks sharing a GPU cross no xGMI
         extras["note_vs_n1"] = ("N = 1 is BASELINE configs[1]: 8 node ranks resident in one GPU's HBM, HBM-bound; "
                                 "N > 1 is one rank per GPU, every rank's chunk crossing xGMI (bound: xgmi_bound_us)")
         form = ("peer-mapped (hipIpc over xGMI): barrier kernel, fold of the owned chunk over the peers' send "
