@@ -1,7 +1,8 @@
 // foldbench.hip -- variant sweep of the node-form fold (R = 8 leaves, fused 8-way fan-out) on one
 // MI355X, interleaved rounds in one process (cdna_hip_programming.md 5.4 rule 24). Also times a
 // float4 copy and a float4 read-reduce over the same byte volume as ceilings.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/foldbench.hip -o foldbench
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/foldbench.hip -o tools/foldbench \
+//          -Lext_mpi_collectives_amd -lext_mpi_amd -Wl,-rpath,'$ORIGIN/../ext_mpi_collectives_amd'
 // Run:   ./foldbench [MiB per rank = 16] [rounds = 7] [launches per round = 20]
 #include <hip/hip_runtime.h>
 #include <algorithm>
@@ -354,7 +355,7 @@ int main(int argc, char **argv) {
       CHECK(hipEventRecord(e0, s));
       for (int i = 0; i < per; i++) {
         emac::Launch L = {&codes, (o ? ebk_prod : ebk_rot)[(k++) % nsets], R, (long)R * (C / 512), C / 512, 1, nullptr, 0, s};
-        emac::launch_one<float, R, 2, false, R>(L);
+        emac::launch_one<float, EMAC_SUM, R, 2, false, R>(L);
       }
       CHECK(hipEventRecord(e1, s));
       CHECK(hipEventSynchronize(e1));

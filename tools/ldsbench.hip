@@ -279,16 +279,16 @@ int main(int argc, char **argv) {
       const long tpb = C / (256 * U);
       emac::Launch L = {&codes, ebk[set], R, tpb * R, tpb, 1, nullptr, 0, s};
       if (U == 2)
-        emac::launch_one<float, R, 2, false, R>(L);
+        emac::launch_one<float, EMAC_SUM, R, 2, false, R>(L);
       else
-        emac::launch_one<float, R, 4, false, R>(L);
+        emac::launch_one<float, EMAC_SUM, R, 4, false, R>(L);
       break;
     }
     case 20: case 21: case 22: case 23: case 24: case 25: case 26: case 27: {
       // production template, U = 2, load issue schedule ISSUE = kind - 20
       const long tpb = C / 512;
       const dim3 g((unsigned)std::min<long>(tpb * R, 8192));
-#define ISS(i) case 20 + i: hipLaunchKernelGGL((emac::fold_kernel<float, R, 2, false, R, i>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, codes); break;
+#define ISS(i) case 20 + i: hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 2, false, R, i>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, codes); break;
       switch (kind) { ISS(0) ISS(1) ISS(2) ISS(3) ISS(4) ISS(5) ISS(6) ISS(7) }
 #undef ISS
       break;
@@ -299,22 +299,22 @@ int main(int argc, char **argv) {
       const long tpb = C / (256 * U);
       const dim3 g((unsigned)std::min<long>(tpb * R, 8192));
       switch (kind) {
-      case 41: hipLaunchKernelGGL((emac::fold_kernel<float, R, 2, true, R, 1>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, tcodes); break;
-      case 43: hipLaunchKernelGGL((emac::fold_kernel<float, R, 2, true, R, 3>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, tcodes); break;
-      case 45: hipLaunchKernelGGL((emac::fold_kernel<float, R, 2, true, R, 5>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, tcodes); break;
-      case 47: hipLaunchKernelGGL((emac::fold_kernel<float, R, 2, true, R, 7>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, tcodes); break;
-      case 51: hipLaunchKernelGGL((emac::fold_kernel<float, R, 4, true, R, 1>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, tcodes); break;
-      case 55: hipLaunchKernelGGL((emac::fold_kernel<float, R, 4, true, R, 5>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, tcodes); break;
+      case 41: hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 2, true, R, 1>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, tcodes); break;
+      case 43: hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 2, true, R, 3>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, tcodes); break;
+      case 45: hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 2, true, R, 5>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, tcodes); break;
+      case 47: hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 2, true, R, 7>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, tcodes); break;
+      case 51: hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 4, true, R, 1>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, tcodes); break;
+      case 55: hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 4, true, R, 5>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, tcodes); break;
       }
       break;
     }
     case 31: case 33: case 35: case 37: {
       const long tpb = C / 1024;
       const dim3 g((unsigned)std::min<long>(tpb * R, 8192));
-      if (kind == 31) hipLaunchKernelGGL((emac::fold_kernel<float, R, 4, false, R, 1>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, codes);
-      if (kind == 33) hipLaunchKernelGGL((emac::fold_kernel<float, R, 4, false, R, 3>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, codes);
-      if (kind == 35) hipLaunchKernelGGL((emac::fold_kernel<float, R, 4, false, R, 5>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, codes);
-      if (kind == 37) hipLaunchKernelGGL((emac::fold_kernel<float, R, 4, false, R, 7>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, codes);
+      if (kind == 31) hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 4, false, R, 1>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, codes);
+      if (kind == 33) hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 4, false, R, 3>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, codes);
+      if (kind == 35) hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 4, false, R, 5>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, codes);
+      if (kind == 37) hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 4, false, R, 7>), g, dim3(256), 0, s, ebk[set], R, tpb * R, tpb, 1, codes);
       break;
     }
     case 2: hipLaunchKernelGGL(read_nt, dim3(8192), dim3(256), 0, s, ca + (i & 1) * cn, cn, dummy); break;
