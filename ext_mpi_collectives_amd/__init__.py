@@ -23,6 +23,7 @@ UNIQUE_ID_BYTES = 128
 MAX_RANKS = 16
 ERRORS = {-1: "ERROR_MALLOC", -2: "ERROR_SHMEM", -3: "ERROR_ARG", -4: "ERROR_UNSUPPORTED",
           -5: "ERROR_DEVICE", -6: "ERROR_TRANSPORT"}
+ERROR_MALLOC, ERROR_SHMEM, ERROR_ARG, ERROR_UNSUPPORTED, ERROR_DEVICE, ERROR_TRANSPORT = -1, -2, -3, -4, -5, -6
 
 _TORCH_DTYPE_CODES = {"torch.float32": FLOAT, "torch.float64": DOUBLE, "torch.int32": INT,
                       "torch.int64": LONG}

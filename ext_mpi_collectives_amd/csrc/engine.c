@@ -23,6 +23,7 @@
  * (H2D before, D2H after, on the same stream); the buffers are page-locked once at init,
  * as the reference maps its XPMEM peers once (src/mpi/ext_mpi_xpmem.c:68-133).
  */
+#include <stddef.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -39,12 +40,15 @@
 
 enum { KIND_NODE = 1, KIND_COMM = 2, KIND_IPC = 3 };
 
-/* one peer allocation mapped into this process (hipIpcOpenMemHandle), shared by the handles that
-   reference the same allocation (the exporter's allocation id and size) and closed when the last
-   of them is done, as the reference closes its cudaIpc mappings in EXT_MPI_Done
-   (src/gpu/cuda_shmem.c:301-314). */
+/* one peer allocation mapped into this process (hipIpcOpenMemHandle), shared by every handle and
+   communicator that references the same allocation (the exporter's handle bytes, allocation id
+   and size) and closed when the last of them is done, as the reference closes its cudaIpc
+   mappings in EXT_MPI_Done (src/gpu/cuda_shmem.c:301-314). The table is process-wide: the
+   runtime sub-allocates small device allocations out of shared chunks, so two communicators'
+   synchronisation blocks (or two handles' buffers) of one peer can share a chunk, and opening
+   the same chunk twice in one process is refused (measured: the second communicator's set-up
+   failed with 8 processes on one MI355X). */
 typedef struct {
-  int peer;
   unsigned long long buf_id;
   long extent;
   unsigned char handle[EMAC_IPC_HANDLE_BYTES];
@@ -73,19 +77,17 @@ typedef struct {
   ext_mpi_amd_allgather_fn ag;
   void *ag_ctx;
   void *sync;                      /* this rank's emac_sync block (uncached device memory) */
+  void *stale_sync[4];             /* blocks of failed set-up rounds (freed with the communicator) */
+  int nstale_sync;
   void *peer_sync[EMAC_MAX_RANKS]; /* every rank's block as mapped here (own at [rank]) */
-  void *peer_sync_base[EMAC_MAX_RANKS]; /* the mappings (hipIpcCloseMemHandle takes the base) */
+  void *peer_sync_base[EMAC_MAX_RANKS]; /* the mappings (shared table, ipc_map_peer) */
   void **d_peer_sync;              /* the same table in device memory */
-  int *err;                        /* pinned host word the barrier kernels report into */
-  unsigned xcc_mask;
+  int *err;                        /* pinned host words the barrier kernels report into, one per slot */
   long timeout_ticks;
   unsigned char slot_used[EMAC_SYNC_SLOTS];
   unsigned long slot_epoch[EMAC_SYNC_SLOTS][2]; /* a slot's epochs continue across its handles */
-  ipc_map *maps;
-  int nmaps;
   ipc_mirror *mirrors;
   int nmirrors;
-  int err_reported;
 } emac_comm;
 
 /* Loopback groups: every rank of the communicator lives in this process; the i-th handle a
@@ -162,6 +164,8 @@ typedef struct {
   void *mapped[2 * EMAC_MAX_RANKS];
   int nmapped;
   int fused; /* whole Allreduce in one launch (emac_gpu_fold_fused) */
+  void *ev_release; /* system-scope release recorded before every phase-0 barrier */
+  emac_launch pull; /* every other owner's result copied into this rank's receive buffer */
   emac_pipe *pipe; /* pipelined host staging (NODE form), or NULL */
 } emac_handle;
 
@@ -175,7 +179,7 @@ static int new_handle_slot(void) {
   return -1;
 }
 
-static void ipc_unmap(emac_comm *cm, void *base);
+static void ipc_unmap(void *base);
 static void mirror_free(emac_handle *h, void *p);
 
 static void pipe_free(emac_pipe *pp) {
@@ -206,6 +210,8 @@ static void release(emac_handle *h) {
   pipe_free(h->pipe);
   emac_gpu_free(h->d_buckets);
   emac_gpu_free(h->d_edges);
+  emac_gpu_free(h->pull.d_buckets);
+  emac_gpu_free(h->pull.d_edges);
   emac_gpu_free(h->staging);
   for (r = 0; r < h->nbuf; r++) {
     int same = h->dsend[r] == h->drecv[r];
@@ -214,7 +220,8 @@ static void release(emac_handle *h) {
     if (h->send_reg[r]) emac_gpu_host_unregister(h->user_send[r]);
     if (h->recv_reg[r]) emac_gpu_host_unregister(h->user_recv[r]);
   }
-  for (r = 0; r < h->nmapped; r++) ipc_unmap(&comms[h->comm], h->mapped[r]);
+  for (r = 0; r < h->nmapped; r++) ipc_unmap(h->mapped[r]);
+  emac_gpu_event_destroy(h->ev_release);
   if (h->kind == KIND_IPC && h->slot_held) {
     emac_comm *cm = &comms[h->comm];
     cm->slot_used[h->slot] = 0;
@@ -314,11 +321,11 @@ static void place_bucket(emac_bucket *b, int nsrc, long off, long len, int tsize
   emac_split_alignment(b, nsrc, len, tsize);
 }
 
-static int upload_launch(const emac_handle *h, emac_launch *L, emac_bucket *b, int nb) {
+static int upload_launch_as(const emac_handle *h, emac_launch *L, emac_bucket *b, int nb, int nsrc, int tree) {
   emac_edge *edges = NULL;
   int rc;
-  if ((rc = emac_layout(b, nb, h->plan.op, h->nsrc, h->plan.codes.nlev > 1, h->fan, &edges, &L->nedges, &L->ntiles,
-                        &L->tiles_per_bucket, &L->all_full, &L->unroll)))
+  if ((rc = emac_layout(b, nb, h->plan.op, nsrc, tree, h->fan, &edges, &L->nedges, &L->ntiles, &L->tiles_per_bucket,
+                        &L->all_full, &L->unroll)))
     return rc;
   L->nb = nb;
   if (nb && (rc = emac_gpu_malloc((void **)&L->d_buckets, sizeof(emac_bucket) * (size_t)nb)) == 0)
@@ -327,6 +334,10 @@ static int upload_launch(const emac_handle *h, emac_launch *L, emac_bucket *b, i
     rc = emac_gpu_memcpy(L->d_edges, edges, sizeof(emac_edge) * (size_t)L->nedges);
   free(edges);
   return rc;
+}
+
+static int upload_launch(const emac_handle *h, emac_launch *L, emac_bucket *b, int nb) {
+  return upload_launch_as(h, L, b, nb, h->nsrc, h->plan.codes.nlev > 1);
 }
 
 static int upload_buckets(emac_handle *h, emac_bucket *b, int nb) {
@@ -578,8 +589,9 @@ int ext_mpi_amd_comm_init_loopback(int size, int *comm_of_rank) {
  * synchronises the ranks with flags in shared memory. Here: hipIpc (dmabuf) mappings, exchanged
  * through the caller's allgather (the MPI layer passes PMPI_Allgather, as the reference does),
  * and stream-ordered barrier kernels over a per-communicator block of uncached device flags
- * (ipc.hip). Start = barrier -> fold of this rank's owner chunks over the peers' send buffers
- * with the fan-out stored straight into every peer's receive buffer -> barrier. */
+ * (ipc.hip). Start = system-scope release -> barrier -> fold of this rank's owner chunks over the
+ * peers' send buffers into its own receive buffer -> barrier -> pull of every other owner's
+ * result from that owner's receive buffer (one launch for small messages). */
 
 static int ipc_agree(emac_comm *cm, int ok_local) {
   int all[EMAC_MAX_RANKS], r;
@@ -589,45 +601,45 @@ static int ipc_agree(emac_comm *cm, int ok_local) {
   return 0;
 }
 
-static void *ipc_map_peer(emac_comm *cm, int peer, const unsigned char *handle, unsigned long long buf_id,
-                          long extent) {
+static ipc_map *g_maps;
+static int g_nmaps;
+
+static void *ipc_map_peer(const unsigned char *handle, unsigned long long buf_id, long extent) {
   int i;
   void *base;
-  for (i = 0; i < cm->nmaps; i++) {
-    ipc_map *m = &cm->maps[i];
-    if (m->base && m->peer == peer && m->extent == extent &&
-        (buf_id ? m->buf_id == buf_id : !memcmp(m->handle, handle, EMAC_IPC_HANDLE_BYTES))) {
+  for (i = 0; i < g_nmaps; i++) {
+    ipc_map *m = &g_maps[i];
+    if (m->base && m->extent == extent && m->buf_id == buf_id && !memcmp(m->handle, handle, EMAC_IPC_HANDLE_BYTES)) {
       m->refs++;
       return m->base;
     }
   }
   if (emac_gpu_ipc_open(handle, &base)) return NULL;
-  for (i = 0; i < cm->nmaps && cm->maps[i].base; i++);
-  if (i == cm->nmaps) {
-    ipc_map *m = (ipc_map *)realloc(cm->maps, sizeof(ipc_map) * (size_t)(cm->nmaps + 1));
+  for (i = 0; i < g_nmaps && g_maps[i].base; i++);
+  if (i == g_nmaps) {
+    ipc_map *m = (ipc_map *)realloc(g_maps, sizeof(ipc_map) * (size_t)(g_nmaps + 1));
     if (!m) {
       emac_gpu_ipc_close(base);
       return NULL;
     }
-    cm->maps = m;
-    cm->nmaps++;
+    g_maps = m;
+    g_nmaps++;
   }
-  cm->maps[i].peer = peer;
-  cm->maps[i].buf_id = buf_id;
-  cm->maps[i].extent = extent;
-  memcpy(cm->maps[i].handle, handle, EMAC_IPC_HANDLE_BYTES);
-  cm->maps[i].base = base;
-  cm->maps[i].refs = 1;
+  g_maps[i].buf_id = buf_id;
+  g_maps[i].extent = extent;
+  memcpy(g_maps[i].handle, handle, EMAC_IPC_HANDLE_BYTES);
+  g_maps[i].base = base;
+  g_maps[i].refs = 1;
   return base;
 }
 
-static void ipc_unmap(emac_comm *cm, void *base) {
+static void ipc_unmap(void *base) {
   int i;
-  for (i = 0; i < cm->nmaps; i++)
-    if (cm->maps[i].refs > 0 && cm->maps[i].base == base) {
-      if (--cm->maps[i].refs == 0) {
+  for (i = 0; i < g_nmaps; i++)
+    if (g_maps[i].refs > 0 && g_maps[i].base == base) {
+      if (--g_maps[i].refs == 0) {
         emac_gpu_ipc_close(base);
-        cm->maps[i].base = NULL;
+        g_maps[i].base = NULL;
       }
       return;
     }
@@ -657,7 +669,25 @@ static int ipc_mirror_get(emac_comm *cm, void **p, size_t bytes) {
 static void ipc_mirror_put(emac_comm *cm, void *p) {
   int i;
   for (i = 0; i < cm->nmirrors; i++)
-    if (cm->mirrors[i].p == p) cm->mirrors[i].busy = 0;
+    if (cm->mirrors[i].p == p && cm->mirrors[i].busy == 1) cm->mirrors[i].busy = 0; /* poisoned ones stay out */
+}
+
+int ext_mpi_amd_comm_malloc(int comm, void **p, unsigned long bytes) {
+  if (!p || comm < 0 || comm >= MAX_COMMS || !comms[comm].used) return EMAC_ERR_ARG;
+  *p = NULL;
+  if (!bytes) return 0;
+  if (emac_gpu_set_device(comms[comm].device)) return EMAC_ERR_DEVICE;
+  return comms[comm].ipc ? ipc_mirror_get(&comms[comm], p, bytes) : emac_gpu_malloc(p, bytes);
+}
+
+int ext_mpi_amd_comm_mfree(int comm, void *p) {
+  if (comm < 0 || comm >= MAX_COMMS || !comms[comm].used) return EMAC_ERR_ARG;
+  if (!p) return 0;
+  if (comms[comm].ipc) {
+    ipc_mirror_put(&comms[comm], p);
+    return 0;
+  }
+  return emac_gpu_free(p);
 }
 
 static int ipc_agree(emac_comm *cm, int ok_local);
@@ -667,15 +697,13 @@ static int ipc_agree(emac_comm *cm, int ok_local);
 static void ipc_comm_release(emac_comm *cm) {
   int r;
   for (r = 0; r < cm->size; r++)
-    if (r != cm->rank && cm->peer_sync_base[r]) emac_gpu_ipc_close(cm->peer_sync_base[r]);
-  for (r = 0; r < cm->nmaps; r++)
-    if (cm->maps[r].base) emac_gpu_ipc_close(cm->maps[r].base);
-  free(cm->maps);
+    if (r != cm->rank && cm->peer_sync_base[r]) ipc_unmap(cm->peer_sync_base[r]);
   if (cm->ag && cm->size > 1) ipc_agree(cm, 1);
   for (r = 0; r < cm->nmirrors; r++) emac_gpu_free(cm->mirrors[r].p);
   free(cm->mirrors);
   emac_gpu_free(cm->d_peer_sync);
   emac_gpu_free(cm->sync);
+  for (r = 0; r < cm->nstale_sync; r++) emac_gpu_free(cm->stale_sync[r]);
   emac_gpu_host_free(cm->err);
   memset(cm, 0, sizeof(*cm));
 }
@@ -692,12 +720,97 @@ typedef struct {
   unsigned char free_slots[EMAC_SYNC_SLOTS / 8]; /* handle set-up: slots this rank can use */
 } ipc_export;
 
+/* The synchronisation blocks: every rank exports its block, maps every peer's and validates the
+   mappings with a write probe (as the buffers, ipc_exchange): each rank flips probe[me][0] in
+   every peer's block through its mapping and checks that its own block shows every peer's flip.
+   The runtime places small allocations side by side in shared chunks, and a second
+   communicator's block mapped by a process that already maps the first one's was measured to
+   miss (8 processes on one MI355X: one rank never saw a peer's flags). A failed round keeps the
+   blocks it allocated (peers may map them; freed with the communicator) and retries with a fresh,
+   larger allocation. Collective: every rank runs every round whatever failed locally (`rc`). */
+#define EMAC_SYNC_ATTEMPTS 4
+static int ipc_sync_exchange(emac_comm *cm, int rc, ipc_export *all) {
+  ipc_export mine;
+  const int R = cm->size;
+  int attempt, r;
+  for (attempt = 0; attempt < EMAC_SYNC_ATTEMPTS; attempt++) {
+    void *pk[EMAC_PROBE_MAX];
+    unsigned char vals[EMAC_PROBE_MAX], seen[EMAC_PROBE_MAX];
+    int n = 0, good = 1, agreed;
+    memset(&mine, 0, sizeof(mine));
+    if (!rc && cm->sync) { /* the previous round's block stays allocated until the communicator goes */
+      cm->stale_sync[cm->nstale_sync++] = cm->sync;
+      cm->sync = NULL;
+    }
+    if (!rc) rc = emac_gpu_malloc_uncached(&cm->sync, sizeof(emac_sync) << attempt);
+    if (!rc) rc = emac_gpu_ipc_export(cm->sync, mine.handle, &mine.offset);
+    if (!rc) {
+      void *b0;
+      mine.extent = emac_gpu_alloc_extent(cm->sync, &b0);
+      mine.buf_id = emac_gpu_buffer_id(b0);
+    }
+    mine.status = rc == 0;
+    if (cm->ag(cm->ag_ctx, &mine, all, (long)sizeof(ipc_export))) return EMAC_ERR_TRANSPORT;
+    for (r = 0; r < R; r++)
+      if (!all[r].status) rc = rc ? rc : EMAC_ERR_TRANSPORT;
+    for (r = 0; !rc && r < R; r++) {
+      if (r == cm->rank) {
+        cm->peer_sync[r] = cm->sync;
+        continue;
+      }
+      cm->peer_sync_base[r] = ipc_map_peer(all[r].handle, all[r].buf_id, all[r].extent);
+      if (!cm->peer_sync_base[r]) {
+        rc = EMAC_ERR_TRANSPORT;
+        break;
+      }
+      cm->peer_sync[r] = (char *)cm->peer_sync_base[r] + all[r].offset;
+      pk[n] = &((emac_sync *)cm->peer_sync[r])->probe[cm->rank][0];
+      vals[n++] = (unsigned char)(0x5A ^ (cm->rank + 1));
+    }
+    if (!rc && R > 1) rc = emac_gpu_poke(pk, vals, n, NULL);
+    agreed = ipc_agree(cm, rc == 0); /* every flip has landed */
+    if (!rc) rc = agreed;
+    if (rc) return rc;
+    for (n = 0, r = 0; r < R; r++)
+      if (r != cm->rank) pk[n++] = &((emac_sync *)cm->sync)->probe[r][0];
+    if ((rc = emac_gpu_peek((const void *const *)pk, seen, n, NULL))) good = 0; /* still in the verdict below */
+    for (n = 0, r = 0; r < R; r++)
+      if (r != cm->rank) {
+        if (!rc && seen[n] != (unsigned char)(0x5A ^ (r + 1))) {
+          good = 0;
+          if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
+            fprintf(stderr, "ipc rank %d: peer %d does not reach my synchronisation block (attempt %d)\n", cm->rank, r,
+                    attempt);
+        }
+        n++;
+      }
+    memset(vals, 0, sizeof(vals));
+    if (!rc) rc = emac_gpu_poke(pk, vals, n, NULL);
+    {
+      int v[2] = {good, rc == 0}, allv[2 * EMAC_MAX_RANKS], ok = 1, fine = 1;
+      if (cm->ag(cm->ag_ctx, v, allv, (long)sizeof(v))) return EMAC_ERR_TRANSPORT;
+      for (r = 0; r < R; r++) {
+        ok &= allv[2 * r];
+        fine &= allv[2 * r + 1];
+      }
+      if (!fine) return rc ? rc : EMAC_ERR_TRANSPORT;
+      if (ok) return 0;
+    }
+    for (r = 0; r < R; r++)
+      if (r != cm->rank && cm->peer_sync_base[r]) {
+        ipc_unmap(cm->peer_sync_base[r]);
+        cm->peer_sync_base[r] = NULL;
+      }
+  }
+  return EMAC_ERR_TRANSPORT;
+}
+
 int ext_mpi_amd_comm_init_ipc(int rank, int size, ext_mpi_amd_allgather_fn allgather, void *ctx, int device,
                               int *comm) {
   emac_comm *cm;
-  ipc_export mine, *all = NULL;
+  ipc_export all[EMAC_MAX_RANKS];
   const char *tmo;
-  int i, r, rc;
+  int i, rc;
   if (!comm || !allgather || size < 1 || size > EMAC_MAX_RANKS || rank < 0 || rank >= size) return EMAC_ERR_ARG;
   *comm = -1;
   for (i = 0; i < MAX_COMMS && comms[i].used; i++);
@@ -712,32 +825,11 @@ int ext_mpi_amd_comm_init_ipc(int rank, int size, ext_mpi_amd_allgather_fn allga
   cm->ag_ctx = ctx;
   /* every rank takes part in every allgather below, whatever failed locally, so that all ranks
      reach the same verdict */
-  memset(&mine, 0, sizeof(mine));
   rc = emac_gpu_device_count() > 0 ? 0 : EMAC_ERR_DEVICE;
   if (!rc && device >= 0) rc = emac_gpu_set_device(device);
   if (!rc) rc = emac_gpu_get_device(&cm->device);
-  if (!rc) rc = emac_gpu_malloc_uncached(&cm->sync, sizeof(emac_sync));
-  if (!rc) rc = emac_gpu_host_alloc_mapped((void **)&cm->err, sizeof(int));
-  if (!rc) rc = emac_gpu_xcc_census(&cm->xcc_mask);
-  if (!rc) rc = emac_gpu_ipc_export(cm->sync, mine.handle, &mine.offset);
-  mine.status = rc == 0;
-  all = (ipc_export *)calloc((size_t)size, sizeof(ipc_export));
-  if (!all) return EMAC_ERR_MALLOC;
-  if (allgather(ctx, &mine, all, (long)sizeof(ipc_export))) {
-    rc = EMAC_ERR_TRANSPORT;
-  } else {
-    for (r = 0; r < size; r++)
-      if (!all[r].status) rc = rc ? rc : EMAC_ERR_TRANSPORT;
-  }
-  for (r = 0; !rc && r < size; r++) {
-    if (r == rank) {
-      cm->peer_sync[r] = cm->sync;
-    } else {
-      rc = emac_gpu_ipc_open(all[r].handle, &cm->peer_sync_base[r]);
-      if (!rc) cm->peer_sync[r] = (char *)cm->peer_sync_base[r] + all[r].offset;
-    }
-  }
-  free(all);
+  if (!rc) rc = emac_gpu_host_alloc_mapped((void **)&cm->err, sizeof(int) * EMAC_SYNC_SLOTS);
+  rc = ipc_sync_exchange(cm, rc, all);
   if (!rc && (rc = emac_gpu_malloc((void **)&cm->d_peer_sync, sizeof(void *) * (size_t)size)) == 0)
     rc = emac_gpu_memcpy(cm->d_peer_sync, cm->peer_sync, sizeof(void *) * (size_t)size);
   {
@@ -859,7 +951,7 @@ static int ipc_exchange(emac_handle *h, emac_comm *cm, int rc, int empty, ipc_ex
           precv[r] = psend[r];
           continue;
         }
-        base = ipc_map_peer(cm, r, e->handle, e->buf_id, e->extent);
+        base = ipc_map_peer(e->handle, e->buf_id, e->extent);
         if (!base) continue;
         h->mapped[h->nmapped++] = base;
         /* a mapping the runtime can describe must hold the peer's whole buffer (one it cannot
@@ -909,6 +1001,12 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
   emac_bucket *b = NULL;
   int R = cm->size, r, t, pc, nb = 0, c, slot, attempt;
   const int empty = h->bytes == 0; /* same count on every rank: nothing to map or fold */
+  /* The write probe below reads, flips and restores the first R bytes of this rank's buffers: work
+     the application still has in flight on them (e.g. the kernel filling the send buffer on its
+     own stream, legal before a persistent init) must have landed first, or the restore would
+     write back bytes read before it (measured: the first two elements of a freshly filled send
+     buffer stayed wrong for the handle's lifetime, 8 processes on one MI355X). */
+  if (!rc && !empty) rc = emac_gpu_device_sync();
   if (!rc && !empty) rc = map_buffers(h, 0, sendbuf, recvbuf);
   for (attempt = 0;; attempt++) {
     int stale[2], v[3], allv[3 * EMAC_MAX_RANKS], again = 0;
@@ -926,7 +1024,7 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
       fprintf(stderr, "ipc rank %d: attempt %d: re-placing%s%s\n", cm->rank, attempt, stale[0] ? " send" : "",
               stale[1] ? " recv" : "");
     if (attempt == EMAC_IPC_ATTEMPTS - 1) return EMAC_ERR_TRANSPORT;
-    for (r = 0; r < h->nmapped; r++) ipc_unmap(cm, h->mapped[r]);
+    for (r = 0; r < h->nmapped; r++) ipc_unmap(h->mapped[r]);
     h->nmapped = 0;
     if (stale[0]) rc = ipc_remirror(h, 0);
     if (!rc && stale[1] && h->dsend[0] != h->drecv[0]) rc = ipc_remirror(h, 1);
@@ -941,28 +1039,58 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
   h->slot = slot;
   cm->slot_used[slot] = 1;
   h->slot_held = 1;
+  cm->err[slot] = 0; /* a failure of the slot's previous handle that nobody waited for */
+  {
+    const char *e = getenv("EXT_MPI_AMD_IPC_RELEASE"); /* diagnosis: 0 leaves the release to the kernel boundary */
+    if (R > 1 && !(e && atoi(e) == 0) && (rc = emac_gpu_event_create_release(&h->ev_release))) return rc;
+  }
   h->epoch[0] = cm->slot_epoch[slot][0];
   h->epoch[1] = cm->slot_epoch[slot][1];
   if (empty) return 0;
-  /* this rank's owner chunks: leaves from the peers' send buffers in the plan's fold order,
-     results into every rank's receive buffer (the fused reduce_copyout push) */
+  /* this rank's owner chunks (reduce_copyin): leaves from the peers' send buffers in the plan's
+     fold order, the result into this rank's own receive buffer. Then (reduce_copyout) every
+     other owner's result is PULLED from that owner's receive buffer into this rank's: a receive
+     buffer is only ever written by its own rank. A peer's stores into it through the peer's
+     mapping did not invalidate copies of its lines in the owner's L2s (measured: stale -1s read
+     by the owner's next kernel after filling the buffer, 8 processes on one MI355X), whereas
+     every remote access of the pull is a system-coherent load. */
   c = h->me_pos;
-  b = (emac_bucket *)calloc((size_t)h->plan.npieces, sizeof(emac_bucket));
+  b = (emac_bucket *)calloc((size_t)h->plan.npieces * (size_t)R, sizeof(emac_bucket));
   if (!b) return EMAC_ERR_MALLOC;
   for (pc = 0; pc < h->plan.npieces; pc++) {
     long off = h->plan.chunk_off[(size_t)pc * R + c], len = h->plan.chunk_len[(size_t)pc * R + c];
     emac_bucket *bk = &b[nb];
     if (len <= 0) continue;
     for (t = 0; t < R; t++) bk->src[t] = psend[h->plan.leaf_rank[c][t]];
-    /* fan-out order rotated by rank (next peer first, own buffer last), so that at any moment
-       the ranks' stores head for different GPUs' links rather than all for rank 0's */
-    for (r = 0; r < R; r++) bk->dst[r] = precv[(cm->rank + 1 + r) % R];
-    bk->ndst = R;
+    bk->dst[0] = precv[cm->rank];
+    bk->ndst = 1;
     place_bucket(bk, R, off, len, h->plan.tsize);
     nb++;
   }
   h->nsrc = R;
-  h->fan = R > 1 ? 2 : 0; /* peer-mapped fan-out: system-coherent launch */
+  h->fan = R > 1 ? 2 : 0; /* peer-mapped: system-coherent launch */
+  if (R > 1) {
+    /* the pull, owners in the order after this rank (next owner first), so that at any moment
+       the ranks' loads head for different GPUs' links */
+    emac_bucket *pb = b + nb;
+    int np = 0, k;
+    for (pc = 0; pc < h->plan.npieces; pc++)
+      for (k = 1; k < R; k++) {
+        const int q = (cm->rank + k) % R, cq = h->plan.rank_pos[q];
+        long off = h->plan.chunk_off[(size_t)pc * R + cq], len = h->plan.chunk_len[(size_t)pc * R + cq];
+        if (len <= 0) continue;
+        pb[np].src[0] = precv[q];
+        pb[np].dst[0] = precv[cm->rank];
+        pb[np].ndst = 1;
+        place_bucket(&pb[np], 1, off, len, h->plan.tsize);
+        np++;
+      }
+    if ((rc = upload_launch_as(h, &h->pull, pb, np, 1, 0))) {
+      free(b);
+      return rc;
+    }
+  }
+
   {
     /* small messages: barrier, fold and barrier in one launch (EXT_MPI_AMD_IPC_FUSED_MAX bytes
        per rank, default 1 MiB; 0 disables) */
@@ -973,6 +1101,10 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
   if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
     fprintf(stderr, "ipc rank %d: own send %p recv %p bytes %zu, %d buckets, slot %d, %d attempt(s)\n", cm->rank,
             h->dsend[0], h->drecv[0], h->bytes, nb, slot, attempt + 1);
+  if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
+    for (t = 0; t < nb; t++)
+      fprintf(stderr, "ipc rank %d: bucket %d: src0 %p dst0 %p head %ld nvec %ld tail %ld scalar %d count %ld\n", cm->rank,
+              t, b[t].src[0], b[t].dst[0], b[t].head, b[t].nvec, b[t].tail, b[t].scalar, b[t].count);
   rc = upload_buckets(h, b, nb);
   free(b);
   return rc;
@@ -1159,26 +1291,39 @@ static emac_handle *get(int handle) {
   return handles[handle];
 }
 
-/* IPC form: node barrier `phase` (0 before the fold: every rank's send buffer is ready and its
-   receive buffer free; 1 after it: every fan-out store has landed) on the handle's stream */
-static int ipc_barrier(emac_handle *h, int phase) {
-  emac_comm *cm = &comms[h->comm];
-  return emac_gpu_node_barrier(cm->sync, (void *const *)cm->d_peer_sync, h->slot, phase, ++h->epoch[phase], cm->size,
-                               cm->rank, cm->xcc_mask, cm->err, cm->timeout_ticks, h->stream);
+static unsigned *ipc_go(const emac_handle *h) {
+  return (unsigned *)((char *)comms[h->comm].sync + offsetof(emac_sync, go)) + h->slot;
 }
 
-/* barrier errors are reported through the communicator's pinned word (timeout: 1, XCC coverage: 2) */
+/* IPC form: node barrier `phase` (0 before the fold: every rank's send buffer is ready and its
+   receive buffer free; 1 after it: every fan-out store has landed) on the handle's stream. The
+   Start is named by its phase-1 epoch (`tag`, ipc_sync.hpp). Phase 0 is preceded by a
+   system-scope release of everything enqueued before it, done by the command processor on every
+   XCD: the peers' loads of this rank's buffers do not depend on where its writers ran. */
+static int ipc_barrier(emac_handle *h, int phase) {
+  emac_comm *cm = &comms[h->comm];
+  int rc;
+  unsigned long epoch, tag;
+  if (phase == 0 && h->ev_release && (rc = emac_gpu_event_record(h->ev_release, h->stream))) return rc;
+  epoch = ++h->epoch[phase];
+  tag = phase ? epoch : h->epoch[1] + 1;
+  return emac_gpu_node_barrier(cm->sync, (void *const *)cm->d_peer_sync, h->slot, phase, epoch, tag, cm->size, cm->rank,
+                               cm->err + h->slot, cm->timeout_ticks, h->stream);
+}
+
+/* barrier errors are reported through the slot's pinned word (ipc_sync.hpp), read and cleared
+   when the Start is waited for: the next Start on the handle synchronises normally */
 static int ipc_status(const emac_handle *h) {
+  volatile int *w;
   int e;
-  if (h->kind != KIND_IPC) return 0;
-  e = *(volatile int *)comms[h->comm].err;
+  if (h->kind != KIND_IPC || !h->slot_held) return 0;
+  w = (volatile int *)comms[h->comm].err + h->slot;
+  e = *w;
   if (!e) return 0;
-  if (!comms[h->comm].err_reported) {
-    comms[h->comm].err_reported = 1;
-    fprintf(stderr, "ext_mpi_amd: rank %d: node barrier failed:%s%s\n", comms[h->comm].rank,
-            (e & 1) ? " a peer did not arrive within EXT_MPI_AMD_BARRIER_TIMEOUT" : "",
-            (e & 2) ? " the barrier launch missed an XCD" : "");
-  }
+  *w = 0;
+  fprintf(stderr, "ext_mpi_amd: rank %d: node barrier failed:%s%s\n", comms[h->comm].rank,
+          (e & EMAC_SYNC_ERR_TIMEOUT) ? " a peer did not arrive within EXT_MPI_AMD_BARRIER_TIMEOUT" : "",
+          (e & EMAC_SYNC_ERR_ABORTED) ? " a peer gave up on this Allreduce" : "");
   return EMAC_ERR_TRANSPORT;
 }
 
@@ -1234,10 +1379,15 @@ int ext_mpi_amd_start_legs(int handle, int legs) {
   if ((legs & EXT_MPI_AMD_LEG_STAGE_IN) && (rc = stage_in(h))) return rc;
   if (h->kind == KIND_IPC && h->fused && (legs & core) == core) {
     emac_comm *cm = &comms[h->comm];
-    const unsigned long e0 = ++h->epoch[0], e1 = ++h->epoch[1];
+    unsigned long e0, e1;
+    if (h->ev_release && (rc = emac_gpu_event_record(h->ev_release, h->stream))) return rc; /* as ipc_barrier(h, 0) */
+    e0 = ++h->epoch[0];
+    e1 = ++h->epoch[1];
     if ((rc = emac_gpu_fold_fused(h->plan.dtype, h->plan.op, h->nsrc, h->unroll, &h->plan.codes, h->d_buckets, h->nb, h->ntiles,
-                                  h->tiles_per_bucket, h->all_full, h->d_edges, h->nedges, cm->sync,
-                                  (void *const *)cm->d_peer_sync, h->slot, cm->size, cm->rank, cm->xcc_mask, cm->err,
+                                  h->tiles_per_bucket, h->all_full, h->d_edges, h->nedges, h->pull.d_buckets, h->pull.nb,
+                                  h->pull.ntiles, h->pull.tiles_per_bucket, h->pull.all_full, h->pull.d_edges,
+                                  h->pull.nedges, cm->sync,
+                                  (void *const *)cm->d_peer_sync, h->slot, cm->size, cm->rank, cm->err + h->slot,
                                   cm->timeout_ticks, e0, e1, h->stream)))
       return rc;
     if ((legs & EXT_MPI_AMD_LEG_STAGE_OUT) && (rc = stage_out(h))) return rc;
@@ -1248,13 +1398,23 @@ int ext_mpi_amd_start_legs(int handle, int legs) {
       (rc = ipc_barrier(h, 0)))
     return rc;
   if ((legs & EXT_MPI_AMD_LEG_REDUCE_SCATTER) && multi && (rc = run_leg(h, EMAC_LEG_RS))) return rc;
-  if ((legs & EXT_MPI_AMD_LEG_FOLD) &&
+  if ((legs & EXT_MPI_AMD_LEG_FOLD) && h->fan == 2 &&
+      (rc = emac_gpu_fold_remote(h->plan.dtype, h->plan.op, h->nsrc, h->unroll, &h->plan.codes, h->d_buckets, h->nb,
+                                 h->ntiles, h->tiles_per_bucket, h->all_full, h->d_edges, h->nedges, ipc_go(h), h->stream)))
+    return rc;
+  if ((legs & EXT_MPI_AMD_LEG_FOLD) && h->fan != 2 &&
       (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, h->fan, h->unroll, &h->plan.codes, h->d_buckets, h->nb, h->ntiles,
                           h->tiles_per_bucket, h->all_full, h->d_edges, h->nedges, h->stream)))
     return rc;
   if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && multi && (rc = run_leg(h, EMAC_LEG_AG))) return rc;
-  if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && h->kind == KIND_IPC && h->plan.nranks > 1 && (rc = ipc_barrier(h, 1)))
-    return rc;
+  if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && h->kind == KIND_IPC && h->plan.nranks > 1) {
+    static const emac_codes copy = {{1}, {1}, 1, 1}; /* one leaf: a copy */
+    if ((rc = ipc_barrier(h, 1))) return rc;
+    if ((rc = emac_gpu_fold_remote(h->plan.dtype, h->plan.op, 1, h->pull.unroll, &copy, h->pull.d_buckets, h->pull.nb,
+                                   h->pull.ntiles, h->pull.tiles_per_bucket, h->pull.all_full, h->pull.d_edges,
+                                   h->pull.nedges, ipc_go(h), h->stream)))
+      return rc;
+  }
   if ((legs & EXT_MPI_AMD_LEG_STAGE_OUT) && (rc = stage_out(h))) return rc;
   h->started = 1;
   return 0;

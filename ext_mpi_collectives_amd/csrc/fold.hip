@@ -96,15 +96,7 @@ int emac_gpu_pick_unroll(int op, int nsrc, int tree, int fan, long total_vectors
   return total_vectors >= 2048L * EMAC_BLOCK * 2 ? sched(2, 1) : sched(1, 1);
 }
 
-int emac_gpu_fold(int dtype, int op, int nsrc, int fan, int unroll, const emac_codes *codes,
-                  const emac_bucket *d_buckets, int nb, long ntiles, long tiles_per_bucket, int all_full,
-                  const emac_edge *d_edges, int nedges, void *stream) {
-  const bool tree = codes->nlev > 1;  /* fan: 0 one destination, 1 node fan-out, 2 peer-mapped fan-out */
-  const emac::Launch L = {codes, d_buckets, nb, ntiles, tiles_per_bucket, all_full, d_edges, nedges,
-                          static_cast<hipStream_t>(stream)};
-  if (op < EMAC_SUM || op > EMAC_MAX) return EMAC_ERR_UNSUPPORTED;
-  if (nb <= 0 || (ntiles <= 0 && nedges <= 0)) return 0;
-  if (codes->nlev > emac::kMaxLevels) return EMAC_ERR_UNSUPPORTED;
+static int fold_dispatch(int dtype, int op, int nsrc, int fan, int unroll, const emac::Launch &L, bool tree) {
   switch (dtype) {
   case EMAC_FLOAT:
     return op == EMAC_SUM ? emac_fold_launch_f32(nsrc, tree, fan, unroll, &L) : emac_fold_launch_f32_mm(op, nsrc, tree, fan, unroll, &L);
@@ -118,27 +110,58 @@ int emac_gpu_fold(int dtype, int op, int nsrc, int fan, int unroll, const emac_c
   return EMAC_ERR_ARG;
 }
 
-int emac_gpu_fold_fused(int dtype, int op, int nsrc, int unroll, const emac_codes *codes, const emac_bucket *d_buckets, int nb,
-                        long ntiles, long tiles_per_bucket, int all_full, const emac_edge *d_edges, int nedges,
-                        void *self_sync, void *const *d_peers, int slot, int nranks, int me, unsigned xcc_expect,
-                        int *err, long timeout_ticks, unsigned long epoch0, unsigned long epoch1, void *stream) {
+int emac_gpu_fold(int dtype, int op, int nsrc, int fan, int unroll, const emac_codes *codes,
+                  const emac_bucket *d_buckets, int nb, long ntiles, long tiles_per_bucket, int all_full,
+                  const emac_edge *d_edges, int nedges, void *stream) {
+  const bool tree = codes->nlev > 1;  /* fan: 0 one destination, 1 node fan-out */
+  const emac::Launch L = {codes, d_buckets, nb, ntiles, tiles_per_bucket, all_full, d_edges, nedges,
+                          static_cast<hipStream_t>(stream), nullptr};
+  if (op < EMAC_SUM || op > EMAC_MAX) return EMAC_ERR_UNSUPPORTED;
+  if (fan != 0 && fan != 1) return EMAC_ERR_ARG; /* peer-mapped launches: emac_gpu_fold_remote */
+  if (nb <= 0 || (ntiles <= 0 && nedges <= 0)) return 0;
+  if (codes->nlev > emac::kMaxLevels) return EMAC_ERR_UNSUPPORTED;
+  return fold_dispatch(dtype, op, nsrc, fan, unroll, L, tree);
+}
+
+int emac_gpu_fold_remote(int dtype, int op, int nsrc, int unroll, const emac_codes *codes, const emac_bucket *d_buckets,
+                         int nb, long ntiles, long tiles_per_bucket, int all_full, const emac_edge *d_edges, int nedges,
+                         const unsigned *go, void *stream) {
   const bool tree = codes->nlev > 1;
   const emac::Launch L = {codes, d_buckets, nb, ntiles, tiles_per_bucket, all_full, d_edges, nedges,
-                          static_cast<hipStream_t>(stream)};
+                          static_cast<hipStream_t>(stream), go};
+  if (op < EMAC_SUM || op > EMAC_MAX) return EMAC_ERR_UNSUPPORTED;
+  if (!go) return EMAC_ERR_ARG;
+  if (nb <= 0 || (ntiles <= 0 && nedges <= 0)) return 0;
+  if (codes->nlev > emac::kMaxLevels) return EMAC_ERR_UNSUPPORTED;
+  return fold_dispatch(dtype, op, nsrc, 2, unroll, L, tree);
+}
+
+int emac_gpu_fold_fused(int dtype, int op, int nsrc, int unroll, const emac_codes *codes, const emac_bucket *d_buckets, int nb,
+                        long ntiles, long tiles_per_bucket, int all_full, const emac_edge *d_edges, int nedges,
+                        const emac_bucket *d_pull, int pnb, long pntiles, long ptiles_per_bucket, int pall_full,
+                        const emac_edge *d_pedges, int pnedges, void *self_sync, void *const *d_peers, int slot,
+                        int nranks, int me, int *err, long timeout_ticks, unsigned long epoch0, unsigned long epoch1,
+                        void *stream) {
+  const bool tree = codes->nlev > 1;
+  const emac::Launch L = {codes, d_buckets, nb, ntiles, tiles_per_bucket, all_full, d_edges, nedges,
+                          static_cast<hipStream_t>(stream), nullptr};
   long work = ntiles + nedges;
+  if (pntiles + pnedges > work) work = pntiles + pnedges;
   emac::FusedLaunch F;
+  F.pull = {d_pull, pnb, pntiles, ptiles_per_bucket, pall_full, d_pedges, pnedges};
   F.ns = {static_cast<emac_sync *>(self_sync), reinterpret_cast<emac_sync *const *>(d_peers), slot, nranks, me,
-          xcc_expect, err, timeout_ticks};
+          err, timeout_ticks, epoch1};
   F.epoch0 = epoch0;
   F.epoch1 = epoch1;
-  /* at least EMAC_SYNC_WG workgroups (XCD coverage of the fences), at most EMAC_FUSED_MAX_WG
-     (all resident while others wait; few CUs held from other streams while a peer is late) */
-  F.grid = (int)(work < EMAC_FUSED_MIN_WG ? EMAC_FUSED_MIN_WG : work > EMAC_FUSED_MAX_WG ? EMAC_FUSED_MAX_WG : work);
+  /* at most EMAC_FUSED_MAX_WG workgroups: all resident while others wait, few CUs held from the
+     rank's other streams while a peer is late */
+  F.grid = (int)(work < 1 ? 1 : work > EMAC_FUSED_MAX_WG ? EMAC_FUSED_MAX_WG : work);
   if (codes->nlev > emac::kMaxLevels || nsrc < 2) return EMAC_ERR_UNSUPPORTED;
   if (op < EMAC_SUM || op > EMAC_MAX) return EMAC_ERR_UNSUPPORTED;
   if (nb > 0 && unroll != emac_gpu_pick_unroll(op, nsrc, tree, 2, 0)) return EMAC_ERR_UNSUPPORTED; /* layout's tiles */
-  if (nb <= 0) {
-    F.grid = EMAC_FUSED_MIN_WG;  /* nothing to fold here: the barriers only */
+  if (pnb > 0 && emac_gpu_pick_unroll(op, 1, 0, 2, 0) != emac::sched(2, 1 | emac::kRemote)) return EMAC_ERR_UNSUPPORTED;
+  if (nb <= 0 && pnb <= 0) {
+    F.grid = 1; /* nothing to fold or pull here: the barriers only */
     return emac_fold_fused_launch_f32(nsrc, false, &L, &F);
   }
   switch (dtype) {
@@ -287,7 +310,7 @@ int ext_mpi_amd_gpu_copy_reduce(int dtype, int op, int nsrc, const void *const *
   emac_codes codes;
   emac_bucket *d = nullptr;
   int tsize = emac_type_size(dtype), rc, i;
-  if (tsize < 0 || nsrc < 1 || nsrc > EMAC_MAX_RANKS || ndst < 0 || ndst > EMAC_MAX_RANKS || count < 0)
+  if (tsize < 0 || nsrc < 1 || nsrc > EMAC_MAX_RANKS || ndst < 1 || ndst > EMAC_MAX_RANKS || count < 0)
     return EMAC_ERR_ARG;
   if (!count) return 0;
   memset(&b, 0, sizeof(b));

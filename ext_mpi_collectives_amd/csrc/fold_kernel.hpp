@@ -164,7 +164,8 @@ __device__ __forceinline__ void fold_scalar_element(const emac_bucket *b, long e
 // (every vector of leaf 0, then leaf 1, ...) instead of vector-major; bits 1.. = s_sleep after
 // every 4 loads (0 = back-to-back burst).
 template <typename T, int OP, int N, int U, bool TREE, int D, bool FULL, int ISSUE = 1>
-__device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_base, long nvec, const emac_codes &c) {
+__device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_base, long nvec, const emac_codes &c,
+                                             bool store = true) {
   typedef typename Lane<T>::V V;
   typedef __attribute__((address_space(1))) V GV;
   constexpr bool SRC_MAJOR = ISSUE & 1;
@@ -194,6 +195,7 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
 #pragma unroll
   for (int u = 0; u < U; ++u) r[u] = fold_leaves<OP, T, N, TREE>(x[u], c);
   // destination pointers are only needed now: their descriptor read overlaps the loads
+  if (!store) return;  // peer-mapped launch whose phase-0 barrier failed (wave-uniform)
 #pragma unroll
   for (int d = 0; d < D; ++d) {
     GV *dst = (GV *)b->dst[d] + tile_base;
@@ -217,8 +219,12 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
 template <typename T, int OP, int N, int U, bool TREE, int D, int ISSUE = 1>
 __global__ __launch_bounds__(EMAC_BLOCK) void fold_kernel(const emac_bucket *__restrict__ bk, int nb,
                                                           long ntiles, long tiles_per_bucket, int all_full,
-                                                          emac_codes codes) {
+                                                          emac_codes codes, const unsigned *go) {
   constexpr long TILE = (long)EMAC_BLOCK * U;
+  // peer-mapped launch: the phase-0 barrier's verdict (ipc_sync.hpp); its load is issued ahead of
+  // the leaf loads and only waited for before the first store
+  bool store = true;
+  if constexpr ((ISSUE & kRemote) != 0) store = __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
   for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     // bucket of this tile: arithmetic when every bucket has the same tile count (equal chunks:
     // the common case), else the last bucket whose first tile is <= tile (wave-uniform search;
@@ -245,9 +251,9 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_kernel(const emac_bucket *__r
     // all_full (host-known: every bucket a whole number of tiles) skips the dependent read of
     // nvec before the first load of the tile
     if (all_full || (t + 1) * TILE <= b->nvec)
-      fold_vectors<T, OP, N, U, TREE, D, true, ISSUE>(b, t * TILE, 0, codes);
+      fold_vectors<T, OP, N, U, TREE, D, true, ISSUE>(b, t * TILE, 0, codes, store);
     else
-      fold_vectors<T, OP, N, U, TREE, D, false, ISSUE>(b, t * TILE, b->nvec, codes);
+      fold_vectors<T, OP, N, U, TREE, D, false, ISSUE>(b, t * TILE, b->nvec, codes, store);
   }
 }
 
@@ -255,8 +261,11 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_kernel(const emac_bucket *__r
 template <typename T, int OP, int N, bool TREE, int D, bool REMOTE = false>
 __global__ __launch_bounds__(EMAC_BLOCK) void fold_edge_kernel(const emac_bucket *__restrict__ bk,
                                                                const emac_edge *__restrict__ items,
-                                                               emac_codes codes) {
+                                                               emac_codes codes, const unsigned *go) {
   constexpr long EPV = 16 / sizeof(typename Lane<T>::S);
+  if constexpr (REMOTE) {
+    if (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) return;
+  }
   const emac_edge it = items[blockIdx.x];
   const emac_bucket *b = bk + it.bucket;
   if (it.mode == 1) {
@@ -272,64 +281,109 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_edge_kernel(const emac_bucket
   if constexpr (REMOTE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// The whole peer-mapped Allreduce in ONE launch, for small messages where the two kernel
-// boundaries of barrier -> fold -> barrier cost as much as the fold (each ≈ 1.5-2 us): node
-// barrier phase 0 (ipc_sync.hpp, every workgroup takes part), the tiles and edge items of every
-// bucket grid-strided over the workgroups with system-coherent accesses (fold_vectors REMOTE),
-// node barrier phase 1. The grid never exceeds one workgroup per CU, so every workgroup is
-// resident while any of them waits.
+// A set of buckets of one launch as kernel arguments (the fused kernel runs two: the fold of
+// this rank's owner chunks and the pull of every other owner's result).
+struct Work {
+  const emac_bucket *b;
+  int nb;
+  long ntiles, tpb;
+  int all_full;
+  const emac_edge *edges;
+  int nedges;
+};
+
+// Every tile and edge item of `w`, grid-strided over the launch's workgroups, with
+// system-coherent accesses (fold_vectors REMOTE). N leaves (N = 1: a copy).
 template <typename T, int OP, int N, int U, bool TREE>
-__global__ __launch_bounds__(EMAC_BLOCK) void ipc_fused_kernel(const emac_bucket *__restrict__ bk, int nb, long ntiles,
-                                                               long tiles_per_bucket, int all_full,
-                                                               const emac_edge *__restrict__ items, int nedges,
-                                                               emac_codes codes, NodeSync ns, unsigned long epoch0,
-                                                               unsigned long epoch1) {
+__device__ __forceinline__ void run_remote(const Work &w, const emac_codes &codes) {
   constexpr int ISSUE = 1 | kRemote;
   constexpr long TILE = (long)EMAC_BLOCK * U;
   constexpr long EPV = 16 / sizeof(typename Lane<T>::S);
-  if (threadIdx.x == 0) node_barrier_lane(ns, 0, epoch0);
-  __syncthreads();
-  for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (long tile = blockIdx.x; tile < w.ntiles; tile += gridDim.x) {
     int bi;
     long t;
-    if (tiles_per_bucket > 0) {
-      bi = (int)((unsigned)tile / (unsigned)tiles_per_bucket);
-      t = tile - (long)bi * tiles_per_bucket;
+    if (w.tpb > 0) {
+      bi = (int)((unsigned)tile / (unsigned)w.tpb);
+      t = tile - (long)bi * w.tpb;
     } else {
-      int lo = 0, hi = nb - 1;
+      int lo = 0, hi = w.nb - 1;
       while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
-        if (bk[mid].tile0 <= tile)
+        if (w.b[mid].tile0 <= tile)
           lo = mid;
         else
           hi = mid - 1;
       }
       bi = lo;
-      t = tile - bk[lo].tile0;
+      t = tile - w.b[lo].tile0;
     }
-    const emac_bucket *b = bk + bi;
-    if (all_full || (t + 1) * TILE <= b->nvec)
-      fold_vectors<T, OP, N, U, TREE, N, true, ISSUE>(b, t * TILE, 0, codes);
+    const emac_bucket *b = w.b + bi;
+    if (w.all_full || (t + 1) * TILE <= b->nvec)
+      fold_vectors<T, OP, N, U, TREE, 1, true, ISSUE>(b, t * TILE, 0, codes);
     else
-      fold_vectors<T, OP, N, U, TREE, N, false, ISSUE>(b, t * TILE, b->nvec, codes);
+      fold_vectors<T, OP, N, U, TREE, 1, false, ISSUE>(b, t * TILE, b->nvec, codes);
   }
-  for (int item = blockIdx.x; item < nedges; item += gridDim.x) {
-    const emac_edge it = items[item];
-    const emac_bucket *b = bk + it.bucket;
+  for (int item = blockIdx.x; item < w.nedges; item += gridDim.x) {
+    const emac_edge it = w.edges[item];
+    const emac_bucket *b = w.b + it.bucket;
     if (it.mode == 1) {
       for (long e = it.start + threadIdx.x; e < it.start + it.count; e += EMAC_BLOCK)
-        fold_scalar_element<T, OP, N, TREE, N, true>(b, e, codes);
+        fold_scalar_element<T, OP, N, TREE, 1, true>(b, e, codes);
     } else {
       const long nsc = b->head + b->tail;
       for (long i = threadIdx.x; i < nsc; i += EMAC_BLOCK) {
         const long e = i < b->head ? i : b->head + b->nvec * EPV + (i - b->head);
-        fold_scalar_element<T, OP, N, TREE, N, true>(b, e, codes);
+        fold_scalar_element<T, OP, N, TREE, 1, true>(b, e, codes);
       }
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every fan-out store acknowledged
+}
+
+// The whole peer-mapped Allreduce in ONE launch, for small messages where the kernel boundaries
+// of barrier -> fold -> barrier -> pull cost as much as the work (each ≈ 1.5-2 us).
+//  phase 0 (ipc_sync.hpp): workgroup 0's first wave signals every peer, the first wave of EVERY
+//          workgroup waits for them (a workgroup folds only after it has seen every peer ready);
+//  fold:   this rank's owner chunks, leaves loaded from the peers' send buffers, the result
+//          stored (write-through) into this rank's own receive buffer only;
+//  phase 1: each workgroup drains its stores and counts itself in arrive[slot]; the last one
+//          signals the peers; every workgroup waits for every peer's signal;
+//  pull:   every other owner's result loaded from that owner's receive buffer and stored into
+//          this rank's own. The receive buffer is only ever written by its own rank: lines of it
+//          that this rank's L2s hold stay coherent with what the application reads next
+//          (measured: a peer's write into them through its mapping left stale lines in the
+//          reader's L2, 8 processes on one MI355X). The next Start's phase 0 keeps every owner
+//          from overwriting its result before the peers have pulled it.
+// The grid never exceeds one workgroup per CU, so every workgroup is resident while any waits.
+template <typename T, int OP, int N, int U, bool TREE>
+__global__ __launch_bounds__(EMAC_BLOCK) void ipc_fused_kernel(Work fold, Work pull, emac_codes codes, NodeSync ns,
+                                                               unsigned long epoch0, unsigned long epoch1) {
+  __shared__ int verdict;
+  if (threadIdx.x < 64) {
+    const bool ok = wave_phase0(ns, epoch0, blockIdx.x == 0);
+    if (threadIdx.x == 0) verdict = ok;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) node_barrier_lane(ns, 1, epoch1);
+  const bool ok = verdict != 0;
+  if (ok) run_remote<T, OP, N, U, TREE>(fold, codes);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of this wave acknowledged
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    unsigned long arrived = 0;
+    if (threadIdx.x == 0)
+      arrived = __hip_atomic_fetch_add(&ns.self->arrive[ns.slot], 1ul, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    arrived = __shfl(arrived, 0);
+    if (arrived == gridDim.x - 1) {  // the last workgroup: every owner chunk of this rank has landed
+      // the next launch on this slot is stream-ordered behind this one
+      if (threadIdx.x == 0) __hip_atomic_store(&ns.self->arrive[ns.slot], 0ul, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      wave_signal(ns, 1, epoch1);
+    }
+    const bool in_time = wave_wait(ns, 1, epoch1);
+    const bool gave_up = peer_gave_up(ns);
+    wave_report(ns, (in_time ? 0 : EMAC_SYNC_ERR_TIMEOUT) | (gave_up ? EMAC_SYNC_ERR_ABORTED : 0));
+    if (threadIdx.x == 0) verdict = ok && in_time && !gave_up;
+  }
+  __syncthreads();
+  if (verdict) run_remote<T, OP, 1, 2, false>(pull, codes);
 }
 
 // ---- instantiation policy (keep in sync with emac_gpu_pick_unroll in fold.hip) ----
@@ -357,6 +411,7 @@ struct Launch {
   const emac_edge *edges;
   int nedges;
   hipStream_t s;
+  const unsigned *go;  // peer-mapped launches: the phase-0 verdict word (emac_sync.go[slot])
 };
 
 template <typename T, int OP, int N, int U, bool TREE, int D, int ISSUE = 1>
@@ -364,10 +419,10 @@ int launch_one(const Launch &L) {
   const long grid = L.ntiles < 8192 ? L.ntiles : 8192;
   if (grid > 0)
     hipLaunchKernelGGL((fold_kernel<T, OP, N, U, TREE, D, ISSUE>), dim3((unsigned)grid), dim3(EMAC_BLOCK), 0, L.s, L.b,
-                       L.nb, L.ntiles, L.tpb, L.all_full, *L.c);
+                       L.nb, L.ntiles, L.tpb, L.all_full, *L.c, L.go);
   if (L.nedges > 0)
     hipLaunchKernelGGL((fold_edge_kernel<T, OP, N, TREE, D, (ISSUE & kRemote) != 0>), dim3((unsigned)L.nedges),
-                       dim3(EMAC_BLOCK), 0, L.s, L.b, L.edges, *L.c);
+                       dim3(EMAC_BLOCK), 0, L.s, L.b, L.edges, *L.c, L.go);
   return hipGetLastError() == hipSuccess ? 0 : EMAC_ERR_DEVICE;
 }
 
@@ -416,13 +471,14 @@ int launch_nf(bool tree, int unroll, const Launch &L) {
   }
 }
 
-// fan: 0 fan-out 1 (comm form), 1 fan-out N (node form), 2 fan-out N peer-mapped (IPC form)
+// fan: 0 fan-out 1 (comm form), 1 fan-out N (node form), 2 peer-mapped (IPC form: leaves or the pulled
+// result in other GPUs' memory, system-coherent accesses, one destination in this rank's memory)
 template <typename T, int OP, int N>
 int launch_n(bool tree, int fan, int unroll, const Launch &L) {
   if constexpr (N == 1) {
     return fan == 2 ? launch_nf<T, OP, 1, false, true>(false, unroll, L) : launch_nf<T, OP, 1, false>(false, unroll, L);
   } else {
-    return fan == 2 ? launch_nf<T, OP, N, true, true>(tree, unroll, L)
+    return fan == 2 ? launch_nf<T, OP, N, false, true>(tree, unroll, L)
                     : fan ? launch_nf<T, OP, N, true>(tree, unroll, L) : launch_nf<T, OP, N, false>(tree, unroll, L);
   }
 }
@@ -431,23 +487,24 @@ struct FusedLaunch {
   NodeSync ns;
   unsigned long epoch0, epoch1;
   int grid;
+  Work pull;  // every other owner's result into this rank's receive buffer (N = 1, U = 2)
 };
 
 // fused peer-mapped launch: the IPC form's schedule of the shape (pick_unroll fan == 2)
 template <typename T, int OP, int N>
 int launch_fused_n(bool tree, const Launch &L, const FusedLaunch &F) {
   constexpr int UR = N > 8 ? 1 : 2;
+  const Work fold = {L.b, L.nb, L.ntiles, L.tpb, L.all_full, L.edges, L.nedges};
   if constexpr (can_tree(N)) {
     if (tree) {
-      hipLaunchKernelGGL((ipc_fused_kernel<T, OP, N, tree_unroll(N), true>), dim3((unsigned)F.grid),
-                         dim3(EMAC_BLOCK), 0, L.s, L.b, L.nb, L.ntiles, L.tpb, L.all_full, L.edges, L.nedges, *L.c, F.ns,
-                         F.epoch0, F.epoch1);
+      hipLaunchKernelGGL((ipc_fused_kernel<T, OP, N, tree_unroll(N), true>), dim3((unsigned)F.grid), dim3(EMAC_BLOCK), 0,
+                         L.s, fold, F.pull, *L.c, F.ns, F.epoch0, F.epoch1);
       return hipGetLastError() == hipSuccess ? 0 : EMAC_ERR_DEVICE;
     }
   }
   if (tree) return EMAC_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL((ipc_fused_kernel<T, OP, N, UR, false>), dim3((unsigned)F.grid), dim3(EMAC_BLOCK), 0, L.s,
-                     L.b, L.nb, L.ntiles, L.tpb, L.all_full, L.edges, L.nedges, *L.c, F.ns, F.epoch0, F.epoch1);
+  hipLaunchKernelGGL((ipc_fused_kernel<T, OP, N, UR, false>), dim3((unsigned)F.grid), dim3(EMAC_BLOCK), 0, L.s, fold,
+                     F.pull, *L.c, F.ns, F.epoch0, F.epoch1);
   return hipGetLastError() == hipSuccess ? 0 : EMAC_ERR_DEVICE;
 }
 

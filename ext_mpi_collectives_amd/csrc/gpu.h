@@ -68,16 +68,23 @@ int emac_gpu_stream_wait(void *stream, void *ev); /* stream waits for ev */
 /* ---- peer-mapped (IPC) form, ipc.hip ----
    Per-communicator synchronisation block, in uncached device memory and mapped by every peer:
    flags[slot][phase][q] = last epoch rank q signalled to this rank for that handle slot and
-   barrier phase (0: before the fold, 1: after it); arrive / xcc are this rank's own barrier
-   bookkeeping (workgroup arrivals, XCC coverage by epoch parity; ipc_sync.hpp). */
+   barrier phase (0: before the fold, 1: after it); arrive = workgroups of this rank's running
+   fused launch that finished their fold (the last one signals phase 1); aborted[slot][t & 1] = t
+   when some peer gave up on the Start tagged t (a phase-0 timeout: it skipped its fold, so this
+   rank's result is incomplete); go[slot] = this rank's phase-0 verdict for the fold launch that
+   follows it on the stream (0: a peer did not arrive, store nothing). ipc_sync.hpp. */
 #define EMAC_SYNC_SLOTS 1024
-#define EMAC_SYNC_WG 16 /* barrier workgroups: dealt round-robin over the 8 XCDs (coverage is checked) */
 #define EMAC_IPC_HANDLE_BYTES 64
 typedef struct {
   unsigned long flags[EMAC_SYNC_SLOTS][2][EMAC_MAX_RANKS];
-  unsigned long arrive[EMAC_SYNC_SLOTS][2]; /* workgroups arrived in the running launch */
-  unsigned int xcc[EMAC_SYNC_SLOTS][2][2];
+  unsigned long arrive[EMAC_SYNC_SLOTS];
+  unsigned long aborted[EMAC_SYNC_SLOTS][2];
+  unsigned int go[EMAC_SYNC_SLOTS];
+  unsigned char probe[EMAC_MAX_RANKS][8]; /* set-up only: byte [q][0] flipped by peer q through its mapping */
 } emac_sync;
+/* barrier error bits (the per-slot pinned host word) */
+#define EMAC_SYNC_ERR_TIMEOUT 1 /* a peer did not arrive within the timeout */
+#define EMAC_SYNC_ERR_ABORTED 2 /* a peer gave up on this Start */
 
 int emac_gpu_ipc_export(const void *p, void *handle, long *offset); /* handle of p's allocation + offset */
 int emac_gpu_ipc_open(const void *handle, void **base);
@@ -94,19 +101,24 @@ int emac_gpu_poke(void *const *ptrs, const unsigned char *vals, int n, void *str
 int emac_gpu_peek(const void *const *ptrs, unsigned char *vals, int n, void *stream);
 int emac_gpu_host_alloc_mapped(void **p, size_t bytes); /* pinned, device-visible, zeroed */
 int emac_gpu_host_free(void *p);
-int emac_gpu_xcc_census(unsigned *mask); /* XCCs a wide launch lands on */
 long emac_gpu_wallclock_hz(void);
-int emac_gpu_node_barrier(void *self, void *const *d_peers, int slot, int phase, unsigned long epoch, int nranks,
-                          int me, unsigned xcc_expect, int *err, long timeout_ticks, void *stream);
-/* the whole peer-mapped Allreduce (barrier, fold, barrier) in one launch, small messages.
-   The grid is kept small (as many workgroups as tiles, 16..64): every workgroup spins while a
+/* system-scope release of everything enqueued on `stream` so far, by the command processor on
+   every XCD's L2 (an event recorded with hipEventReleaseToSystem): the peers' loads of this
+   rank's buffers after the next barrier see it wherever its writers ran */
+int emac_gpu_event_create_release(void **ev);
+/* node barrier `phase` of the Start tagged `tag` (its phase-1 epoch) on `stream`: one wave */
+int emac_gpu_node_barrier(void *self, void *const *d_peers, int slot, int phase, unsigned long epoch, unsigned long tag,
+                          int nranks, int me, int *err, long timeout_ticks, void *stream);
+/* the whole peer-mapped Allreduce (barrier, fold, barrier, pull) in one launch, small messages.
+   The grid is kept small (as many workgroups as tiles, at most 64): every workgroup spins while a
    peer is late, and a wide grid would hold that many CUs from the rank's other streams. */
-#define EMAC_FUSED_MIN_WG EMAC_SYNC_WG
 #define EMAC_FUSED_MAX_WG 64
 int emac_gpu_fold_fused(int dtype, int op, int nsrc, int unroll, const emac_codes *codes, const emac_bucket *d_buckets, int nb,
                         long ntiles, long tiles_per_bucket, int all_full, const emac_edge *d_edges, int nedges,
-                        void *self_sync, void *const *d_peers, int slot, int nranks, int me, unsigned xcc_expect,
-                        int *err, long timeout_ticks, unsigned long epoch0, unsigned long epoch1, void *stream);
+                        const emac_bucket *d_pull, int pnb, long pntiles, long ptiles_per_bucket, int pall_full,
+                        const emac_edge *d_pedges, int pnedges, void *self_sync, void *const *d_peers, int slot,
+                        int nranks, int me, int *err, long timeout_ticks, unsigned long epoch0, unsigned long epoch1,
+                        void *stream);
 
 /* Launch schedule: unroll U (16-byte vectors per lane per leaf; a tile covers EMAC_BLOCK * U
    vectors) in the low 4 bits, load-issue schedule above (fold_kernel.hpp). fan: the fan-out
@@ -119,6 +131,11 @@ int emac_gpu_pick_unroll(int op, int nsrc, int tree, int fan, long total_vectors
 int emac_gpu_fold(int dtype, int op, int nsrc, int fan, int unroll, const emac_codes *codes,
                   const emac_bucket *d_buckets, int nb, long ntiles, long tiles_per_bucket, int all_full,
                   const emac_edge *d_edges, int nedges, void *stream);
+/* the same for a peer-mapped launch (fan 2): `go` is the device word the phase-0 barrier before
+   it wrote (emac_sync.go[slot]); a workgroup that reads 0 stores nothing */
+int emac_gpu_fold_remote(int dtype, int op, int nsrc, int unroll, const emac_codes *codes, const emac_bucket *d_buckets,
+                         int nb, long ntiles, long tiles_per_bucket, int all_full, const emac_edge *d_edges, int nedges,
+                         const unsigned *go, void *stream);
 
 /* layout.c: alignment split of a bucket whose pointers sit at its first element, and the
    launch layout (tiles, uniform tiles per bucket, unroll, edge items; caller frees edges). */

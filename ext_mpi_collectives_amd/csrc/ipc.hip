@@ -12,18 +12,15 @@
 //   node_barrier(in)  -> fold over peer-mapped leaves, fan-out into every peer's recv -> node_barrier(out)
 //
 // Visibility across GPUs: every XCD of a gfx950 has its own L2, and the L2 is neither written
-// back nor invalidated for other agents by plain stores/loads. The fold between the barriers
-// is system-coherent by itself (sc0 sc1 loads and write-through stores), so what remains is
-// the application's side: before the fold a barrier workgroup runs a system-scope release
-// (L2 write-back of its XCD: the send buffer the peers will read), after each barrier a
-// system-scope acquire (L2 invalidate: the receive buffer the peers have written, and lines of
-// the peers' buffers left by earlier kernels of this process), and the barrier is
-// launched wide enough to cover every XCD: the workgroups OR their XCC id into a mask, and the rank's last arriver checks the
-// mask against the census taken at communicator set-up before it signals the peers (a missed
-// XCD is reported as a transport error instead of silently risking stale lines). Flags live in
-// uncached device memory and are written with system-scope atomics: one 8-byte word per
-// (handle slot, phase, peer), holding the last epoch that peer signalled. Every wait is bounded
-// by a wall-clock timeout that sets an error word in pinned host memory and lets the kernel end.
+// back nor invalidated for other agents by plain stores/loads. Nothing here relies on where a
+// workgroup lands: the application's writes to this rank's buffers are released to system scope
+// by the command processor on every XCD before the phase-0 barrier (emac_gpu_event_create_release,
+// recorded by engine.c), the fold between the barriers is system-coherent by itself (sc0 sc1
+// loads, write-through stores drained before the phase-1 signal), and the flags live in
+// uncached device memory, written and polled with system-scope atomics: one 8-byte word per
+// (handle slot, phase, peer), holding the last epoch that peer signalled (ipc_sync.hpp). Every
+// wait is bounded by a wall-clock timeout that sets the slot's error word in pinned host memory
+// and lets the kernel end; a phase-0 timeout also cancels this rank's fold (emac_sync.go).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -49,13 +46,15 @@ inline void clear_error(const char *what) {
     fprintf(stderr, "ext_mpi_amd: %s: cleared %s\n", what, hipGetErrorString(e));
 }
 
-__global__ void xcc_census_kernel(unsigned *mask) {
-  if (threadIdx.x == 0) atomicOr(mask, 1u << emac::xcc_id());
-}
-
-// The stand-alone node barrier (ipc_sync.hpp): EMAC_SYNC_WG one-lane workgroups.
+// The stand-alone node barrier (ipc_sync.hpp): one wave, lane q talks to peer q. Phase 0 also
+// leaves its verdict in go[slot] for the fold launch behind it.
 __global__ __launch_bounds__(64) void node_barrier_kernel(emac::NodeSync ns, int phase, unsigned long epoch) {
-  if (threadIdx.x == 0) emac::node_barrier_lane(ns, phase, epoch);
+  if (phase == 0) {
+    const bool ok = emac::wave_phase0(ns, epoch, true);
+    if (threadIdx.x == 0) __hip_atomic_store(&ns.self->go[ns.slot], ok ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+    emac::wave_phase1(ns, epoch);
+  }
 }
 
 // Byte probes of the IPC set-up (engine.c ipc_exchange): one lane per byte. Stores are
@@ -208,19 +207,11 @@ int emac_gpu_host_alloc_mapped(void **p, size_t bytes) {
 
 int emac_gpu_host_free(void *p) { return p ? ok(hipHostFree(p)) : 0; }
 
-int emac_gpu_xcc_census(unsigned *mask) {
-  unsigned *d = nullptr;
-  int rc;
-  *mask = 0;
-  if (hipMalloc(&d, sizeof(unsigned)) != hipSuccess) return EMAC_ERR_MALLOC;
-  rc = ok(hipMemset(d, 0, sizeof(unsigned)));
-  if (!rc) {
-    hipLaunchKernelGGL(xcc_census_kernel, dim3(4096), dim3(64), 0, 0, d);
-    rc = ok(hipGetLastError());
-  }
-  if (!rc) rc = ok(hipMemcpy(mask, d, sizeof(unsigned), hipMemcpyDeviceToHost));
-  (void)hipFree(d);
-  return rc;
+int emac_gpu_event_create_release(void **ev) {
+  hipEvent_t e;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToSystem) != hipSuccess) return EMAC_ERR_DEVICE;
+  *ev = e;
+  return 0;
 }
 
 long emac_gpu_wallclock_hz(void) {
@@ -231,12 +222,11 @@ long emac_gpu_wallclock_hz(void) {
   return (long)khz * 1000L;
 }
 
-int emac_gpu_node_barrier(void *self, void *const *d_peers, int slot, int phase, unsigned long epoch, int nranks,
-                          int me, unsigned xcc_expect, int *err, long timeout_ticks, void *stream) {
+int emac_gpu_node_barrier(void *self, void *const *d_peers, int slot, int phase, unsigned long epoch, unsigned long tag,
+                          int nranks, int me, int *err, long timeout_ticks, void *stream) {
   const emac::NodeSync ns = {static_cast<emac_sync *>(self), reinterpret_cast<emac_sync *const *>(d_peers), slot,
-                             nranks, me, xcc_expect, err, timeout_ticks};
-  hipLaunchKernelGGL(node_barrier_kernel, dim3(EMAC_SYNC_WG), dim3(64), 0, static_cast<hipStream_t>(stream), ns, phase,
-                     epoch);
+                             nranks, me, err, timeout_ticks, tag};
+  hipLaunchKernelGGL(node_barrier_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), ns, phase, epoch);
   return ok(hipGetLastError());
 }
 

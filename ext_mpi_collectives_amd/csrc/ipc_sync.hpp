@@ -1,17 +1,26 @@
-// ipc_sync.hpp -- the node-barrier protocol of the peer-mapped (IPC) form as a device function,
-// shared by the stand-alone barrier launch (ipc.hip) and the fused small-message Allreduce
-// (fold_kernel.hpp ipc_fused_kernel). It replaces the reference's CPU spin barriers on
+// ipc_sync.hpp -- the node-barrier protocol of the peer-mapped (IPC) form as wave-level device
+// functions, shared by the stand-alone barrier launch (ipc.hip) and the fused small-message
+// Allreduce (fold_kernel.hpp ipc_fused_kernel). It replaces the reference's CPU spin barriers on
 // shared-memory flags (src/mpi/ext_mpi_native_exec.c:21-84, OPCODE_NODEBARRIER_ATOMIC_SET/_WAIT
 // :513-528).
 //
-// One lane per workgroup takes part. Every workgroup records its XCC and arrives on this rank's
-// per-(slot, phase) counter; the last arriver resets the counter, checks that the launch covered
-// every XCD of the census taken at communicator set-up and stores the epoch into every peer's
-// flag (system-scope atomic on uncached memory). Every workgroup then waits for every peer's
-// flag and acquires at system scope (its XCD's L2 drops lines the peers have since rewritten).
-// Phase 0 (before the fold) also releases first: the application's stores into this rank's send
-// buffer may sit dirty in any XCD's L2, and the peers read that buffer from memory.
-// Every wait is bounded by a wall-clock timeout that sets the error word and lets the kernel end.
+// Placement-free by construction: nothing here depends on which XCD a workgroup lands on.
+//  * Flags live in uncached device memory (hipDeviceMallocUncached) and are accessed with
+//    system-scope atomics, so no L2 ever holds them.
+//  * The data the barrier orders needs no cache maintenance from the barrier's own workgroups:
+//    the application's writes to this rank's buffers are released to system scope by the command
+//    processor on every XCD's L2 before the phase-0 barrier (an event recorded with
+//    hipEventReleaseToSystem, engine.c), and the fold between the barriers is system-coherent
+//    by itself (sc0 sc1 loads, write-through stores drained before the phase-1 signal;
+//    fold_kernel.hpp kRemote).
+// One wave takes part: lane q signals peer q (stores the epoch into the peer's flag for this rank)
+// and waits for peer q's flag, so a barrier over R ranks is R-1 parallel one-way hops.
+// Every wait is bounded by a wall-clock timeout. A rank that times out in phase 0 skips its fold
+// (nothing stored into a peer that may not have released its receive buffer) and tells every
+// peer so (aborted[slot][tag & 1] = tag, before its phase-1 signal); a rank that then completes
+// phase 1 of the same Start finds the mark and reports the Start as failed too, because its
+// result lacks the chunks the quitter owns. Epochs keep counting on every rank, so the next
+// Start on the slot synchronises normally: a timeout costs that one Start, not the communicator.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -19,60 +28,78 @@
 
 namespace emac {
 
-__device__ __forceinline__ unsigned xcc_id() {
-  unsigned v;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
-  return v;
-}
-
 struct NodeSync {
   emac_sync *self;
   emac_sync *const *peers;
   int slot, nranks, me;
-  unsigned xcc_expect;
-  int *err;
+  int *err;  // this slot's error word (pinned host memory)
   long timeout;
+  unsigned long tag;  // the Start's phase-1 epoch: names the Start in aborted[]
 };
 
-// called by lane 0 of every workgroup of the launch
-__device__ __forceinline__ void node_barrier_lane(const NodeSync &s, int phase, unsigned long epoch) {
-  if (phase == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: L2 write-back
-    // hipcc drops the wait behind buffer_wbl2 when nothing else is outstanding
-    // (MI355X_MICROARCH.md, compiler hazard): the arrival below must follow the write-back
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  const int slot = s.slot;
-  atomicOr(&s.self->xcc[slot][phase][epoch & 1], 1u << xcc_id());
-  // (relaxed: the release above has already drained before this add issues)
-  const unsigned long arrived =
-      __hip_atomic_fetch_add(&s.self->arrive[slot][phase], 1ul, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (arrived == gridDim.x - 1) {  // last workgroup of this rank: every XCD has released
-    // the next launch on this slot and phase is stream-ordered behind this one
-    __hip_atomic_store(&s.self->arrive[slot][phase], 0ul, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned seen =
-        __hip_atomic_load(&s.self->xcc[slot][phase][epoch & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((seen & s.xcc_expect) != s.xcc_expect) __hip_atomic_fetch_or(s.err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&s.self->xcc[slot][phase][(epoch + 1) & 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int q = 0; q < s.nranks; ++q)
-      if (q != s.me)
-        __hip_atomic_store(&s.peers[q]->flags[slot][phase][s.me], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  // every workgroup waits for every peer itself (one hop less than waiting on the last arriver)
-  const long t0 = wall_clock64();
-  for (int q = 0; q < s.nranks; ++q) {
-    if (q == s.me) continue;
-    while (__hip_atomic_load(&s.self->flags[slot][phase][q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-      __builtin_amdgcn_s_sleep(4);
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// lane q < nranks, q != me: store `epoch` into peer q's flag for this rank
+__device__ __forceinline__ void wave_signal(const NodeSync &s, int phase, unsigned long epoch) {
+  const int q = lane_id();
+  if (q < s.nranks && q != s.me)
+    __hip_atomic_store(&s.peers[q]->flags[s.slot][phase][s.me], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// lane q waits for peer q's flag to reach `epoch`; true (on every lane) iff every peer arrived in time
+__device__ __forceinline__ bool wave_wait(const NodeSync &s, int phase, unsigned long epoch) {
+  const int q = lane_id();
+  int late = 0;
+  if (q < s.nranks && q != s.me) {
+    const unsigned long *f = &s.self->flags[s.slot][phase][q];
+    const long t0 = wall_clock64();
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+      __builtin_amdgcn_s_sleep(2);
       if (wall_clock64() - t0 > s.timeout) {
-        __hip_atomic_fetch_or(s.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        q = s.nranks;
+        late = 1;
         break;
       }
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: L2 invalidate
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  return __ballot(late) == 0;
+}
+
+__device__ __forceinline__ void wave_report(const NodeSync &s, int e) {
+  if (e && lane_id() == 0) __hip_atomic_fetch_or(s.err, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// has a peer given up on this Start? (a mark stored before that peer's phase-1 signal)
+__device__ __forceinline__ bool peer_gave_up(const NodeSync &s) {
+  return __hip_atomic_load(&s.self->aborted[s.slot][s.tag & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == s.tag;
+}
+
+// Phase 0 (before the fold) for one wave: signal, wait, and decide whether this rank may fold.
+// On a timeout the Start is marked abandoned in every peer's block; the marks are acknowledged
+// by the peers' memory before the wave goes on (so before this rank's phase-1 signal). A rank
+// that arrives after a peer gave up does not fold either.
+__device__ __forceinline__ bool wave_phase0(const NodeSync &s, unsigned long epoch, bool signal) {
+  if (signal) wave_signal(s, 0, epoch);
+  if (!wave_wait(s, 0, epoch)) {
+    const int q = lane_id();
+    wave_report(s, EMAC_SYNC_ERR_TIMEOUT);
+    if (q < s.nranks && q != s.me)
+      __hip_atomic_store(&s.peers[q]->aborted[s.slot][s.tag & 1], s.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return false;
+  }
+  if (peer_gave_up(s)) {
+    wave_report(s, EMAC_SYNC_ERR_ABORTED);
+    return false;
+  }
+  return true;
+}
+
+// Phase 1 (after every fan-out store of this rank has been acknowledged): signal, wait, and
+// report a timeout or a peer that gave up on this Start (its result lacks the quitter's chunks).
+__device__ __forceinline__ void wave_phase1(const NodeSync &s, unsigned long epoch) {
+  wave_signal(s, 1, epoch);
+  const bool in_time = wave_wait(s, 1, epoch);
+  wave_report(s, (in_time ? 0 : EMAC_SYNC_ERR_TIMEOUT) | (peer_gave_up(s) ? EMAC_SYNC_ERR_ABORTED : 0));
 }
 
 }  // namespace emac

@@ -278,8 +278,9 @@ static int known_answer_test(void *recvbuf, int in_place, int count, int tsize, 
   kat_fill(hs, count, tsize, world_rank, on_dev ? 0 : 73);
   PMPI_Allreduce(hs, ref, count, tsize == 8 ? MPI_LONG : MPI_INT, MPI_SUM, comm);
   if (on_dev) {
-    if ((rc = ext_mpi_amd_gpu_malloc(&dr, bytes))) goto out;
-    if (!in_place && (rc = ext_mpi_amd_gpu_malloc(&ds, bytes))) goto out;
+    /* communicator-owned: released below while slower peers may still map them */
+    if ((rc = ext_mpi_amd_comm_malloc(ext_comm, &dr, bytes))) goto out;
+    if (!in_place && (rc = ext_mpi_amd_comm_malloc(ext_comm, &ds, bytes))) goto out;
     if ((rc = ext_mpi_amd_gpu_memcpy_hd(in_place ? dr : ds, hs, bytes))) goto out;
     rc = ext_mpi_amd_allreduce_init(in_place ? dr : ds, dr, count, itype, EXT_MPI_AMD_SUM, ext_comm, copyin, &h);
   } else {
@@ -298,8 +299,8 @@ static int known_answer_test(void *recvbuf, int in_place, int count, int tsize, 
     }
   }
 out:
-  ext_mpi_amd_gpu_free(ds);
-  ext_mpi_amd_gpu_free(dr);
+  ext_mpi_amd_comm_mfree(ext_comm, ds);
+  ext_mpi_amd_comm_mfree(ext_comm, dr);
   free(hs);
   free(hr);
   free(ref);
@@ -359,7 +360,8 @@ static int bcomm_delete(MPI_Comm comm, int keyval, void *attr, void *extra) {
   (void)extra;
   if (b) {
     for (i = 0; i < BCACHE; i++) bcomm_drop(b, i);
-    ext_mpi_amd_gpu_free(b->scratch);
+    /* the scratch belongs to the engine communicator (freed with it if that went first) */
+    if (b->scratch) ext_mpi_amd_comm_mfree(b->ext_comm, b->scratch);
     free(b);
   }
   return MPI_SUCCESS;
@@ -467,10 +469,11 @@ static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int
     if (b->scratch_bytes < need) {
       for (i = 0; i < BCACHE; i++)
         if (b->cache[i].handle >= 0 && b->cache[i].send == b->scratch) bcomm_drop(b, i);
-      ext_mpi_amd_gpu_free(b->scratch);
+      /* communicator-owned (peers may still map the old scratch): back to its pool, not freed */
+      ext_mpi_amd_comm_mfree(b->ext_comm, b->scratch);
       b->scratch = NULL;
       b->scratch_bytes = 0;
-      if ((rc = ext_mpi_amd_gpu_malloc(&b->scratch, need))) return rc;
+      if ((rc = ext_mpi_amd_comm_malloc(b->ext_comm, &b->scratch, need))) return rc;
       b->scratch_bytes = need;
     }
     s = b->scratch;

@@ -94,6 +94,14 @@ int ext_mpi_amd_comm_init_ipc(int rank, int size, ext_mpi_amd_allgather_fn allga
                               int *comm);
 int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, int dtype, int op, int comm,
                                const char *copyin, int *handle);
+/* Device memory owned by communicator `comm`, for buffers the caller itself hands to
+ * ext_mpi_amd_allreduce_init (the MPI layer's self-test and blocking scratch). On a peer-mapped
+ * communicator it comes from the pool of exported allocations that only the collective
+ * ext_mpi_amd_comm_free returns to the runtime: a buffer released here while a slower peer still
+ * maps it is never freed under that peer (freeing an exported allocation before every importer
+ * has closed it corrupts later allocations). Elsewhere plain device memory. */
+int ext_mpi_amd_comm_malloc(int comm, void **p, unsigned long bytes);
+int ext_mpi_amd_comm_mfree(int comm, void *p);
 
 /* ---- execution (stream-ordered on the handle's own HIP stream) ---- */
 int ext_mpi_amd_start(int handle);

@@ -48,6 +48,8 @@ def cases(R):
                 (emac.FLOAT, 64 << 20, full, False, False, 1)]
     if R == 3:
         out += [(emac.DOUBLE, 99999, "6;2 -3 3", True, False, 2)]
+    if R == 8 and os.environ.get("IPC_BIG8"):  # BASELINE configs[3]: double, 256 MiB per rank, random values
+        out += [(emac.DOUBLE, 32 << 20, full, False, False, 2), (emac.DOUBLE, 32 << 20, "6;1 -2 -2 -2 2 2 2", False, False, 1)]
     return out + fuzz_cases(R, int(os.environ.get("IPC_FUZZ", "0")))
 
 
@@ -69,6 +71,52 @@ def fuzz_cases(R, n):
     return out
 
 
+def timeout_recovery(rank, world):
+    """A late rank costs one Start, not the communicator (ipc_sync.hpp): on a communicator with a
+    0.3 s barrier timeout, rank 1 starts its second Allreduce 1 s late. Every rank must report
+    that Start as failed (ERROR_TRANSPORT: the others time out and skip their folds, rank 1 finds
+    their marks), and the next Start on the same handle must be bit-exact again. Both the fused
+    one-launch path (small message) and barrier -> fold -> barrier (4 MiB per rank)."""
+    saved = os.environ.get("EXT_MPI_AMD_BARRIER_TIMEOUT")
+    os.environ["EXT_MPI_AMD_BARRIER_TIMEOUT"] = "0.3"
+    comm = emac.comm_init_ipc(rank, world, emac.torch_allgather(), int(os.environ.get("IPC_DEVICE", "0")))
+    if saved is None:
+        del os.environ["EXT_MPI_AMD_BARRIER_TIMEOUT"]
+    else:
+        os.environ["EXT_MPI_AMD_BARRIER_TIMEOUT"] = saved
+    ok = True
+    for n in (1000, 1 << 20):
+        x = torch.full((n,), float(rank + 1), device="cuda")
+        y = torch.empty_like(x)
+        h = emac.allreduce_init(x.data_ptr(), y.data_ptr(), n, emac.FLOAT, comm)
+        verdicts = []
+        for it in range(3):
+            dist.barrier()
+            y.fill_(-1.0)
+            torch.cuda.synchronize()
+            if it == 1 and rank == 1:
+                time.sleep(1.0)
+            try:
+                emac.start(h)
+                emac.wait(h)
+                bad = (y != world * (world + 1) / 2).nonzero().flatten()
+                if bad.numel():
+                    print(f"rank {rank}: recovery n={n} it={it}: {bad.numel()} wrong, first {bad[:4].tolist()} "
+                          f"values {y[bad[:4]].tolist()}", file=sys.stderr, flush=True)
+                verdicts.append("wrong" if bad.numel() else "ok")
+            except emac.ExtMpiError as e:
+                verdicts.append("failed" if e.code == emac.ERROR_TRANSPORT else str(e))
+        dist.barrier()
+        emac.done(h)
+        good = verdicts == ["ok", "failed", "ok"]
+        if not good:
+            print(f"rank {rank}: timeout recovery n={n}: {verdicts}", file=sys.stderr, flush=True)
+        ok &= good
+    emac.comm_free(comm)
+    print(f"IPC rank {rank}/{world} timeout recovery: {'ok' if ok else 'MISMATCH'}", flush=True)
+    return ok
+
+
 def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dev = int(os.environ.get("IPC_DEVICE", "0"))
@@ -76,6 +124,12 @@ def main():
     dist.init_process_group("gloo")
     comm = emac.comm_init_ipc(rank, world, emac.torch_allgather(), dev)
     failures = 0
+    if os.environ.get("IPC_RECOVERY_ONLY"):  # diagnosis
+        failures += not timeout_recovery(rank, world)
+        emac.comm_free(comm)
+        dist.barrier()
+        dist.destroy_process_group()
+        sys.exit(1 if failures else 0)
     only = os.environ.get("IPC_CASES")  # diagnosis: comma-separated case indices, in order, repeats allowed
     order = [int(x) for x in only.split(",")] if only else list(range(len(cases(world))))
     for k in order:
@@ -216,6 +270,7 @@ def main():
             emac.done(h)
     failures += not ok
     print(f"IPC rank {rank}/{world} slot recycling (1200 handles): {'ok' if ok else 'MISMATCH'}", flush=True)
+    failures += not timeout_recovery(rank, world)
     emac.comm_free(comm)
     dist.barrier()
     dist.destroy_process_group()

@@ -229,21 +229,47 @@ def test_config3_int_long_4mib_bitexact(oracle, code):
         assert_bitwise(run_node(sends, code, copyin), oracle.allreduce(sends, copyin), f"config 3 {copyin}")
 
 
-def test_large_double_properties():
-    """256 MiB double per rank x 8 ranks (config 4's message size) without the oracle: integer-valued
-    doubles make every order exact, so the result must equal the closed-form sum everywhere."""
+def _assert_ranks_bitwise(got, want, what):
+    """every rank's result against the oracle's (all equal for a correct schedule)"""
+    for r, g in enumerate(got):
+        if not np.array_equal(g.view(np.uint8), want[r].view(np.uint8)):
+            bad = np.flatnonzero(g.view(np.uint8) != want[r].view(np.uint8))
+            raise AssertionError(f"{what}: rank {r}: {bad.size} differing bytes, first at byte {bad[0]}")
+
+
+@pytest.mark.parametrize("copyin", ["6;1 -8 8", "6;1 -2 -2 -2 2 2 2"])
+def test_config4_random_double_256mib_node(oracle, copyin):
+    """BASELINE configs[3]'s message (double MPI_SUM, 256 MiB per rank, 8 ranks) with random
+    non-integer doubles, so every summation order gives different bits: the node form must
+    reproduce the reference's order exactly (0 ulp against the oracle)."""
     count = (256 << 20) // 8
-    R = 8
-    sends = [torch.arange(count, dtype=torch.float64, device="cuda") * (r + 1) + r for r in range(R)]
-    recvs = [torch.empty(count, dtype=torch.float64, device="cuda") for _ in range(R)]
-    h = emac.node_allreduce_init([t.data_ptr() for t in sends], [t.data_ptr() for t in recvs], count, emac.DOUBLE,
-                                 "6;1 -2 -2 -2 2 2 2")
-    emac.start(h)
-    emac.wait(h)
-    emac.done(h)
-    want = torch.arange(count, dtype=torch.float64, device="cuda") * (R * (R + 1) // 2) + R * (R - 1) // 2
-    for r in recvs:
-        assert torch.equal(r, want)
+    sends = xorshift_inputs(8, count, emac.DOUBLE, seed_base=0xC4D00000)
+    want = oracle.allreduce(sends, copyin)
+    got = run_node(sends, emac.DOUBLE, copyin)
+    _assert_ranks_bitwise(got, want, f"config 4 node {copyin}")
+
+
+@pytest.mark.parametrize("copyin", ["6;1 -8 8", "6;1 -2 -2 -2 2 2 2"])
+def test_config4_random_double_256mib_comm_loopback(oracle, copyin):
+    """The same message through the communicator form (staging slots, reduce-scatter and
+    allgather leg programs, the owner's fold; loopback transport on the one GPU)."""
+    count = (256 << 20) // 8
+    sends = xorshift_inputs(8, count, emac.DOUBLE, seed_base=0xC4D10000)
+    want = oracle.allreduce(sends, copyin)
+    got = run_comm_loopback(sends, emac.DOUBLE, copyin)
+    _assert_ranks_bitwise(got, want, f"config 4 comm {copyin}")
+
+
+@pytest.mark.parametrize("nbytes", [8, 512 << 20])
+def test_config5_float_sweep_endpoints(oracle, nbytes):
+    """BASELINE configs[4]'s sweep endpoints (float MPI_SUM, 8 B and 512 MiB per rank, 8 ranks)."""
+    count = nbytes // 4
+    for copyin in ("6;1 -8 8",) if nbytes > 8 else ("6;1 -8 8", "6;-64 -8 8", "6;1 -2 -2 -2 2 2 2"):
+        sends = xorshift_inputs(8, count, emac.FLOAT, seed_base=0xC5E00000 + nbytes)
+        want = oracle.allreduce(sends, copyin)
+        got = run_node(sends, emac.FLOAT, copyin)
+        _assert_ranks_bitwise(got, want, f"config 5 {nbytes} B {copyin}")
+        del sends, want, got
 
 
 def test_comm_single_rank_rccl():
