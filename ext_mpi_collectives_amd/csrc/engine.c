@@ -1041,8 +1041,13 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
   h->slot_held = 1;
   cm->err[slot] = 0; /* a failure of the slot's previous handle that nobody waited for */
   {
-    const char *e = getenv("EXT_MPI_AMD_IPC_RELEASE"); /* diagnosis: 0 leaves the release to the kernel boundary */
-    if (R > 1 && !(e && atoi(e) == 0) && (rc = emac_gpu_event_create_release(&h->ev_release))) return rc;
+    /* EXT_MPI_AMD_IPC_RELEASE=1: an explicit system-scope release (command processor, every XCD)
+       before each phase-0 barrier. Off by default: the packet boundary between the application's
+       producer kernel and the barrier launch already writes back every XCD's L2 (device memory
+       only is ever exported), and the event cost 5 us per Start with 2 processes, 9 us with 4
+       (profiles/r02_ipc_latency_release.json). */
+    const char *e = getenv("EXT_MPI_AMD_IPC_RELEASE");
+    if (R > 1 && e && atoi(e) > 0 && (rc = emac_gpu_event_create_release(&h->ev_release))) return rc;
   }
   h->epoch[0] = cm->slot_epoch[slot][0];
   h->epoch[1] = cm->slot_epoch[slot][1];
