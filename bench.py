@@ -273,38 +273,49 @@ def comm_shape_fold(R, chunk, tdtype, code, steps):
             "gbps_reduced": round(R * nbytes / t / 1e9, 1), "achieved_gbps": round((R + 1) * nbytes / t / 1e9, 1)}
 
 
-def read_probe(steps=20):
-    """Read-dominated ceiling measured with the library's own kernel: 16 leaves of 64 MiB folded
-    into one 64 MiB destination (17 x 64 MiB of HBM traffic, 94 % reads), two rotated sets
-    (2.1 GiB). The fold kernel's achieved rate is reported against this as well as the spec."""
+def _ceiling_lib():
+    """tools/libceiling.so (built by __graft_entry__.build()): measured-ceiling kernels, or None."""
+    path = os.path.join(ROOT, "tools", "libceiling.so")
+    if not os.path.exists(path):
+        return None
+    L = ctypes.CDLL(path)
+    L.ceiling_read_glds.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    L.ceiling_copy_nt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_void_p]
+    return L
+
+
+def measured_ceilings(steps=10):
+    """Best HBM rates measured on this GPU in this run: a read-only LDS-DMA stream
+    (global_load_lds_dwordx4 nt, tools/ceiling.hip; round 1's best read, ~6.99 TB/s) and a
+    nontemporal copy (1 byte written per byte read: the node-form fold's mix), over 4 GiB
+    (past the 256 MiB Infinity Cache). GB/s of algorithmic bytes (read, or read + write)."""
     import torch
-    import ext_mpi_collectives_amd as emac
-    n = (64 * MIB) // 4
-    sets = []
-    stream = torch.cuda.Stream()
-    for st in range(2):
-        srcs = [DevBuf(n * 4) for _ in range(16)]
-        for i, b in enumerate(srcs):
-            b.upload(host_random(n, np.float32, 1000 + 16 * st + i))
-        dst = DevBuf(n * 4)
-        h = emac.fold_init([b.data_ptr() for b in srcs], [dst.data_ptr()], n, emac.FLOAT)
-        emac.set_stream(h, stream.cuda_stream)
-        sets.append((h, srcs + [dst]))
-    for k in range(4):
-        emac.start(sets[k % 2][0])
+    L = _ceiling_lib()
+    if L is None:
+        return {}
+    n = 4 << 30
+    a = torch.empty(n // 4, dtype=torch.float32, device="cuda")
+    a.uniform_(-1, 1)
+    sink = torch.zeros(4, device="cuda")
+    stream = torch.cuda.current_stream()
+    out = {}
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    stream.synchronize()
+    L.ceiling_read_glds(a.data_ptr(), n, 2, sink.data_ptr(), stream.cuda_stream)
     e0.record(stream)
-    for k in range(steps):
-        emac.start(sets[k % 2][0])
+    assert L.ceiling_read_glds(a.data_ptr(), n, steps, sink.data_ptr(), stream.cuda_stream) == 0
     e1.record(stream)
-    stream.synchronize()
-    t = e0.elapsed_time(e1) * 1e-3 / steps
-    for h, bufs in sets:
-        emac.done(h)
-        for b in bufs:
-            b.free()
-    return 17 * n * 4 / t / 1e9
+    torch.cuda.synchronize()
+    out["read_glds_gbps"] = round(steps * n / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+    half = n // 2
+    L.ceiling_copy_nt(a.data_ptr(), a.data_ptr() + half, half, 2, stream.cuda_stream)
+    e0.record(stream)
+    assert L.ceiling_copy_nt(a.data_ptr(), a.data_ptr() + half, half, steps, stream.cuda_stream) == 0
+    e1.record(stream)
+    torch.cuda.synchronize()
+    out["copy_nt_gbps"] = round(steps * 2 * half / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+    del a, sink
+    torch.cuda.empty_cache()
+    return out
 
 
 def stream_copy_peak():
@@ -329,18 +340,42 @@ def stream_copy_peak():
     return gbps
 
 
+def host_l3_bytes():
+    """Total L3 of this host (sum over distinct L3 domains), or None."""
+    base, seen, total = "/sys/devices/system/cpu", set(), 0
+    try:
+        for cpu in os.listdir(base):
+            idx = os.path.join(base, cpu, "cache", "index3")
+            if not cpu.startswith("cpu") or not os.path.isdir(idx):
+                continue
+            shared = open(os.path.join(idx, "shared_cpu_list")).read().strip()
+            if shared in seen:
+                continue
+            seen.add(shared)
+            size = open(os.path.join(idx, "size")).read().strip()
+            total += int(size[:-1]) * (1024 if size.endswith("K") else 1 << 20 if size.endswith("M") else 1)
+    except (OSError, ValueError):
+        return None
+    return total or None
+
+
 def cpu_baseline(R, count, np_dtype, copyin, seconds):
-    """The oracle's threaded CPU restatement of the reference path on a bounded sample."""
+    """The oracle's threaded CPU restatement of the reference path on a bounded sample. Buffer
+    sets rotate every Allreduce so the working set (>= 2x the host's L3, at least 1 GiB) is
+    memory-resident, as the GPU leg's rotated sets are HBM-resident."""
     from oracle import oracle
     rng = np.random.default_rng(0x5EED0000)
-    sends = [(rng.random(count) * 2 - 1).astype(np_dtype) for _ in range(R)]
-    recvs = [np.empty_like(s) for s in sends]
-    iters, t = 1, 0.0
+    set_bytes = 2 * R * count * np.dtype(np_dtype).itemsize
+    l3 = host_l3_bytes()
+    nsets = max(2, math.ceil(max(1 << 30, 2 * (l3 or 0)) / max(1, set_bytes)))
+    base = [(rng.random(count) * 2 - 1).astype(np_dtype) for _ in range(R)]
+    sets = [([b.copy() for b in base], [np.empty_like(b) for b in base]) for _ in range(nsets)]
+    iters, t = nsets, 0.0
     budget_left = seconds
     # tests/benchmark.c:92-157 doubles the iteration count until a run takes >= 2 s; here until
     # >= 8 s (a 10-30 s sample of CPU work in all, bounded by `seconds`)
     while True:
-        t = oracle.cpu_allreduce_threads(sends, recvs, copyin, iters)
+        t = oracle.cpu_allreduce_threads_sets(sets, copyin, iters)
         budget_left -= t
         if t >= 8.0 or budget_left < 2.5 * t:
             break
@@ -348,9 +383,10 @@ def cpu_baseline(R, count, np_dtype, copyin, seconds):
     return {"value": round(iters * R * count * np.dtype(np_dtype).itemsize / t / 1e9, 3), "unit": "GB/s",
             "cores": R, "kind": "port",
             "sample": f"{iters} Allreduce(s) of {R} ranks x {count * np.dtype(np_dtype).itemsize // MIB} MiB "
-                      f"'{copyin}' in {t:.2f} s: R pthreads replaying each rank's SMEMCPY/SREDUCE program "
-                      f"(gcc -O3 restatement of ext_mpi_native_exec.c:207-234) with spin barriers; "
-                      f"host nproc={os.cpu_count()}"}
+                      f"'{copyin}' in {t:.2f} s over {nsets} rotated buffer sets ({nsets * set_bytes // MIB} MiB; "
+                      f"host L3 {l3 // MIB if l3 else '?'} MiB): R pthreads replaying each rank's SMEMCPY/SREDUCE "
+                      f"program (gcc -O3 restatement of ext_mpi_native_exec.c:207-234) with spin barriers, one "
+                      f"thread per rank as the reference runs one process per rank; host nproc={os.cpu_count()}"}
 
 
 def cpu_config0():
@@ -416,10 +452,14 @@ def single_gpu(args):
         extras = {}
         try:
             extras["stream_copy_gbps"] = round(stream_copy_peak(), 1)
-            extras["read_probe_gbps"] = round(read_probe(), 1)
-            out["roofline"]["measured_read_ceiling"] = extras["read_probe_gbps"]
-            out["roofline"]["frac_of_measured_read_ceiling"] = round(achieved / extras["read_probe_gbps"], 4)
-        except RuntimeError as e:
+            ceil = measured_ceilings()
+            extras.update(ceil)
+            if ceil:
+                out["roofline"]["measured_read_ceiling"] = ceil["read_glds_gbps"]
+                out["roofline"]["frac_of_measured_read_ceiling"] = round(achieved / ceil["read_glds_gbps"], 4)
+                out["roofline"]["measured_copy_ceiling"] = ceil["copy_nt_gbps"]
+                out["roofline"]["frac_of_measured_copy_ceiling"] = round(achieved / ceil["copy_nt_gbps"], 4)
+        except (RuntimeError, AssertionError) as e:
             log("ceiling probes failed:", e)
         big = (256 * MIB) // tsize
         r256 = node_run(R, big, tdtype, code, copyin, max(4, args.steps // 5), 2, alloc=args.alloc)
@@ -429,8 +469,8 @@ def single_gpu(args):
             "achieved_gbps": round(2 * R * big * tsize / k256 / 1e9, 1),
             "frac_of_peak": round(2 * R * big * tsize / k256 / 1e9 / HBM_PEAK_GBPS, 4),
             "frac_of_guide_measured_copy": round(2 * R * big * tsize / k256 / 1e9 / HBM_GUIDE_COPY_GBPS, 4),
-            "frac_of_measured_read_ceiling": round(2 * R * big * tsize / k256 / 1e9 / extras["read_probe_gbps"], 4)
-            if "read_probe_gbps" in extras else None,
+            "frac_of_measured_read_ceiling": round(2 * R * big * tsize / k256 / 1e9 / extras["read_glds_gbps"], 4)
+            if "read_glds_gbps" in extras else None,
             "read_gbps": round(R * big * tsize / k256 / 1e9, 1),
             "avg_launch_us": round(k256 * 1e6, 1), "checked": r256["checked"]}
         # latency -> bandwidth crossover of the node form (cf. BASELINE configs[4] on 8 GPUs);
@@ -446,14 +486,28 @@ def single_gpu(args):
                           "gbps_reduced": round(R * cnt * tsize * st / r["wall_s"] / 1e9, 2),
                           "checked": r["checked"]})
         extras["sweep_node_form"] = sweep
-        chains = {}
-        for cp in ("6;1 -2 -2 -2 2 2 2", "6;1 -4 -2 2 4", "6;-64 -8 8"):
-            r = node_run(R, count, tdtype, code, cp, 20, 3, alloc=args.alloc)
-            k = r["event_ms"] * 1e-3 / 20
+        # radix chains (compile-time fold trees) against the linear fold, measured alike and
+        # alternated twice (median of each), so a drifting clock does not favour either
+        chains, runs = {}, {}
+        for rep in range(2):
+            for cp in (copyin, "6;1 -2 -2 -2 2 2 2", "6;1 -4 -2 2 4", "6;1 -2 -4 4 2", "6;-64 -8 8"):
+                r = node_run(R, count, tdtype, code, cp, args.steps, args.warmup, alloc=args.alloc)
+                runs.setdefault(cp, []).append((r["event_ms"] * 1e-3 / args.steps, r["checked"]))
+        lin = min(t for t, _ in runs[copyin])
+        for cp, v in runs.items():
+            k = min(t for t, _ in v)
             chains[cp] = {"gbps_reduced": round(R * S / k / 1e9, 1), "avg_launch_us": round(k * 1e6, 2),
-                          "checked": r["checked"]}
+                          "vs_linear": round(lin / k, 4), "checked": all(c for _, c in v)}
         extras["radix_chains_16MiB"] = chains
         extras["fold_comm_shape"] = comm_shape_fold(R, count // R, tdtype, code, 200)
+        # SURVEY.md 8(d)'s local fold at the north-star size: the owner's fold of the COMM / IPC
+        # forms (R leaves of C = 256 MiB / R -> one destination, read-dominated), where the
+        # ">= 80 % of HBM read bandwidth" target is defined
+        lf = comm_shape_fold(R, big // R, tdtype, code, 40)
+        lf["frac_of_peak"] = round(lf["achieved_gbps"] / HBM_PEAK_GBPS, 4)
+        if "read_glds_gbps" in extras:
+            lf["frac_of_measured_read_ceiling"] = round(lf["achieved_gbps"] / extras["read_glds_gbps"], 4)
+        extras["local_fold_256MiB"] = lf
         hst = node_run(R, count, tdtype, code, copyin, 10, 3, host=True)
         os.environ["EXT_MPI_AMD_HOST_DIRECT"] = "0"  # staged through device mirrors, for comparison
         hst0 = node_run(R, count, tdtype, code, copyin, 10, 3, host=True)
@@ -794,19 +848,25 @@ def multi_gpu(args):
         extras["local_fold_rate_retained"] = r.get("local_fold")
         extras["host_buffers_pcie_inclusive"] = r.get("host_buffers")
         chunk = S / world
-        if primary == "ipc":
-            algo = 2 * world * chunk  # R leaf reads (R-1 over xGMI) + R fan-out writes (R-1 over xGMI)
-            remote = 2 * (world - 1) * chunk
-        else:
-            algo = (world + 1) * chunk  # R leaf reads from staging + 1 write of the owned chunk
-            remote = 0
-        achieved = algo / kf / 1e9
+        # the fold leg of the run's own transport: R leaf reads (R-1 of them over xGMI in the IPC
+        # form, from staging in the RCCL form) + 1 write of the owned chunk
+        algo = (world + 1) * chunk
+        remote = (world - 1) * chunk if primary == "ipc" else 0
         extras.update({
             "fold_us_all_gpus": round(kf * 1e6, 2), "fold_us_rank0_alone": round(r["alone_s"] * 1e6, 2),
+            "fold_algorithmic_bytes": int(algo),
             "per_gpu_fold_rate_retained": round(r["alone_s"] / kf, 3),
             "fold_xgmi_gbps_per_gpu": round(remote / kf / 1e9, 1) if remote else None,
+            "value_per_gpu_gbps": round(S * args.steps / wall / 1e9, 2),
             "end_to_end_algbw_gbps_per_gpu": round(S * args.steps / wall / 1e9, 2),
             "xgmi_bound_us": round(2 * (world - 1) / world * S / (min(world - 1, 7) * 153e9) * 1e6, 1)})
+        # roofline: the LOCAL fold kernel of SURVEY.md 8(d) (R leaves of this run's chunk -> 1
+        # destination, all in this GPU's HBM) timed on every GPU at once inside the N-GPU job: the
+        # HBM-bound kernel. The transport's own fold reads R-1 leaves over xGMI and is priced
+        # against the xGMI links in extras (fold_xgmi_gbps_per_gpu, xgmi_bound_us).
+        lfd = r.get("local_fold") or {}
+        kl = lfd.get("us_all_gpus", kf * 1e6) * 1e-6
+        achieved = algo / kl / 1e9
         # the N > 1 Allreduce is bound by xGMI (each GPU moves 2(N-1)/N S over its links), not by
         # HBM as the N = 1 kernel-only workload (8 node ranks in one HBM) is: its fraction of
         # that bound, and what N = 1 measures instead
@@ -816,7 +876,7 @@ def multi_gpu(args):
         extras["note_vs_n1"] = ("N = 1 is BASELINE configs[1]: 8 node ranks resident in one GPU's HBM, HBM-bound; "
                                 "N > 1 is one rank per GPU, every rank's chunk crossing xGMI (bound: xgmi_bound_us)")
         form = ("peer-mapped (hipIpc over xGMI): barrier kernel, fold of the owned chunk over the peers' send "
-                "buffers with the fan-out stored into every peer's receive buffer, barrier kernel"
+                "buffers into the own receive buffer, barrier kernel, pull of the other owners' chunks"
                 if primary == "ipc" else
                 "reduce-scatter + allgather legs over RCCL/xGMI, fold on the owner GPU")
         out = {
@@ -827,12 +887,14 @@ def multi_gpu(args):
             "vs_baseline": None, "dtype": dname,
             "data": "synthetic: uniform [-1,1) per rank (seeded), device-resident (hipMalloc)",
             "config": {"workload": f"persistent Allreduce {args.dtype} MPI_SUM, {S // MIB} MiB per rank, one rank per "
-                                   f"GPU, EXT_MPI_COPYIN '{copyin}': {form}",
+                                   f"GPU, EXT_MPI_COPYIN '{copyin}': {form}; value = bytes reduced by the whole job "
+                                   f"per second (N x {S // MIB} MiB per step), extras.value_per_gpu_gbps = value / N",
                        "ranks": world, "message_bytes_per_rank": S, "copyin": copyin, "layout": "rank-per-gpu",
                        "transport": primary, "checked_vs_fp64_sum": checked},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None, "kernel": "fold_kernel",
-                         "algorithmic_bytes_per_launch": int(algo), "avg_launch_us": round(kf * 1e6, 2)},
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "kernel": "fold_kernel (local fold: R leaves of the run's chunk -> 1, this GPU's HBM)",
+                         "algorithmic_bytes_per_launch": int(algo), "avg_launch_us": round(kl * 1e6, 2)},
             "extras": extras,
         }
         print(json.dumps(out), flush=True)

@@ -337,14 +337,15 @@ static int upload_launch_as(const emac_handle *h, emac_launch *L, emac_bucket *b
 }
 
 static int upload_launch(const emac_handle *h, emac_launch *L, emac_bucket *b, int nb) {
-  return upload_launch_as(h, L, b, nb, h->nsrc, h->plan.codes.nlev > 1);
+  return upload_launch_as(h, L, b, nb, h->nsrc, emac_tree_kind(&h->plan.codes, h->plan.op) == 1);
 }
 
 static int upload_buckets(emac_handle *h, emac_bucket *b, int nb) {
   emac_edge *edges = NULL;
   int rc;
   /* (fan | EMAC_FAN_HOST: the schedule for buffers across PCIe, emac_gpu_pick_unroll) */
-  if ((rc = emac_layout(b, nb, h->plan.op, h->nsrc, h->plan.codes.nlev > 1, h->fan | (h->host_direct ? EMAC_FAN_HOST : 0),
+  if ((rc = emac_layout(b, nb, h->plan.op, h->nsrc, emac_tree_kind(&h->plan.codes, h->plan.op) == 1,
+                        h->fan | (h->host_direct ? EMAC_FAN_HOST : 0),
                         &edges, &h->nedges, &h->ntiles, &h->tiles_per_bucket, &h->all_full, &h->unroll)))
     return rc;
   h->nb = nb;
@@ -1090,7 +1091,7 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
         place_bucket(&pb[np], 1, off, len, h->plan.tsize);
         np++;
       }
-    if ((rc = upload_launch_as(h, &h->pull, pb, np, 1, 0))) {
+    if ((rc = upload_launch_as(h, &h->pull, pb, np, 1, 0))) { /* a copy: the schedule of nsrc 1 for every op */
       free(b);
       return rc;
     }
@@ -1415,7 +1416,7 @@ int ext_mpi_amd_start_legs(int handle, int legs) {
   if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && h->kind == KIND_IPC && h->plan.nranks > 1) {
     static const emac_codes copy = {{1}, {1}, 1, 1}; /* one leaf: a copy */
     if ((rc = ipc_barrier(h, 1))) return rc;
-    if ((rc = emac_gpu_fold_remote(h->plan.dtype, h->plan.op, 1, h->pull.unroll, &copy, h->pull.d_buckets, h->pull.nb,
+    if ((rc = emac_gpu_fold_remote(h->plan.dtype, EMAC_SUM, 1, h->pull.unroll, &copy, h->pull.d_buckets, h->pull.nb,
                                    h->pull.ntiles, h->pull.tiles_per_bucket, h->pull.all_full, h->pull.d_edges,
                                    h->pull.nedges, ipc_go(h), h->stream)))
       return rc;
@@ -1600,7 +1601,7 @@ int ext_mpi_amd_check_node_layout(int nranks, long count, int dtype, int op, con
   nb = node_buckets(h, 0, count, b);
   if (!h->fan)
     for (i = 0; i < nb; i++) b[i].ndst = 1; /* COMM-like fan-out 1: only the first destination */
-  if ((rc = emac_layout(b, nb, op, h->nsrc, h->plan.codes.nlev > 1, h->fan, &edges, &L.nedges, &L.ntiles,
+  if ((rc = emac_layout(b, nb, op, h->nsrc, emac_tree_kind(&h->plan.codes, op) == 1, h->fan, &edges, &L.nedges, &L.ntiles,
                         &L.tiles_per_bucket, &L.all_full, &L.unroll))) {
     rc = -1;
     goto out;

@@ -26,11 +26,11 @@
 #include "gpu.h"
 
 extern "C" {
-#define EMAC_DECL(n)                                                                       \
-  int emac_fold_launch_##n(int nsrc, bool tree, int fan, int unroll, const emac::Launch *L); \
-  int emac_fold_launch_##n##_mm(int op, int nsrc, bool tree, int fan, int unroll, const emac::Launch *L); \
-  int emac_fold_fused_launch_##n(int nsrc, bool tree, const emac::Launch *L, const emac::FusedLaunch *F); \
-  int emac_fold_fused_launch_##n##_mm(int op, int nsrc, bool tree, const emac::Launch *L, const emac::FusedLaunch *F);
+#define EMAC_DECL(n)                                                                                         \
+  int emac_fold_launch_##n(int nsrc, int ch, int fan, int unroll, const emac::Launch *L);                   \
+  int emac_fold_launch_##n##_mm(int op, int fan, int unroll, const emac::Launch *L);                        \
+  int emac_fold_fused_launch_##n(int nsrc, int ch, const emac::Launch *L, const emac::FusedLaunch *F);       \
+  int emac_fold_fused_launch_##n##_mm(int op, const emac::Launch *L, const emac::FusedLaunch *F);
 EMAC_DECL(f32)
 EMAC_DECL(f64)
 EMAC_DECL(i32)
@@ -59,28 +59,29 @@ inline void clear_error(const char *what) {
 extern "C" {
 
 int emac_gpu_pick_unroll(int op, int nsrc, int tree, int fan, long total_vectors) {
-  // returns U | ISSUE << 4 (fold_kernel.hpp, instantiation policy). Measured on MI355X with the
-  // production template, R = 8 float, node form (tools/ldsbench.hip, profiles/r01_ldsbench_issue_*):
-  // a back-to-back burst of every load of a tile wins at <= 2 MiB and >= 64 MiB per rank;
-  // between them U = 4 with an s_sleep after every 4 loads is 4-8 % faster (16 MiB: 41.9 vs
-  // 45.2-45.4 us); 64 MiB per rank prefers U = 2 (183 vs 194 us), >= 128 MiB U = 4.
+  // returns U | ISSUE << 4 (fold_kernel.hpp, instantiation policy). `tree`: a runtime-code tree
+  // (compile-time radix chains take the linear schedules). Measured on MI355X, R = 8 float:
+  //  * node form (tools/ldsbench.hip, profiles/r01_ldsbench_issue_*): a back-to-back burst of
+  //    every load of a tile wins at <= 2 MiB and >= 64 MiB per rank; between them U = 4 with an
+  //    s_sleep after every 4 loads is 4-8 % faster (16 MiB: 41.9 vs 45.2-45.4 us); 64 MiB per
+  //    rank prefers U = 2 (183 vs 194 us), >= 128 MiB U = 4;
+  //  * one destination (the COMM / IPC owner's local fold, tools/localbench.hip,
+  //    profiles/r02_localbench_*): U = 1 up to 1 MiB per leaf, U = 2 at 2 MiB, U = 4 from 4 MiB
+  //    (8 x 32 MiB -> 1: 48.2 us at U = 4 against 50.2-50.5 at U = 2; U = 8 within 0.5 % of U = 4).
   using emac::sched;
   const int host = fan & EMAC_FAN_HOST;
   fan &= ~EMAC_FAN_HOST;
-  if (op != EMAC_SUM && fan != 2) {  // MIN / MAX: the burst schedule of the shape (fold_kernel.hpp)
-    if (tree && nsrc > 1) return sched(emac::tree_unroll(nsrc), 1);
-    return sched(nsrc > 8 ? 1 : 2, 1);
-  }
+  if (op != EMAC_SUM && nsrc > 1) return sched(1, fan == 2 ? 1 | emac::kRemote : 1); /* runtime-leaf-count kernels */
   if (fan == 2) {  // peer-mapped (IPC) form: one system-coherent schedule per shape
-    if (tree && nsrc > 1) return sched(nsrc <= 4 ? 4 : (nsrc <= 8 ? 2 : 1), 1 | emac::kRemote);
+    if (tree && nsrc > 1) return sched(emac::tree_unroll(nsrc), 1 | emac::kRemote);
     return sched(nsrc > 8 ? 1 : 2, 1 | emac::kRemote);
   }
   if (nsrc == 1) return total_vectors >= 2048L * EMAC_BLOCK * 2 ? sched(2, 1) : sched(1, 1);
   if (tree) {
     // radix-chain trees at U = 2 (5 <= leaves <= 8): the same staggered issue wins in the
     // middle range (16 MiB x 8, '-2 -2 -2': 44.2 vs 47.4 us), bursts at the ends
-    if (nsrc > 4 && nsrc <= 8 && total_vectors >= (192L << 10) && total_vectors < (3L << 20)) return sched(2, 5);
-    return sched(nsrc <= 4 ? 4 : (nsrc <= 8 ? 2 : 1), 1);
+    if (fan && nsrc > 4 && nsrc <= 8 && total_vectors >= (192L << 10) && total_vectors < (3L << 20)) return sched(2, 5);
+    return sched(emac::tree_unroll(nsrc), 1);
   }
   if (nsrc > 8) return sched(1, 1);
   if (fan) {
@@ -93,19 +94,21 @@ int emac_gpu_pick_unroll(int op, int nsrc, int tree, int fan, long total_vectors
     if (total_vectors < (6L << 20)) return sched(2, 1);
     return sched(4, 1);
   }
+  if (nsrc <= 8 && total_vectors >= (256L << 10)) return sched(4, 1); /* >= 4 MiB per leaf */
+  if (nsrc <= 8 && total_vectors >= (128L << 10)) return sched(2, 1);
   return total_vectors >= 2048L * EMAC_BLOCK * 2 ? sched(2, 1) : sched(1, 1);
 }
 
-static int fold_dispatch(int dtype, int op, int nsrc, int fan, int unroll, const emac::Launch &L, bool tree) {
+static int fold_dispatch(int dtype, int op, int nsrc, int fan, int unroll, const emac::Launch &L, int ch) {
   switch (dtype) {
   case EMAC_FLOAT:
-    return op == EMAC_SUM ? emac_fold_launch_f32(nsrc, tree, fan, unroll, &L) : emac_fold_launch_f32_mm(op, nsrc, tree, fan, unroll, &L);
+    return op == EMAC_SUM ? emac_fold_launch_f32(nsrc, ch, fan, unroll, &L) : emac_fold_launch_f32_mm(op, fan, unroll, &L);
   case EMAC_DOUBLE:
-    return op == EMAC_SUM ? emac_fold_launch_f64(nsrc, tree, fan, unroll, &L) : emac_fold_launch_f64_mm(op, nsrc, tree, fan, unroll, &L);
+    return op == EMAC_SUM ? emac_fold_launch_f64(nsrc, ch, fan, unroll, &L) : emac_fold_launch_f64_mm(op, fan, unroll, &L);
   case EMAC_INT:
-    return op == EMAC_SUM ? emac_fold_launch_i32(nsrc, tree, fan, unroll, &L) : emac_fold_launch_i32_mm(op, nsrc, tree, fan, unroll, &L);
+    return op == EMAC_SUM ? emac_fold_launch_i32(nsrc, ch, fan, unroll, &L) : emac_fold_launch_i32_mm(op, fan, unroll, &L);
   case EMAC_LONG:
-    return op == EMAC_SUM ? emac_fold_launch_i64(nsrc, tree, fan, unroll, &L) : emac_fold_launch_i64_mm(op, nsrc, tree, fan, unroll, &L);
+    return op == EMAC_SUM ? emac_fold_launch_i64(nsrc, ch, fan, unroll, &L) : emac_fold_launch_i64_mm(op, fan, unroll, &L);
   }
   return EMAC_ERR_ARG;
 }
@@ -113,27 +116,27 @@ static int fold_dispatch(int dtype, int op, int nsrc, int fan, int unroll, const
 int emac_gpu_fold(int dtype, int op, int nsrc, int fan, int unroll, const emac_codes *codes,
                   const emac_bucket *d_buckets, int nb, long ntiles, long tiles_per_bucket, int all_full,
                   const emac_edge *d_edges, int nedges, void *stream) {
-  const bool tree = codes->nlev > 1;  /* fan: 0 one destination, 1 node fan-out */
+  const int ch = emac_tree_kind(codes, op); /* fan: 0 one destination, 1 node fan-out */
   const emac::Launch L = {codes, d_buckets, nb, ntiles, tiles_per_bucket, all_full, d_edges, nedges,
-                          static_cast<hipStream_t>(stream), nullptr};
+                          static_cast<hipStream_t>(stream), nullptr, nsrc};
   if (op < EMAC_SUM || op > EMAC_MAX) return EMAC_ERR_UNSUPPORTED;
   if (fan != 0 && fan != 1) return EMAC_ERR_ARG; /* peer-mapped launches: emac_gpu_fold_remote */
   if (nb <= 0 || (ntiles <= 0 && nedges <= 0)) return 0;
   if (codes->nlev > emac::kMaxLevels) return EMAC_ERR_UNSUPPORTED;
-  return fold_dispatch(dtype, op, nsrc, fan, unroll, L, tree);
+  return fold_dispatch(dtype, op, nsrc, fan, unroll, L, ch);
 }
 
 int emac_gpu_fold_remote(int dtype, int op, int nsrc, int unroll, const emac_codes *codes, const emac_bucket *d_buckets,
                          int nb, long ntiles, long tiles_per_bucket, int all_full, const emac_edge *d_edges, int nedges,
                          const unsigned *go, void *stream) {
-  const bool tree = codes->nlev > 1;
+  const int ch = emac_tree_kind(codes, op);
   const emac::Launch L = {codes, d_buckets, nb, ntiles, tiles_per_bucket, all_full, d_edges, nedges,
-                          static_cast<hipStream_t>(stream), go};
+                          static_cast<hipStream_t>(stream), go, nsrc};
   if (op < EMAC_SUM || op > EMAC_MAX) return EMAC_ERR_UNSUPPORTED;
   if (!go) return EMAC_ERR_ARG;
   if (nb <= 0 || (ntiles <= 0 && nedges <= 0)) return 0;
   if (codes->nlev > emac::kMaxLevels) return EMAC_ERR_UNSUPPORTED;
-  return fold_dispatch(dtype, op, nsrc, 2, unroll, L, tree);
+  return fold_dispatch(dtype, op, nsrc, 2, unroll, L, ch);
 }
 
 int emac_gpu_fold_fused(int dtype, int op, int nsrc, int unroll, const emac_codes *codes, const emac_bucket *d_buckets, int nb,
@@ -142,9 +145,9 @@ int emac_gpu_fold_fused(int dtype, int op, int nsrc, int unroll, const emac_code
                         const emac_edge *d_pedges, int pnedges, void *self_sync, void *const *d_peers, int slot,
                         int nranks, int me, int *err, long timeout_ticks, unsigned long epoch0, unsigned long epoch1,
                         void *stream) {
-  const bool tree = codes->nlev > 1;
+  const int ch = emac_tree_kind(codes, op);
   const emac::Launch L = {codes, d_buckets, nb, ntiles, tiles_per_bucket, all_full, d_edges, nedges,
-                          static_cast<hipStream_t>(stream), nullptr};
+                          static_cast<hipStream_t>(stream), nullptr, nsrc};
   long work = ntiles + nedges;
   if (pntiles + pnedges > work) work = pntiles + pnedges;
   emac::FusedLaunch F;
@@ -158,21 +161,21 @@ int emac_gpu_fold_fused(int dtype, int op, int nsrc, int unroll, const emac_code
   F.grid = (int)(work < 1 ? 1 : work > EMAC_FUSED_MAX_WG ? EMAC_FUSED_MAX_WG : work);
   if (codes->nlev > emac::kMaxLevels || nsrc < 2) return EMAC_ERR_UNSUPPORTED;
   if (op < EMAC_SUM || op > EMAC_MAX) return EMAC_ERR_UNSUPPORTED;
-  if (nb > 0 && unroll != emac_gpu_pick_unroll(op, nsrc, tree, 2, 0)) return EMAC_ERR_UNSUPPORTED; /* layout's tiles */
-  if (pnb > 0 && emac_gpu_pick_unroll(op, 1, 0, 2, 0) != emac::sched(2, 1 | emac::kRemote)) return EMAC_ERR_UNSUPPORTED;
+  if (nb > 0 && unroll != emac_gpu_pick_unroll(op, nsrc, ch == 1, 2, 0)) return EMAC_ERR_UNSUPPORTED; /* layout's tiles */
+  if (pnb > 0 && emac_gpu_pick_unroll(EMAC_SUM, 1, 0, 2, 0) != emac::sched(2, 1 | emac::kRemote)) return EMAC_ERR_UNSUPPORTED;
   if (nb <= 0 && pnb <= 0) {
     F.grid = 1; /* nothing to fold or pull here: the barriers only */
-    return emac_fold_fused_launch_f32(nsrc, false, &L, &F);
+    return emac_fold_fused_launch_f32(nsrc, 0, &L, &F);
   }
   switch (dtype) {
   case EMAC_FLOAT:
-    return op == EMAC_SUM ? emac_fold_fused_launch_f32(nsrc, tree, &L, &F) : emac_fold_fused_launch_f32_mm(op, nsrc, tree, &L, &F);
+    return op == EMAC_SUM ? emac_fold_fused_launch_f32(nsrc, ch, &L, &F) : emac_fold_fused_launch_f32_mm(op, &L, &F);
   case EMAC_DOUBLE:
-    return op == EMAC_SUM ? emac_fold_fused_launch_f64(nsrc, tree, &L, &F) : emac_fold_fused_launch_f64_mm(op, nsrc, tree, &L, &F);
+    return op == EMAC_SUM ? emac_fold_fused_launch_f64(nsrc, ch, &L, &F) : emac_fold_fused_launch_f64_mm(op, &L, &F);
   case EMAC_INT:
-    return op == EMAC_SUM ? emac_fold_fused_launch_i32(nsrc, tree, &L, &F) : emac_fold_fused_launch_i32_mm(op, nsrc, tree, &L, &F);
+    return op == EMAC_SUM ? emac_fold_fused_launch_i32(nsrc, ch, &L, &F) : emac_fold_fused_launch_i32_mm(op, &L, &F);
   case EMAC_LONG:
-    return op == EMAC_SUM ? emac_fold_fused_launch_i64(nsrc, tree, &L, &F) : emac_fold_fused_launch_i64_mm(op, nsrc, tree, &L, &F);
+    return op == EMAC_SUM ? emac_fold_fused_launch_i64(nsrc, ch, &L, &F) : emac_fold_fused_launch_i64_mm(op, &L, &F);
   }
   return EMAC_ERR_ARG;
 }

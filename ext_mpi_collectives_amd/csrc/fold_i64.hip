@@ -1,11 +1,11 @@
-// fold_i64.hip -- long instantiations of the fold kernels (one translation unit per element type so
-// that the kernel set compiles in parallel). See fold_kernel.hpp.
+// fold_i64.hip -- long int SUM instantiations of the fold kernels (one translation unit per element
+// type so that the kernel set compiles in parallel). See fold_kernel.hpp.
 #include "fold_kernel.hpp"
 
-extern "C" int emac_fold_launch_i64(int nsrc, bool tree, int fan, int unroll, const emac::Launch *L) {
-  return emac::launch_t<long, EMAC_SUM>(nsrc, tree, fan, unroll, *L);
+extern "C" int emac_fold_launch_i64(int nsrc, int ch, int fan, int unroll, const emac::Launch *L) {
+  return emac::launch_sum_t<long>(nsrc, ch, fan, unroll, *L);
 }
 
-extern "C" int emac_fold_fused_launch_i64(int nsrc, bool tree, const emac::Launch *L, const emac::FusedLaunch *F) {
-  return emac::launch_fused_t<long, EMAC_SUM>(nsrc, tree, *L, *F);
+extern "C" int emac_fold_fused_launch_i64(int nsrc, int ch, const emac::Launch *L, const emac::FusedLaunch *F) {
+  return emac::launch_fused_sum_t<long>(nsrc, ch, *L, *F);
 }

@@ -98,17 +98,52 @@ constexpr bool can_tree(int n) {
   return false;
 }
 
+// Fold-tree shape as a template parameter CH:
+//   0   linear: one reduce-scatter radix, ((x0 + x1) + x2) + ...
+//   1   multi-level tree replayed from the plan's runtime level codes (any radix chain)
+//   >1  a radix chain known at compile time, packed 5 bits per level, level 0 (the fastest
+//       leaf digit, the first reduce-scatter radix of the copy-in string) lowest: the same nested
+//       left folds as the runtime codes, but straight-line adds (plan.c build_codes)
+constexpr int chain(int r0, int r1, int r2 = 0, int r3 = 0) { return r0 | r1 << 5 | r2 << 10 | r3 << 15; }
+constexpr int ch_levels(int ch) { return ch == 0 ? 0 : 1 + ch_levels(ch >> 5); }
+constexpr int ch_rad(int ch, int l) { return (ch >> (5 * l)) & 31; }
+constexpr int ch_group(int ch, int l) { return l < 0 ? 1 : ch_rad(ch, l) * ch_group(ch, l - 1); }  // leaves per level-l group
+
+// value of the level-L group of chain CH starting at leaf BASE: its first level-(L-1) partial, then
+// the others in order (J = 1 .. radix - 1), each combined into the accumulator from the right
+template <int OP, typename T, int CH, int L, int BASE, int J, typename X, int N>
+__device__ __forceinline__ X chain_rest(const X (&x)[N], X acc);
+template <int OP, typename T, int CH, int L, int BASE, typename X, int N>
+__device__ __forceinline__ X chain_group(const X (&x)[N]) {
+  if constexpr (L < 0) {
+    return x[BASE];
+  } else {
+    return chain_rest<OP, T, CH, L, BASE, 1>(x, chain_group<OP, T, CH, L - 1, BASE>(x));
+  }
+}
+template <int OP, typename T, int CH, int L, int BASE, int J, typename X, int N>
+__device__ __forceinline__ X chain_rest(const X (&x)[N], X acc) {
+  if constexpr (J == ch_rad(CH, L)) {
+    return acc;
+  } else {
+    constexpr int SUB = ch_group(CH, L - 1);
+    return chain_rest<OP, T, CH, L, BASE, J + 1>(x, combine<OP, T>(acc, chain_group<OP, T, CH, L - 1, BASE + J * SUB>(x)));
+  }
+}
+
 // Replay the fold tree over the leaf values x[0..N) (leaf order of plan.c).
-// Linear form (one reduce-scatter radix): ((x0 + x1) + x2) + ...
-// Tree form: nested left folds, level l accumulates the completed level-(l-1) partials.
-template <int OP, typename T, int N, bool TREE, typename X>
+template <int OP, typename T, int N, int CH, typename X>
 __device__ __forceinline__ X fold_leaves(const X (&x)[N], const emac_codes &c) {
-  if constexpr (!TREE) {
+  if constexpr (CH == 0) {
     X acc = x[0];
 #pragma unroll
     for (int t = 1; t < N; ++t) acc = combine<OP, T>(acc, x[t]);
     return acc;
+  } else if constexpr (CH > 1) {
+    static_assert(ch_group(CH, ch_levels(CH) - 1) == N, "chain does not span the leaves");
+    return chain_group<OP, T, CH, ch_levels(CH) - 1, 0>(x);
   } else {
+    // runtime codes: level l accumulates the completed level-(l-1) partials
     X cur = x[0];
     X acc[kMaxLevels] = {cur, cur, cur, cur};
 #pragma unroll
@@ -129,7 +164,7 @@ __device__ __forceinline__ X fold_leaves(const X (&x)[N], const emac_codes &c) {
 
 // D = fan-out width, a compile-time constant: N for the node form (every rank's receive
 // buffer), 1 for the communicator form. All destination pointers are then loaded up front.
-template <typename T, int OP, int N, bool TREE, int D, bool REMOTE = false>
+template <typename T, int OP, int N, int CH, int D, bool REMOTE = false>
 __device__ __forceinline__ void fold_scalar_element(const emac_bucket *b, long e, const emac_codes &c) {
   typedef typename Lane<T>::S S;
   const long k = e - b->head;  // bucket pointers sit at element `head`
@@ -142,7 +177,7 @@ __device__ __forceinline__ void fold_scalar_element(const emac_bucket *b, long e
     else
       x[s] = *p;
   }
-  const S r = fold_leaves<OP, T, N, TREE>(x, c);
+  const S r = fold_leaves<OP, T, N, CH>(x, c);
 #pragma unroll
   for (int d = 0; d < D; ++d) {
     S *p = static_cast<S *>(b->dst[d]) + k;
@@ -163,7 +198,7 @@ __device__ __forceinline__ void fold_scalar_element(const emac_bucket *b, long e
 // ISSUE (load issue schedule, measured in tools/ldsbench.hip): bit 0 = source-major order
 // (every vector of leaf 0, then leaf 1, ...) instead of vector-major; bits 1.. = s_sleep after
 // every 4 loads (0 = back-to-back burst).
-template <typename T, int OP, int N, int U, bool TREE, int D, bool FULL, int ISSUE = 1>
+template <typename T, int OP, int N, int U, int CH, int D, bool FULL, int ISSUE = 1>
 __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_base, long nvec, const emac_codes &c,
                                              bool store = true) {
   typedef typename Lane<T>::V V;
@@ -193,7 +228,7 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
   }
   V r[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u) r[u] = fold_leaves<OP, T, N, TREE>(x[u], c);
+  for (int u = 0; u < U; ++u) r[u] = fold_leaves<OP, T, N, CH>(x[u], c);
   // destination pointers are only needed now: their descriptor read overlaps the loads
   if (!store) return;  // peer-mapped launch whose phase-0 barrier failed (wave-uniform)
 #pragma unroll
@@ -214,13 +249,104 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
   if constexpr (REMOTE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---- runtime leaf count (N = 0 in the templates below): MIN / MAX ----
+// The reference's CPU reduction also takes MIN and MAX (ext_mpi_native_exec.c:240-318); they are
+// off the hot path (its GPU kernel only sums), so they run ONE kernel per element type, operation
+// and fan-out form: up to kRtMax leaves read with wave-uniform guards, the plan's runtime level
+// codes (nlev 1 for a linear fold), one 16-byte vector per lane and leaf. D = 1: one destination;
+// D = 0: `n` destinations (the node form's fan-out).
+constexpr int kRtMax = EMAC_MAX_RANKS;
+
+template <int OP, typename T, typename X>
+__device__ __forceinline__ X fold_leaves_rt(const X (&x)[kRtMax], int n, const emac_codes &c) {
+  X cur = x[0];
+  X acc[kMaxLevels] = {cur, cur, cur, cur};
+#pragma unroll
+  for (int t = 0; t < kRtMax; ++t) {
+    if (t < n) {  // wave-uniform
+      cur = x[t];
+#pragma unroll
+      for (int l = 0; l < kMaxLevels; ++l) {
+        if (l < c.nlev) {
+          if (l == 0 || c.close[t] >= l) acc[l] = ((c.first[t] >> l) & 1) ? cur : combine<OP, T>(acc[l], cur);
+          cur = acc[l];
+        }
+      }
+    }
+  }
+  return cur;
+}
+
+template <typename T, int OP, int D, bool REMOTE>
+__device__ __forceinline__ void fold_scalar_rt(const emac_bucket *b, long e, const emac_codes &c, int n) {
+  typedef typename Lane<T>::S S;
+  const long k = e - b->head;
+  S x[kRtMax];
+#pragma unroll
+  for (int s = 0; s < kRtMax; ++s) {
+    if (s < n) {
+      const S *p = static_cast<const S *>(b->src[s]) + k;
+      if constexpr (REMOTE)
+        x[s] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      else
+        x[s] = *p;
+    }
+  }
+  const S r = fold_leaves_rt<OP, T>(x, n, c);
+  const int nd = D ? 1 : n;
+#pragma unroll
+  for (int d = 0; d < kRtMax; ++d) {
+    if (d < nd) {
+      S *p = static_cast<S *>(b->dst[d]) + k;
+      if constexpr (REMOTE)
+        __hip_atomic_store(p, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      else
+        *p = r;
+    }
+  }
+}
+
+template <typename T, int OP, int D, bool FULL, bool REMOTE>
+__device__ __forceinline__ void fold_vectors_rt(const emac_bucket *b, long tile_base, long nvec, const emac_codes &c,
+                                                int n, bool store) {
+  typedef typename Lane<T>::V V;
+  typedef __attribute__((address_space(1))) V GV;
+  const long left = nvec - tile_base;
+  const unsigned v = threadIdx.x;
+  V x[kRtMax];
+#pragma unroll
+  for (int s = 0; s < kRtMax; ++s) {
+    if (s < n && (FULL || (long)v < left)) {
+      const GV *src = (const GV *)b->src[s] + tile_base;
+      if constexpr (REMOTE)
+        x[s] = sys_load16<V>((const void *)src, v * 16u);
+      else
+        x[s] = __builtin_nontemporal_load(src + v);
+    }
+  }
+  const V r = fold_leaves_rt<OP, T>(x, n, c);
+  if (!store || !(FULL || (long)v < left)) return;
+  const int nd = D ? 1 : n;
+#pragma unroll
+  for (int d = 0; d < kRtMax; ++d) {
+    if (d < nd) {
+      GV *dst = (GV *)b->dst[d] + tile_base;
+      if constexpr (REMOTE)
+        sys_store16<V>((void *)dst, v * 16u, r);
+      else
+        __builtin_nontemporal_store(r, dst + v);
+    }
+  }
+}
+
 // Streaming body: one workgroup per tile (grid-stride); a tile is EMAC_BLOCK*U consecutive
 // 16-byte vectors of one bucket. Nothing element-granular runs here (see fold_edge_kernel).
-template <typename T, int OP, int N, int U, bool TREE, int D, int ISSUE = 1>
+template <typename T, int OP, int N, int U, int CH, int D, int ISSUE = 1>
 __global__ __launch_bounds__(EMAC_BLOCK) void fold_kernel(const emac_bucket *__restrict__ bk, int nb,
                                                           long ntiles, long tiles_per_bucket, int all_full,
-                                                          emac_codes codes, const unsigned *go) {
+                                                          emac_codes codes, const unsigned *go, int nrt) {
   constexpr long TILE = (long)EMAC_BLOCK * U;
+  static_assert(N > 0 || U == 1, "runtime leaf counts use one vector per lane");
   // peer-mapped launch: the phase-0 barrier's verdict (ipc_sync.hpp); its load is issued ahead of
   // the leaf loads and only waited for before the first store
   bool store = true;
@@ -250,33 +376,44 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_kernel(const emac_bucket *__r
     const emac_bucket *b = bk + bi;
     // all_full (host-known: every bucket a whole number of tiles) skips the dependent read of
     // nvec before the first load of the tile
-    if (all_full || (t + 1) * TILE <= b->nvec)
-      fold_vectors<T, OP, N, U, TREE, D, true, ISSUE>(b, t * TILE, 0, codes, store);
-    else
-      fold_vectors<T, OP, N, U, TREE, D, false, ISSUE>(b, t * TILE, b->nvec, codes, store);
+    if constexpr (N == 0) {
+      constexpr bool REMOTE = (ISSUE & kRemote) != 0;
+      if (all_full || (t + 1) * TILE <= b->nvec)
+        fold_vectors_rt<T, OP, D, true, REMOTE>(b, t * TILE, 0, codes, nrt, store);
+      else
+        fold_vectors_rt<T, OP, D, false, REMOTE>(b, t * TILE, b->nvec, codes, nrt, store);
+      if constexpr (REMOTE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (all_full || (t + 1) * TILE <= b->nvec)
+        fold_vectors<T, OP, N, U, CH, D, true, ISSUE>(b, t * TILE, 0, codes, store);
+      else
+        fold_vectors<T, OP, N, U, CH, D, false, ISSUE>(b, t * TILE, b->nvec, codes, store);
+    }
   }
 }
 
 // Element-granular work: unaligned heads/tails and misaligned buckets, one workgroup per item.
-template <typename T, int OP, int N, bool TREE, int D, bool REMOTE = false>
+template <typename T, int OP, int N, int CH, int D, bool REMOTE = false>
 __global__ __launch_bounds__(EMAC_BLOCK) void fold_edge_kernel(const emac_bucket *__restrict__ bk,
                                                                const emac_edge *__restrict__ items,
-                                                               emac_codes codes, const unsigned *go) {
+                                                               emac_codes codes, const unsigned *go, int nrt) {
   constexpr long EPV = 16 / sizeof(typename Lane<T>::S);
   if constexpr (REMOTE) {
     if (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) return;
   }
   const emac_edge it = items[blockIdx.x];
   const emac_bucket *b = bk + it.bucket;
+  auto one = [&](long e) {
+    if constexpr (N == 0)
+      fold_scalar_rt<T, OP, D, REMOTE>(b, e, codes, nrt);
+    else
+      fold_scalar_element<T, OP, N, CH, D, REMOTE>(b, e, codes);
+  };
   if (it.mode == 1) {
-    for (long e = it.start + threadIdx.x; e < it.start + it.count; e += EMAC_BLOCK)
-      fold_scalar_element<T, OP, N, TREE, D, REMOTE>(b, e, codes);
+    for (long e = it.start + threadIdx.x; e < it.start + it.count; e += EMAC_BLOCK) one(e);
   } else {
     const long nsc = b->head + b->tail;
-    for (long i = threadIdx.x; i < nsc; i += EMAC_BLOCK) {
-      const long e = i < b->head ? i : b->head + b->nvec * EPV + (i - b->head);
-      fold_scalar_element<T, OP, N, TREE, D, REMOTE>(b, e, codes);
-    }
+    for (long i = threadIdx.x; i < nsc; i += EMAC_BLOCK) one(i < b->head ? i : b->head + b->nvec * EPV + (i - b->head));
   }
   if constexpr (REMOTE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -294,8 +431,8 @@ struct Work {
 
 // Every tile and edge item of `w`, grid-strided over the launch's workgroups, with
 // system-coherent accesses (fold_vectors REMOTE). N leaves (N = 1: a copy).
-template <typename T, int OP, int N, int U, bool TREE>
-__device__ __forceinline__ void run_remote(const Work &w, const emac_codes &codes) {
+template <typename T, int OP, int N, int U, int CH>
+__device__ __forceinline__ void run_remote(const Work &w, const emac_codes &codes, int nrt = 0) {
   constexpr int ISSUE = 1 | kRemote;
   constexpr long TILE = (long)EMAC_BLOCK * U;
   constexpr long EPV = 16 / sizeof(typename Lane<T>::S);
@@ -318,23 +455,32 @@ __device__ __forceinline__ void run_remote(const Work &w, const emac_codes &code
       t = tile - w.b[lo].tile0;
     }
     const emac_bucket *b = w.b + bi;
-    if (w.all_full || (t + 1) * TILE <= b->nvec)
-      fold_vectors<T, OP, N, U, TREE, 1, true, ISSUE>(b, t * TILE, 0, codes);
-    else
-      fold_vectors<T, OP, N, U, TREE, 1, false, ISSUE>(b, t * TILE, b->nvec, codes);
+    if constexpr (N == 0) {
+      if (w.all_full || (t + 1) * TILE <= b->nvec)
+        fold_vectors_rt<T, OP, 1, true, true>(b, t * TILE, 0, codes, nrt, true);
+      else
+        fold_vectors_rt<T, OP, 1, false, true>(b, t * TILE, b->nvec, codes, nrt, true);
+    } else {
+      if (w.all_full || (t + 1) * TILE <= b->nvec)
+        fold_vectors<T, OP, N, U, CH, 1, true, ISSUE>(b, t * TILE, 0, codes);
+      else
+        fold_vectors<T, OP, N, U, CH, 1, false, ISSUE>(b, t * TILE, b->nvec, codes);
+    }
   }
   for (int item = blockIdx.x; item < w.nedges; item += gridDim.x) {
     const emac_edge it = w.edges[item];
     const emac_bucket *b = w.b + it.bucket;
+    auto one = [&](long e) {
+      if constexpr (N == 0)
+        fold_scalar_rt<T, OP, 1, true>(b, e, codes, nrt);
+      else
+        fold_scalar_element<T, OP, N, CH, 1, true>(b, e, codes);
+    };
     if (it.mode == 1) {
-      for (long e = it.start + threadIdx.x; e < it.start + it.count; e += EMAC_BLOCK)
-        fold_scalar_element<T, OP, N, TREE, 1, true>(b, e, codes);
+      for (long e = it.start + threadIdx.x; e < it.start + it.count; e += EMAC_BLOCK) one(e);
     } else {
       const long nsc = b->head + b->tail;
-      for (long i = threadIdx.x; i < nsc; i += EMAC_BLOCK) {
-        const long e = i < b->head ? i : b->head + b->nvec * EPV + (i - b->head);
-        fold_scalar_element<T, OP, N, TREE, 1, true>(b, e, codes);
-      }
+      for (long i = threadIdx.x; i < nsc; i += EMAC_BLOCK) one(i < b->head ? i : b->head + b->nvec * EPV + (i - b->head));
     }
   }
 }
@@ -354,9 +500,9 @@ __device__ __forceinline__ void run_remote(const Work &w, const emac_codes &code
 //          reader's L2, 8 processes on one MI355X). The next Start's phase 0 keeps every owner
 //          from overwriting its result before the peers have pulled it.
 // The grid never exceeds one workgroup per CU, so every workgroup is resident while any waits.
-template <typename T, int OP, int N, int U, bool TREE>
+template <typename T, int OP, int N, int U, int CH>
 __global__ __launch_bounds__(EMAC_BLOCK) void ipc_fused_kernel(Work fold, Work pull, emac_codes codes, NodeSync ns,
-                                                               unsigned long epoch0, unsigned long epoch1) {
+                                                               unsigned long epoch0, unsigned long epoch1, int nrt) {
   __shared__ int verdict;
   if (threadIdx.x < 64) {
     const bool ok = wave_phase0(ns, epoch0, blockIdx.x == 0);
@@ -364,7 +510,7 @@ __global__ __launch_bounds__(EMAC_BLOCK) void ipc_fused_kernel(Work fold, Work p
   }
   __syncthreads();
   const bool ok = verdict != 0;
-  if (ok) run_remote<T, OP, N, U, TREE>(fold, codes);
+  if (ok) run_remote<T, OP, N, U, CH>(fold, codes, nrt);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of this wave acknowledged
   __syncthreads();
   if (threadIdx.x < 64) {
@@ -383,24 +529,24 @@ __global__ __launch_bounds__(EMAC_BLOCK) void ipc_fused_kernel(Work fold, Work p
     if (threadIdx.x == 0) verdict = ok && in_time && !gave_up;
   }
   __syncthreads();
-  if (verdict) run_remote<T, OP, 1, 2, false>(pull, codes);
+  if (verdict) run_remote<T, OP, 1, 2, 0>(pull, codes);
 }
 
 // ---- instantiation policy (keep in sync with emac_gpu_pick_unroll in fold.hip) ----
-// A launch schedule is encoded as U | ISSUE << 4 (EMAC_SCHED).
-// linear, fan-out N (node / IPC form):  N <= 8 -> (U 2, burst), (U 4, burst), (U 4, s_sleep 2
-//                                        every 4 loads), (U 1, burst: page-locked host buffers);
-//                                        N > 8 -> (U 1, burst)
-// linear, fan-out 1 (comm form):        N <= 8 -> U in {1, 2}, burst;  N > 8 -> U = 1
-// tree (composite N), either fan-out:   U = 4 / 2 / 1 for N <= 4 / <= 8 / > 8, burst; U = 2 also
-//                                        with s_sleep 2 every 4 loads
+// A launch schedule is encoded as U | ISSUE << 4 (sched). SUM, per fold-tree kind CH:
+// linear or compile-time chain (gpu.h EMAC_CHAINS), fan-out N (node form):
+//        N <= 8 -> (U 2, burst), (U 4, burst), (U 4, s_sleep 2 every 4 loads), (U 1, burst: host
+//        buffers); N > 8 -> (U 1, burst)
+// linear or chain, fan-out 1 (comm form, one-chunk fold): N <= 8 -> U in {1, 2, 4}, burst;
+//        N > 8 -> U = 1
+// runtime-code tree (composite N, any chain), either fan-out: U = 4 / 2 / 1 for N <= 4 / <= 8 /
+//        > 8, burst; U = 2 also with s_sleep 2 every 4 loads (node form)
+// peer-mapped (IPC, ISSUE | kRemote): (U 2, burst) up to 8 leaves, (U 1) above; runtime trees U
+//        = tree_unroll(N)
 // (burst = ISSUE 1: every load of a tile back to back, source-major)
-// MIN / MAX (any fan-out, not peer-mapped): the burst schedule only -- U = tree_unroll(N) for
-// trees, else U = 2 (N <= 8) / 1 -- so the two extra operations add two kernels per shape.
+// MIN / MAX: one runtime-leaf-count kernel per element type and fan-out form (N = 0, U = 1).
 constexpr int tree_unroll(int n) { return n <= 4 ? 4 : (n <= 8 ? 2 : 1); }
 constexpr int sched(int u, int issue) { return u | issue << 4; }
-// peer-mapped (IPC) launches: (U 2, burst) linear <= 8 leaves, (U 1) above, the tree's U for
-// composite trees -- all with system-coherent accesses (ISSUE | kRemote)
 
 struct Launch {
   const emac_codes *c;
@@ -412,75 +558,102 @@ struct Launch {
   int nedges;
   hipStream_t s;
   const unsigned *go;  // peer-mapped launches: the phase-0 verdict word (emac_sync.go[slot])
+  int nrt;             // leaves (the runtime-leaf-count kernels)
 };
 
-template <typename T, int OP, int N, int U, bool TREE, int D, int ISSUE = 1>
+template <typename T, int OP, int N, int U, int CH, int D, int ISSUE = 1>
 int launch_one(const Launch &L) {
   const long grid = L.ntiles < 8192 ? L.ntiles : 8192;
   if (grid > 0)
-    hipLaunchKernelGGL((fold_kernel<T, OP, N, U, TREE, D, ISSUE>), dim3((unsigned)grid), dim3(EMAC_BLOCK), 0, L.s, L.b,
-                       L.nb, L.ntiles, L.tpb, L.all_full, *L.c, L.go);
+    hipLaunchKernelGGL((fold_kernel<T, OP, N, U, CH, D, ISSUE>), dim3((unsigned)grid), dim3(EMAC_BLOCK), 0, L.s, L.b, L.nb,
+                       L.ntiles, L.tpb, L.all_full, *L.c, L.go, L.nrt);
   if (L.nedges > 0)
-    hipLaunchKernelGGL((fold_edge_kernel<T, OP, N, TREE, D, (ISSUE & kRemote) != 0>), dim3((unsigned)L.nedges),
-                       dim3(EMAC_BLOCK), 0, L.s, L.b, L.edges, *L.c, L.go);
+    hipLaunchKernelGGL((fold_edge_kernel<T, OP, N, CH, D, (ISSUE & kRemote) != 0>), dim3((unsigned)L.nedges),
+                       dim3(EMAC_BLOCK), 0, L.s, L.b, L.edges, *L.c, L.go, L.nrt);
   return hipGetLastError() == hipSuccess ? 0 : EMAC_ERR_DEVICE;
 }
 
-template <typename T, int OP, int N, bool FAN, bool REMOTE = false>
-int launch_nf(bool tree, int unroll, const Launch &L) {
+// SUM over N leaves, fold-tree kind CH. FAN: fan-out N (node form); REMOTE: peer-mapped.
+template <typename T, int N, bool FAN, bool REMOTE, int CH>
+int launch_sum(int unroll, const Launch &L) {
+  constexpr int OP = EMAC_SUM;
   constexpr int D = FAN ? N : 1;
   if constexpr (REMOTE) {
-    // peer-mapped launches: one schedule per shape (U = 2 linear up to 8 leaves, else the tree's
-    // or 1), system-coherent accesses
-    constexpr int UR = N > 8 ? 1 : 2;
-    if constexpr (can_tree(N)) {
-      if (tree) return unroll == sched(tree_unroll(N), 1 | kRemote) ? launch_one<T, OP, N, tree_unroll(N), true, D, 1 | kRemote>(L)
-                                                                    : EMAC_ERR_UNSUPPORTED;
+    constexpr int UR = CH == 1 ? tree_unroll(N) : (N > 8 ? 1 : 2);
+    return unroll == sched(UR, 1 | kRemote) ? launch_one<T, OP, N, UR, CH, D, 1 | kRemote>(L) : EMAC_ERR_UNSUPPORTED;
+  } else if constexpr (CH == 1) {
+    if (unroll == sched(tree_unroll(N), 1)) return launch_one<T, OP, N, tree_unroll(N), 1, D>(L);
+    if constexpr (FAN && tree_unroll(N) == 2) {
+      if (unroll == sched(2, 5)) return launch_one<T, OP, N, 2, 1, D, 5>(L);
     }
-    if (tree) return EMAC_ERR_UNSUPPORTED;
-    return unroll == sched(UR, 1 | kRemote) ? launch_one<T, OP, N, UR, false, D, 1 | kRemote>(L) : EMAC_ERR_UNSUPPORTED;
-  } else if constexpr (OP != EMAC_SUM) {
-    // MIN / MAX: one burst schedule per shape (canonical_sched)
-    if constexpr (can_tree(N)) {
-      if (tree) return unroll == sched(tree_unroll(N), 1) ? launch_one<T, OP, N, tree_unroll(N), true, D>(L) : EMAC_ERR_UNSUPPORTED;
-    }
-    if (tree) return EMAC_ERR_UNSUPPORTED;
-    constexpr int UL = N > 8 ? 1 : 2;
-    return unroll == sched(UL, 1) ? launch_one<T, OP, N, UL, false, D>(L) : EMAC_ERR_UNSUPPORTED;
+    return EMAC_ERR_UNSUPPORTED;
+  } else if constexpr (N > 8) {
+    return unroll == sched(1, 1) ? launch_one<T, OP, N, 1, CH, D>(L) : EMAC_ERR_UNSUPPORTED;
+  } else if constexpr (FAN) {
+    if (unroll == sched(1, 1)) return launch_one<T, OP, N, 1, CH, D, 1>(L);  // host buffers
+    if (unroll == sched(4, 5)) return launch_one<T, OP, N, 4, CH, D, 5>(L);
+    if (unroll == sched(4, 1)) return launch_one<T, OP, N, 4, CH, D, 1>(L);
+    if (unroll == sched(2, 1)) return launch_one<T, OP, N, 2, CH, D, 1>(L);
+    return EMAC_ERR_UNSUPPORTED;
   } else {
-    if constexpr (can_tree(N)) {
-      if (tree && unroll == sched(tree_unroll(N), 1)) return launch_one<T, OP, N, tree_unroll(N), true, D>(L);
-      if constexpr (tree_unroll(N) == 2) {
-        if (tree && unroll == sched(2, 5)) return launch_one<T, OP, N, 2, true, D, 5>(L);
-      }
-      if (tree) return EMAC_ERR_UNSUPPORTED;
-    }
-    if (tree) return EMAC_ERR_UNSUPPORTED;
-    if constexpr (N > 8) {
-      return unroll == sched(1, 1) ? launch_one<T, OP, N, 1, false, D>(L) : EMAC_ERR_UNSUPPORTED;
-    } else if constexpr (FAN) {
-      if (unroll == sched(1, 1)) return launch_one<T, OP, N, 1, false, D, 1>(L);  // host buffers
-      if (unroll == sched(4, 5)) return launch_one<T, OP, N, 4, false, D, 5>(L);
-      if (unroll == sched(4, 1)) return launch_one<T, OP, N, 4, false, D, 1>(L);
-      if (unroll == sched(2, 1)) return launch_one<T, OP, N, 2, false, D, 1>(L);
-    } else {
-      if (unroll == sched(2, 1)) return launch_one<T, OP, N, 2, false, D>(L);
-      if (unroll == sched(1, 1)) return launch_one<T, OP, N, 1, false, D>(L);
-    }
+    if (unroll == sched(4, 1)) return launch_one<T, OP, N, 4, CH, D>(L);
+    if (unroll == sched(2, 1)) return launch_one<T, OP, N, 2, CH, D>(L);
+    if (unroll == sched(1, 1)) return launch_one<T, OP, N, 1, CH, D>(L);
     return EMAC_ERR_UNSUPPORTED;
   }
 }
 
+// the compile-time chains of gpu.h EMAC_CHAINS for N leaves (else the runtime-code kernel)
+template <typename T, int N, bool FAN, bool REMOTE>
+int launch_sum_ch(int ch, int unroll, const Launch &L) {
+  if (ch == 0) return launch_sum<T, N, FAN, REMOTE, 0>(unroll, L);
+  if constexpr (can_tree(N)) {
+    if (ch == 1) return launch_sum<T, N, FAN, REMOTE, 1>(unroll, L);
+  }
+  if constexpr (N == 4) {
+    if (ch == chain(2, 2)) return launch_sum<T, N, FAN, REMOTE, chain(2, 2)>(unroll, L);
+  } else if constexpr (N == 8) {
+    if (ch == chain(2, 2, 2)) return launch_sum<T, N, FAN, REMOTE, chain(2, 2, 2)>(unroll, L);
+    if (ch == chain(4, 2)) return launch_sum<T, N, FAN, REMOTE, chain(4, 2)>(unroll, L);
+    if (ch == chain(2, 4)) return launch_sum<T, N, FAN, REMOTE, chain(2, 4)>(unroll, L);
+  } else if constexpr (N == 16) {
+    if (ch == chain(2, 2, 2, 2)) return launch_sum<T, N, FAN, REMOTE, chain(2, 2, 2, 2)>(unroll, L);
+    if (ch == chain(4, 4)) return launch_sum<T, N, FAN, REMOTE, chain(4, 4)>(unroll, L);
+  }
+  return EMAC_ERR_UNSUPPORTED;
+}
+
 // fan: 0 fan-out 1 (comm form), 1 fan-out N (node form), 2 peer-mapped (IPC form: leaves or the pulled
 // result in other GPUs' memory, system-coherent accesses, one destination in this rank's memory)
-template <typename T, int OP, int N>
-int launch_n(bool tree, int fan, int unroll, const Launch &L) {
+template <typename T, int N>
+int launch_sum_n(int ch, int fan, int unroll, const Launch &L) {
   if constexpr (N == 1) {
-    return fan == 2 ? launch_nf<T, OP, 1, false, true>(false, unroll, L) : launch_nf<T, OP, 1, false>(false, unroll, L);
+    return fan == 2 ? launch_sum<T, 1, false, true, 0>(unroll, L) : launch_sum<T, 1, false, false, 0>(unroll, L);
   } else {
-    return fan == 2 ? launch_nf<T, OP, N, false, true>(tree, unroll, L)
-                    : fan ? launch_nf<T, OP, N, true>(tree, unroll, L) : launch_nf<T, OP, N, false>(tree, unroll, L);
+    return fan == 2 ? launch_sum_ch<T, N, false, true>(ch, unroll, L)
+                    : fan ? launch_sum_ch<T, N, true, false>(ch, unroll, L) : launch_sum_ch<T, N, false, false>(ch, unroll, L);
   }
+}
+
+template <typename T>
+int launch_sum_t(int nsrc, int ch, int fan, int unroll, const Launch &L) {
+  switch (nsrc) {
+#define EMAC_CASE(n) \
+  case n: return launch_sum_n<T, n>(ch, fan, unroll, L);
+    EMAC_CASE(1) EMAC_CASE(2) EMAC_CASE(3) EMAC_CASE(4) EMAC_CASE(5) EMAC_CASE(6) EMAC_CASE(7) EMAC_CASE(8)
+    EMAC_CASE(9) EMAC_CASE(10) EMAC_CASE(11) EMAC_CASE(12) EMAC_CASE(13) EMAC_CASE(14) EMAC_CASE(15) EMAC_CASE(16)
+#undef EMAC_CASE
+  }
+  return EMAC_ERR_UNSUPPORTED;
+}
+
+// MIN / MAX: the runtime-leaf-count kernel of the fan-out form (L.nrt leaves)
+template <typename T, int OP>
+int launch_rt(int fan, int unroll, const Launch &L) {
+  if (L.nrt < 1 || L.nrt > kRtMax) return EMAC_ERR_UNSUPPORTED;
+  if (fan == 2) return unroll == sched(1, 1 | kRemote) ? launch_one<T, OP, 0, 1, 1, 1, 1 | kRemote>(L) : EMAC_ERR_UNSUPPORTED;
+  if (unroll != sched(1, 1)) return EMAC_ERR_UNSUPPORTED;
+  return fan ? launch_one<T, OP, 0, 1, 1, 0>(L) : launch_one<T, OP, 0, 1, 1, 1>(L);
 }
 
 struct FusedLaunch {
@@ -490,29 +663,40 @@ struct FusedLaunch {
   Work pull;  // every other owner's result into this rank's receive buffer (N = 1, U = 2)
 };
 
-// fused peer-mapped launch: the IPC form's schedule of the shape (pick_unroll fan == 2)
-template <typename T, int OP, int N>
-int launch_fused_n(bool tree, const Launch &L, const FusedLaunch &F) {
-  constexpr int UR = N > 8 ? 1 : 2;
+template <typename T, int OP, int N, int U, int CH>
+int launch_fused_one(const Launch &L, const FusedLaunch &F) {
   const Work fold = {L.b, L.nb, L.ntiles, L.tpb, L.all_full, L.edges, L.nedges};
-  if constexpr (can_tree(N)) {
-    if (tree) {
-      hipLaunchKernelGGL((ipc_fused_kernel<T, OP, N, tree_unroll(N), true>), dim3((unsigned)F.grid), dim3(EMAC_BLOCK), 0,
-                         L.s, fold, F.pull, *L.c, F.ns, F.epoch0, F.epoch1);
-      return hipGetLastError() == hipSuccess ? 0 : EMAC_ERR_DEVICE;
-    }
-  }
-  if (tree) return EMAC_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL((ipc_fused_kernel<T, OP, N, UR, false>), dim3((unsigned)F.grid), dim3(EMAC_BLOCK), 0, L.s, fold,
-                     F.pull, *L.c, F.ns, F.epoch0, F.epoch1);
+  hipLaunchKernelGGL((ipc_fused_kernel<T, OP, N, U, CH>), dim3((unsigned)F.grid), dim3(EMAC_BLOCK), 0, L.s, fold, F.pull,
+                     *L.c, F.ns, F.epoch0, F.epoch1, L.nrt);
   return hipGetLastError() == hipSuccess ? 0 : EMAC_ERR_DEVICE;
 }
 
-template <typename T, int OP>
-int launch_fused_t(int nsrc, bool tree, const Launch &L, const FusedLaunch &F) {
+// fused peer-mapped launch: the IPC form's schedule of the shape (pick_unroll fan == 2)
+template <typename T, int N>
+int launch_fused_sum_n(int ch, const Launch &L, const FusedLaunch &F) {
+  constexpr int UR = N > 8 ? 1 : 2;
+  if (ch == 0) return launch_fused_one<T, EMAC_SUM, N, UR, 0>(L, F);
+  if constexpr (can_tree(N)) {
+    if (ch == 1) return launch_fused_one<T, EMAC_SUM, N, tree_unroll(N), 1>(L, F);
+  }
+  if constexpr (N == 4) {
+    if (ch == chain(2, 2)) return launch_fused_one<T, EMAC_SUM, N, UR, chain(2, 2)>(L, F);
+  } else if constexpr (N == 8) {
+    if (ch == chain(2, 2, 2)) return launch_fused_one<T, EMAC_SUM, N, UR, chain(2, 2, 2)>(L, F);
+    if (ch == chain(4, 2)) return launch_fused_one<T, EMAC_SUM, N, UR, chain(4, 2)>(L, F);
+    if (ch == chain(2, 4)) return launch_fused_one<T, EMAC_SUM, N, UR, chain(2, 4)>(L, F);
+  } else if constexpr (N == 16) {
+    if (ch == chain(2, 2, 2, 2)) return launch_fused_one<T, EMAC_SUM, N, UR, chain(2, 2, 2, 2)>(L, F);
+    if (ch == chain(4, 4)) return launch_fused_one<T, EMAC_SUM, N, UR, chain(4, 4)>(L, F);
+  }
+  return EMAC_ERR_UNSUPPORTED;
+}
+
+template <typename T>
+int launch_fused_sum_t(int nsrc, int ch, const Launch &L, const FusedLaunch &F) {
   switch (nsrc) {
 #define EMAC_CASE(n) \
-  case n: return launch_fused_n<T, OP, n>(tree, L, F);
+  case n: return launch_fused_sum_n<T, n>(ch, L, F);
     EMAC_CASE(2) EMAC_CASE(3) EMAC_CASE(4) EMAC_CASE(5) EMAC_CASE(6) EMAC_CASE(7) EMAC_CASE(8)
     EMAC_CASE(9) EMAC_CASE(10) EMAC_CASE(11) EMAC_CASE(12) EMAC_CASE(13) EMAC_CASE(14) EMAC_CASE(15) EMAC_CASE(16)
 #undef EMAC_CASE
@@ -521,15 +705,9 @@ int launch_fused_t(int nsrc, bool tree, const Launch &L, const FusedLaunch &F) {
 }
 
 template <typename T, int OP>
-int launch_t(int nsrc, bool tree, int fan, int unroll, const Launch &L) {
-  switch (nsrc) {
-#define EMAC_CASE(n) \
-  case n: return launch_n<T, OP, n>(tree, fan, unroll, L);
-    EMAC_CASE(1) EMAC_CASE(2) EMAC_CASE(3) EMAC_CASE(4) EMAC_CASE(5) EMAC_CASE(6) EMAC_CASE(7) EMAC_CASE(8)
-    EMAC_CASE(9) EMAC_CASE(10) EMAC_CASE(11) EMAC_CASE(12) EMAC_CASE(13) EMAC_CASE(14) EMAC_CASE(15) EMAC_CASE(16)
-#undef EMAC_CASE
-  }
-  return EMAC_ERR_UNSUPPORTED;
+int launch_fused_rt(const Launch &L, const FusedLaunch &F) {
+  if (L.nrt < 2 || L.nrt > kRtMax) return EMAC_ERR_UNSUPPORTED;
+  return launch_fused_one<T, OP, 0, 1, 1>(L, F);
 }
 
 }  // namespace emac

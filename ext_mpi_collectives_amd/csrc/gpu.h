@@ -137,9 +137,20 @@ int emac_gpu_fold_remote(int dtype, int op, int nsrc, int unroll, const emac_cod
                          int nb, long ntiles, long tiles_per_bucket, int all_full, const emac_edge *d_edges, int nedges,
                          const unsigned *go, void *stream);
 
+/* Fold-tree kind of a plan's codes (fold_kernel.hpp template parameter CH): 0 linear (one
+   radix), a packed compile-time radix chain (5 bits per level, level 0 lowest) when the kernels
+   instantiate it -- EMAC_CHAINS: -2 -2, -2 -2 -2, -4 -2, -2 -4, -2 -2 -2 -2, -4 -4 -- else 1
+   (replayed from the runtime level codes). SUM only; MIN / MAX always take the runtime codes. */
+#define EMAC_CH(r0, r1, r2, r3) ((r0) | (r1) << 5 | (r2) << 10 | (r3) << 15)
+#define EMAC_CHAINS                                                                             \
+  { EMAC_CH(2, 2, 0, 0), EMAC_CH(2, 2, 2, 0), EMAC_CH(4, 2, 0, 0), EMAC_CH(2, 4, 0, 0), EMAC_CH(2, 2, 2, 2), \
+    EMAC_CH(4, 4, 0, 0) }
+int emac_tree_kind(const emac_codes *codes, int op);
+
 /* layout.c: alignment split of a bucket whose pointers sit at its first element, and the
    launch layout (tiles, uniform tiles per bucket, unroll, edge items; caller frees edges). */
 void emac_split_alignment(emac_bucket *b, int nsrc, long len, int tsize);
+/* tree: 1 for a runtime-code tree (emac_tree_kind == 1), which has its own launch schedules */
 int emac_layout(emac_bucket *b, int nb, int op, int nsrc, int tree, int fan, emac_edge **edges, int *nedges,
                 long *ntiles, long *tiles_per_bucket, int *all_full, int *unroll);
 

@@ -38,6 +38,27 @@ void emac_split_alignment(emac_bucket *b, int nsrc, long len, int tsize) {
   for (i = 0; i < b->ndst; i++) b->dst[i] = (char *)b->dst[i] + head * tsize;
 }
 
+int emac_tree_kind(const emac_codes *c, int op) {
+  static const int chains[] = EMAC_CHAINS;
+  int rad[EMAC_MAX_LEVELS], l, t, g = 1, ch = 0;
+  unsigned k;
+  if (c->nlev <= 1) return 0;
+  if (op != EMAC_SUM || c->nlev > 4) return 1;
+  /* level-l group size = 1 + the first leaf that closes level l (plan.c build_codes) */
+  for (l = 0; l < c->nlev; l++) {
+    for (t = 0; t < c->nleaf && c->close[t] <= l; t++);
+    if (t == c->nleaf || (t + 1) % g) return 1;
+    rad[l] = (t + 1) / g;
+    g = t + 1;
+    if (rad[l] < 2 || rad[l] > 31) return 1;
+    ch |= rad[l] << (5 * l);
+  }
+  if (g != c->nleaf) return 1;
+  for (k = 0; k < sizeof(chains) / sizeof(chains[0]); k++)
+    if (chains[k] == ch) return ch;
+  return 1;
+}
+
 int emac_layout(emac_bucket *b, int nb, int op, int nsrc, int tree, int fan, emac_edge **edges_out, int *nedges,
                 long *ntiles_out, long *tpb_out, int *all_full_out, int *unroll_out) {
   long total = 0, tv, tiles = 0, uniform = -1;

@@ -76,6 +76,10 @@ def lib():
         _lib.ref_cpu_allreduce_threads.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_int,
                                                    ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p),
                                                    ctypes.POINTER(ctypes.c_void_p), ctypes.c_long]
+        _lib.ref_cpu_allreduce_threads_sets.restype = ctypes.c_double
+        _lib.ref_cpu_allreduce_threads_sets.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_char_p,
+                                                        ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                                        ctypes.POINTER(ctypes.c_void_p), ctypes.c_long]
     return _lib
 
 
@@ -153,6 +157,21 @@ def cpu_allreduce_threads(sends, recvs, copyin, iters):
             np.dtype(np.int32): INT}[sends[0].dtype]
     t = lib().ref_cpu_allreduce_threads(R, sends[0].size, code, copyin.encode(), _ptrs(sends),
                                         _ptrs(recvs), iters)
+    if t < 0:
+        raise ValueError("cpu baseline failed")
+    return t
+
+
+def cpu_allreduce_threads_sets(sets, copyin, iters):
+    """The threaded CPU baseline over rotated buffer sets: `sets` is a list of (sends, recvs)
+    pairs of R arrays each; iteration i runs on set i % len(sets). Returns elapsed seconds."""
+    R = len(sets[0][0])
+    code = {np.dtype(np.float64): DOUBLE, np.dtype(np.int64): LONG, np.dtype(np.float32): FLOAT,
+            np.dtype(np.int32): INT}[sets[0][0][0].dtype]
+    sends = [a for s, _ in sets for a in s]
+    recvs = [a for _, r in sets for a in r]
+    t = lib().ref_cpu_allreduce_threads_sets(R, sets[0][0][0].size, code, copyin.encode(), len(sets), _ptrs(sends),
+                                             _ptrs(recvs), iters)
     if t < 0:
         raise ValueError("cpu baseline failed")
     return t

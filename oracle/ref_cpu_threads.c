@@ -41,7 +41,7 @@ static void barrier_wait(spin_barrier *b, int *local_sense) {
 }
 
 typedef struct {
-  int R, r, dtype;
+  int R, r, dtype, nsets;
   long iters;
   rank_prog *prog;
   void *const *send;
@@ -65,6 +65,9 @@ static void *worker(void *varg) {
   t0 = now_s();
   for (it = 0; it < a->iters; it++) {
     int pc;
+    /* buffer set of this iteration (sets rotate so the working set can exceed the host caches) */
+    void *const *send = a->send + (size_t)(it % a->nsets) * (size_t)a->R;
+    void *const *recv = a->recv + (size_t)(it % a->nsets) * (size_t)a->R;
     for (pc = 0; pc < a->prog->n; pc++) {
       const ref_op *o = &a->prog->ops[pc];
       if (o->op == REF_OP_PHASE) {
@@ -72,9 +75,8 @@ static void *worker(void *varg) {
         continue;
       }
       {
-        char *dst = (char *)(o->dbuf == REF_BUF_RECV ? a->recv : a->send)[(a->r + o->drel) % a->R] + o->doff;
-        const char *src =
-            (const char *)(o->sbuf == REF_BUF_RECV ? a->recv : a->send)[(a->r + o->srel) % a->R] + o->soff;
+        char *dst = (char *)(o->dbuf == REF_BUF_RECV ? recv : send)[(a->r + o->drel) % a->R] + o->doff;
+        const char *src = (const char *)(o->sbuf == REF_BUF_RECV ? recv : send)[(a->r + o->srel) % a->R] + o->soff;
         if (o->op == REF_OP_COPY)
           memcpy(dst, src, (size_t)o->bytes);
         else
@@ -87,15 +89,17 @@ static void *worker(void *varg) {
   return NULL;
 }
 
-double ref_cpu_allreduce_threads(int R, long count, int dtype, const char *copyin,
-                                 void *const *sendbufs, void *const *recvbufs, long iters) {
+/* nsets buffer sets of R send and R receive buffers (set k at [k * R, (k + 1) * R)); iteration i
+   runs on set i % nsets. */
+double ref_cpu_allreduce_threads_sets(int R, long count, int dtype, const char *copyin, int nsets,
+                                      void *const *sendbufs, void *const *recvbufs, long iters) {
   rank_prog *progs;
   pthread_t *th;
   worker_arg *args;
   spin_barrier bar;
   double elapsed = -1.0;
   int r;
-  if (R < 2) return -1.0;
+  if (R < 2 || nsets < 1) return -1.0;
   progs = (rank_prog *)calloc((size_t)R, sizeof(rank_prog));
   if (ref_build_programs_(R, count, dtype, copyin, 0, progs)) goto done;
   atomic_init(&bar.count, 0);
@@ -107,6 +111,7 @@ double ref_cpu_allreduce_threads(int R, long count, int dtype, const char *copyi
     args[r].R = R;
     args[r].r = r;
     args[r].dtype = dtype;
+    args[r].nsets = nsets;
     args[r].iters = iters;
     args[r].prog = &progs[r];
     args[r].send = sendbufs;
@@ -122,4 +127,9 @@ done:
   for (r = 0; r < R; r++) free(progs[r].ops);
   free(progs);
   return elapsed;
+}
+
+double ref_cpu_allreduce_threads(int R, long count, int dtype, const char *copyin,
+                                 void *const *sendbufs, void *const *recvbufs, long iters) {
+  return ref_cpu_allreduce_threads_sets(R, count, dtype, copyin, 1, sendbufs, recvbufs, iters);
 }

@@ -96,6 +96,10 @@ void ref_kat_fill(void *buf, long count, int tsize, int world_rank, long add);
  */
 double ref_cpu_allreduce_threads(int R, long count, int dtype, const char *copyin,
                                  void *const *sendbufs, void *const *recvbufs, long iters);
+/* The same over nsets rotated buffer sets (set k = buffers [k * R, (k + 1) * R); iteration i
+   uses set i % nsets), so the working set can exceed the host's caches. */
+double ref_cpu_allreduce_threads_sets(int R, long count, int dtype, const char *copyin, int nsets,
+                                      void *const *sendbufs, void *const *recvbufs, long iters);
 
 #ifdef __cplusplus
 }

@@ -47,8 +47,9 @@ def test_version_and_no_gpu_error():
 
 def test_launch_schedule_policy():
     """emac_gpu_pick_unroll (host code, no GPU): the HBM-tuned node schedule (U = 4, staggered, at
-    16 MiB x 8 float), the smallest tile for page-locked host buffers (EMAC_FAN_HOST = 4), and
-    MIN / MAX keeping their one burst schedule whatever the buffers."""
+    16 MiB x 8 float), the smallest tile for page-locked host buffers (EMAC_FAN_HOST = 4), the
+    wide tile of the one-destination local fold at 32 MiB per leaf, and MIN / MAX on their
+    runtime-leaf-count kernel (one vector per lane) whatever the buffers."""
     f = emac.lib().emac_gpu_pick_unroll
     f.restype = ctypes.c_int
     f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]
@@ -59,5 +60,11 @@ def test_launch_schedule_policy():
     assert f(emac.SUM, 8, 0, 1 | 4, 64) == sched(1, 1)
     assert f(emac.SUM, 8, 0, 1 | 4, 1 << 24) == sched(1, 1)
     assert f(emac.SUM, 8, 1, 1 | 4, nvec) == f(emac.SUM, 8, 1, 1, nvec)  # trees: their own schedule
+    assert f(emac.SUM, 8, 0, 0, (32 << 20) // 16) == sched(4, 1)  # local fold, 8 x 32 MiB -> 1
+    assert f(emac.SUM, 8, 0, 0, (2 << 20) // 16) == sched(2, 1)
+    assert f(emac.SUM, 8, 0, 0, (1 << 20) // 16) == sched(1, 1)
+    kremote = 256
     for op in (emac.MIN, emac.MAX):
-        assert f(op, 8, 0, 1 | 4, nvec) == f(op, 8, 0, 1, nvec) == sched(2, 1)
+        assert f(op, 8, 0, 1 | 4, nvec) == f(op, 8, 0, 1, nvec) == f(op, 8, 1, 0, nvec) == sched(1, 1)
+        assert f(op, 8, 0, 2, nvec) == sched(1, 1 | kremote)
+        assert f(op, 1, 0, 2, nvec) == f(emac.SUM, 1, 0, 2, nvec)  # the IPC pull is a copy whatever the op

@@ -1,0 +1,65 @@
+// ceiling.hip -- measured HBM ceilings for bench.py's roofline context (not part of the product
+// library; built into tools/libceiling.so by __graft_entry__.build()).
+//
+//   ceiling_read_glds: a read-only stream through LDS-DMA (global_load_lds_dwordx4, nontemporal):
+//                      the best read rate measured on MI355X in round 1 (tools/ldsbench.hip,
+//                      ~6.99 TB/s at 4 GiB against ~6.07 TB/s with nt loads into VGPRs).
+//   ceiling_copy_nt:   a nontemporal copy, 1 byte written per byte read (the node-form fold's mix).
+// Each call enqueues `iters` launches over `bytes` (a multiple of 16 KiB) on `stream`.
+#include <hip/hip_runtime.h>
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) f4 G4;
+typedef __attribute__((address_space(3))) f4 L4;
+
+namespace {
+
+__device__ __forceinline__ void glds16(const f4 *g, L4 *l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                   (__attribute__((address_space(3))) void *)l, 16, 0, 2 /* nt */);
+}
+
+// each workgroup streams 8 x 4 KiB per pass into LDS and reads one vector back per pass
+__global__ __launch_bounds__(256) void read_glds(const f4 *__restrict__ a, long n, float *out) {
+  __shared__ f4 lds[8 * 256];
+  f4 acc = {0, 0, 0, 0};
+  const long step = (long)gridDim.x * 256 * 8;
+  for (long i0 = (long)blockIdx.x * 256 * 8; i0 < n; i0 += step) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) glds16(a + i0 + k * 256 + threadIdx.x, (L4 *)(lds + k * 256 + (threadIdx.x & ~63u)));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    acc += lds[threadIdx.x];
+    __syncthreads();
+  }
+  if (acc.x == 12345.f) out[0] = acc.y + acc.z + acc.w;
+}
+
+__global__ __launch_bounds__(256) void copy_nt(const f4 *__restrict__ a, f4 *__restrict__ b, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    __builtin_nontemporal_store(__builtin_nontemporal_load((const G4 *)a + i), (G4 *)b + i);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ceiling_read_glds(const void *buf, long bytes, int iters, float *sink, void *stream) {
+  const long n = bytes / 16;
+  if (n % (256 * 8) || iters < 1) return -3;
+  for (int i = 0; i < iters; i++)
+    hipLaunchKernelGGL(read_glds, dim3(2048), dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<const f4 *>(buf), n,
+                       sink);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+int ceiling_copy_nt(const void *src, void *dst, long bytes, int iters, void *stream) {
+  const long n = bytes / 16;
+  if (n % 256 || iters < 1) return -3;
+  for (int i = 0; i < iters; i++)
+    hipLaunchKernelGGL(copy_nt, dim3(8192), dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<const f4 *>(src),
+                       static_cast<f4 *>(dst), n);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+}  // extern "C"
