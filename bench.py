@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=30.0, help="bound of the CPU baseline sample")
     ap.add_argument("--transport", default="ipc", choices=["ipc", "rccl"],
                     help="N > 1: peer-mapped hipIpc form (default) or RCCL point-to-point legs")
+    ap.add_argument("--shape", default=None, choices=["local256", "node256", "node16"],
+                    help="profiling: run only this fold shape (40 launches) and exit (PMC passes, tools/gpu_pmc_r02.sh)")
     ap.add_argument("--child-transport", default=None, choices=["ipc", "rccl"], help=argparse.SUPPRESS)
     ap.add_argument("--child-full", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--child-result", default=None, help=argparse.SUPPRESS)
@@ -472,7 +474,8 @@ def single_gpu(args):
             "frac_of_measured_read_ceiling": round(2 * R * big * tsize / k256 / 1e9 / extras["read_glds_gbps"], 4)
             if "read_glds_gbps" in extras else None,
             "read_gbps": round(R * big * tsize / k256 / 1e9, 1),
-            "avg_launch_us": round(k256 * 1e6, 1), "checked": r256["checked"]}
+            "avg_launch_us": round(k256 * 1e6, 1), "checked": r256["checked"],
+            "traffic": traffic_from_profiles(f"node_r{R}_256mib_{args.dtype}")}
         # latency -> bandwidth crossover of the node form (cf. BASELINE configs[4] on 8 GPUs);
         # small points reuse one buffer set (as the reference's latency runs do), large ones rotate
         sweep = []
@@ -505,6 +508,8 @@ def single_gpu(args):
         # ">= 80 % of HBM read bandwidth" target is defined
         lf = comm_shape_fold(R, big // R, tdtype, code, 40)
         lf["frac_of_peak"] = round(lf["achieved_gbps"] / HBM_PEAK_GBPS, 4)
+        lf["algorithmic_bytes_per_launch"] = (R + 1) * lf["chunk_bytes"]
+        lf["traffic"] = traffic_from_profiles(f"local_r{R}_{lf['chunk_bytes'] // MIB}mib_{args.dtype}")
         if "read_glds_gbps" in extras:
             lf["frac_of_measured_read_ceiling"] = round(lf["achieved_gbps"] / extras["read_glds_gbps"], 4)
         extras["local_fold_256MiB"] = lf
@@ -902,9 +907,26 @@ def multi_gpu(args):
     dist.destroy_process_group()
 
 
+def shape_only(args):
+    """One fold shape alone (for rocprofv3 PMC passes): the local fold (8 x 32 MiB -> 1) or the
+    node-form Allreduce at 256 / 16 MiB per rank, 40 launches after warm-up."""
+    import torch
+    import ext_mpi_collectives_amd as emac
+    emac.lib()
+    MB = (256 if args.shape != "node16" else 16) * MIB
+    if args.shape == "local256":
+        r = comm_shape_fold(8, MB // 8 // 4, torch.float32, emac.FLOAT, 40)
+    else:
+        r = node_run(8, MB // 4, torch.float32, emac.FLOAT, "6;1 -8 8", 40, 4, alloc="hip")
+        r = {"avg_launch_us": round(r["event_ms"] * 1e3 / 40, 2), "checked": r["checked"]}
+    print(json.dumps({"shape": args.shape, **r}), flush=True)
+
+
 def main():
     args = parse()
-    if args.child_transport:
+    if args.shape:
+        shape_only(args)
+    elif args.child_transport:
         transport_child(args)
     elif int(os.environ.get("WORLD_SIZE", "1")) > 1:
         multi_gpu(args)

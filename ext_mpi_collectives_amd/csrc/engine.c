@@ -166,6 +166,8 @@ typedef struct {
   int fused; /* whole Allreduce in one launch (emac_gpu_fold_fused) */
   void *ev_release; /* system-scope release recorded before every phase-0 barrier */
   emac_launch pull; /* every other owner's result copied into this rank's receive buffer */
+  void *graph[32];  /* COMM form: captured legs, per subset of EXT_MPI_AMD_LEG_* (graph_ok) */
+  unsigned char graph_failed[32];
   emac_pipe *pipe; /* pipelined host staging (NODE form), or NULL */
 } emac_handle;
 
@@ -222,6 +224,7 @@ static void release(emac_handle *h) {
   }
   for (r = 0; r < h->nmapped; r++) ipc_unmap(h->mapped[r]);
   emac_gpu_event_destroy(h->ev_release);
+  for (r = 0; r < 32; r++) emac_gpu_graph_destroy(h->graph[r]);
   if (h->kind == KIND_IPC && h->slot_held) {
     emac_comm *cm = &comms[h->comm];
     cm->slot_used[h->slot] = 0;
@@ -1374,14 +1377,11 @@ static int pipe_start(emac_handle *h) {
   return 0;
 }
 
-int ext_mpi_amd_start_legs(int handle, int legs) {
-  emac_handle *h = get(handle);
+/* Everything a Start (or a subset of its legs) enqueues on the handle's stream. */
+static int enqueue_legs(emac_handle *h, int legs) {
   int rc, multi;
   const int core = EXT_MPI_AMD_LEG_REDUCE_SCATTER | EXT_MPI_AMD_LEG_FOLD | EXT_MPI_AMD_LEG_ALLGATHER;
-  if (!h) return EMAC_ERR_ARG;
   multi = h->kind == KIND_COMM && h->plan.nranks > 1;
-  if (emac_gpu_set_device(h->device)) return EMAC_ERR_DEVICE;
-  if (h->pipe && (legs & EXT_MPI_AMD_LEG_ALL) == EXT_MPI_AMD_LEG_ALL) return pipe_start(h);
   if ((legs & EXT_MPI_AMD_LEG_STAGE_IN) && (rc = stage_in(h))) return rc;
   if (h->kind == KIND_IPC && h->fused && (legs & core) == core) {
     emac_comm *cm = &comms[h->comm];
@@ -1397,7 +1397,6 @@ int ext_mpi_amd_start_legs(int handle, int legs) {
                                   cm->timeout_ticks, e0, e1, h->stream)))
       return rc;
     if ((legs & EXT_MPI_AMD_LEG_STAGE_OUT) && (rc = stage_out(h))) return rc;
-    h->started = 1;
     return 0;
   }
   if ((legs & EXT_MPI_AMD_LEG_REDUCE_SCATTER) && h->kind == KIND_IPC && h->plan.nranks > 1 &&
@@ -1422,6 +1421,46 @@ int ext_mpi_amd_start_legs(int handle, int legs) {
       return rc;
   }
   if ((legs & EXT_MPI_AMD_LEG_STAGE_OUT) && (rc = stage_out(h))) return rc;
+  return 0;
+}
+
+/* COMM form with device buffers: the legs of a Start captured once into a HIP graph (RCCL's
+   grouped send/recv, the fold and its edge launch) and replayed by one hipGraphLaunch, per
+   subset of legs. EXT_MPI_AMD_GRAPH=0 disables it; a capture that fails falls back to eager
+   launches for good (graph_failed). Host buffers (pageable staging copies) are never captured. */
+static int graph_ok(const emac_handle *h) {
+  const char *e = getenv("EXT_MPI_AMD_GRAPH");
+  int r;
+  if (h->kind != KIND_COMM || (e && atoi(e) <= 0)) return 0;
+  for (r = 0; r < h->nbuf; r++)
+    if (h->send_mirror[r] || h->recv_mirror[r]) return 0;
+  return 1;
+}
+
+int ext_mpi_amd_start_legs(int handle, int legs) {
+  emac_handle *h = get(handle);
+  int rc, key;
+  if (!h) return EMAC_ERR_ARG;
+  if (emac_gpu_set_device(h->device)) return EMAC_ERR_DEVICE;
+  if (h->pipe && (legs & EXT_MPI_AMD_LEG_ALL) == EXT_MPI_AMD_LEG_ALL) return pipe_start(h);
+  key = legs & EXT_MPI_AMD_LEG_ALL;
+  if (graph_ok(h) && !h->graph[key] && !h->graph_failed[key]) {
+    if (emac_gpu_capture_begin(h->stream) == 0) {
+      const int erc = enqueue_legs(h, legs);
+      const int crc = emac_gpu_capture_end(h->stream, &h->graph[key]);
+      if (erc || crc) {
+        h->graph[key] = NULL;
+        h->graph_failed[key] = 1;
+      }
+    } else {
+      h->graph_failed[key] = 1;
+    }
+  }
+  if (h->graph[key]) {
+    if ((rc = emac_gpu_graph_launch(h->graph[key], h->stream))) return rc;
+  } else if ((rc = enqueue_legs(h, legs))) {
+    return rc;
+  }
   h->started = 1;
   return 0;
 }

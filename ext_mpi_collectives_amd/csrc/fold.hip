@@ -279,6 +279,27 @@ int emac_gpu_event_record(void *ev, void *stream) {
 int emac_gpu_stream_wait(void *stream, void *ev) {
   return ok(hipStreamWaitEvent(static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(ev), 0));
 }
+int emac_gpu_capture_begin(void *stream) {
+  return ok(hipStreamBeginCapture(static_cast<hipStream_t>(stream), hipStreamCaptureModeThreadLocal));
+}
+int emac_gpu_capture_end(void *stream, void **exec) {
+  hipGraph_t g = nullptr;
+  hipGraphExec_t x = nullptr;
+  *exec = nullptr;
+  int rc = ok(hipStreamEndCapture(static_cast<hipStream_t>(stream), &g));
+  if (!rc && g) rc = ok(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
+  if (g) (void)hipGraphDestroy(g);
+  if (rc || !x) {
+    clear_error("emac_gpu_capture_end");
+    return rc ? rc : EMAC_ERR_DEVICE;
+  }
+  *exec = x;
+  return 0;
+}
+int emac_gpu_graph_launch(void *exec, void *stream) {
+  return ok(hipGraphLaunch(static_cast<hipGraphExec_t>(exec), static_cast<hipStream_t>(stream)));
+}
+int emac_gpu_graph_destroy(void *exec) { return exec ? ok(hipGraphExecDestroy(static_cast<hipGraphExec_t>(exec))) : 0; }
 
 }  // extern "C"
 

@@ -64,6 +64,11 @@ int emac_gpu_event_create(void **ev); /* timing disabled */
 int emac_gpu_event_destroy(void *ev);
 int emac_gpu_event_record(void *ev, void *stream);
 int emac_gpu_stream_wait(void *stream, void *ev); /* stream waits for ev */
+/* stream capture into an instantiated graph (thread-local capture mode) */
+int emac_gpu_capture_begin(void *stream);
+int emac_gpu_capture_end(void *stream, void **exec); /* ends the capture; exec NULL on failure */
+int emac_gpu_graph_launch(void *exec, void *stream);
+int emac_gpu_graph_destroy(void *exec);
 
 /* ---- peer-mapped (IPC) form, ipc.hip ----
    Per-communicator synchronisation block, in uncached device memory and mapped by every peer:

@@ -317,7 +317,7 @@ def test_fold_handle_and_copy_reduce(code, nsrc, ndst):
             assert np.array_equal(d.cpu().numpy().view(np.uint8), want.view(np.uint8)), (how, nsrc, ndst)
 
 
-def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=None, op=emac.SUM):
+def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=None, op=emac.SUM, repeats=1):
     """COMM form (one rank per communicator) on the in-process loopback transport: the legs run
     on every rank in lock-step -- stage-in, reduce-scatter, fold, all-gather, stage-out -- so
     the staging slots, fold buckets and leg programs of the multi-GPU path execute on one GPU."""
@@ -342,12 +342,17 @@ def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=Non
     try:
         for r in range(R):
             hs.append(emac.allreduce_init(ptrs[r][0], ptrs[r][1], count, code, comms[r], copyin, op=op))
-        torch.cuda.synchronize()
-        for leg in (emac.LEG_STAGE_IN, emac.LEG_REDUCE_SCATTER, emac.LEG_FOLD, emac.LEG_ALLGATHER, emac.LEG_STAGE_OUT):
-            for h in hs:
-                emac.start_legs(h, leg)
-            for h in hs:
-                emac.wait(h)
+        for rep in range(repeats):
+            if rep and not host and not in_place:  # the receive buffers forget the previous result
+                for t in rbufs:
+                    t.fill_(-1)
+            torch.cuda.synchronize()
+            for leg in (emac.LEG_STAGE_IN, emac.LEG_REDUCE_SCATTER, emac.LEG_FOLD, emac.LEG_ALLGATHER,
+                        emac.LEG_STAGE_OUT):
+                for h in hs:
+                    emac.start_legs(h, leg)
+                for h in hs:
+                    emac.wait(h)
     finally:
         for h in hs:
             emac.done(h)
@@ -369,6 +374,41 @@ def test_comm_form_loopback_parity(oracle, R, copyin, code):
         want = oracle.allreduce(sends, copyin)
         got = run_comm_loopback(sends, code, copyin, phase=[(r * 3) % 4 for r in range(R)])
         assert_bitwise(got, want, f"comm R={R} {copyin} code={code} n={count}")
+
+
+@pytest.mark.parametrize("graph", ["0", "1"])
+def test_comm_form_graph_and_eager(oracle, monkeypatch, graph):
+    """The COMM form's legs captured into HIP graphs (one per subset of legs, replayed by
+    hipGraphLaunch) and launched eagerly (EXT_MPI_AMD_GRAPH=0): both bit-exact against the oracle
+    on the loopback transport, every leg's graph replayed three times (receive buffers reset
+    between replays)."""
+    monkeypatch.setenv("EXT_MPI_AMD_GRAPH", graph)
+    for R, copyin, code in [(4, "6;1 -2 -2 2 2", emac.FLOAT), (8, "6;1 -8 8", emac.DOUBLE), (3, "6;-64 -3 3", emac.INT)]:
+        sends = xorshift_inputs(R, 4099 + R, code, seed_base=0x6A0000 + R)
+        want = oracle.allreduce(sends, copyin)
+        got = run_comm_loopback(sends, code, copyin, phase=[(r * 3) % 4 for r in range(R)], repeats=3)
+        assert_bitwise(got, want, f"graph={graph} R={R} {copyin}")
+
+
+def test_comm_single_rank_rccl_graph_replays(monkeypatch):
+    """One persistent handle on a 1-rank RCCL communicator started 5 times with new data: the
+    graph captured at the first Start is replayed and sees every new input."""
+    monkeypatch.setenv("EXT_MPI_AMD_GRAPH", "1")
+    uid = emac.get_unique_id()
+    comm = emac.comm_init(0, 1, uid, 0)
+    x = torch.empty(70001, dtype=torch.float32, device="cuda")
+    y = torch.empty_like(x)
+    h = emac.allreduce_init(x.data_ptr(), y.data_ptr(), x.numel(), emac.FLOAT, comm)
+    try:
+        for it in range(5):
+            x.uniform_(-1, 1)
+            torch.cuda.synchronize()
+            emac.start(h)
+            emac.wait(h)
+            assert torch.equal(x, y), it
+    finally:
+        emac.done(h)
+        emac.comm_free(comm)
 
 
 @pytest.mark.parametrize("in_place", [False, True])
