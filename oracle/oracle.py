@@ -2,8 +2,10 @@
 
 Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg may import this
 module. It loads ``oracle/liboracle.so`` (built by ``oracle/Makefile``), a C restatement of the
-reference's method-6 schedule (src/core/reduce_copyin.c:375-427, :482-486, :674-842,
-:970-1084, :1418-1681) and of its MPI_SUM loops (src/mpi/ext_mpi_native_exec.c:207-234).
+reference's copy-in schedules -- method 6 recursive (src/core/reduce_copyin.c:674-842), 5 cyclic
+(:531-634), 7 tree (:844-968), 8-10 the same on a staging copy, with :375-427, :482-486,
+:970-1084, :1418-1681 around them -- of the buffer-table rotation (src/mpi/ext_mpi_xpmem.c:114-130)
+and of its SUM/MIN/MAX loops (src/mpi/ext_mpi_native_exec.c:207-318).
 See oracle/ref_oracle.h for the per-function citations.
 """
 import ctypes
@@ -76,6 +78,15 @@ def lib():
         _lib.ref_cpu_allreduce_threads.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_int,
                                                    ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p),
                                                    ctypes.POINTER(ctypes.c_void_p), ctypes.c_long]
+        _lib.ref_emulate_op_s.restype = ctypes.c_int
+        _lib.ref_emulate_op_s.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                                          ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                          ctypes.POINTER(ctypes.c_void_p)]
+        _lib.ref_get_rank_cyclic.restype = ctypes.c_int
+        _lib.ref_get_rank_cyclic.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                             ctypes.c_int]
+        _lib.ref_decode_peer.restype = ctypes.c_int
+        _lib.ref_decode_peer.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         _lib.ref_cpu_allreduce_threads_sets.restype = ctypes.c_double
         _lib.ref_cpu_allreduce_threads_sets.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_char_p,
                                                         ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
@@ -122,8 +133,9 @@ def _ptrs(arrays):
     return (ctypes.c_void_p * len(arrays))(*[a.ctypes.data for a in arrays])
 
 
-def allreduce(sends, copyin, in_place=False, op=SUM):
-    """Reference result of an R-rank Allreduce(op: SUM, MIN or MAX) of the host arrays ``sends``.
+def allreduce(sends, copyin, in_place=False, op=SUM, num_sockets=1):
+    """Reference result of an R-rank Allreduce(op: SUM, MIN or MAX) of the host arrays ``sends``
+    (copy-in methods 5-10 of the reference's single-node generators, num_sockets per node).
 
     Returns the list of R receive arrays (all equal for a correct schedule).
     """
@@ -136,7 +148,8 @@ def allreduce(sends, copyin, in_place=False, op=SUM):
         recvs = [s.copy() for s in sends]
     else:
         recvs = [np.full_like(s, -1) for s in sends]
-    rc = lib().ref_emulate_op(R, a0.size, code, op, copyin.encode(), int(in_place), _ptrs(sends), _ptrs(recvs))
+    rc = lib().ref_emulate_op_s(R, a0.size, code, op, copyin.encode(), int(in_place), num_sockets, _ptrs(sends),
+                                _ptrs(recvs))
     if rc != 0:
         raise ValueError(f"oracle rejected copyin {copyin!r} for R={R}")
     return recvs
@@ -175,3 +188,14 @@ def cpu_allreduce_threads_sets(sets, copyin, iters):
     if t < 0:
         raise ValueError("cpu baseline failed")
     return t
+
+
+def get_rank_cyclic(num_sockets, R, ranks, me_pos, other_pos):
+    """reduce_copyin.c:482-486: the buffer-table index of position other_pos seen from me_pos."""
+    arr = (ctypes.c_int * R)(*ranks)
+    return lib().ref_get_rank_cyclic(num_sockets, R, arr, me_pos, other_pos)
+
+
+def decode_peer(num_sockets, R, me, index):
+    """ext_mpi_xpmem.c:114-130: node rank whose buffer sits at table index `index` of node rank me."""
+    return lib().ref_decode_peer(num_sockets, R, me, index)

@@ -1,7 +1,7 @@
 /*
  * ref_emulate.c -- TEST INFRASTRUCTURE ONLY.
  *
- * Single-process emulator of an R-rank, single-node ext_mpi Allreduce (copy-in method 6):
+ * Single-process emulator of an R-rank, single-node ext_mpi Allreduce (copy-in methods 5-10):
  * every rank's copy-in and copy-out program (ref_schedule.c) is executed against host
  * buffers, phase by phase. A phase ends at a SET_NODE_BARRIER line; the reference orders
  * each step after its partners' previous step with pairwise spin flags
@@ -21,22 +21,22 @@ typedef struct {
   int pc;
 } rank_prog;
 
-static int build_programs(int R, long count, int dtype, const char *copyin, int in_place,
+static int build_programs(int R, long count, int dtype, const char *copyin, int in_place, int num_sockets,
                           rank_prog *progs) {
   int method, factors[MAX_FACTORS], nf, r, cap;
   long bytes = count * (long)ref_type_size(dtype);
   nf = ref_parse_copyin(copyin, &method, factors, MAX_FACTORS);
   if (nf < 1) return -1;
   cap = 8 * R * (R + 8) * (factors[0] > 0 ? factors[0] : 1) + 256;
-  if (method != 6 && method != 9) return -1; /* 9 = the same generator on shm staging */
+  if (method < 5 || method > 10) return -1; /* 8 / 9 / 10 = 5 / 6 / 7 on shm staging */
   for (r = 0; r < R; r++) {
     int n1, n2;
     progs[r].ops = (ref_op *)malloc(sizeof(ref_op) * (size_t)cap * 2);
     progs[r].pc = 0;
-    n1 = ref_schedule(R, r, bytes, dtype, factors, nf, in_place, 1, progs[r].ops, cap);
+    n1 = ref_schedule_m(R, r, bytes, dtype, method, num_sockets, factors, nf, in_place, 1, progs[r].ops, cap);
     if (n1 < 0) return -1;
     progs[r].ops[n1].op = REF_OP_PHASE; /* copy-in and copy-out are separate stages */
-    n2 = ref_schedule(R, r, bytes, dtype, factors, nf, in_place, 2, progs[r].ops + n1 + 1, cap);
+    n2 = ref_schedule_m(R, r, bytes, dtype, method, num_sockets, factors, nf, in_place, 2, progs[r].ops + n1 + 1, cap);
     if (n2 < 0) return -1;
     progs[r].n = n1 + 1 + n2;
   }
@@ -60,6 +60,11 @@ int ref_emulate(int R, long count, int dtype, const char *copyin, int in_place,
 
 int ref_emulate_op(int R, long count, int dtype, int red, const char *copyin, int in_place,
                    void *const *sendbufs, void *const *recvbufs) {
+  return ref_emulate_op_s(R, count, dtype, red, copyin, in_place, 1, sendbufs, recvbufs);
+}
+
+int ref_emulate_op_s(int R, long count, int dtype, int red, const char *copyin, int in_place, int num_sockets,
+                     void *const *sendbufs, void *const *recvbufs) {
   rank_prog *progs;
   void *const *send = in_place ? recvbufs : sendbufs;
   int r, active, rc = 0;
@@ -69,7 +74,7 @@ int ref_emulate_op(int R, long count, int dtype, int red, const char *copyin, in
     return 0;
   }
   progs = (rank_prog *)calloc((size_t)R, sizeof(rank_prog));
-  if (build_programs(R, count, dtype, copyin, in_place, progs)) {
+  if (build_programs(R, count, dtype, copyin, in_place, num_sockets, progs)) {
     rc = -1;
     goto done;
   }
@@ -97,5 +102,5 @@ void ref_kat_fill(void *buf, long count, int tsize, int world_rank, long add) {
 
 /* exported for the threaded baseline */
 int ref_build_programs_(int R, long count, int dtype, const char *copyin, int in_place, void *progs_out) {
-  return build_programs(R, count, dtype, copyin, in_place, (rank_prog *)progs_out);
+  return build_programs(R, count, dtype, copyin, in_place, 1, (rank_prog *)progs_out);
 }

@@ -1,25 +1,32 @@
 /*
  * ref_oracle.h -- TEST INFRASTRUCTURE ONLY (the parity checker, never the product).
  *
- * CPU restatement of ext_mpi_collectives' single-node, copy-in method 6 ("recursive")
- * Allreduce schedule and of its element-wise MPI_SUM loops. Only tests/, the smoke()
+ * CPU restatement of ext_mpi_collectives' single-node copy-in schedules -- methods 5
+ * ("cyclic"), 6 ("recursive") and 7 ("tree"), 8 / 9 / 10 being the same on a staging copy --
+ * and of its element-wise MPI_SUM / MIN / MAX loops. Only tests/, the smoke()
  * hook and bench.py's cpu_baseline leg may load this library.
  *
  * Reference files restated (paths relative to the reference checkout):
  *   src/mpi/ext_mpi_native_exec.c:207-318    reduction(), SUM/MIN/MAX      -> ref_reduction.c
  *   src/core/reduce_copyin.c:396-427         ext_mpi_sizes_displs          -> ref_schedule.c
  *   src/core/reduce_copyin.c:375-394         ext_mpi_rank_order            -> ref_schedule.c
- *   src/core/reduce_copyin.c:482-486         get_rank_cyclic (1 socket)    -> ref_schedule.c
+ *   src/core/reduce_copyin.c:482-486         get_rank_cyclic               -> ref_schedule.c
+ *   src/core/reduce_copyin.c:531-634         reduce_copies_cyclic          -> ref_schedule.c
+ *   src/core/reduce_copyin.c:844-968         reduce_copies_tree            -> ref_schedule.c
  *   src/core/reduce_copyin.c:674-842         reduce_copies_recursive       -> ref_schedule.c
  *   src/core/reduce_copyin.c:970-1084        reduce_copies_one_socket      -> ref_schedule.c
  *   src/core/reduce_copyin.c:1418-1681       allreduce_copyin / _copyout   -> ref_schedule.c
- *   src/mpi/ext_mpi_xpmem.c:114-130          rank-relative buffer rotation -> ref_emulate.c
+ *   src/mpi/ext_mpi_xpmem.c:114-130          rank-relative buffer rotation -> ref_emulate.c, ref_schedule.c
+ *   src/gpu/cuda_shmem.c:280-296             (the same rotation, device)   -> ref_schedule.c
  *   src/mpi/ext_mpi_native_exec.c:21-84      node barriers (as phases)     -> ref_emulate.c
  *   src/mpi/debug_persistent.c:426-497       known-answer input pattern    -> ref_emulate.c
  *
  * Parity pinning: the reference's own known-answer test pattern (debug_persistent.c) and the
  * method-6 schedules captured from the reference generators, both
  * committed under tests/golden/. The reference itself may not be executed here.
+ * Methods 5 / 7 / 8 / 10 and num_sockets > 1 have no captured schedule: they are pinned by the
+ * known-answer pattern (integer sums) and by an independent algebraic statement of each fold
+ * order in tests/test_oracle.py -- "restatement-pinned", see DESIGN.md section 2.
  */
 #ifndef REF_ORACLE_H_
 #define REF_ORACLE_H_
@@ -71,6 +78,13 @@ int ref_parse_copyin(const char *s, int *method, int *factors, int max_factors);
  */
 int ref_schedule(int R, int node_rank, long bytes, int dtype, const int *factors, int nfactors,
                  int in_place, int stage, ref_op *out, int cap);
+/* the same for copy-in method 5..10 and EXT_MPI_NUM_SOCKETS_PER_NODE = num_sockets */
+int ref_schedule_m(int R, int node_rank, long bytes, int dtype, int method, int num_sockets, const int *factors,
+                   int nfactors, int in_place, int stage, ref_op *out, int cap);
+/* get_rank_cyclic (reduce_copyin.c:482-486) and the buffer table that decodes it
+   (ext_mpi_xpmem.c:114-130): the node rank found at table index `index` of node rank `me` */
+int ref_get_rank_cyclic(int num_sockets, int R, const int *ranks, int me_pos, int other_pos);
+int ref_decode_peer(int num_sockets, int R, int me, int index);
 
 /*
  * Single-process emulation of an R-rank Allreduce: executes every rank's copy-in then
@@ -84,6 +98,9 @@ int ref_emulate(int R, long count, int dtype, const char *copyin, int in_place,
 /* the same with element operation `op` (REF_RED_*) on every SREDUCE line */
 int ref_emulate_op(int R, long count, int dtype, int op, const char *copyin, int in_place,
                    void *const *sendbufs, void *const *recvbufs);
+/* ... and with num_sockets sockets per node (changes the tree method's roots) */
+int ref_emulate_op_s(int R, long count, int dtype, int op, const char *copyin, int in_place, int num_sockets,
+                     void *const *sendbufs, void *const *recvbufs);
 
 /* Known-answer input pattern of debug_persistent.c:491-497 (CPU: add=73, GPU: add=0). */
 void ref_kat_fill(void *buf, long count, int tsize, int world_rank, long add);

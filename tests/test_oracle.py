@@ -53,21 +53,25 @@ def test_sizes_displs(oracle):
 
 
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(HERE, "golden", "kat_*.npz"))))
-@pytest.mark.parametrize("copyin_kind", ["linear", "chain"])
+@pytest.mark.parametrize("copyin_kind", ["linear", "chain", "cyclic", "cyclic_chain", "tree", "tree2s", "staged"])
 def test_known_answer(oracle, path, copyin_kind):
+    # the known answer holds for every copy-in method (5 cyclic, 6 recursive, 7 tree; 8-10 the
+    # same on a staging copy) and for two sockets per node
     f = np.load(path)
     R, count, itemsize, add = (int(x) for x in f["meta"])
-    if copyin_kind == "linear":
-        copyin = f"6;1 -{R} {R}"
-    else:
-        copyin = "6;1 " + " ".join(["-2"] * (R.bit_length() - 1) + ["2"] * (R.bit_length() - 1))
+    k = R.bit_length() - 1
+    chain = " ".join(["-2"] * k + ["2"] * k)
+    copyin, sockets = {"linear": (f"6;1 -{R} {R}", 1), "chain": ("6;1 " + chain, 1),
+                       "cyclic": (f"5;1 -{R} {R}", 1), "cyclic_chain": ("5;1 " + chain, 2),
+                       "tree": ("7;1 " + chain, 1), "tree2s": ("7;1 " + chain, 2),
+                       "staged": (f"10;2 -{R} {R}", 1)}[copyin_kind]
     code = oracle.INT if itemsize == 4 else oracle.LONG
     ins = [oracle.kat_fill(count, code, r, add) for r in range(R)]
     for r in range(R):
         assert np.array_equal(ins[r], f["inputs"][r])  # the C fill restates debug_persistent.c
-    for out in oracle.allreduce(ins, copyin):
+    for out in oracle.allreduce(ins, copyin, num_sockets=sockets):
         assert np.array_equal(out, f["expected"])
-    for out in oracle.allreduce([x.copy() for x in ins], copyin, in_place=True):
+    for out in oracle.allreduce([x.copy() for x in ins], copyin, in_place=True, num_sockets=sockets):
         assert np.array_equal(out, f["expected"])
 
 
@@ -143,3 +147,128 @@ def test_min_max_nan_follows_the_accumulator_rule(oracle):
     z = [np.array([0.0, -0.0], np.float64), np.array([-0.0, 0.0], np.float64)]
     out = oracle.allreduce(z, "6;1 -2 2", op=oracle.MIN)[0]
     assert np.signbit(out).tolist() == [False, False]
+
+
+@pytest.mark.parametrize("R,sockets", [(2, 2), (4, 2), (6, 2), (6, 3), (8, 2), (8, 4), (12, 3), (16, 2), (16, 4)])
+def test_get_rank_cyclic_decodes_to_the_node_rank(oracle, R, sockets):
+    # reduce_copyin.c:482-486 encodes a peer position as a buffer-table index; the table of
+    # ext_mpi_xpmem.c:114-130 (socket-base rotation, then a per-socket rotation) must decode it
+    # to the peer's node rank for every rank order the generators use
+    for ranks in (list(range(R)), oracle.rank_order(R, [-2] * (R.bit_length() - 1)) if R & (R - 1) == 0
+                  else list(range(R))[::-1]):
+        for me in range(R):
+            for other in range(R):
+                idx = oracle.get_rank_cyclic(sockets, R, ranks, me, other)
+                assert 0 <= idx < R
+                assert oracle.decode_peer(sockets, R, ranks[me], idx) == ranks[other]
+                # with one socket the encoding is the plain rank difference
+                assert oracle.get_rank_cyclic(1, R, ranks, me, other) == (ranks[other] - ranks[me]) % R
+
+
+def _chunks(oracle, n, R, f0, itemsize):
+    """element ranges [lo, hi) of chunk j of every piece (reduce_copyin.c:396-427, :1035-1081)"""
+    pieces = []
+    if f0 < 0:
+        s, d = oracle.sizes_displs(R, n * itemsize, itemsize, -f0)
+        return [[(d[j] // itemsize, (d[j] + s[j]) // itemsize) for j in range(R)]]
+    base, extra = divmod(n, f0)
+    first = 0
+    for i in range(f0):
+        ln = base + (i < extra)
+        s, d = oracle.sizes_displs(R, ln * itemsize, itemsize)
+        pieces.append([(first + d[j] // itemsize, first + (d[j] + s[j]) // itemsize) for j in range(R)])
+        first += ln
+    return pieces
+
+
+def _fold(vals):
+    acc = vals[0].copy()
+    for v in vals[1:]:
+        acc = (acc + v).astype(acc.dtype)
+    return acc
+
+
+def _cyclic_statement(sends, R, rs):
+    """Method 5 (reduce_copyin.c:531-634) as algebra: after step s, position p holds for chunk
+    c in [p, p + gb_s) the left fold [own, p - gb_s, p - 2 gb_s, ...] of the step s-1 partials;
+    chunk c ends complete at position c. Identity rank order. Returns value(c) callables."""
+    gbs = [int(np.prod(rs[s + 1:])) for s in range(len(rs))]
+
+    def v(s, p, c, lo, hi):
+        if s < 0:
+            return sends[p][lo:hi]
+        return _fold([v(s - 1, (p - gbs[s] * q) % R, c, lo, hi) for q in range(rs[s])])
+    return lambda c, lo, hi: v(len(rs) - 1, c, c, lo, hi)
+
+
+def _tree_statement(sends, R, rs, ranks, sockets):
+    """Method 7 (reduce_copyin.c:844-968) as algebra over positions: step s folds, into the
+    buffer of root = gb_s * sock + r, the step s-1 partials of positions gb_s * q + r (root
+    first, then q != sock ascending); sock = p / (R / |f_s|) at gb_s == 1 with several sockets."""
+    gbs = [int(np.prod(rs[s + 1:])) for s in range(len(rs))]
+
+    def sock(s, p):
+        return p // (R // rs[s]) if sockets > 1 and gbs[s] == 1 else 0
+
+    def v(s, rho, j, lo, hi):
+        if s < 0:
+            return sends[ranks[rho]][lo:hi]
+        gb = gbs[s]
+        r = rho % gb
+        k = sock(s, (j // gb) * gb + r)
+        assert rho == gb * k + r
+        return _fold([v(s - 1, rho, j, lo, hi)] + [v(s - 1, gb * q + r, j, lo, hi) for q in range(rs[s]) if q != k])
+    last = len(rs) - 1
+    return lambda j, lo, hi: v(last, sock(last, j), j, lo, hi)
+
+
+@pytest.mark.parametrize("copyin,R,sockets", [
+    ("5;1 -4 4", 4, 1), ("5;1 -2 -2 2 2", 4, 1), ("5;1 -2 -3 3 2", 6, 1), ("5;1 -2 -2 -2 2 2 2", 8, 2),
+    ("5;3 -4 -2 8", 8, 1), ("5;-40 -4 4", 4, 1), ("8;1 -3 -2 6", 6, 1),
+    ("7;1 -2 -2 2 2", 4, 1), ("7;1 -2 -2 -2 2 2 2", 8, 1), ("7;1 -2 -2 -2 2 2 2", 8, 2), ("7;1 -4 -2 2 4", 8, 2),
+    ("7;1 -2 -4 4 2", 8, 4), ("7;1 -3 -2 2 3", 6, 2), ("7;1 -3 -2 2 3", 6, 3), ("7;2 -2 -2 2 2", 4, 1),
+    ("10;1 -2 -3 3 2", 6, 3), ("7;1 -8 8", 8, 1)])
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_cyclic_and_tree_fold_order_independent_statement(oracle, copyin, R, sockets, dt):
+    method, factors = oracle.parse_copyin(copyin)
+    base = method - 3 if method >= 8 else method
+    rs = [-f for f in factors[1:] if f < 0]
+    rng = np.random.default_rng(R * 31 + len(rs))
+    n = 397
+    sends = [((rng.random(n) * 2 - 1) * 10.0 ** rng.integers(-3, 4, n)).astype(dt) for _ in range(R)]
+    if base == 5:
+        value = _cyclic_statement(sends, R, rs)
+    else:
+        ranks = oracle.rank_order(R, [f for f in factors[1:] if f < 0])
+        value = _tree_statement(sends, R, rs, ranks, sockets)
+    want = np.empty(n, dt)
+    for piece in _chunks(oracle, n, R, factors[0], np.dtype(dt).itemsize):
+        for j, (lo, hi) in enumerate(piece):
+            if hi > lo:
+                want[lo:hi] = value(j, lo, hi)
+    for out in oracle.allreduce(sends, copyin, num_sockets=sockets):
+        assert np.array_equal(out.view(np.uint8), want.view(np.uint8)), copyin
+    for out in oracle.allreduce([x.copy() for x in sends], copyin, in_place=True, num_sockets=sockets):
+        assert np.array_equal(out.view(np.uint8), want.view(np.uint8)), copyin
+
+
+def test_methods_give_distinct_fold_orders(oracle):
+    # the cyclic and tree parity tests only bite if their bits differ from method 6's (radix-2
+    # steps are commutative single adds, so only radices > 2 separate the orders; the socket
+    # count moves the tree's last-step roots, visible with a last radix > 2)
+    rng = np.random.default_rng(3)
+    sends = [(rng.random(4096) * 2 - 1).astype(np.float32) for _ in range(8)]
+    outs = {c: oracle.allreduce(sends, c, num_sockets=s)[0] for c, s in
+            (("6;1 -4 -2 2 4", 1), ("5;1 -4 -2 2 4", 1), ("7;1 -4 -2 2 4", 1), ("7;1 -2 -4 4 2", 1),
+             ("7;1 -2 -4 4 2", 4))}
+    keys = list(outs)
+    for i in range(len(keys)):
+        for j in range(i + 1, len(keys)):
+            assert not np.array_equal(outs[keys[i]], outs[keys[j]]), (keys[i], keys[j])
+
+
+def test_tree_without_allgather_radices_is_rejected(oracle):
+    # reduce_copyin.c:962-964: "reduce_copies_tree not implemented"
+    sends = [np.ones(16, np.float32)] * 4
+    with pytest.raises(ValueError):
+        oracle.allreduce(sends, "7;1 -4")
