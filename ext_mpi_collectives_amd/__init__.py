@@ -102,6 +102,8 @@ def lib():
                                                 P(ctypes.c_ubyte), P(c_int)]
         L.ext_mpi_amd_comm_program.argtypes = [c_int, c_int, c_long, c_int, ctypes.c_char_p, c_long,
                                                P(P2P), c_int, P(c_int), P(FoldDesc), c_int, P(c_int), P(c_long)]
+        L.ext_mpi_amd_set_num_sockets.argtypes = [c_int]
+        L.ext_mpi_amd_set_num_sockets.restype = c_int
         L.ext_mpi_amd_version.restype = ctypes.c_char_p
         L.ext_mpi_amd_gpu_malloc.argtypes = [P(c_void_p), ctypes.c_size_t]
         L.ext_mpi_amd_gpu_free.argtypes = [c_void_p]
@@ -286,6 +288,27 @@ def comm_program(nranks, rank, count, dtype, copyin=None, send_phase=0, max_ops=
     o = [(x.leg, x.peer, x.is_send, x.buf, x.offset, x.bytes) for x in ops[:nops.value]]
     f = [(x.offset, x.count, [(x.buf[t], x.leaf_offset[t]) for t in range(nranks)]) for x in folds[:nf.value]]
     return o, f, stage.value
+
+
+def set_num_sockets(sockets):
+    """EXT_MPI_NUM_SOCKETS_PER_NODE for every handle / plan made afterwards; returns the previous
+    value. Sockets move the tree method's (7 / 10) last-step roots, nothing else."""
+    return _check("ext_mpi_amd_set_num_sockets", lib().ext_mpi_amd_set_num_sockets(sockets))
+
+
+class num_sockets:
+    """``with num_sockets(2): ...`` -- set_num_sockets for the block, restored after."""
+
+    def __init__(self, sockets):
+        self.sockets = sockets
+
+    def __enter__(self):
+        self.prev = set_num_sockets(self.sockets)
+        return self
+
+    def __exit__(self, *exc):
+        set_num_sockets(self.prev)
+        return False
 
 
 def version():

@@ -360,13 +360,26 @@ static int upload_buckets(emac_handle *h, emac_bucket *b, int nb) {
   return rc;
 }
 
+/* EXT_MPI_NUM_SOCKETS_PER_NODE as the reference keeps it: one process-wide parameter read at
+   init (ext_mpi.c:43-187), applied to every plan built afterwards */
+static int g_num_sockets = 1;
+
+int ext_mpi_amd_set_num_sockets(int sockets) {
+  const int prev = g_num_sockets;
+  if (sockets < 1 || sockets > EMAC_MAX_RANKS) return EMAC_ERR_ARG;
+  g_num_sockets = sockets;
+  return prev;
+}
+
 static int parse_cfg(const char *copyin, int nranks, emac_copyin *cfg) {
+  int rc = 0;
   /* one rank: the generator returns before reading the factors (reduce_copyin.c:975) */
-  if (!copyin || !*copyin || nranks == 1) {
+  if (!copyin || !*copyin || nranks == 1)
     emac_default_copyin(nranks, cfg);
-    return 0;
-  }
-  return emac_parse_copyin(copyin, cfg);
+  else
+    rc = emac_parse_copyin(copyin, cfg);
+  cfg->sockets = g_num_sockets;
+  return rc;
 }
 
 static int finish_init(emac_handle *h, int *handle) {

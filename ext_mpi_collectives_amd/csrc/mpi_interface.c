@@ -15,7 +15,8 @@
  * broadcasts): EXT_MPI_COPYIN, EXT_MPI_VERBOSE, EXT_MPI_DEBUG (default 1: the known-answer
  * self-test of debug_persistent.c:393-568 runs inside every Allreduce_init),
  * EXT_MPI_NUM_SOCKETS_PER_NODE (any divisor of the node size: sockets change the reference's
- * partner encoding and barrier scope, not the fold arithmetic -- see oracle/ref_schedule.c). MPI_Info
+ * partner encoding and barrier scope, and the tree method's last-step roots -- the one place
+ * they reach the fold arithmetic, ext_mpi_amd_set_num_sockets). MPI_Info
  * key "ext_mpi_copyin" overrides nothing the environment sets (num_ports_factors.c:25-36:
  * env > info > default).
  *
@@ -90,6 +91,7 @@ static void read_env(void) {
   PMPI_Bcast(&len, 1, MPI_INT, 0, MPI_COMM_WORLD);
   if (len > 0) PMPI_Bcast(cfg_copyin, len, MPI_CHAR, 0, MPI_COMM_WORLD);
   cfg_has_copyin = len > 0;
+  if (cfg_num_sockets > 0) ext_mpi_amd_set_num_sockets(cfg_num_sockets);
 }
 
 /* ------------------------------------------- request -> handle map (hash_table.c:8-58) */
@@ -432,7 +434,7 @@ static int blocking_select_row(const bcomm *b, int side, long bytes) {
 static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int dtype, int op, int tsize, bcomm *b,
                               MPI_Comm comm) {
   size_t bytes = (size_t)count * (size_t)tsize, need, stride;
-  int on_dev, side, row, i, rc, slot = -1, in_place, rank;
+  int on_dev, side, row, i, rc, slot = -1, in_place, rank, row_sockets = 0;
   const char *copyin = NULL;
   const void *s;
   void *r;
@@ -454,6 +456,7 @@ static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int
     if (b->row[side][row].nodes != 1) return 1; /* inter-node row: not this path */
     if (b->row[side][row].sockets < 1 || size % b->row[side][row].sockets) return 1;
     copyin = b->row[side][row].copyin;
+    row_sockets = b->row[side][row].sockets;
   } else if (cfg_has_copyin) {
     copyin = cfg_copyin;
   }
@@ -512,7 +515,11 @@ static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int
     }
     bcomm_drop(b, slot);
     e = &b->cache[slot];
-    if ((rc = ext_mpi_amd_allreduce_init(s, r, count, dtype, op, b->ext_comm, copyin, &e->handle))) {
+    /* a parameter-file row names its own socket count (ext_mpi_native_blocking.c:189-290) */
+    const int prev_sockets = row_sockets > 0 ? ext_mpi_amd_set_num_sockets(row_sockets) : 0;
+    rc = ext_mpi_amd_allreduce_init(s, r, count, dtype, op, b->ext_comm, copyin, &e->handle);
+    if (prev_sockets > 0) ext_mpi_amd_set_num_sockets(prev_sockets);
+    if (rc) {
       e->handle = -1;
       return rc;
     }
@@ -580,7 +587,7 @@ int EXT_MPI_Allreduce_init(const void *sendbuf, void *recvbuf, int count, MPI_Da
   if (!initialised) EXT_MPI_Init();
   if (dtype < 0 || eop < 0 || count < 0) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
   if (sendbuf == MPI_IN_PLACE) sendbuf = recvbuf; /* ext_mpi.c:651-653 */
-  /* sockets only change the reference's partner encoding, not the arithmetic (plan.h) */
+  /* sockets change the partner encoding and the tree method's last roots (plan.h) */
   if (cfg_num_sockets > 1) {
     int size;
     PMPI_Comm_size(comm, &size);

@@ -82,10 +82,19 @@ void emac_default_copyin(int nranks, emac_copyin *out) {
   out->lv[0].ag[0] = nranks;
 }
 
+int emac_method_base(int method) { return method >= 8 && method <= 10 ? method - 3 : method; }
+
 int emac_validate_copyin(const emac_copyin *c, int nranks) {
-  int i, L, size = nranks, nlev = 0;
-  if (c->method != 6 && c->method != 9) return EMAC_ERR_UNSUPPORTED;
+  int i, L, size = nranks, nlev = 0, base = emac_method_base(c->method);
+  if (base < 5 || base > 7) return EMAC_ERR_UNSUPPORTED;
   if (c->nlv < 1) return EMAC_ERR_ARG;
+  if (c->sockets < 0 || (c->sockets > 1 && nranks % c->sockets)) return EMAC_ERR_ARG;
+  /* the cyclic and tree generators index their partners over the whole node: a sub-split
+     level would mix rank-relative and level-relative positions (reduce_copyin.c:540-560,
+     :866-880); only the recursive generator is defined on one */
+  if (base != 6 && c->nlv > 1) return EMAC_ERR_UNSUPPORTED;
+  /* reduce_copyin.c:962-964: the tree without allgather radices is not implemented */
+  if (base == 7 && c->lv[0].nag == 0) return EMAC_ERR_UNSUPPORTED;
   for (L = 0; L < c->nlv; L++) {
     const emac_level *v = &c->lv[L];
     int prs = 1, pag = 1, members = size;
@@ -196,6 +205,45 @@ static void tree_leaves(const emac_plan *pl, int L, int s, int P, int *out, int 
     if (q != qme) tree_leaves(pl, L, s - 1, base + (mbase + gb * q + m % gb) * g + o, out, k);
 }
 
+/* Method 5 (reduce_copyin.c:531-634): after step s position p holds, for its chunks, the left fold
+   of its own step s-1 partial and those of p - gb_s * q (q = 1 .. rs[s]-1, mod R); positions are
+   node ranks (identity order). */
+static void cyclic_leaves(const emac_plan *pl, int s, int p, int *out, int *k) {
+  const emac_level *v = &pl->cfg.lv[0];
+  const int R = pl->nranks;
+  int gb = 1, i, q;
+  if (s < 0) {
+    out[(*k)++] = pl->pos_rank[p];
+    return;
+  }
+  for (i = s + 1; i < v->nrs; i++) gb *= v->rs[i];
+  for (q = 0; q < v->rs[s]; q++) cyclic_leaves(pl, s - 1, ((p - gb * q) % R + R) % R, out, k);
+}
+
+/* Method 7 (reduce_copyin.c:844-968): step s folds into position rho = gb_s * socket + r the
+   step s-1 partials of rho, then of gb_s * q + r (q != socket ascending), r = rho mod gb_s;
+   socket = p / (R / rs[s]) for the writer p = (j / gb_s) * gb_s + r of chunk j at the step with
+   gb_s == 1 on a multi-socket node (:860-864), else 0. */
+static int tree_socket(const emac_plan *pl, int s, int gb, int p) {
+  const emac_level *v = &pl->cfg.lv[0];
+  return pl->cfg.sockets > 1 && gb == 1 ? p / (pl->nranks / v->rs[s]) : 0;
+}
+
+static void tree7_leaves(const emac_plan *pl, int s, int rho, int j, int *out, int *k) {
+  const emac_level *v = &pl->cfg.lv[0];
+  int gb = 1, i, q, r, sock;
+  if (s < 0) {
+    out[(*k)++] = pl->pos_rank[rho];
+    return;
+  }
+  for (i = s + 1; i < v->nrs; i++) gb *= v->rs[i];
+  r = rho % gb;
+  sock = tree_socket(pl, s, gb, (j / gb) * gb + r);
+  tree7_leaves(pl, s - 1, rho, j, out, k);
+  for (q = 0; q < v->rs[s]; q++)
+    if (q != sock) tree7_leaves(pl, s - 1, gb * q + r, j, out, k);
+}
+
 /* Replay codes of the composite tree: its levels are the reduce-scatter radices of level 0,
    then of level 1, ... (level 0's are the fastest-varying digits of the leaf index). */
 static void build_codes(const emac_copyin *c, emac_codes *codes) {
@@ -272,9 +320,10 @@ int emac_plan_build(emac_plan *p, int nranks, long count, int dtype, int op, con
     int rc = emac_validate_copyin(&p->cfg, nranks);
     if (rc) return rc;
   }
-  /* rank order from the leading reduce-scatter radices (ext_mpi_native.c:715-724) */
+  /* rank order from the leading reduce-scatter radices (ext_mpi_native.c:715-724); the cyclic
+     generator keeps the identity order (reduce_copyin.c:1487-1504) */
   for (i = 0; i < nranks; i++) p->pos_rank[i] = i;
-  position_order(nranks, p->cfg.lv[0].nrs, p->cfg.lv[0].rs, p->pos_rank);
+  if (emac_method_base(p->cfg.method) != 5) position_order(nranks, p->cfg.lv[0].nrs, p->cfg.lv[0].rs, p->pos_rank);
   for (i = 0; i < nranks; i++) p->rank_pos[p->pos_rank[i]] = i;
 
   p->npieces = 1;
@@ -301,10 +350,15 @@ int emac_plan_build(emac_plan *p, int nranks, long count, int dtype, int op, con
   free(clen);
   for (i = 0; i < nranks; i++) {
     k = 0;
+    const int last = p->cfg.lv[p->cfg.nlv - 1].nrs - 1;
     if (nranks == 1)
       p->leaf_rank[0][k++] = 0;
+    else if (emac_method_base(p->cfg.method) == 5)
+      cyclic_leaves(p, last, i, p->leaf_rank[i], &k);
+    else if (emac_method_base(p->cfg.method) == 7)
+      tree7_leaves(p, last, tree_socket(p, last, 1, i), i, p->leaf_rank[i], &k);
     else
-      tree_leaves(p, p->cfg.nlv - 1, p->cfg.lv[p->cfg.nlv - 1].nrs - 1, i, p->leaf_rank[i], &k);
+      tree_leaves(p, p->cfg.nlv - 1, last, i, p->leaf_rank[i], &k);
   }
   build_codes(&p->cfg, &p->codes);
   return EMAC_OK;

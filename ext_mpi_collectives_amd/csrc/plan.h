@@ -9,9 +9,18 @@
  *     sub-splits of the factor list (reduce_copies_one_socket, reduce_copyin.c:970-1084),
  *   - the permuted rank order of radix chains (reduce_copyin.c:375-394),
  *   - for every owner chunk, the exact fold tree its elements are summed in: the left fold
- *     of each recursive-halving step (own partial first, partners by ascending substep) nested
- *     step over step (reduce_copyin.c:687-744), flattened to a leaf order plus per-leaf
- *     level codes that a register-resident kernel replays without any intermediate buffer.
+ *     of each reduce-scatter step nested step over step, flattened to a leaf order plus
+ *     per-leaf level codes that a register-resident kernel replays without any intermediate
+ *     buffer. The three copy-in generators differ only in which partials a step folds and
+ *     where the result lands, never in the tree's shape:
+ *       method 6 recursive (reduce_copyin.c:687-744): own partial first, then the radix
+ *         group's partners by ascending substep, positions from ext_mpi_rank_order;
+ *       method 5 cyclic (:531-634): own partial, then positions p - gb, p - 2 gb, ...
+ *         (mod R), identity rank order; the chunk completes at its own position;
+ *       method 7 tree (:844-968): the partial at root gb * socket + p mod gb first, then
+ *         positions gb * q + p mod gb for q != socket ascending; socket is p / (R / radix) at
+ *         the last step when the node has several sockets, else 0.
+ *     Who folds a chunk (here: its owner position, one pass) is free; the order is not.
  *
  * Because every leaf is read exactly once and the tree is evaluated in registers, a whole
  * multi-step reduce-scatter (and the allgather fan-out) becomes ONE pass over HBM while the
@@ -56,10 +65,14 @@ typedef struct {
 } emac_level;
 
 typedef struct {
-  int method; /* 6 (recursive); 9 is accepted as its shm-staged alias */
+  int method;  /* 5 cyclic, 6 recursive, 7 tree; 8 / 9 / 10 are their shm-staged aliases */
+  int sockets; /* EXT_MPI_NUM_SOCKETS_PER_NODE (0 or 1: one); moves the tree method's last roots */
   int nlv;
   emac_level lv[EMAC_MAX_SPLITS];
 } emac_copyin;
+
+/* the generator family of a method: 5, 6 or 7 (reduce_copyin.c:1525-1526 map 8-10 to 5-7) */
+int emac_method_base(int method);
 
 int emac_parse_copyin(const char *s, emac_copyin *out);
 void emac_default_copyin(int nranks, emac_copyin *out); /* "6;1 -R R" */

@@ -30,8 +30,9 @@
  * returned, never fatal.
  *
  * Configuration: `copyin` is an EXT_MPI_COPYIN string ("6;1 -8 8", "6;1 -2 -2 -2 2 2 2",
- * "6;-64 -8 8", "9;..." as alias of 6); NULL means "6;1 -R R" (the reference requires the
- * variable, README "Installation"). Threading: MPI_THREAD_SERIALIZED, like the reference.
+ * "6;-64 -8 8"; method 5 cyclic, 6 recursive, 7 tree, 8 / 9 / 10 as their staged aliases);
+ * NULL means "6;1 -R R" (the reference requires the variable, README "Installation").
+ * Threading: MPI_THREAD_SERIALIZED, like the reference.
  */
 #ifndef EXT_MPI_AMD_H_
 #define EXT_MPI_AMD_H_
@@ -150,6 +151,12 @@ typedef struct {
 int ext_mpi_amd_comm_program(int nranks, int rank, long count, int dtype, const char *copyin, long send_phase,
                              ext_mpi_amd_p2p *ops, int max_ops, int *nops, ext_mpi_amd_fold *folds, int max_folds,
                              int *nfolds, long *staging_bytes);
+
+/* EXT_MPI_NUM_SOCKETS_PER_NODE (src/mpi/ext_mpi.c:43-187, a process-wide parameter): sockets per
+ * node for every handle / plan made afterwards. It moves the tree method's (7 / 10) last-step
+ * roots (reduce_copyin.c:860-864) and nothing else in the arithmetic. Returns the previous value,
+ * or EXT_MPI_AMD_ERROR_ARG. A node size it does not divide is rejected at init. */
+int ext_mpi_amd_set_num_sockets(int sockets);
 
 const char *ext_mpi_amd_version(void);
 

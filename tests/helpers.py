@@ -23,14 +23,15 @@ def xorshift_inputs(R, count, code, seed_base=0x5EED0000):
     return out
 
 
-def replay_plan(sends, code, copyin):
+def replay_plan(sends, code, copyin, sockets=1):
     """Evaluate the product planner's fold trees (plan_describe) with numpy, element-wise in the
     element type (IEEE round-to-nearest per add, integer wrap)."""
     R = len(sends)
     count = sends[0].size
     out = np.empty_like(sends[0])
     for pos in range(R):
-        d = emac.plan_describe(R, count, code, copyin, pos)
+        with emac.num_sockets(sockets):
+            d = emac.plan_describe(R, count, code, copyin, pos)
         for off, ln in d["pieces"]:
             if ln <= 0:
                 continue

@@ -50,6 +50,12 @@ def cases(R):
         out += [(emac.DOUBLE, 99999, "6;2 -3 3", True, False, 2)]
     if R == 8 and os.environ.get("IPC_BIG8"):  # BASELINE configs[3]: double, 256 MiB per rank, random values
         out += [(emac.DOUBLE, 32 << 20, full, False, False, 2), (emac.DOUBLE, 32 << 20, "6;1 -2 -2 -2 2 2 2", False, False, 1)]
+    # copy-in methods 5 cyclic / 7 tree (reduce_copyin.c:531-634, :844-968)
+    if R == 4:
+        out += [(emac.FLOAT, 100003, "7;1 -2 -2 2 2", False, False, 1), (emac.DOUBLE, 4099, "5;1 -4 4", True, False, 1)]
+    if R == 8:
+        out += [(emac.DOUBLE, 100001, "7;1 -4 -2 2 4", False, False, 1),
+                (emac.FLOAT, 65539, "5;1 -2 -2 -2 2 2 2", False, False, 1)]
     return out + fuzz_cases(R, int(os.environ.get("IPC_FUZZ", "0")))
 
 

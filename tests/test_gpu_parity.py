@@ -77,6 +77,52 @@ def test_node_parity_vs_oracle(oracle, R, copyin, code):
         assert_bitwise(got, want, f"R={R} {copyin} code={code} n={count}")
 
 
+# copy-in methods 5 cyclic / 7 tree (8 / 10 staged aliases) and sockets per node (the tree's roots)
+METHOD_CONFIGS = [
+    (4, "5;1 -4 4", 1), (6, "5;1 -2 -3 3 2", 1), (8, "5;1 -2 -2 -2 2 2 2", 2), (8, "5;1 -4 -2 2 4", 1),
+    (8, "8;3 -8 8", 1), (16, "5;1 -4 -4 4 4", 4),
+    (4, "7;1 -4 4", 2), (6, "7;1 -2 -3 3 2", 3), (8, "7;1 -2 -2 -2 2 2 2", 2), (8, "7;1 -2 -4 4 2", 4),
+    (8, "7;1 -4 -2 2 4", 1), (8, "10;-64 -8 8", 1), (12, "7;1 -3 -4 4 3", 4), (16, "7;1 -4 -4 4 4", 2),
+]
+
+
+@pytest.mark.parametrize("R,copyin,sockets", METHOD_CONFIGS)
+@pytest.mark.parametrize("code", CODES)
+def test_node_methods_vs_oracle(oracle, R, copyin, sockets, code):
+    for count in (0, 1, 5, 1031, 65536 + 3):
+        sends = xorshift_inputs(R, count, code, seed_base=0x5EED7000 + count)
+        want = oracle.allreduce(sends, copyin, num_sockets=sockets)
+        with emac.num_sockets(sockets):
+            got = run_node(sends, code, copyin)
+        assert_bitwise(got, want, f"R={R} {copyin} sockets={sockets} code={code} n={count}")
+
+
+@pytest.mark.parametrize("R,copyin,sockets", [(8, "7;1 -2 -4 4 2", 4), (8, "5;1 -4 -2 2 4", 1),
+                                              (6, "7;1 -3 -2 2 3", 2)])
+def test_comm_loopback_methods_vs_oracle(oracle, R, copyin, sockets):
+    for code in (emac.FLOAT, emac.DOUBLE):
+        for count in (1, 1031, 65536 + 5):
+            sends = xorshift_inputs(R, count, code, seed_base=0xC0A70000 + count)
+            want = oracle.allreduce(sends, copyin, num_sockets=sockets)
+            with emac.num_sockets(sockets):
+                got = run_comm_loopback(sends, code, copyin, phase=[(r * 3) % 4 for r in range(R)])
+            assert_bitwise(got, want, f"comm R={R} {copyin} sockets={sockets} code={code} n={count}")
+
+
+def test_methods_full_size_random_double(oracle):
+    """configs[3]-sized (256 MiB per rank, random doubles) tree with two sockets and cyclic
+    methods: bit-exact against the oracle's emulation of the same generator."""
+    rng = np.random.default_rng(0x7EE)
+    count = 32 << 20
+    sends = [rng.standard_normal(count) for _ in range(8)]
+    for copyin, sockets in (("7;1 -2 -4 4 2", 2), ("5;1 -8 8", 1)):
+        want = oracle.allreduce(sends, copyin, num_sockets=sockets)
+        with emac.num_sockets(sockets):
+            got = run_node(sends, emac.DOUBLE, copyin)
+        assert_bitwise(got, want, f"{copyin} sockets={sockets}")
+        del want, got
+
+
 @pytest.mark.parametrize("code", CODES)
 def test_node_in_place(oracle, code):
     sends = xorshift_inputs(8, 100003, code)

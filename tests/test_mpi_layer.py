@@ -104,6 +104,10 @@ def test_mpi_blocking_single_rank_gpu(tmp_path, args, copyin):
     (4, [100003, "f", "dev", "blocking"], {"EXT_MPI_BLOCKING": "1"}),
     (2, [4099, "d", "host", "inplace", "blocking"], {"EXT_MPI_BLOCKING": "1"}),
     (4, [65536, "f", "dev"], {"EXT_MPI_COPYIN": "6;1 -2 -2 2 2"}),
+    # the cyclic and tree generators, and two sockets per node (the tree's last roots move)
+    (4, [100003, "i", "dev"], {"EXT_MPI_COPYIN": "7;1 -2 -2 2 2", "EXT_MPI_NUM_SOCKETS_PER_NODE": "2"}),
+    (4, [65537, "l", "host", "inplace"], {"EXT_MPI_COPYIN": "5;1 -4 4"}),
+    (4, [4099, "i", "dev"], {"EXT_MPI_COPYIN": "10;1 -4 4", "EXT_MPI_NUM_SOCKETS_PER_NODE": "2"}),
     # MPI_MIN / MPI_MAX (get_reduction_op, ext_mpi_native.h:77-140): persistent and blocking
     (4, [100003, "d", "dev", "min"], {}), (2, [4099, "i", "host", "inplace", "max"], {}),
     (4, [65536, "l", "dev", "blocking", "max"], {"EXT_MPI_BLOCKING": "1"}),

@@ -54,7 +54,62 @@ def test_chain_leaf_order():
     assert d5["owner"] == 5 and d5["pieces"] == [(10240, 2048)]
 
 
-@pytest.mark.parametrize("bad", ["6;1 -3 3", "6;1 -2 -2 2", "5;1 -4 4", "6;1 4 -4", "6;1 -4 1 4", "garbage", "6;",
+# copy-in methods 5 (cyclic) / 7 (tree) and their staged aliases 8 / 10, with 1..4 sockets per node
+METHODS = [
+    (2, "5;1 -2 2", 1), (3, "5;1 -3 3", 1), (4, "5;1 -4 4", 1), (4, "5;1 -2 -2 2 2", 2), (6, "5;1 -2 -3 3 2", 1),
+    (6, "5;1 -3 -2 6", 3), (8, "5;1 -4 -2 2 4", 1), (8, "5;3 -2 -4 8", 2), (8, "5;-64 -8 8", 1),
+    (8, "8;1 -2 -2 -2 2 2 2", 1), (16, "5;1 -4 -4 4 4", 4), (12, "5;1 -2 -2 -3 3 2 2", 1),
+    (2, "7;1 -2 2", 1), (2, "7;1 -2 2", 2), (4, "7;1 -4 4", 1), (4, "7;1 -4 4", 2), (4, "7;1 -2 -2 2 2", 2),
+    (6, "7;1 -3 -2 2 3", 2), (6, "7;1 -2 -3 3 2", 3), (8, "7;1 -4 -2 2 4", 2), (8, "7;1 -2 -4 4 2", 4),
+    (8, "7;2 -2 -2 -2 2 2 2", 2), (8, "7;-40 -8 8", 1), (8, "10;1 -2 -4 4 2", 2), (12, "7;1 -3 -4 4 3", 4),
+    (16, "7;1 -4 -4 4 4", 2), (16, "7;1 -2 -2 -4 4 2 2", 4), (16, "10;1 -16 16", 8),
+]
+
+
+@pytest.mark.parametrize("R,copyin,sockets", METHODS)
+@pytest.mark.parametrize("code", CODES)
+def test_methods_replay_equals_oracle(oracle, R, copyin, sockets, code):
+    for count in (0, 1, 7, 1000, 4099):
+        sends = xorshift_inputs(R, count, code)
+        want = oracle.allreduce(sends, copyin, num_sockets=sockets)
+        got = replay_plan(sends, code, copyin, sockets)
+        for w in want:
+            assert np.array_equal(w.view(np.uint8), got.view(np.uint8)), (R, copyin, sockets, code, count)
+
+
+def test_sockets_move_only_the_tree_roots():
+    # sockets reach the arithmetic only through the tree's last-step root (reduce_copyin.c:
+    # 860-864): recursive and cyclic orders are unchanged, the tree's "-4 -2" order is not
+    for copyin in ("6;1 -2 -4 4 2", "5;1 -2 -4 4 2"):
+        a = [emac.plan_describe(8, 800, emac.FLOAT, copyin, p)["leaves"] for p in range(8)]
+        with emac.num_sockets(4):
+            b = [emac.plan_describe(8, 800, emac.FLOAT, copyin, p)["leaves"] for p in range(8)]
+        assert a == b
+    a = [emac.plan_describe(8, 800, emac.FLOAT, "7;1 -4 -2 2 4", p)["leaves"] for p in range(8)]
+    with emac.num_sockets(2):
+        b = [emac.plan_describe(8, 800, emac.FLOAT, "7;1 -4 -2 2 4", p)["leaves"] for p in range(8)]
+    assert a != b
+
+
+@pytest.mark.parametrize("bad,sockets", [("7;1 -4", 1), ("7;1 -2 -2", 1), ("5;1 -2 2 1 2 1 -2 2", 1),
+                                         ("7;1 -2 2 1 2 1 -2 2", 1), ("7;1 -4 4", 3), ("11;1 -4 4", 1),
+                                         ("4;1 -4 4", 1)])
+def test_method_limits_rejected(bad, sockets):
+    # the tree needs allgather radices (reduce_copyin.c:962-964); cyclic/tree are whole-node
+    # generators (no sub-splits); sockets must divide the node; methods outside 5..10
+    with emac.num_sockets(sockets):
+        with pytest.raises(emac.ExtMpiError):
+            emac.plan_describe(4, 100, emac.FLOAT, bad, 0)
+
+
+def test_set_num_sockets_validates():
+    with pytest.raises(emac.ExtMpiError):
+        emac.set_num_sockets(0)
+    prev = emac.set_num_sockets(2)
+    assert emac.set_num_sockets(prev) == 2
+
+
+@pytest.mark.parametrize("bad", ["6;1 -3 3", "6;1 -2 -2 2", "5;1 -4 -2 2", "6;1 4 -4", "6;1 -4 1 4", "garbage", "6;",
                                  "6;1 -2 2 1 2 1 -4 4", "6;1 -2 2 1 3 1 -2 2", "6;1 -4 4 1 4 1 -1 1"])
 def test_invalid_copyin_rejected(bad):
     # (R=4) chain/level size mismatches, a sub-split whose members do not divide the level
