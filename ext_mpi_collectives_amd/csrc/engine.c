@@ -877,7 +877,7 @@ int ext_mpi_amd_comm_init_ipc(int rank, int size, ext_mpi_amd_allgather_fn allga
    The probe touches the first R bytes of each buffer during set-up only: the buffers must not be
    written by the device while the set-up runs. */
 #define EMAC_PROBE_FLIP 0x5A
-#define EMAC_IPC_ATTEMPTS 4
+#define EMAC_IPC_ATTEMPTS 8
 
 static void ipc_mirror_poison(emac_comm *cm, void *p) {
   int i;
@@ -1040,7 +1040,11 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
     if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
       fprintf(stderr, "ipc rank %d: attempt %d: re-placing%s%s\n", cm->rank, attempt, stale[0] ? " send" : "",
               stale[1] ? " recv" : "");
-    if (attempt == EMAC_IPC_ATTEMPTS - 1) return EMAC_ERR_TRANSPORT;
+    if (attempt == EMAC_IPC_ATTEMPTS - 1) {
+      fprintf(stderr, "ext_mpi_amd: rank %d: peer mappings still unreachable after %d set-up rounds (%s%s)\n",
+              cm->rank, EMAC_IPC_ATTEMPTS, stale[0] ? "send " : "", stale[1] ? "recv" : "");
+      return EMAC_ERR_TRANSPORT;
+    }
     for (r = 0; r < h->nmapped; r++) ipc_unmap(h->mapped[r]);
     h->nmapped = 0;
     if (stale[0]) rc = ipc_remirror(h, 0);

@@ -12,6 +12,8 @@ import os
 import socket
 import subprocess
 import sys
+import tempfile
+import time
 
 import pytest
 
@@ -41,23 +43,31 @@ WORLDS = [int(w) for w in os.environ.get("IPC_TEST_WORLDS", "2,3,4,8").split(","
 @pytest.mark.parametrize("world", WORLDS)
 def test_ipc_ranks_share_one_gpu(world):
     port = _port()
-    procs = []
+    procs, logs = [], []
+    # each rank writes to its own file: pipes read one after the other would fill up and block a
+    # rank mid-print (then every peer waits for it in the next collective)
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), IPC_DEVICE="0", EXT_MPI_AMD_BARRIER_TIMEOUT="20")
         env.setdefault("IPC_FUZZ", "16")  # seeded random cases beside the fixed ones (ipc_worker.fuzz_cases)
+        logs.append(tempfile.TemporaryFile(mode="w+"))
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "ipc_worker.py")], env=env,
-                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
-    outs, codes = [], []
+                                      stdout=logs[-1], stderr=subprocess.STDOUT, text=True))
+    deadline = time.monotonic() + 150
+    codes = []
     for p in procs:
         try:
-            out, _ = p.communicate(timeout=150)
+            p.wait(timeout=max(1.0, deadline - time.monotonic()))
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
-            out, _ = p.communicate()
-        outs.append(out)
+            p.wait()
         codes.append(p.returncode)
+    outs = []
+    for f in logs:
+        f.seek(0)
+        outs.append(f.read())
+        f.close()
     report = "\n".join(outs)
     print(report)
     assert codes == [0] * world, report
