@@ -8,11 +8,12 @@
 //  * Flags live in uncached device memory (hipDeviceMallocUncached) and are accessed with
 //    system-scope atomics, so no L2 ever holds them.
 //  * The data the barrier orders needs no cache maintenance from the barrier's own workgroups:
-//    the application's writes to this rank's buffers are released to system scope by the command
-//    processor on every XCD's L2 before the phase-0 barrier (an event recorded with
-//    hipEventReleaseToSystem, engine.c), and the fold between the barriers is system-coherent
-//    by itself (sc0 sc1 loads, write-through stores drained before the phase-1 signal;
-//    fold_kernel.hpp kRemote).
+//    the application's writes to this rank's buffers are written back from every XCD's L2 by
+//    the command processor at the end of the producing kernel (the packet boundary before the
+//    barrier launch; EXT_MPI_AMD_IPC_RELEASE=1 adds an explicit hipEventReleaseToSystem record,
+//    engine.c), the fold between the barriers reads peers with system-coherent sc0 sc1 loads and
+//    stores only into this rank's own receive buffer, drained before the phase-1 signal
+//    (fold_kernel.hpp kRemote), and the copy-out pulls the other owners' results the same way.
 // One wave takes part: lane q signals peer q (stores the epoch into the peer's flag for this rank)
 // and waits for peer q's flag, so a barrier over R ranks is R-1 parallel one-way hops.
 // Every wait is bounded by a wall-clock timeout. A rank that times out in phase 0 skips its fold
