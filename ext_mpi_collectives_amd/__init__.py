@@ -37,7 +37,8 @@ class P2P(ctypes.Structure):
 
 class FoldDesc(ctypes.Structure):
     _fields_ = [("piece", ctypes.c_int), ("offset", ctypes.c_long), ("count", ctypes.c_long),
-                ("buf", ctypes.c_int * MAX_RANKS), ("leaf_offset", ctypes.c_long * MAX_RANKS)]
+                ("buf", ctypes.c_int * MAX_RANKS), ("leaf_offset", ctypes.c_long * MAX_RANKS),
+                ("nleaf", ctypes.c_int), ("leg", ctypes.c_int)]
 
 
 BUF_SEND, BUF_RECV, BUF_STAGE = 0, 1, 2
@@ -102,6 +103,9 @@ def lib():
                                                 P(ctypes.c_ubyte), P(c_int)]
         L.ext_mpi_amd_comm_program.argtypes = [c_int, c_int, c_long, c_int, ctypes.c_char_p, c_long,
                                                P(P2P), c_int, P(c_int), P(FoldDesc), c_int, P(c_int), P(c_long)]
+        L.ext_mpi_amd_comm_program_nodes.argtypes = [c_int, c_int, c_int, c_long, c_int, ctypes.c_char_p, c_long,
+                                                     P(P2P), c_int, P(c_int), P(FoldDesc), c_int, P(c_int), P(c_long)]
+        L.ext_mpi_amd_comm_set_nodes.argtypes = [c_int, c_int]
         L.ext_mpi_amd_set_num_sockets.argtypes = [c_int]
         L.ext_mpi_amd_set_num_sockets.restype = c_int
         L.ext_mpi_amd_version.restype = ctypes.c_char_p
@@ -238,7 +242,11 @@ def done(h):
 
 
 LEG_STAGE_IN, LEG_REDUCE_SCATTER, LEG_FOLD, LEG_ALLGATHER, LEG_STAGE_OUT = 1, 2, 4, 8, 16
-LEG_STAGE, LEG_ALL = 17, 31
+LEG_NODES_RS, LEG_NODES_FOLD, LEG_NODES_AG = 32, 64, 128  # two nodes (comm_set_nodes)
+LEG_STAGE, LEG_ALL = 17, 255
+# the order Start runs them in
+LEG_ORDER = (LEG_STAGE_IN, LEG_REDUCE_SCATTER, LEG_FOLD, LEG_NODES_RS, LEG_NODES_FOLD, LEG_NODES_AG, LEG_ALLGATHER,
+             LEG_STAGE_OUT)
 
 
 def start_legs(h, legs):
@@ -279,15 +287,30 @@ def comm_program(nranks, rank, count, dtype, copyin=None, send_phase=0, max_ops=
 
     Returns (ops, folds, staging_bytes): ops = [(leg, peer, is_send, buf, offset, bytes)],
     folds = [(offset, count, [(buf, leaf_offset)] in fold order)]."""
+    o, f, stage = comm_program_nodes(1, nranks, rank, count, dtype, copyin, send_phase, max_ops, max_folds)
+    return o, [(off, n, leaves) for off, n, leaves, _ in f], stage
+
+
+def comm_program_nodes(nodes, ranks_per_node, rank, count, dtype, copyin=None, send_phase=0, max_ops=65536,
+                       max_folds=4096):
+    """comm_program over ``nodes`` (1 or 2) nodes; ``rank`` is global (node-major). Folds are
+    (offset, count, [(buf, leaf_offset)], leg) with leg LEG_FOLD (the node's fold) or
+    LEG_NODES_FOLD (this node's partial, then the other node's)."""
     ops = (P2P * max_ops)()
     folds = (FoldDesc * max_folds)()
     nops, nf, stage = ctypes.c_int(), ctypes.c_int(), ctypes.c_long()
-    _check("ext_mpi_amd_comm_program",
-           lib().ext_mpi_amd_comm_program(nranks, rank, count, dtype, _enc(copyin), send_phase, ops, max_ops,
-                                          ctypes.byref(nops), folds, max_folds, ctypes.byref(nf), ctypes.byref(stage)))
+    _check("ext_mpi_amd_comm_program_nodes",
+           lib().ext_mpi_amd_comm_program_nodes(nodes, ranks_per_node, rank, count, dtype, _enc(copyin), send_phase,
+                                                ops, max_ops, ctypes.byref(nops), folds, max_folds, ctypes.byref(nf),
+                                                ctypes.byref(stage)))
     o = [(x.leg, x.peer, x.is_send, x.buf, x.offset, x.bytes) for x in ops[:nops.value]]
-    f = [(x.offset, x.count, [(x.buf[t], x.leaf_offset[t]) for t in range(nranks)]) for x in folds[:nf.value]]
+    f = [(x.offset, x.count, [(x.buf[t], x.leaf_offset[t]) for t in range(x.nleaf)], x.leg) for x in folds[:nf.value]]
     return o, f, stage.value
+
+
+def comm_set_nodes(comm, nodes):
+    """Declare ranks [0, size/2) and [size/2, size) of an RCCL / loopback communicator two nodes."""
+    return _check("ext_mpi_amd_comm_set_nodes", lib().ext_mpi_amd_comm_set_nodes(comm, nodes))
 
 
 def set_num_sockets(sockets):

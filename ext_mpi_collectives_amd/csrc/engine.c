@@ -70,6 +70,7 @@ typedef struct {
 typedef struct {
   int used;
   int rank, size, device;
+  int nodes; /* COMM form: ranks [n * size / nodes, (n + 1) * size / nodes) form node n (0: one node) */
   ncclComm_t nccl;
   int loop_group; /* >= 0: in-process loopback communicator (testing transport), no RCCL */
   /* peer-mapped transport (ext_mpi_amd_comm_init_ipc) */
@@ -166,8 +167,10 @@ typedef struct {
   int fused; /* whole Allreduce in one launch (emac_gpu_fold_fused) */
   void *ev_release; /* system-scope release recorded before every phase-0 barrier */
   emac_launch pull; /* every other owner's result copied into this rank's receive buffer */
-  void *graph[32];  /* COMM form: captured legs, per subset of EXT_MPI_AMD_LEG_* (graph_ok) */
-  unsigned char graph_failed[32];
+  int nodes;         /* COMM form over two nodes: the node-pair legs run (emac_comm_program_nodes) */
+  emac_launch xfold; /* ... and fold this node's partial with the other node's (two leaves) */
+  void *graph[EXT_MPI_AMD_LEG_ALL + 1]; /* COMM form: captured legs, per subset of EXT_MPI_AMD_LEG_* */
+  unsigned char graph_failed[EXT_MPI_AMD_LEG_ALL + 1];
   emac_pipe *pipe; /* pipelined host staging (NODE form), or NULL */
 } emac_handle;
 
@@ -214,6 +217,8 @@ static void release(emac_handle *h) {
   emac_gpu_free(h->d_edges);
   emac_gpu_free(h->pull.d_buckets);
   emac_gpu_free(h->pull.d_edges);
+  emac_gpu_free(h->xfold.d_buckets);
+  emac_gpu_free(h->xfold.d_edges);
   emac_gpu_free(h->staging);
   for (r = 0; r < h->nbuf; r++) {
     int same = h->dsend[r] == h->drecv[r];
@@ -224,7 +229,7 @@ static void release(emac_handle *h) {
   }
   for (r = 0; r < h->nmapped; r++) ipc_unmap(h->mapped[r]);
   emac_gpu_event_destroy(h->ev_release);
-  for (r = 0; r < 32; r++) emac_gpu_graph_destroy(h->graph[r]);
+  for (r = 0; r <= EXT_MPI_AMD_LEG_ALL; r++) emac_gpu_graph_destroy(h->graph[r]);
   if (h->kind == KIND_IPC && h->slot_held) {
     emac_comm *cm = &comms[h->comm];
     cm->slot_used[h->slot] = 0;
@@ -708,6 +713,7 @@ int ext_mpi_amd_comm_mfree(int comm, void *p) {
 }
 
 static int ipc_agree(emac_comm *cm, int ok_local);
+static char *leg_base(const emac_handle *h, int buf);
 
 /* Collective: every rank first closes its mappings of the others' memory, then all agree, and
    only then is this rank's exported memory (synchronisation block, mirror pool) freed. */
@@ -1167,7 +1173,7 @@ int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, i
   if (!handle || comm < 0 || comm >= MAX_COMMS || !comms[comm].used || count < 0) return EMAC_ERR_ARG;
   *handle = -1;
   cm = &comms[comm];
-  R = cm->size;
+  R = cm->size / (cm->nodes > 1 && !cm->ipc ? cm->nodes : 1); /* ranks of one node */
   if ((rc = parse_cfg(copyin, R, &cfg))) return rc;
   if (emac_gpu_set_device(cm->device)) return EMAC_ERR_DEVICE;
   h = (emac_handle *)calloc(1, sizeof(emac_handle));
@@ -1178,8 +1184,9 @@ int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, i
   rc = emac_plan_build(&h->plan, R, count, dtype, op, &cfg);
   if (!rc) {
     h->me = cm->rank;
-    h->me_pos = h->plan.rank_pos[h->me];
+    h->me_pos = h->plan.rank_pos[h->me % R];
     h->bytes = (size_t)count * (size_t)h->plan.tsize;
+    h->nodes = cm->size / R;
   }
   h->nbuf = 1;
   h->nsrc = R;
@@ -1194,28 +1201,38 @@ int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, i
   {
     emac_fold *folds = NULL;
     int nf = 0, f;
-    if ((rc = emac_comm_program(&h->plan, h->me, (long)((unsigned long)h->dsend[0] & 15ul), &h->ops, &h->nops, &folds,
-                                &nf, &stage_total)))
+    emac_bucket *xb = NULL;
+    int nxb = 0;
+    if ((rc = emac_comm_program_nodes(&h->plan, h->nodes, h->me / R, h->me % R,
+                                      (long)((unsigned long)h->dsend[0] & 15ul), &h->ops, &h->nops, &folds, &nf,
+                                      &stage_total)))
       goto fail;
     b = (emac_bucket *)calloc((size_t)nf + 1, sizeof(emac_bucket));
-    if (!b || (rc = emac_gpu_malloc(&h->staging, (size_t)stage_total))) {
+    xb = (emac_bucket *)calloc((size_t)nf + 1, sizeof(emac_bucket));
+    if (!b || !xb || (rc = emac_gpu_malloc(&h->staging, (size_t)(stage_total > 0 ? stage_total : 16)))) {
       free(folds);
+      free(xb);
       rc = rc ? rc : EMAC_ERR_MALLOC;
       goto fail;
     }
     for (f = 0; f < nf; f++) {
-      emac_bucket *bk = &b[nb++];
+      const int node_pair = folds[f].leg == EMAC_LEG_NODES_FOLD;
+      emac_bucket *bk = node_pair ? &xb[nxb++] : &b[nb++];
       long off = folds[f].offset / h->plan.tsize;
-      for (t = 0; t < R; t++) {
-        /* leaf pointers are shifted back by the chunk offset: split_alignment adds it */
-        const char *base = folds[f].buf[t] == EMAC_BUF_SEND ? (const char *)h->dsend[0] : (const char *)h->staging;
-        bk->src[t] = base + folds[f].loff[t] - folds[f].offset;
+      for (t = 0; t < folds[f].nleaf; t++) {
+        /* leaf pointers are shifted back by the result's offset: split_alignment adds it */
+        bk->src[t] = leg_base(h, folds[f].buf[t]) + folds[f].loff[t] - folds[f].offset;
       }
       bk->dst[0] = h->drecv[0];
       bk->ndst = 1;
-      place_bucket(bk, R, off, folds[f].count, h->plan.tsize);
+      place_bucket(bk, folds[f].nleaf, off, folds[f].count, h->plan.tsize);
     }
     free(folds);
+    if (h->nodes > 1 && nxb && (rc = upload_launch_as(h, &h->xfold, xb, nxb, 2, 0))) {
+      free(xb);
+      goto fail;
+    }
+    free(xb);
   }
   if ((rc = upload_buckets(h, b, nb))) goto fail;
   free(b);
@@ -1428,6 +1445,18 @@ static int enqueue_legs(emac_handle *h, int legs) {
       (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, h->fan, h->unroll, &h->plan.codes, h->d_buckets, h->nb, h->ntiles,
                           h->tiles_per_bucket, h->all_full, h->d_edges, h->nedges, h->stream)))
     return rc;
+  if (h->kind == KIND_COMM && h->nodes > 1) {
+    /* two nodes: the node-pair exchange of the owned chunk's halves, their two-leaf fold, the
+       exchange back (emac_comm_program_nodes) */
+    static const emac_codes pair = {{1, 0}, {0, 1}, 1, 2};
+    if ((legs & EXT_MPI_AMD_LEG_NODES_RS) && (rc = run_leg(h, EMAC_LEG_NODES_RS))) return rc;
+    if ((legs & EXT_MPI_AMD_LEG_NODES_FOLD) && h->xfold.nb &&
+        (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, 2, 0, h->xfold.unroll, &pair, h->xfold.d_buckets, h->xfold.nb,
+                            h->xfold.ntiles, h->xfold.tiles_per_bucket, h->xfold.all_full, h->xfold.d_edges,
+                            h->xfold.nedges, h->stream)))
+      return rc;
+    if ((legs & EXT_MPI_AMD_LEG_NODES_AG) && (rc = run_leg(h, EMAC_LEG_NODES_AG))) return rc;
+  }
   if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && multi && (rc = run_leg(h, EMAC_LEG_AG))) return rc;
   if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && h->kind == KIND_IPC && h->plan.nranks > 1) {
     static const emac_codes copy = {{1}, {1}, 1, 1}; /* one leaf: a copy */
@@ -1561,15 +1590,32 @@ int ext_mpi_amd_plan_describe(int nranks, long count, int dtype, const char *cop
 int ext_mpi_amd_comm_program(int nranks, int rank, long count, int dtype, const char *copyin, long send_phase,
                              ext_mpi_amd_p2p *ops, int max_ops, int *nops, ext_mpi_amd_fold *folds, int max_folds,
                              int *nfolds, long *staging_bytes) {
+  return ext_mpi_amd_comm_program_nodes(1, nranks, rank, count, dtype, copyin, send_phase, ops, max_ops, nops, folds,
+                                        max_folds, nfolds, staging_bytes);
+}
+
+int ext_mpi_amd_comm_set_nodes(int comm, int nodes) {
+  if (comm < 0 || comm >= MAX_COMMS || !comms[comm].used) return EMAC_ERR_ARG;
+  if (nodes < 1 || comms[comm].size % nodes) return EMAC_ERR_ARG;
+  if (nodes > EMAC_MAX_NODES || (nodes > 1 && comms[comm].ipc)) return EMAC_ERR_UNSUPPORTED;
+  comms[comm].nodes = nodes;
+  return 0;
+}
+
+int ext_mpi_amd_comm_program_nodes(int nodes, int ranks_per_node, int rank, long count, int dtype, const char *copyin,
+                                   long send_phase, ext_mpi_amd_p2p *ops, int max_ops, int *nops,
+                                   ext_mpi_amd_fold *folds, int max_folds, int *nfolds, long *staging_bytes) {
   emac_plan p;
   emac_copyin cfg;
   emac_p2p *o = NULL;
   emac_fold *f = NULL;
+  const int R = ranks_per_node;
   int rc, i, t, no = 0, nf = 0;
-  if (nranks < 1 || nranks > EMAC_MAX_RANKS || rank < 0 || rank >= nranks) return EMAC_ERR_ARG;
-  if ((rc = parse_cfg(copyin, nranks, &cfg))) return rc;
-  if ((rc = emac_plan_build(&p, nranks, count, dtype, EMAC_SUM, &cfg))) return rc;
-  if ((rc = emac_comm_program(&p, rank, send_phase, &o, &no, &f, &nf, staging_bytes))) goto out;
+  if (R < 1 || R > EMAC_MAX_RANKS || nodes < 1 || nodes > EMAC_MAX_NODES || rank < 0 || rank >= nodes * R)
+    return EMAC_ERR_ARG;
+  if ((rc = parse_cfg(copyin, R, &cfg))) return rc;
+  if ((rc = emac_plan_build(&p, R, count, dtype, EMAC_SUM, &cfg))) return rc;
+  if ((rc = emac_comm_program_nodes(&p, nodes, rank / R, rank % R, send_phase, &o, &no, &f, &nf, staging_bytes))) goto out;
   if (no > max_ops || nf > max_folds) {
     rc = EMAC_ERR_ARG;
     goto out;
@@ -1583,10 +1629,13 @@ int ext_mpi_amd_comm_program(int nranks, int rank, long count, int dtype, const 
     ops[i].bytes = o[i].bytes;
   }
   for (i = 0; i < nf; i++) {
+    memset(&folds[i], 0, sizeof(folds[i]));
     folds[i].piece = f[i].piece;
     folds[i].offset = f[i].offset;
     folds[i].count = f[i].count;
-    for (t = 0; t < nranks; t++) {
+    folds[i].nleaf = f[i].nleaf;
+    folds[i].leg = f[i].leg;
+    for (t = 0; t < f[i].nleaf; t++) {
       folds[i].buf[t] = f[i].buf[t];
       folds[i].leaf_offset[t] = f[i].loff[t];
     }

@@ -32,8 +32,10 @@
  * other rank with hipIpc, as the reference maps them with cudaIpc (src/gpu/cuda_shmem.c:218-299),
  * bootstrapped with PMPI_Allgather; "rccl" runs the legs as RCCL point-to-point rounds,
  * bootstrapped with PMPI_Bcast of the unique id. One engine communicator per MPI communicator,
- * cached as an MPI attribute and destroyed with it. The communicator must lie within one node
- * (the reference's inter-node legs are out of this path's scope).
+ * cached as an MPI attribute and destroyed with it. The communicator lies within one node, or
+ * spans two nodes of equal size in node-major rank order: then the legs run over RCCL with the
+ * reference's one-port two-node schedule (ext_mpi_amd_comm_set_nodes); other inter-node shapes
+ * return EXT_MPI_AMD_ERROR_UNSUPPORTED (the blocking front end hands them to PMPI).
  */
 #include <mpi.h>
 #include <stdio.h>
@@ -190,7 +192,7 @@ static int comm_attr_delete(MPI_Comm comm, int keyval, void *attr, void *extra) 
 
 static int node_comm(MPI_Comm comm, const void *devbuf, int *ext_comm) {
   comm_attr *a;
-  int flag, size, rank, nsize, nrank, device, ndev, rc;
+  int flag, size, rank, nsize, nrank, device, ndev, rc, nodes;
   MPI_Comm node;
   unsigned char id[EXT_MPI_AMD_UNIQUE_ID_BYTES];
   if (comm_keyval == MPI_KEYVAL_INVALID) return EXT_MPI_AMD_ERROR_ARG;
@@ -205,16 +207,23 @@ static int node_comm(MPI_Comm comm, const void *devbuf, int *ext_comm) {
   PMPI_Comm_size(node, &nsize);
   PMPI_Comm_rank(node, &nrank);
   PMPI_Comm_free(&node);
-  flag = nsize == size;
-  PMPI_Allreduce(MPI_IN_PLACE, &flag, 1, MPI_INT, MPI_MIN, comm);
-  if (!flag) return EXT_MPI_AMD_ERROR_UNSUPPORTED; /* inter-node legs: out of scope */
+  {
+    /* one node, or two nodes of equal size in node-major rank order (the reference's row layout,
+       ext_mpi_native.c:879-960): the second runs the one-port two-node schedule over RCCL */
+    int v[2];
+    v[0] = nsize == size;
+    v[1] = size == 2 * nsize && nrank == rank % nsize;
+    PMPI_Allreduce(MPI_IN_PLACE, v, 2, MPI_INT, MPI_MIN, comm);
+    if (!v[0] && !v[1]) return EXT_MPI_AMD_ERROR_UNSUPPORTED; /* other inter-node shapes: out of scope */
+    nodes = v[0] ? 1 : 2;
+  }
   ndev = ext_mpi_amd_gpu_device_count();
   device = ext_mpi_amd_gpu_device_of(devbuf);
   if (device < 0) device = ndev > 0 ? nrank % ndev : -1;
   a = (comm_attr *)calloc(1, sizeof(comm_attr));
   if (!a) return EXT_MPI_AMD_ERROR_MALLOC;
   a->boot = MPI_COMM_NULL;
-  if (!cfg_rccl) {
+  if (!cfg_rccl && nodes == 1) { /* peer mappings reach the ranks of one node only */
     PMPI_Comm_dup(comm, &a->boot);
     /* collective even without a device: every rank reaches the same verdict */
     rc = ext_mpi_amd_comm_init_ipc(rank, size, mpi_allgather_cb, a, ndev > 0 ? device : -1, ext_comm);
@@ -227,6 +236,7 @@ static int node_comm(MPI_Comm comm, const void *devbuf, int *ext_comm) {
     if (rank == 0 && (rc = ext_mpi_amd_get_unique_id(id))) memset(id, 0, sizeof(id));
     PMPI_Bcast(id, EXT_MPI_AMD_UNIQUE_ID_BYTES, MPI_BYTE, 0, comm);
     rc = ndev > 0 ? ext_mpi_amd_comm_init(rank, size, id, device, ext_comm) : EXT_MPI_AMD_ERROR_DEVICE;
+    if (rc == 0 && nodes > 1 && (rc = ext_mpi_amd_comm_set_nodes(*ext_comm, nodes))) ext_mpi_amd_comm_free(*ext_comm);
     flag = rc == 0;
     PMPI_Allreduce(MPI_IN_PLACE, &flag, 1, MPI_INT, MPI_MIN, comm);
     if (!flag) {

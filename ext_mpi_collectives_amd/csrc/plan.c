@@ -377,15 +377,29 @@ void emac_plan_free(emac_plan *p) {
    each owned chunk, one 16-byte aligned slot per peer. */
 int emac_comm_program(const emac_plan *p, int me, long send_phase, emac_p2p **ops_out, int *nops_out,
                       emac_fold **folds_out, int *nfolds_out, long *staging_bytes) {
-  int R = p->nranks, me_pos = p->rank_pos[me], pc, q, t, nops = 0, nf = 0, leg;
+  return emac_comm_program_nodes(p, 1, 0, me, send_phase, ops_out, nops_out, folds_out, nfolds_out, staging_bytes);
+}
+
+int emac_comm_program_nodes(const emac_plan *p, int nodes, int node, int me, long send_phase, emac_p2p **ops_out,
+                            int *nops_out, emac_fold **folds_out, int *nfolds_out, long *staging_bytes) {
+  int R = p->nranks, me_pos, pc, q, t, nops = 0, nf = 0, leg, g0, partner;
   long ts = p->tsize, total = 0;
-  long *slot0 = (long *)malloc(sizeof(long) * (size_t)p->npieces);
-  long *stride = (long *)malloc(sizeof(long) * (size_t)p->npieces);
-  emac_p2p *ops = (emac_p2p *)malloc(sizeof(emac_p2p) * (size_t)(4 * p->npieces * R + 1));
-  emac_fold *folds = (emac_fold *)calloc((size_t)p->npieces + 1, sizeof(emac_fold));
-  if (!slot0 || !stride || !ops || !folds) {
+  long *slot0, *stride, *xslot;
+  emac_p2p *ops;
+  emac_fold *folds;
+  if (nodes < 1 || nodes > EMAC_MAX_NODES || node < 0 || node >= nodes || me < 0 || me >= R) return EMAC_ERR_ARG;
+  me_pos = p->rank_pos[me];
+  g0 = node * R;                      /* global rank of this node's first rank */
+  partner = (nodes - 1 - node) * R + me; /* the same rank of the other node */
+  slot0 = (long *)malloc(sizeof(long) * (size_t)p->npieces);
+  stride = (long *)malloc(sizeof(long) * (size_t)p->npieces);
+  xslot = (long *)malloc(sizeof(long) * (size_t)p->npieces);
+  ops = (emac_p2p *)malloc(sizeof(emac_p2p) * (size_t)(4 * p->npieces * R + 4 * p->npieces + 1));
+  folds = (emac_fold *)calloc((size_t)(2 * p->npieces) + 1, sizeof(emac_fold));
+  if (!slot0 || !stride || !xslot || !ops || !folds) {
     free(slot0);
     free(stride);
+    free(xslot);
     free(ops);
     free(folds);
     return EMAC_ERR_MALLOC;
@@ -397,6 +411,15 @@ int emac_comm_program(const emac_plan *p, int me, long send_phase, emac_p2p **op
     slot0[pc] = total + phase;
     total += (long)(R - 1) * stride[pc];
   }
+  /* two nodes: one slot per piece for the other node's partial of the half this rank keeps,
+     at the 16-byte phase that half has in the receive buffer (send_phase stands for it) */
+  for (pc = 0; pc < p->npieces && nodes > 1; pc++) {
+    long off = p->chunk_off[(size_t)pc * R + me_pos], len = p->chunk_len[(size_t)pc * R + me_pos];
+    long hoff = node ? (len + 1) / 2 : 0, hlen = node ? len / 2 : (len + 1) / 2;
+    total = (total + 15) / 16 * 16;
+    xslot[pc] = total + ((send_phase + (off + hoff) * ts) & 15);
+    total += ((hlen * ts + 15) / 16) * 16 + 16;
+  }
 #define SLOT(pc, q) (slot0[pc] + (long)(((q) - me - 1 + R) % R) * stride[pc])
   for (leg = 0; leg < 2; leg++) {
     for (pc = 0; pc < p->npieces; pc++) {
@@ -407,11 +430,11 @@ int emac_comm_program(const emac_plan *p, int me, long send_phase, emac_p2p **op
         qoff = p->chunk_off[(size_t)pc * R + p->rank_pos[q]] * ts;
         qlen = p->chunk_len[(size_t)pc * R + p->rank_pos[q]] * ts;
         if (leg == 0) {
-          if (qlen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_RS, q, 1, EMAC_BUF_SEND, qoff, qlen};
-          if (mylen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_RS, q, 0, EMAC_BUF_STAGE, SLOT(pc, q), mylen};
+          if (qlen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_RS, g0 + q, 1, EMAC_BUF_SEND, qoff, qlen};
+          if (mylen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_RS, g0 + q, 0, EMAC_BUF_STAGE, SLOT(pc, q), mylen};
         } else {
-          if (mylen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_AG, q, 1, EMAC_BUF_RECV, myoff, mylen};
-          if (qlen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_AG, q, 0, EMAC_BUF_RECV, qoff, qlen};
+          if (mylen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_AG, g0 + q, 1, EMAC_BUF_RECV, myoff, mylen};
+          if (qlen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_AG, g0 + q, 0, EMAC_BUF_RECV, qoff, qlen};
         }
       }
     }
@@ -423,6 +446,8 @@ int emac_comm_program(const emac_plan *p, int me, long send_phase, emac_p2p **op
     f->piece = pc;
     f->offset = off * ts;
     f->count = len;
+    f->nleaf = R;
+    f->leg = EMAC_LEG_FOLD;
     for (t = 0; t < R; t++) {
       q = p->leaf_rank[me_pos][t];
       f->buf[t] = q == me ? EMAC_BUF_SEND : EMAC_BUF_STAGE;
@@ -431,8 +456,35 @@ int emac_comm_program(const emac_plan *p, int me, long send_phase, emac_p2p **op
     nf++;
   }
 #undef SLOT
+  for (pc = 0; pc < p->npieces && nodes > 1; pc++) {
+    long off = p->chunk_off[(size_t)pc * R + me_pos], len = p->chunk_len[(size_t)pc * R + me_pos];
+    /* half 0 = the first ceil(len / 2) elements, finished on node 0; half 1 on node 1 */
+    long hoff[2], hlen[2];
+    int keep = node, give = 1 - node;
+    hoff[0] = off;
+    hlen[0] = (len + 1) / 2;
+    hoff[1] = off + hlen[0];
+    hlen[1] = len - hlen[0];
+    if (hlen[give] > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS, partner, 1, EMAC_BUF_RECV, hoff[give] * ts, hlen[give] * ts};
+    if (hlen[keep] > 0) {
+      emac_fold *f = &folds[nf++];
+      ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS, partner, 0, EMAC_BUF_STAGE, xslot[pc], hlen[keep] * ts};
+      f->piece = pc;
+      f->offset = hoff[keep] * ts;
+      f->count = hlen[keep];
+      f->nleaf = 2;
+      f->leg = EMAC_LEG_NODES_FOLD;
+      f->buf[0] = EMAC_BUF_RECV; /* this node's partial first */
+      f->loff[0] = hoff[keep] * ts;
+      f->buf[1] = EMAC_BUF_STAGE;
+      f->loff[1] = xslot[pc];
+      ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG, partner, 1, EMAC_BUF_RECV, hoff[keep] * ts, hlen[keep] * ts};
+    }
+    if (hlen[give] > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG, partner, 0, EMAC_BUF_RECV, hoff[give] * ts, hlen[give] * ts};
+  }
   free(slot0);
   free(stride);
+  free(xslot);
   *ops_out = ops;
   *nops_out = nops;
   *folds_out = folds;

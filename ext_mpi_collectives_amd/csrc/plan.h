@@ -106,7 +106,18 @@ typedef struct {
  * Built once per handle; the RCCL executor (engine.c) only walks it. Exported through
  * ext_mpi_amd_comm_program so the same program can be executed by a host transport in tests. */
 enum { EMAC_BUF_SEND = 0, EMAC_BUF_RECV = 1, EMAC_BUF_STAGE = 2 };
-enum { EMAC_LEG_RS = 2, EMAC_LEG_AG = 8 };
+/* legs, as the EXT_MPI_AMD_LEG_* bits of include/ext_mpi_amd.h: the node's reduce-scatter, its
+   fold, [two nodes: the node-pair exchange of the owned chunk's halves, their fold, the exchange
+   back,] the node's allgather */
+enum {
+  EMAC_LEG_RS = 2,
+  EMAC_LEG_FOLD = 4,
+  EMAC_LEG_AG = 8,
+  EMAC_LEG_NODES_RS = 32,
+  EMAC_LEG_NODES_FOLD = 64,
+  EMAC_LEG_NODES_AG = 128
+};
+#define EMAC_MAX_NODES 2
 
 typedef struct {
   int leg;     /* EMAC_LEG_RS or EMAC_LEG_AG */
@@ -119,10 +130,12 @@ typedef struct {
 
 typedef struct {
   int piece;
-  long offset;                   /* byte offset of the owned chunk in send / recv buffers */
+  long offset;                   /* byte offset of the result in the receive buffer */
   long count;                    /* elements */
-  int buf[EMAC_MAX_RANKS];       /* per leaf (plan leaf order): EMAC_BUF_SEND or EMAC_BUF_STAGE */
-  long loff[EMAC_MAX_RANKS];     /* per leaf: byte offset of the chunk's first element */
+  int buf[EMAC_MAX_RANKS];       /* per leaf (plan leaf order): EMAC_BUF_SEND, _RECV or _STAGE */
+  long loff[EMAC_MAX_RANKS];     /* per leaf: byte offset of the first element */
+  int nleaf;                     /* the node's R, or 2 for the two nodes' partials */
+  int leg;                       /* EMAC_LEG_FOLD or EMAC_LEG_NODES_FOLD */
 } emac_fold;
 
 /* Program of node rank `me`: ops (reduce-scatter ops first, then allgather ops), one fold per
@@ -130,6 +143,16 @@ typedef struct {
    so they share the 16-byte phase of the send buffer. Caller frees *ops and *folds. */
 int emac_comm_program(const emac_plan *p, int me, long send_phase, emac_p2p **ops, int *nops, emac_fold **folds,
                       int *nfolds, long *staging_bytes);
+/* The same for rank `me` of node `node` out of `nodes` (1 or 2) nodes of p->nranks ranks each
+   (global rank = node * p->nranks + me, the peers in *ops are global ranks). Two nodes, one port
+   (EXT_MPI_NUM_PORTS "-1 1", src/core/allreduce_recursive.c:222-453 as ext_mpi_native.c:879-960
+   composes it): after the node's reduce-scatter and fold each owner chunk holds the node's
+   partial; the owners of the same chunk on the two nodes (same rank in their node) swap halves
+   (NODES_RS), fold the half they keep -- own partial, then the other node's: one two-operand
+   reduction -- (NODES_FOLD), swap the finished halves back (NODES_AG); the node's allgather
+   then distributes the finished chunk. */
+int emac_comm_program_nodes(const emac_plan *p, int nodes, int node, int me, long send_phase, emac_p2p **ops,
+                            int *nops, emac_fold **folds, int *nfolds, long *staging_bytes);
 
 /* Build the plan of an nranks-rank Allreduce of `count` elements. 0 or an EMAC_ERR_* code. */
 int emac_plan_build(emac_plan *p, int nranks, long count, int dtype, int op, const emac_copyin *cfg);

@@ -120,7 +120,11 @@ int ext_mpi_amd_set_stream(int handle, void *hip_stream);
 #define EXT_MPI_AMD_LEG_ALLGATHER 8      /* COMM form: owned chunk to every peer (reduce_copyout) */
 #define EXT_MPI_AMD_LEG_STAGE_OUT 16     /* D2H of host receive buffers */
 #define EXT_MPI_AMD_LEG_STAGE 17         /* both staging copies */
-#define EXT_MPI_AMD_LEG_ALL 31
+/* COMM form over two nodes (ext_mpi_amd_comm_set_nodes), between the fold and the allgather: */
+#define EXT_MPI_AMD_LEG_NODES_RS 32      /* owned chunk's halves swapped with the other node's owner */
+#define EXT_MPI_AMD_LEG_NODES_FOLD 64    /* kept half: this node's partial + the other node's */
+#define EXT_MPI_AMD_LEG_NODES_AG 128     /* finished halves swapped back */
+#define EXT_MPI_AMD_LEG_ALL 255
 int ext_mpi_amd_start_legs(int handle, int legs);
 
 /* ---- introspection (no GPU needed) ----
@@ -143,14 +147,30 @@ typedef struct {
 } ext_mpi_amd_p2p;
 typedef struct {
   int piece;
-  long offset; /* bytes: owned chunk in send / recv */
+  long offset; /* bytes: the result in recv */
   long count;  /* elements */
   int buf[EXT_MPI_AMD_MAX_RANKS];
   long leaf_offset[EXT_MPI_AMD_MAX_RANKS];
+  int nleaf; /* leaves used: nranks (the node's fold) or 2 (the two nodes' partials) */
+  int leg;   /* EXT_MPI_AMD_LEG_FOLD or EXT_MPI_AMD_LEG_NODES_FOLD */
 } ext_mpi_amd_fold;
 int ext_mpi_amd_comm_program(int nranks, int rank, long count, int dtype, const char *copyin, long send_phase,
                              ext_mpi_amd_p2p *ops, int max_ops, int *nops, ext_mpi_amd_fold *folds, int max_folds,
                              int *nfolds, long *staging_bytes);
+/* The same for `nodes` (1 or 2) nodes of ranks_per_node ranks; `rank` is global (node-major). */
+int ext_mpi_amd_comm_program_nodes(int nodes, int ranks_per_node, int rank, long count, int dtype, const char *copyin,
+                                   long send_phase, ext_mpi_amd_p2p *ops, int max_ops, int *nops,
+                                   ext_mpi_amd_fold *folds, int max_folds, int *nfolds, long *staging_bytes);
+
+/* ---- two nodes (§8f row 3, the inter-node ports schedule for two nodes, one port) ----
+ * The reference runs an Allreduce over several nodes as: the node's copy-in (the same
+ * reduce_copies_* emission as one node, into shared memory), the inter-node algorithm of
+ * src/core/allreduce_recursive.c:222-453 over the node partials (EXT_MPI_NUM_PORTS, here one
+ * port: "-1 1"), the node's copy-out (src/mpi/ext_mpi_native.c:879-1000). On an RCCL (or loopback)
+ * communicator whose ranks [0, size/2) and [size/2, size) are two nodes of equal size, set before
+ * ext_mpi_amd_allreduce_init; copyin then describes ONE node (its ranks_per_node positions).
+ * Peer-mapped communicators are single-node (EXT_MPI_AMD_ERROR_UNSUPPORTED). */
+int ext_mpi_amd_comm_set_nodes(int comm, int nodes);
 
 /* EXT_MPI_NUM_SOCKETS_PER_NODE (src/mpi/ext_mpi.c:43-187, a process-wide parameter): sockets per
  * node for every handle / plan made afterwards. It moves the tree method's (7 / 10) last-step

@@ -82,6 +82,10 @@ def lib():
         _lib.ref_emulate_op_s.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
                                           ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                                           ctypes.POINTER(ctypes.c_void_p)]
+        _lib.ref_emulate_nodes.restype = ctypes.c_int
+        _lib.ref_emulate_nodes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                           ctypes.POINTER(ctypes.c_void_p)]
         _lib.ref_get_rank_cyclic.restype = ctypes.c_int
         _lib.ref_get_rank_cyclic.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int,
                                              ctypes.c_int]
@@ -152,6 +156,22 @@ def allreduce(sends, copyin, in_place=False, op=SUM, num_sockets=1):
                                 _ptrs(recvs))
     if rc != 0:
         raise ValueError(f"oracle rejected copyin {copyin!r} for R={R}")
+    return recvs
+
+
+def allreduce_nodes(sends, copyin, nodes=2, in_place=False, op=SUM, num_sockets=1):
+    """Reference result over `nodes` (1 or 2) nodes of len(sends) // nodes ranks each (node-major):
+    each node's copy-in, the node partials reduced once per element (one port), the copy-out."""
+    W = len(sends)
+    a0 = np.ascontiguousarray(sends[0])
+    code = {np.dtype(np.float64): DOUBLE, np.dtype(np.int64): LONG, np.dtype(np.float32): FLOAT,
+            np.dtype(np.int32): INT}[a0.dtype]
+    sends = [np.ascontiguousarray(s) for s in sends]
+    recvs = [s.copy() for s in sends] if in_place else [np.full_like(s, -1) for s in sends]
+    rc = lib().ref_emulate_nodes(nodes, W // nodes, a0.size, code, op, copyin.encode(), int(in_place), num_sockets,
+                                 _ptrs(sends), _ptrs(recvs))
+    if rc != 0:
+        raise ValueError(f"oracle rejected copyin {copyin!r} for {nodes} x {W // nodes}")
     return recvs
 
 

@@ -93,6 +93,31 @@ done:
   return rc;
 }
 
+/* Two nodes, one port (EXT_MPI_NUM_PORTS "-1 1"). ext_mpi_native.c:879-1000 composes: the node's
+   copy-in -- reduce_copies_one_socket with in_out = 1 and one_node = 0 (reduce_copyin.c:1497-1500):
+   the same reduce-scatter emission as one node, into shared memory -- then the inter-node
+   algorithm of allreduce_recursive.c:222-453 over the node partials: with one port a single
+   radix-2 step, each line reduced from the two nodes' partials of it (:248-347, reducefrom of the
+   own line and the line received from the partner node), the lines exchanged back (:406-437), then
+   the node's copy-out. Every element thus ends as ONE two-operand reduction of the two node
+   partials; a two-operand SUM is commutative, so which partial is the accumulator changes no bit
+   (MIN / MAX with NaNs or signed zeros would depend on it: node 0's partial is taken first here,
+   parity for those inputs is unpinned). Ranks [0, R) are node 0, [R, 2R) node 1. */
+int ref_emulate_nodes(int nodes, int R, long count, int dtype, int red, const char *copyin, int in_place,
+                      int num_sockets, void *const *sendbufs, void *const *recvbufs) {
+  int n, r, rc;
+  const size_t bytes = (size_t)count * (size_t)ref_type_size(dtype);
+  if (nodes < 1 || nodes > 2 || R < 1 || ref_type_size(dtype) <= 0) return -1;
+  for (n = 0; n < nodes; n++)
+    if ((rc = ref_emulate_op_s(R, count, dtype, red, copyin, in_place, num_sockets, sendbufs + n * R, recvbufs + n * R)))
+      return rc;
+  if (nodes == 2) {
+    ref_reduction_op(red, dtype, recvbufs[0], recvbufs[R], count); /* node 0's partial, then node 1's */
+    for (r = 1; r < 2 * R; r++) memcpy(recvbufs[r], recvbufs[0], bytes);
+  }
+  return 0;
+}
+
 /* debug_persistent.c:491-497 (host pattern, add = 73) and :426-432 (device pattern, add = 0) */
 void ref_kat_fill(void *buf, long count, int tsize, int world_rank, long add) {
   long i, words = (count * tsize) / (long)sizeof(long int);

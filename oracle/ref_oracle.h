@@ -20,6 +20,8 @@
  *   src/gpu/cuda_shmem.c:280-296             (the same rotation, device)   -> ref_schedule.c
  *   src/mpi/ext_mpi_native_exec.c:21-84      node barriers (as phases)     -> ref_emulate.c
  *   src/mpi/debug_persistent.c:426-497       known-answer input pattern    -> ref_emulate.c
+ *   src/mpi/ext_mpi_native.c:879-1000,
+ *   src/core/allreduce_recursive.c:222-453   two nodes, one port           -> ref_emulate.c
  *
  * Parity pinning: the reference's own known-answer test pattern (debug_persistent.c) and the
  * method-6 schedules captured from the reference generators, both
@@ -101,6 +103,12 @@ int ref_emulate_op(int R, long count, int dtype, int op, const char *copyin, int
 /* ... and with num_sockets sockets per node (changes the tree method's roots) */
 int ref_emulate_op_s(int R, long count, int dtype, int op, const char *copyin, int in_place, int num_sockets,
                      void *const *sendbufs, void *const *recvbufs);
+
+/* Two nodes of R ranks, one port (src/mpi/ext_mpi_native.c:879-1000 with
+   src/core/allreduce_recursive.c:222-453): each node's copy-in, the two node partials reduced
+   once per element, the copy-out. 2R buffers, node-major. nodes = 1 is ref_emulate_op_s. */
+int ref_emulate_nodes(int nodes, int R, long count, int dtype, int red, const char *copyin, int in_place,
+                      int num_sockets, void *const *sendbufs, void *const *recvbufs);
 
 /* Known-answer input pattern of debug_persistent.c:491-497 (CPU: add=73, GPU: add=0). */
 void ref_kat_fill(void *buf, long count, int tsize, int world_rank, long add);

@@ -90,6 +90,78 @@ def test_comm_program_over_gloo(world, cases):
     assert [f for r in results for f in r] == []
 
 
+def _nodes_worker(rank, world, port, cases, q):
+    """two nodes of world // 2 ranks: the node legs, the node-pair legs and both folds"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle
+    failures = []
+    R = world // 2
+    for code, count, copyin in cases:
+        sends = xorshift_inputs(world, count, code, seed_base=0x2A0DE000 + count)
+        dt = NP[code]
+        itemsize = np.dtype(dt).itemsize
+        ops, folds, stage = emac.comm_program_nodes(2, R, rank, count, code, copyin)
+        bufs = {emac.BUF_SEND: sends[rank].view(np.uint8).copy(),
+                emac.BUF_RECV: np.full(count * itemsize, 0xAB, dtype=np.uint8),
+                emac.BUF_STAGE: np.zeros(max(stage, 1), dtype=np.uint8)}
+        desc = emac.plan_describe(R, count, code, copyin, 0)
+        _run_leg(ops, LEG_RS, bufs)
+        _fold([f[:3] for f in folds if f[3] == emac.LEG_FOLD], bufs, code, desc)
+        _run_leg(ops, emac.LEG_NODES_RS, bufs)
+        for off, n, leaves, leg in folds:
+            if leg != emac.LEG_NODES_FOLD:
+                continue
+            (b0, o0), (b1, o1) = leaves
+            x0 = bufs[b0][o0:o0 + n * itemsize].view(dt)
+            x1 = bufs[b1][o1:o1 + n * itemsize].view(dt)
+            with np.errstate(over="ignore"):
+                bufs[emac.BUF_RECV][off:off + n * itemsize].view(dt)[:] = x0 + x1
+        _run_leg(ops, emac.LEG_NODES_AG, bufs)
+        _run_leg(ops, LEG_AG, bufs)
+        want = oracle.allreduce_nodes(sends, copyin, 2)[rank]
+        if not np.array_equal(bufs[emac.BUF_RECV], want.view(np.uint8)):
+            failures.append((rank, code, count, copyin))
+    q.put(failures)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,cases", [
+    (2, [(emac.FLOAT, 100003, "6;1 -1 1"), (emac.INT, 7, "6;1 -1 1"), (emac.DOUBLE, 1, "6;1 -1 1")]),
+    (4, [(emac.FLOAT, 65539, "6;1 -2 2"), (emac.DOUBLE, 4099, "6;3 -2 2"), (emac.LONG, 1001, "6;-5 -2 2"),
+         (emac.FLOAT, 0, "6;1 -2 2"), (emac.FLOAT, 3, "6;1 -2 2")]),
+    (8, [(emac.FLOAT, 30011, "6;1 -2 -2 2 2"), (emac.DOUBLE, 9999, "7;1 -4 4"), (emac.INT, 5003, "5;1 -4 4"),
+         (emac.FLOAT, 20000, "6;1 -2 2 1 2 1 -2 2")]),
+])
+def test_two_node_program_over_gloo(world, cases):
+    """§8(f3), two nodes and one port: the COMM program of emac_comm_program_nodes executed over
+    gloo (ranks [0, world/2) are node 0) equals the oracle's two-node emulation bitwise."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29800 + world * 7 + os.getpid() % 200
+    procs = [ctx.Process(target=_nodes_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert [f for r in results for f in r] == []
+
+
+def test_two_node_program_shape():
+    # rank 5 = node 1, local rank 1 of 4: node legs with ranks 4..7, node-pair legs with rank 1
+    ops, folds, stage = emac.comm_program_nodes(2, 4, 5, 4 * 1000, emac.FLOAT, "6;1 -4 4")
+    assert {o[1] for o in ops if o[0] in (LEG_RS, LEG_AG)} == {4, 6, 7}
+    pair = [o for o in ops if o[0] in (emac.LEG_NODES_RS, emac.LEG_NODES_AG)]
+    assert {o[1] for o in pair} == {1} and len(pair) == 4
+    node_folds = [f for f in folds if f[3] == emac.LEG_NODES_FOLD]
+    assert len(node_folds) == 1
+    off, n, leaves, _ = node_folds[0]
+    assert (off, n) == ((1000 + 500) * 4, 500)  # node 1 finishes the second half of chunk 1
+    assert leaves[0] == (emac.BUF_RECV, off) and leaves[1][0] == emac.BUF_STAGE
+
+
 def test_comm_program_shape():
     ops, folds, stage = emac.comm_program(8, 3, 8 * 1000, emac.FLOAT, "6;1 -8 8")
     rs = [o for o in ops if o[0] == LEG_RS]

@@ -363,12 +363,16 @@ def test_fold_handle_and_copy_reduce(code, nsrc, ndst):
             assert np.array_equal(d.cpu().numpy().view(np.uint8), want.view(np.uint8)), (how, nsrc, ndst)
 
 
-def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=None, op=emac.SUM, repeats=1):
+def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=None, op=emac.SUM, repeats=1, nodes=1):
     """COMM form (one rank per communicator) on the in-process loopback transport: the legs run
-    on every rank in lock-step -- stage-in, reduce-scatter, fold, all-gather, stage-out -- so
-    the staging slots, fold buckets and leg programs of the multi-GPU path execute on one GPU."""
+    on every rank in lock-step -- stage-in, reduce-scatter, fold, [the two-node legs,] all-gather,
+    stage-out -- so the staging slots, fold buckets and leg programs of the multi-GPU path execute
+    on one GPU. nodes=2: ranks [0, R/2) and [R/2, R) are two nodes (ext_mpi_amd_comm_set_nodes)."""
     R, count = len(sends), sends[0].size
     comms = emac.comm_init_loopback(R)
+    if nodes > 1:
+        for c in comms:
+            emac.comm_set_nodes(c, nodes)
     phase = phase or [0] * R
     keep = []
     if host:
@@ -393,8 +397,7 @@ def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=Non
                 for t in rbufs:
                     t.fill_(-1)
             torch.cuda.synchronize()
-            for leg in (emac.LEG_STAGE_IN, emac.LEG_REDUCE_SCATTER, emac.LEG_FOLD, emac.LEG_ALLGATHER,
-                        emac.LEG_STAGE_OUT):
+            for leg in emac.LEG_ORDER:
                 for h in hs:
                     emac.start_legs(h, leg)
                 for h in hs:
@@ -420,6 +423,30 @@ def test_comm_form_loopback_parity(oracle, R, copyin, code):
         want = oracle.allreduce(sends, copyin)
         got = run_comm_loopback(sends, code, copyin, phase=[(r * 3) % 4 for r in range(R)])
         assert_bitwise(got, want, f"comm R={R} {copyin} code={code} n={count}")
+
+
+@pytest.mark.parametrize("R,copyin", [(2, "6;1 -1 1"), (4, "6;1 -2 2"), (8, "6;1 -4 4"), (8, "6;1 -2 -2 2 2"),
+                                      (16, "6;1 -8 8"), (8, "7;1 -4 4"), (6, "5;1 -3 3"), (8, "6;-64 -4 4")])
+@pytest.mark.parametrize("code", CODES)
+def test_comm_two_nodes_loopback_vs_oracle(oracle, R, copyin, code):
+    """§8(f3): two nodes of R/2 ranks, one port -- the node's legs and fold, the node-pair swap of
+    the owned chunk's halves, their two-leaf fold, the swap back, the node's allgather -- bitwise
+    against the oracle's two-node emulation, with per-rank 16-byte phase shifts."""
+    for count in (0, 1, 7, 1031, 65536 + 5):
+        sends = xorshift_inputs(R, count, code, seed_base=0x20DE0000 + count)
+        want = oracle.allreduce_nodes(sends, copyin, 2)
+        got = run_comm_loopback(sends, code, copyin, phase=[(r * 3) % 4 for r in range(R)], nodes=2)
+        assert_bitwise(got, want, f"two nodes R={R} {copyin} code={code} n={count}")
+
+
+def test_comm_two_nodes_loopback_in_place_host_repeats(oracle):
+    sends = xorshift_inputs(8, 100003, emac.FLOAT, seed_base=0x20DE7000)
+    want = oracle.allreduce_nodes(sends, "6;1 -4 4", 2, in_place=True)
+    assert_bitwise(run_comm_loopback(sends, emac.FLOAT, "6;1 -4 4", in_place=True, nodes=2), want,
+                   "two nodes in place")
+    want = oracle.allreduce_nodes(sends, "6;1 -2 -2 2 2", 2)
+    assert_bitwise(run_comm_loopback(sends, emac.FLOAT, "6;1 -2 -2 2 2", host=True, nodes=2), want,
+                   "two nodes host buffers")
 
 
 @pytest.mark.parametrize("graph", ["0", "1"])

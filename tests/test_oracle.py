@@ -272,3 +272,29 @@ def test_tree_without_allgather_radices_is_rejected(oracle):
     sends = [np.ones(16, np.float32)] * 4
     with pytest.raises(ValueError):
         oracle.allreduce(sends, "7;1 -4")
+
+
+@pytest.mark.parametrize("R,copyin", [(1, "6;1 -1 1"), (2, "6;1 -2 2"), (4, "6;1 -2 -2 2 2"), (4, "7;1 -4 4"),
+                                      (8, "5;1 -8 8")])
+def test_two_nodes_known_answer(oracle, R, copyin):
+    # ext_mpi_native.c:879-1000 + allreduce_recursive.c:222-453 (one port): integer sums over both
+    # nodes' ranks exactly, in place and out of place
+    W = 2 * R
+    for count, code in ((1000, oracle.INT), (777, oracle.LONG)):
+        ins = [oracle.kat_fill(count, code, r, 73) for r in range(W)]
+        want = np.sum(np.stack(ins).astype(np.int64), axis=0).astype(ins[0].dtype)
+        for in_place in (False, True):
+            for out in oracle.allreduce_nodes([x.copy() for x in ins], copyin, 2, in_place=in_place):
+                assert np.array_equal(out, want)
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_two_nodes_fold_is_one_reduction_of_the_node_partials(oracle, dt):
+    # every element = (node 0's single-node result) + (node 1's): one two-operand add, commutative
+    rng = np.random.default_rng(5)
+    R = 4
+    sends = [((rng.random(1003) * 2 - 1) * 10.0 ** rng.integers(-3, 4, 1003)).astype(dt) for _ in range(2 * R)]
+    p0 = oracle.allreduce(sends[:R], "6;1 -4 4")[0]
+    p1 = oracle.allreduce(sends[R:], "6;1 -4 4")[0]
+    for out in oracle.allreduce_nodes(sends, "6;1 -4 4", 2):
+        assert np.array_equal(out, (p0 + p1).astype(dt)) and np.array_equal(out, (p1 + p0).astype(dt))
