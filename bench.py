@@ -559,7 +559,7 @@ def single_gpu(args):
         out["cpu_baseline"] = cpu_baseline(R, count, np_dtype, copyin, args.cpu_seconds)
         if not args.no_extras:
             out["cpu_baseline"]["config0_64KiB_4ranks"] = cpu_config0()
-    print(json.dumps(out), flush=True)
+    emit(out)
 
 
 def _comm_run(emac, comm, count, tdtype, code, dname, copyin, steps, warmup, rank, world, dist, torch, check=True,
@@ -840,10 +840,10 @@ def multi_gpu(args):
         if "rccl_allreduce_baseline" in results[t]:  # whichever role RCCL had
             extras["rccl_allreduce_baseline"] = results[t]["rccl_allreduce_baseline"]
     if rank == 0 and primary is None:
-        print(json.dumps({"metric": "device-resident GB/s reduced (float32 MPI_SUM) per GPU; % HBM3E roofline",
+        emit(({"metric": "device-resident GB/s reduced (float32 MPI_SUM) per GPU; % HBM3E roofline",
                           "value": 0.0, "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dname,
-                          "error": "no transport completed", "extras": extras}), flush=True)
+                          "error": "no transport completed", "extras": extras}))
     if rank == 0 and primary is not None:
         r = results[primary]
         wall, checked, kf = r["wall"], r["checked"], r["fold_s"]
@@ -902,7 +902,7 @@ def multi_gpu(args):
                          "algorithmic_bytes_per_launch": int(algo), "avg_launch_us": round(kl * 1e6, 2)},
             "extras": extras,
         }
-        print(json.dumps(out), flush=True)
+        emit(out)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -919,11 +919,31 @@ def shape_only(args):
     else:
         r = node_run(8, MB // 4, torch.float32, emac.FLOAT, "6;1 -8 8", 40, 4, alloc="hip")
         r = {"avg_launch_us": round(r["event_ms"] * 1e3 / 40, 2), "checked": r["checked"]}
-    print(json.dumps({"shape": args.shape, **r}), flush=True)
+    emit({"shape": args.shape, **r})
+
+
+_RESULT_FD = None
+
+
+def emit(obj):
+    """The result line, on the real stdout: everything else -- library banners, gloo and RCCL
+    chatter of this process and its children -- goes to stderr (see main)."""
+    line = (json.dumps(obj) + "\n").encode()
+    if _RESULT_FD is None:
+        sys.stdout.write(line.decode())
+        sys.stdout.flush()
+    else:
+        os.write(_RESULT_FD, line)
 
 
 def main():
+    global _RESULT_FD
     args = parse()
+    # keep stdout for the one result line: fd 1 (C-level writers included, and every child
+    # process) goes to stderr, the line is written to a saved copy of the original stdout
+    sys.stdout.flush()
+    _RESULT_FD = os.dup(1)
+    os.dup2(2, 1)
     if args.shape:
         shape_only(args)
     elif args.child_transport:

@@ -32,8 +32,9 @@ def test_bench_multi_rank_transport_isolation_without_gpu():
                         os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1"],
                        capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
-    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, p.stdout
+    # stdout carries the one result line and nothing else (gloo / RCCL chatter goes to stderr)
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["value"] == 0.0 and out["error"] == "no transport completed"
     ex = out["extras"]
