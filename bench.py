@@ -479,10 +479,12 @@ def single_gpu(args):
         # latency -> bandwidth crossover of the node form (cf. BASELINE configs[4] on 8 GPUs);
         # small points reuse one buffer set (as the reference's latency runs do), large ones rotate
         sweep = []
-        for nbytes in (8, 1024, 64 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20):
+        # (to configs[4]'s 512 MiB endpoint: one buffer set of 8 GiB is far past the Infinity Cache)
+        for nbytes in (8, 1024, 64 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20, 512 << 20):
             cnt = max(1, nbytes // tsize)
-            st = 200 if nbytes <= (1 << 20) else 40
-            r = node_run(R, cnt, tdtype, code, copyin, st, 5, min_set_bytes=0 if nbytes < (16 << 20) else 640 * MIB,
+            st = 200 if nbytes <= (1 << 20) else 40 if nbytes <= (64 << 20) else 5
+            r = node_run(R, cnt, tdtype, code, copyin, st, 2 if nbytes > (64 << 20) else 5,
+                         min_set_bytes=0 if nbytes < (16 << 20) or nbytes > (64 << 20) else 640 * MIB,
                          alloc=args.alloc)
             sweep.append({"bytes_per_rank": cnt * tsize, "us_per_allreduce": round(r["wall_s"] * 1e6 / st, 2),
                           "gpu_us_per_allreduce": round(r["event_ms"] * 1e3 / st, 2),
@@ -724,7 +726,7 @@ def transport_child(args):
             res["rccl_allreduce_baseline"] = _rccl_allreduce_baseline(rank, world, dist, torch)
         if full:
             # BASELINE configs[3] (double, 256 MiB per rank) and a configs[4]-style size sweep
-            points = [(args.dtype, n) for n in (8, 64 << 10, 1 << 20, 16 << 20, 64 << 20, 256 << 20)]
+            points = [(args.dtype, n) for n in (8, 64 << 10, 1 << 20, 16 << 20, 64 << 20, 256 << 20, 512 << 20)]
             points.append(("double", 256 << 20))
             sweep = []
             for dname_p, nbytes in points:
