@@ -14,6 +14,8 @@
  * Configuration as the reference reads it (ext_mpi.c:43-187; rank 0 reads the environment and
  * broadcasts): EXT_MPI_COPYIN, EXT_MPI_VERBOSE, EXT_MPI_DEBUG (default 1: the known-answer
  * self-test of debug_persistent.c:393-568 runs inside every Allreduce_init),
+ * EXT_MPI_NUM_TASKS_PER_SOCKET (ranks per socket: with the sockets, the node size -- a physical
+ * node may hold two logical ones), EXT_MPI_NUM_PORTS (two nodes: one port, every entry +-1),
  * EXT_MPI_NUM_SOCKETS_PER_NODE (any divisor of the node size: sockets change the reference's
  * partner encoding and barrier scope, and the tree method's last-step roots -- the one place
  * they reach the fold arithmetic, ext_mpi_amd_set_num_sockets). MPI_Info
@@ -54,6 +56,8 @@ static int cfg_has_copyin = 0;
 static int cfg_verbose = 0;
 static int cfg_debug = 1;
 static int cfg_num_sockets = -1;
+static int cfg_tasks_per_socket = -1; /* EXT_MPI_NUM_TASKS_PER_SOCKET: ranks of a (logical) socket */
+static int cfg_ports_ok = 1;          /* EXT_MPI_NUM_PORTS names the one-port schedule (or is unset) */
 static int cfg_blocking = 0;
 static int cfg_rccl = 0; /* EXT_MPI_AMD_TRANSPORT=rccl: legs over RCCL instead of hipIpc mappings */
 static int initialised = 0;
@@ -79,6 +83,28 @@ static void read_env(void) {
     cfg_blocking = getenv("EXT_MPI_BLOCKING") != NULL; /* ext_mpi_interface.c:46-51 */
     env_int("EXT_MPI_DEBUG", &cfg_debug);
     env_int("EXT_MPI_NUM_SOCKETS_PER_NODE", &cfg_num_sockets);
+    env_int("EXT_MPI_NUM_TASKS_PER_SOCKET", &cfg_tasks_per_socket);
+    {
+      /* EXT_MPI_NUM_PORTS "p0 p1 ..." (ports_groups.c:37-74, "(groups)" parts ignored): the
+         inter-node schedule here is the one-port one, radix 2 per step -- every entry +-1 */
+      const char *pp = getenv("EXT_MPI_NUM_PORTS");
+      while (pp && *pp) {
+        char *end;
+        long v;
+        if (*pp == '(') {
+          while (*pp && *pp != ')') pp++;
+          if (*pp) pp++;
+          continue;
+        }
+        v = strtol(pp, &end, 10);
+        if (end == pp) {
+          pp++;
+          continue;
+        }
+        if (v != 1 && v != -1) cfg_ports_ok = 0;
+        pp = end;
+      }
+    }
     cfg_rccl = getenv("EXT_MPI_AMD_TRANSPORT") && !strcmp(getenv("EXT_MPI_AMD_TRANSPORT"), "rccl");
     if (c) {
       strncpy(cfg_copyin, c, sizeof(cfg_copyin) - 1);
@@ -89,6 +115,8 @@ static void read_env(void) {
   PMPI_Bcast(&cfg_blocking, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_debug, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_num_sockets, 1, MPI_INT, 0, MPI_COMM_WORLD);
+  PMPI_Bcast(&cfg_tasks_per_socket, 1, MPI_INT, 0, MPI_COMM_WORLD);
+  PMPI_Bcast(&cfg_ports_ok, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_rccl, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&len, 1, MPI_INT, 0, MPI_COMM_WORLD);
   if (len > 0) PMPI_Bcast(cfg_copyin, len, MPI_CHAR, 0, MPI_COMM_WORLD);
@@ -207,6 +235,15 @@ static int node_comm(MPI_Comm comm, const void *devbuf, int *ext_comm) {
   PMPI_Comm_size(node, &nsize);
   PMPI_Comm_rank(node, &nrank);
   PMPI_Comm_free(&node);
+  if (cfg_tasks_per_socket > 0) {
+    /* the reference's node = EXT_MPI_NUM_TASKS_PER_SOCKET x sockets consecutive ranks
+       (ext_mpi.c:195-215, :638): a physical node may hold several logical ones */
+    const int lsize = cfg_tasks_per_socket * (cfg_num_sockets > 0 ? cfg_num_sockets : 1);
+    if (lsize <= nsize && nsize % lsize == 0) {
+      nsize = lsize;
+      nrank = rank % lsize;
+    }
+  }
   {
     /* one node, or two nodes of equal size in node-major rank order (the reference's row layout,
        ext_mpi_native.c:879-960): the second runs the one-port two-node schedule over RCCL */
@@ -216,6 +253,7 @@ static int node_comm(MPI_Comm comm, const void *devbuf, int *ext_comm) {
     PMPI_Allreduce(MPI_IN_PLACE, v, 2, MPI_INT, MPI_MIN, comm);
     if (!v[0] && !v[1]) return EXT_MPI_AMD_ERROR_UNSUPPORTED; /* other inter-node shapes: out of scope */
     nodes = v[0] ? 1 : 2;
+    if (nodes > 1 && !cfg_ports_ok) return EXT_MPI_AMD_ERROR_UNSUPPORTED; /* several ports: not built */
   }
   ndev = ext_mpi_amd_gpu_device_count();
   device = ext_mpi_amd_gpu_device_of(devbuf);

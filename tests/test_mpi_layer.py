@@ -58,6 +58,23 @@ def test_mpi_layer_single_rank_gpu(tmp_path, args):
     assert res and res[0].startswith("RESULT ok"), out
 
 
+@pytest.mark.parametrize("env,want", [
+    ({"EXT_MPI_NUM_TASKS_PER_SOCKET": "1"}, "RESULT no-device"),                 # two logical nodes of 1
+    ({"EXT_MPI_NUM_TASKS_PER_SOCKET": "1", "EXT_MPI_NUM_PORTS": "-1 1"}, "RESULT no-device"),
+    ({"EXT_MPI_NUM_TASKS_PER_SOCKET": "1", "EXT_MPI_NUM_PORTS": "-2 2"}, "RESULT fail rc=-4"),
+])
+def test_mpi_logical_nodes_without_gpu(tmp_path, env, want):
+    """EXT_MPI_NUM_TASKS_PER_SOCKET splits the ranks into logical nodes (ext_mpi.c:195-215): two of
+    them take the two-node schedule over RCCL (no device here: ERROR_DEVICE on every rank); a
+    several-port EXT_MPI_NUM_PORTS is refused (ERROR_UNSUPPORTED) instead of computed otherwise."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    exe = _build(tmp_path)
+    res, out = _run(exe, 2, [1000, "i", "dev"], env=env)
+    assert res and res[0].startswith(want), out
+
+
 def test_mpi_blocking_without_gpu(tmp_path):
     """EXT_MPI_BLOCKING routes MPI_Allreduce(SUM) to the engine, which fails loudly without a GPU."""
     import torch
