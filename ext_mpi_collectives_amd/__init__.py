@@ -242,11 +242,27 @@ def done(h):
 
 
 LEG_STAGE_IN, LEG_REDUCE_SCATTER, LEG_FOLD, LEG_ALLGATHER, LEG_STAGE_OUT = 1, 2, 4, 8, 16
-LEG_NODES_RS, LEG_NODES_FOLD, LEG_NODES_AG = 32, 64, 128  # two nodes (comm_set_nodes)
+LEG_NODES_RS, LEG_NODES_FOLD, LEG_NODES_AG = 32, 64, 128  # 2^k nodes (comm_set_nodes), per step
 LEG_STAGE, LEG_ALL = 17, 255
-# the order Start runs them in
-LEG_ORDER = (LEG_STAGE_IN, LEG_REDUCE_SCATTER, LEG_FOLD, LEG_NODES_RS, LEG_NODES_FOLD, LEG_NODES_AG, LEG_ALLGATHER,
-             LEG_STAGE_OUT)
+LEG_STEP_SHIFT = 8  # node legs / folds carry their step: leg | step << 8
+
+
+def LEG_STEP(s):
+    """start_legs selector: the node legs of step s alone (loopback lock-step)"""
+    return (s + 1) << LEG_STEP_SHIFT
+
+
+def lockstep_legs(nodes=1):
+    """The legs of one Start in the order a lock-step driver runs them on every rank: stage-in,
+    reduce-scatter, fold, per node step the pair exchange and its fold, the exchanges back in
+    reverse step order, allgather, stage-out."""
+    k = max(0, (nodes - 1).bit_length())
+    legs = [LEG_STAGE_IN, LEG_REDUCE_SCATTER, LEG_FOLD]
+    for st in range(k):
+        legs += [LEG_NODES_RS | LEG_STEP(st), LEG_NODES_FOLD | LEG_STEP(st)]
+    legs += [LEG_NODES_AG | LEG_STEP(st) for st in reversed(range(k))]
+    return legs + [LEG_ALLGATHER, LEG_STAGE_OUT]
+
 
 
 def start_legs(h, legs):
@@ -309,7 +325,8 @@ def comm_program_nodes(nodes, ranks_per_node, rank, count, dtype, copyin=None, s
 
 
 def comm_set_nodes(comm, nodes):
-    """Declare ranks [0, size/2) and [size/2, size) of an RCCL / loopback communicator two nodes."""
+    """Declare the ranks of an RCCL / loopback communicator `nodes` (a power of two) nodes of
+    size / nodes consecutive ranks each."""
     return _check("ext_mpi_amd_comm_set_nodes", lib().ext_mpi_amd_comm_set_nodes(comm, nodes))
 
 

@@ -167,8 +167,8 @@ typedef struct {
   int fused; /* whole Allreduce in one launch (emac_gpu_fold_fused) */
   void *ev_release; /* system-scope release recorded before every phase-0 barrier */
   emac_launch pull; /* every other owner's result copied into this rank's receive buffer */
-  int nodes;         /* COMM form over two nodes: the node-pair legs run (emac_comm_program_nodes) */
-  emac_launch xfold; /* ... and fold this node's partial with the other node's (two leaves) */
+  int nodes;            /* COMM form over 2^k nodes: the node-pair legs run (emac_comm_program_nodes) */
+  emac_launch xfold[4]; /* ... and, per step, fold this node's partial with the partner node's */
   void *graph[EXT_MPI_AMD_LEG_ALL + 1]; /* COMM form: captured legs, per subset of EXT_MPI_AMD_LEG_* */
   unsigned char graph_failed[EXT_MPI_AMD_LEG_ALL + 1];
   emac_pipe *pipe; /* pipelined host staging (NODE form), or NULL */
@@ -217,8 +217,10 @@ static void release(emac_handle *h) {
   emac_gpu_free(h->d_edges);
   emac_gpu_free(h->pull.d_buckets);
   emac_gpu_free(h->pull.d_edges);
-  emac_gpu_free(h->xfold.d_buckets);
-  emac_gpu_free(h->xfold.d_edges);
+  for (r = 0; r < 4; r++) {
+    emac_gpu_free(h->xfold[r].d_buckets);
+    emac_gpu_free(h->xfold[r].d_edges);
+  }
   emac_gpu_free(h->staging);
   for (r = 0; r < h->nbuf; r++) {
     int same = h->dsend[r] == h->drecv[r];
@@ -1209,13 +1211,14 @@ int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, i
     emac_fold *folds = NULL;
     int nf = 0, f;
     emac_bucket *xb = NULL;
-    int nxb = 0;
+    int nxb[4] = {0, 0, 0, 0}, st, nsteps = 0;
+    while ((1 << nsteps) < h->nodes) nsteps++;
     if ((rc = emac_comm_program_nodes(&h->plan, h->nodes, h->me / R, h->me % R,
                                       (long)((unsigned long)h->dsend[0] & 15ul), &h->ops, &h->nops, &folds, &nf,
                                       &stage_total)))
       goto fail;
     b = (emac_bucket *)calloc((size_t)nf + 1, sizeof(emac_bucket));
-    xb = (emac_bucket *)calloc((size_t)nf + 1, sizeof(emac_bucket));
+    xb = (emac_bucket *)calloc(4 * ((size_t)nf + 1), sizeof(emac_bucket));
     if (!b || !xb || (rc = emac_gpu_malloc(&h->staging, (size_t)(stage_total > 0 ? stage_total : 16)))) {
       free(folds);
       free(xb);
@@ -1223,8 +1226,9 @@ int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, i
       goto fail;
     }
     for (f = 0; f < nf; f++) {
-      const int node_pair = folds[f].leg == EMAC_LEG_NODES_FOLD;
-      emac_bucket *bk = node_pair ? &xb[nxb++] : &b[nb++];
+      const int node_pair = (folds[f].leg & ((1 << EMAC_LEG_STEP_SHIFT) - 1)) == EMAC_LEG_NODES_FOLD;
+      const int step = folds[f].leg >> EMAC_LEG_STEP_SHIFT;
+      emac_bucket *bk = node_pair ? &xb[(size_t)step * ((size_t)nf + 1) + (size_t)nxb[step]++] : &b[nb++];
       long off = folds[f].offset / h->plan.tsize;
       for (t = 0; t < folds[f].nleaf; t++) {
         /* leaf pointers are shifted back by the result's offset: split_alignment adds it */
@@ -1235,10 +1239,11 @@ int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, i
       place_bucket(bk, folds[f].nleaf, off, folds[f].count, h->plan.tsize);
     }
     free(folds);
-    if (h->nodes > 1 && nxb && (rc = upload_launch_as(h, &h->xfold, xb, nxb, 2, 0))) {
-      free(xb);
-      goto fail;
-    }
+    for (st = 0; st < nsteps; st++)
+      if (nxb[st] && (rc = upload_launch_as(h, &h->xfold[st], xb + (size_t)st * ((size_t)nf + 1), nxb[st], 2, 0))) {
+        free(xb);
+        goto fail;
+      }
     free(xb);
   }
   if ((rc = upload_buckets(h, b, nb))) goto fail;
@@ -1453,16 +1458,28 @@ static int enqueue_legs(emac_handle *h, int legs) {
                           h->tiles_per_bucket, h->all_full, h->d_edges, h->nedges, h->stream)))
     return rc;
   if (h->kind == KIND_COMM && h->nodes > 1) {
-    /* two nodes: the node-pair exchange of the owned chunk's halves, their two-leaf fold, the
-       exchange back (emac_comm_program_nodes) */
+    /* 2^k nodes: per step the node-pair exchange of the owned range's halves and their two-leaf
+       fold, then the exchanges back in reverse step order (emac_comm_program_nodes). A step
+       selector in the legs' high bits (EXT_MPI_AMD_LEG_STEP) runs that step's legs alone. */
     static const emac_codes pair = {{1, 0}, {0, 1}, 1, 2};
-    if ((legs & EXT_MPI_AMD_LEG_NODES_RS) && (rc = run_leg(h, EMAC_LEG_NODES_RS))) return rc;
-    if ((legs & EXT_MPI_AMD_LEG_NODES_FOLD) && h->xfold.nb &&
-        (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, 2, 0, h->xfold.unroll, &pair, h->xfold.d_buckets, h->xfold.nb,
-                            h->xfold.ntiles, h->xfold.tiles_per_bucket, h->xfold.all_full, h->xfold.d_edges,
-                            h->xfold.nedges, h->stream)))
-      return rc;
-    if ((legs & EXT_MPI_AMD_LEG_NODES_AG) && (rc = run_leg(h, EMAC_LEG_NODES_AG))) return rc;
+    int st, nsteps = 0;
+    const int only = (legs >> EMAC_LEG_STEP_SHIFT) & 31;
+    while ((1 << nsteps) < h->nodes) nsteps++;
+    for (st = 0; st < nsteps; st++) {
+      const emac_launch *X = &h->xfold[st];
+      if (only && st != only - 1) continue;
+      if ((legs & EXT_MPI_AMD_LEG_NODES_RS) && (rc = run_leg(h, EMAC_LEG_NODES_RS | st << EMAC_LEG_STEP_SHIFT)))
+        return rc;
+      if ((legs & EXT_MPI_AMD_LEG_NODES_FOLD) && X->nb &&
+          (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, 2, 0, X->unroll, &pair, X->d_buckets, X->nb, X->ntiles,
+                              X->tiles_per_bucket, X->all_full, X->d_edges, X->nedges, h->stream)))
+        return rc;
+    }
+    for (st = nsteps - 1; st >= 0; st--) {
+      if (only && st != only - 1) continue;
+      if ((legs & EXT_MPI_AMD_LEG_NODES_AG) && (rc = run_leg(h, EMAC_LEG_NODES_AG | st << EMAC_LEG_STEP_SHIFT)))
+        return rc;
+    }
   }
   if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && multi && (rc = run_leg(h, EMAC_LEG_AG))) return rc;
   if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && h->kind == KIND_IPC && h->plan.nranks > 1) {
@@ -1500,6 +1517,11 @@ int ext_mpi_amd_start_legs(int handle, int legs) {
   if (emac_gpu_set_device(h->device)) return EMAC_ERR_DEVICE;
   if (h->pipe && (legs & EXT_MPI_AMD_LEG_ALL) == EXT_MPI_AMD_LEG_ALL) return pipe_start(h);
   key = legs & EXT_MPI_AMD_LEG_ALL;
+  if (legs >> EMAC_LEG_STEP_SHIFT) { /* one node step alone (loopback lock-step): never captured */
+    if ((rc = enqueue_legs(h, legs))) return rc;
+    h->started = 1;
+    return 0;
+  }
   if (graph_ok(h) && !h->graph[key] && !h->graph_failed[key]) {
     if (emac_gpu_capture_begin(h->stream) == 0) {
       const int erc = enqueue_legs(h, legs);
@@ -1603,7 +1625,7 @@ int ext_mpi_amd_comm_program(int nranks, int rank, long count, int dtype, const 
 
 int ext_mpi_amd_comm_set_nodes(int comm, int nodes) {
   if (comm < 0 || comm >= MAX_COMMS || !comms[comm].used) return EMAC_ERR_ARG;
-  if (nodes < 1 || comms[comm].size % nodes) return EMAC_ERR_ARG;
+  if (nodes < 1 || comms[comm].size % nodes || (nodes & (nodes - 1))) return EMAC_ERR_ARG;
   if (nodes > EMAC_MAX_NODES || (nodes > 1 && comms[comm].ipc)) return EMAC_ERR_UNSUPPORTED;
   comms[comm].nodes = nodes;
   return 0;

@@ -15,7 +15,8 @@
  * broadcasts): EXT_MPI_COPYIN, EXT_MPI_VERBOSE, EXT_MPI_DEBUG (default 1: the known-answer
  * self-test of debug_persistent.c:393-568 runs inside every Allreduce_init),
  * EXT_MPI_NUM_TASKS_PER_SOCKET (ranks per socket: with the sockets, the node size -- a physical
- * node may hold two logical ones), EXT_MPI_NUM_PORTS (two nodes: one port, every entry +-1),
+ * node may hold several logical ones), EXT_MPI_NUM_PORTS (several nodes: one port per step, every
+ * entry +-1, log2(nodes) reduce-scatter steps),
  * EXT_MPI_NUM_SOCKETS_PER_NODE (any divisor of the node size: sockets change the reference's
  * partner encoding and barrier scope, and the tree method's last-step roots -- the one place
  * they reach the fold arithmetic, ext_mpi_amd_set_num_sockets). MPI_Info
@@ -35,9 +36,9 @@
  * bootstrapped with PMPI_Allgather; "rccl" runs the legs as RCCL point-to-point rounds,
  * bootstrapped with PMPI_Bcast of the unique id. One engine communicator per MPI communicator,
  * cached as an MPI attribute and destroyed with it. The communicator lies within one node, or
- * spans two nodes of equal size in node-major rank order: then the legs run over RCCL with the
- * reference's one-port two-node schedule (ext_mpi_amd_comm_set_nodes); other inter-node shapes
- * return EXT_MPI_AMD_ERROR_UNSUPPORTED (the blocking front end hands them to PMPI).
+ * spans 2^k nodes (<= 16) of equal size in node-major rank order: then the legs run over RCCL with
+ * the reference's one-port inter-node schedule (ext_mpi_amd_comm_set_nodes); other inter-node
+ * shapes return EXT_MPI_AMD_ERROR_UNSUPPORTED (the blocking front end hands them to PMPI).
  */
 #include <mpi.h>
 #include <stdio.h>
@@ -58,6 +59,7 @@ static int cfg_debug = 1;
 static int cfg_num_sockets = -1;
 static int cfg_tasks_per_socket = -1; /* EXT_MPI_NUM_TASKS_PER_SOCKET: ranks of a (logical) socket */
 static int cfg_ports_ok = 1;          /* EXT_MPI_NUM_PORTS names the one-port schedule (or is unset) */
+static int cfg_ports_steps = -1;      /* ... with this many reduce-scatter steps (-1: unset) */
 static int cfg_blocking = 0;
 static int cfg_rccl = 0; /* EXT_MPI_AMD_TRANSPORT=rccl: legs over RCCL instead of hipIpc mappings */
 static int initialised = 0;
@@ -102,6 +104,7 @@ static void read_env(void) {
           continue;
         }
         if (v != 1 && v != -1) cfg_ports_ok = 0;
+        if (v == -1) cfg_ports_steps = cfg_ports_steps < 0 ? 1 : cfg_ports_steps + 1;
         pp = end;
       }
     }
@@ -117,6 +120,7 @@ static void read_env(void) {
   PMPI_Bcast(&cfg_num_sockets, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_tasks_per_socket, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_ports_ok, 1, MPI_INT, 0, MPI_COMM_WORLD);
+  PMPI_Bcast(&cfg_ports_steps, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_rccl, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&len, 1, MPI_INT, 0, MPI_COMM_WORLD);
   if (len > 0) PMPI_Bcast(cfg_copyin, len, MPI_CHAR, 0, MPI_COMM_WORLD);
@@ -245,15 +249,19 @@ static int node_comm(MPI_Comm comm, const void *devbuf, int *ext_comm) {
     }
   }
   {
-    /* one node, or two nodes of equal size in node-major rank order (the reference's row layout,
-       ext_mpi_native.c:879-960): the second runs the one-port two-node schedule over RCCL */
-    int v[2];
+    /* one node, or 2^k nodes of equal size in node-major rank order (the reference's row layout,
+       ext_mpi_native.c:879-960): those run the one-port inter-node schedule over RCCL */
+    int v[2], k = 0;
+    nodes = nsize > 0 && size % nsize == 0 ? size / nsize : 0;
+    while ((1 << k) < nodes) k++;
     v[0] = nsize == size;
-    v[1] = size == 2 * nsize && nrank == rank % nsize;
+    v[1] = nodes >= 2 && nodes <= 16 && (1 << k) == nodes && nrank == rank % nsize;
     PMPI_Allreduce(MPI_IN_PLACE, v, 2, MPI_INT, MPI_MIN, comm);
     if (!v[0] && !v[1]) return EXT_MPI_AMD_ERROR_UNSUPPORTED; /* other inter-node shapes: out of scope */
-    nodes = v[0] ? 1 : 2;
-    if (nodes > 1 && !cfg_ports_ok) return EXT_MPI_AMD_ERROR_UNSUPPORTED; /* several ports: not built */
+    if (v[0]) nodes = 1;
+    /* several ports per step are not built, nor a step count other than log2(nodes) */
+    if (nodes > 1 && (!cfg_ports_ok || (cfg_ports_steps >= 0 && cfg_ports_steps != k)))
+      return EXT_MPI_AMD_ERROR_UNSUPPORTED;
   }
   ndev = ext_mpi_amd_gpu_device_count();
   device = ext_mpi_amd_gpu_device_of(devbuf);

@@ -380,22 +380,30 @@ int emac_comm_program(const emac_plan *p, int me, long send_phase, emac_p2p **op
   return emac_comm_program_nodes(p, 1, 0, me, send_phase, ops_out, nops_out, folds_out, nfolds_out, staging_bytes);
 }
 
+/* log2 of a power of two, -1 otherwise */
+static int log2_exact(int n) {
+  int k = 0;
+  if (n < 1) return -1;
+  while ((1 << k) < n) k++;
+  return (1 << k) == n ? k : -1;
+}
+
 int emac_comm_program_nodes(const emac_plan *p, int nodes, int node, int me, long send_phase, emac_p2p **ops_out,
                             int *nops_out, emac_fold **folds_out, int *nfolds_out, long *staging_bytes) {
-  int R = p->nranks, me_pos, pc, q, t, nops = 0, nf = 0, leg, g0, partner;
+  const int k = log2_exact(nodes);
+  int R = p->nranks, me_pos, pc, q, t, nops = 0, nf = 0, leg, g0, st;
   long ts = p->tsize, total = 0;
   long *slot0, *stride, *xslot;
   emac_p2p *ops;
   emac_fold *folds;
-  if (nodes < 1 || nodes > EMAC_MAX_NODES || node < 0 || node >= nodes || me < 0 || me >= R) return EMAC_ERR_ARG;
+  if (k < 0 || nodes > EMAC_MAX_NODES || node < 0 || node >= nodes || me < 0 || me >= R) return EMAC_ERR_ARG;
   me_pos = p->rank_pos[me];
-  g0 = node * R;                      /* global rank of this node's first rank */
-  partner = (nodes - 1 - node) * R + me; /* the same rank of the other node */
+  g0 = node * R; /* global rank of this node's first rank */
   slot0 = (long *)malloc(sizeof(long) * (size_t)p->npieces);
   stride = (long *)malloc(sizeof(long) * (size_t)p->npieces);
-  xslot = (long *)malloc(sizeof(long) * (size_t)p->npieces);
-  ops = (emac_p2p *)malloc(sizeof(emac_p2p) * (size_t)(4 * p->npieces * R + 4 * p->npieces + 1));
-  folds = (emac_fold *)calloc((size_t)(2 * p->npieces) + 1, sizeof(emac_fold));
+  xslot = (long *)malloc(sizeof(long) * (size_t)p->npieces * (size_t)(k > 0 ? k : 1));
+  ops = (emac_p2p *)malloc(sizeof(emac_p2p) * (size_t)(4 * p->npieces * R + 4 * k * p->npieces + 1));
+  folds = (emac_fold *)calloc((size_t)((1 + k) * p->npieces) + 1, sizeof(emac_fold));
   if (!slot0 || !stride || !xslot || !ops || !folds) {
     free(slot0);
     free(stride);
@@ -411,14 +419,19 @@ int emac_comm_program_nodes(const emac_plan *p, int nodes, int node, int me, lon
     slot0[pc] = total + phase;
     total += (long)(R - 1) * stride[pc];
   }
-  /* two nodes: one slot per piece for the other node's partial of the half this rank keeps,
-     at the 16-byte phase that half has in the receive buffer (send_phase stands for it) */
-  for (pc = 0; pc < p->npieces && nodes > 1; pc++) {
-    long off = p->chunk_off[(size_t)pc * R + me_pos], len = p->chunk_len[(size_t)pc * R + me_pos];
-    long hoff = node ? (len + 1) / 2 : 0, hlen = node ? len / 2 : (len + 1) / 2;
-    total = (total + 15) / 16 * 16;
-    xslot[pc] = total + ((send_phase + (off + hoff) * ts) & 15);
-    total += ((hlen * ts + 15) / 16) * 16 + 16;
+  /* node steps: one slot per piece and step for the partner node's partial of the half this rank
+     keeps, at the 16-byte phase that half has in the receive buffer (send_phase stands for it) */
+  for (pc = 0; pc < p->npieces; pc++) {
+    long lo = p->chunk_off[(size_t)pc * R + me_pos], n = p->chunk_len[(size_t)pc * R + me_pos];
+    for (st = 0; st < k; st++) {
+      const int bit = (node >> st) & 1;
+      const long h0 = (n + 1) / 2;
+      if (bit) lo += h0;
+      n = bit ? n - h0 : h0;
+      total = (total + 15) / 16 * 16;
+      xslot[(size_t)pc * k + st] = total + ((send_phase + lo * ts) & 15);
+      total += ((n * ts + 15) / 16) * 16 + 16;
+    }
   }
 #define SLOT(pc, q) (slot0[pc] + (long)(((q) - me - 1 + R) % R) * stride[pc])
   for (leg = 0; leg < 2; leg++) {
@@ -456,32 +469,46 @@ int emac_comm_program_nodes(const emac_plan *p, int nodes, int node, int me, lon
     nf++;
   }
 #undef SLOT
-  for (pc = 0; pc < p->npieces && nodes > 1; pc++) {
-    long off = p->chunk_off[(size_t)pc * R + me_pos], len = p->chunk_len[(size_t)pc * R + me_pos];
-    /* half 0 = the first ceil(len / 2) elements, finished on node 0; half 1 on node 1 */
-    long hoff[2], hlen[2];
-    int keep = node, give = 1 - node;
-    hoff[0] = off;
-    hlen[0] = (len + 1) / 2;
-    hoff[1] = off + hlen[0];
-    hlen[1] = len - hlen[0];
-    if (hlen[give] > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS, partner, 1, EMAC_BUF_RECV, hoff[give] * ts, hlen[give] * ts};
-    if (hlen[keep] > 0) {
-      emac_fold *f = &folds[nf++];
-      ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS, partner, 0, EMAC_BUF_STAGE, xslot[pc], hlen[keep] * ts};
-      f->piece = pc;
-      f->offset = hoff[keep] * ts;
-      f->count = hlen[keep];
-      f->nleaf = 2;
-      f->leg = EMAC_LEG_NODES_FOLD;
-      f->buf[0] = EMAC_BUF_RECV; /* this node's partial first */
-      f->loff[0] = hoff[keep] * ts;
-      f->buf[1] = EMAC_BUF_STAGE;
-      f->loff[1] = xslot[pc];
-      ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG, partner, 1, EMAC_BUF_RECV, hoff[keep] * ts, hlen[keep] * ts};
+  /* 2^k nodes, one port (allreduce_recursive.c:222-453): step st pairs this node with node ^ 2^st
+     (the reference's radix-2 steps in its permuted node order, ext_mpi_native.c:879-912, pair
+     tasks by their highest bit first, i.e. nodes by their lowest); the owned range halves at
+     every step -- the node with bit st clear keeps the lower half -- and the ranges come back in
+     the reverse order. Each step's fold is one two-operand reduction: own partial, partner's. */
+  for (st = 0; st < k; st++)
+    for (pc = 0; pc < p->npieces; pc++) {
+      long lo = p->chunk_off[(size_t)pc * R + me_pos], n = p->chunk_len[(size_t)pc * R + me_pos];
+      long hoff[2], hlen[2];
+      const int partner = (node ^ (1 << st)) * R + me, bit = (node >> st) & 1, lg = st << EMAC_LEG_STEP_SHIFT;
+      int s2;
+      for (s2 = 0; s2 < st; s2++) { /* this step's range */
+        const long h0 = (n + 1) / 2;
+        if ((node >> s2) & 1) lo += h0;
+        n = ((node >> s2) & 1) ? n - h0 : h0;
+      }
+      hoff[0] = lo;
+      hlen[0] = (n + 1) / 2;
+      hoff[1] = lo + hlen[0];
+      hlen[1] = n - hlen[0];
+      if (hlen[1 - bit] > 0)
+        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, partner, 1, EMAC_BUF_RECV, hoff[1 - bit] * ts, hlen[1 - bit] * ts};
+      if (hlen[bit] > 0) {
+        emac_fold *f = &folds[nf++];
+        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, partner, 0, EMAC_BUF_STAGE, xslot[(size_t)pc * k + st],
+                                 hlen[bit] * ts};
+        f->piece = pc;
+        f->offset = hoff[bit] * ts;
+        f->count = hlen[bit];
+        f->nleaf = 2;
+        f->leg = EMAC_LEG_NODES_FOLD | lg;
+        f->buf[0] = EMAC_BUF_RECV; /* this node's partial first */
+        f->loff[0] = hoff[bit] * ts;
+        f->buf[1] = EMAC_BUF_STAGE;
+        f->loff[1] = xslot[(size_t)pc * k + st];
+        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | lg, partner, 1, EMAC_BUF_RECV, hoff[bit] * ts, hlen[bit] * ts};
+      }
+      if (hlen[1 - bit] > 0)
+        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | lg, partner, 0, EMAC_BUF_RECV, hoff[1 - bit] * ts, hlen[1 - bit] * ts};
     }
-    if (hlen[give] > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG, partner, 0, EMAC_BUF_RECV, hoff[give] * ts, hlen[give] * ts};
-  }
   free(slot0);
   free(stride);
   free(xslot);

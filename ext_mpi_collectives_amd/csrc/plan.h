@@ -117,7 +117,8 @@ enum {
   EMAC_LEG_NODES_FOLD = 64,
   EMAC_LEG_NODES_AG = 128
 };
-#define EMAC_MAX_NODES 2
+#define EMAC_MAX_NODES 16    /* a power of two: one radix-2 step per factor */
+#define EMAC_LEG_STEP_SHIFT 8 /* node-pair legs and folds carry their step: leg | step << 8 */
 
 typedef struct {
   int leg;     /* EMAC_LEG_RS or EMAC_LEG_AG */
@@ -143,14 +144,15 @@ typedef struct {
    so they share the 16-byte phase of the send buffer. Caller frees *ops and *folds. */
 int emac_comm_program(const emac_plan *p, int me, long send_phase, emac_p2p **ops, int *nops, emac_fold **folds,
                       int *nfolds, long *staging_bytes);
-/* The same for rank `me` of node `node` out of `nodes` (1 or 2) nodes of p->nranks ranks each
-   (global rank = node * p->nranks + me, the peers in *ops are global ranks). Two nodes, one port
-   (EXT_MPI_NUM_PORTS "-1 1", src/core/allreduce_recursive.c:222-453 as ext_mpi_native.c:879-960
-   composes it): after the node's reduce-scatter and fold each owner chunk holds the node's
-   partial; the owners of the same chunk on the two nodes (same rank in their node) swap halves
-   (NODES_RS), fold the half they keep -- own partial, then the other node's: one two-operand
-   reduction -- (NODES_FOLD), swap the finished halves back (NODES_AG); the node's allgather
-   then distributes the finished chunk. */
+/* The same for rank `me` of node `node` out of `nodes` (a power of two, 1..16) nodes of p->nranks
+   ranks each (global rank = node * p->nranks + me, the peers in *ops are global ranks). One port
+   per step (EXT_MPI_NUM_PORTS "-1 ... 1 ...", src/core/allreduce_recursive.c:222-453 as
+   ext_mpi_native.c:879-960 composes it): after the node's reduce-scatter and fold each owner
+   chunk holds the node's partial; at step st the owners of the same chunk on nodes n and
+   n ^ 2^st (same rank in their node) swap halves of their current range (NODES_RS | st << 8),
+   fold the half they keep -- own partial, then the partner's: one two-operand reduction --
+   (NODES_FOLD | st << 8), and after the last step the finished ranges are swapped back in the
+   reverse step order (NODES_AG | st << 8); the node's allgather then distributes the chunk. */
 int emac_comm_program_nodes(const emac_plan *p, int nodes, int node, int me, long send_phase, emac_p2p **ops,
                             int *nops, emac_fold **folds, int *nfolds, long *staging_bytes);
 

@@ -120,11 +120,14 @@ int ext_mpi_amd_set_stream(int handle, void *hip_stream);
 #define EXT_MPI_AMD_LEG_ALLGATHER 8      /* COMM form: owned chunk to every peer (reduce_copyout) */
 #define EXT_MPI_AMD_LEG_STAGE_OUT 16     /* D2H of host receive buffers */
 #define EXT_MPI_AMD_LEG_STAGE 17         /* both staging copies */
-/* COMM form over two nodes (ext_mpi_amd_comm_set_nodes), between the fold and the allgather: */
-#define EXT_MPI_AMD_LEG_NODES_RS 32      /* owned chunk's halves swapped with the other node's owner */
-#define EXT_MPI_AMD_LEG_NODES_FOLD 64    /* kept half: this node's partial + the other node's */
-#define EXT_MPI_AMD_LEG_NODES_AG 128     /* finished halves swapped back */
+/* COMM form over 2^k nodes (ext_mpi_amd_comm_set_nodes), between the fold and the allgather: */
+#define EXT_MPI_AMD_LEG_NODES_RS 32      /* per step: owned range's halves swapped with the partner node's owner */
+#define EXT_MPI_AMD_LEG_NODES_FOLD 64    /* per step: kept half = this node's partial + the partner's */
+#define EXT_MPI_AMD_LEG_NODES_AG 128     /* finished ranges swapped back, last step first */
 #define EXT_MPI_AMD_LEG_ALL 255
+/* legs | EXT_MPI_AMD_LEG_STEP(s): the node legs of step s alone (a testing transport driving the
+   steps in lock-step); without it every step runs, in order */
+#define EXT_MPI_AMD_LEG_STEP(s) (((s) + 1) << 8)
 int ext_mpi_amd_start_legs(int handle, int legs);
 
 /* ---- introspection (no GPU needed) ----
@@ -151,25 +154,27 @@ typedef struct {
   long count;  /* elements */
   int buf[EXT_MPI_AMD_MAX_RANKS];
   long leaf_offset[EXT_MPI_AMD_MAX_RANKS];
-  int nleaf; /* leaves used: nranks (the node's fold) or 2 (the two nodes' partials) */
-  int leg;   /* EXT_MPI_AMD_LEG_FOLD or EXT_MPI_AMD_LEG_NODES_FOLD */
+  int nleaf; /* leaves used: nranks (the node's fold) or 2 (two nodes' partials) */
+  int leg;   /* EXT_MPI_AMD_LEG_FOLD, or EXT_MPI_AMD_LEG_NODES_FOLD | step << 8 */
 } ext_mpi_amd_fold;
 int ext_mpi_amd_comm_program(int nranks, int rank, long count, int dtype, const char *copyin, long send_phase,
                              ext_mpi_amd_p2p *ops, int max_ops, int *nops, ext_mpi_amd_fold *folds, int max_folds,
                              int *nfolds, long *staging_bytes);
-/* The same for `nodes` (1 or 2) nodes of ranks_per_node ranks; `rank` is global (node-major). */
+/* The same for `nodes` (a power of two, 1..16) nodes of ranks_per_node ranks; `rank` is global
+   (node-major); node legs and folds carry their step in leg >> 8. */
 int ext_mpi_amd_comm_program_nodes(int nodes, int ranks_per_node, int rank, long count, int dtype, const char *copyin,
                                    long send_phase, ext_mpi_amd_p2p *ops, int max_ops, int *nops,
                                    ext_mpi_amd_fold *folds, int max_folds, int *nfolds, long *staging_bytes);
 
-/* ---- two nodes (§8f row 3, the inter-node ports schedule for two nodes, one port) ----
+/* ---- several nodes (§8f row 3, the inter-node ports schedule, one port per step) ----
  * The reference runs an Allreduce over several nodes as: the node's copy-in (the same
  * reduce_copies_* emission as one node, into shared memory), the inter-node algorithm of
  * src/core/allreduce_recursive.c:222-453 over the node partials (EXT_MPI_NUM_PORTS, here one
- * port: "-1 1"), the node's copy-out (src/mpi/ext_mpi_native.c:879-1000). On an RCCL (or loopback)
- * communicator whose ranks [0, size/2) and [size/2, size) are two nodes of equal size, set before
- * ext_mpi_amd_allreduce_init; copyin then describes ONE node (its ranks_per_node positions).
- * Peer-mapped communicators are single-node (EXT_MPI_AMD_ERROR_UNSUPPORTED). */
+ * port per step: "-1 ... 1 ..."), the node's copy-out (src/mpi/ext_mpi_native.c:879-1000). On an
+ * RCCL (or loopback) communicator whose ranks [n * size/nodes, (n + 1) * size/nodes) form node n,
+ * nodes a power of two up to 16, set before ext_mpi_amd_allreduce_init; copyin then describes
+ * ONE node (its ranks_per_node positions). Peer-mapped communicators are single-node
+ * (EXT_MPI_AMD_ERROR_UNSUPPORTED). */
 int ext_mpi_amd_comm_set_nodes(int comm, int nodes);
 
 /* EXT_MPI_NUM_SOCKETS_PER_NODE (src/mpi/ext_mpi.c:43-187, a process-wide parameter): sockets per

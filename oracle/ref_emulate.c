@@ -93,7 +93,7 @@ done:
   return rc;
 }
 
-/* Two nodes, one port (EXT_MPI_NUM_PORTS "-1 1"). ext_mpi_native.c:879-1000 composes: the node's
+/* Several nodes, one port per step (EXT_MPI_NUM_PORTS "-1 1", "-1 -1 1 1", ...). ext_mpi_native.c:879-1000 composes: the node's
    copy-in -- reduce_copies_one_socket with in_out = 1 and one_node = 0 (reduce_copyin.c:1497-1500):
    the same reduce-scatter emission as one node, into shared memory -- then the inter-node
    algorithm of allreduce_recursive.c:222-453 over the node partials: with one port a single
@@ -105,16 +105,21 @@ done:
    parity for those inputs is unpinned). Ranks [0, R) are node 0, [R, 2R) node 1. */
 int ref_emulate_nodes(int nodes, int R, long count, int dtype, int red, const char *copyin, int in_place,
                       int num_sockets, void *const *sendbufs, void *const *recvbufs) {
-  int n, r, rc;
+  int n, r, b, rc;
   const size_t bytes = (size_t)count * (size_t)ref_type_size(dtype);
-  if (nodes < 1 || nodes > 2 || R < 1 || ref_type_size(dtype) <= 0) return -1;
+  if (nodes < 1 || nodes > 16 || (nodes & (nodes - 1)) || R < 1 || ref_type_size(dtype) <= 0) return -1;
   for (n = 0; n < nodes; n++)
     if ((rc = ref_emulate_op_s(R, count, dtype, red, copyin, in_place, num_sockets, sendbufs + n * R, recvbufs + n * R)))
       return rc;
-  if (nodes == 2) {
-    ref_reduction_op(red, dtype, recvbufs[0], recvbufs[R], count); /* node 0's partial, then node 1's */
-    for (r = 1; r < 2 * R; r++) memcpy(recvbufs[r], recvbufs[0], bytes);
-  }
+  /* 2^k nodes: k radix-2 steps. allreduce_core pairs task t with t ^ 2^(k-1-s) at step s
+     (:261-284, highest bit first), and ext_mpi_native.c:879-912 runs it on tasks permuted by
+     ext_mpi_rank_order over the factors (2, ..., 2) -- a bit reversal, task t = node bitrev(t)
+     (rank_permutation.c:133-139, :176-200) -- so in node order step s pairs n with n ^ 2^s: the
+     partials combine as a balanced pairwise tree, lowest node bit first, each combination one
+     two-operand reduction (node n's partial first here; commutative for SUM) */
+  for (b = 1; b < nodes; b <<= 1)
+    for (n = 0; n < nodes; n += 2 * b) ref_reduction_op(red, dtype, recvbufs[n * R], recvbufs[(n + b) * R], count);
+  for (r = 1; r < nodes * R; r++) memcpy(recvbufs[r], recvbufs[0], bytes);
   return 0;
 }
 

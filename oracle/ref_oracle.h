@@ -104,9 +104,9 @@ int ref_emulate_op(int R, long count, int dtype, int op, const char *copyin, int
 int ref_emulate_op_s(int R, long count, int dtype, int op, const char *copyin, int in_place, int num_sockets,
                      void *const *sendbufs, void *const *recvbufs);
 
-/* Two nodes of R ranks, one port (src/mpi/ext_mpi_native.c:879-1000 with
-   src/core/allreduce_recursive.c:222-453): each node's copy-in, the two node partials reduced
-   once per element, the copy-out. 2R buffers, node-major. nodes = 1 is ref_emulate_op_s. */
+/* nodes (a power of two, <= 16) nodes of R ranks, one port per step (src/mpi/ext_mpi_native.c:879-1000
+   with src/core/allreduce_recursive.c:222-453 and rank_permutation.c): each node's copy-in, the node
+   partials combined pairwise (lowest node bit first), the copy-out. nodes * R buffers, node-major. */
 int ref_emulate_nodes(int nodes, int R, long count, int dtype, int red, const char *copyin, int in_place,
                       int num_sockets, void *const *sendbufs, void *const *recvbufs);
 

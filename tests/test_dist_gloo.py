@@ -90,36 +90,41 @@ def test_comm_program_over_gloo(world, cases):
     assert [f for r in results for f in r] == []
 
 
-def _nodes_worker(rank, world, port, cases, q):
-    """two nodes of world // 2 ranks: the node legs, the node-pair legs and both folds"""
+def _nodes_worker(rank, world, port, cases, q, nodes=2):
+    """`nodes` nodes of world // nodes ranks: the node legs, per step the node-pair legs and
+    their fold, the exchanges back in reverse step order"""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import oracle
     failures = []
-    R = world // 2
+    R = world // nodes
+    k = (nodes - 1).bit_length()
+    SH = emac.LEG_STEP_SHIFT
     for code, count, copyin in cases:
         sends = xorshift_inputs(world, count, code, seed_base=0x2A0DE000 + count)
         dt = NP[code]
         itemsize = np.dtype(dt).itemsize
-        ops, folds, stage = emac.comm_program_nodes(2, R, rank, count, code, copyin)
+        ops, folds, stage = emac.comm_program_nodes(nodes, R, rank, count, code, copyin)
         bufs = {emac.BUF_SEND: sends[rank].view(np.uint8).copy(),
                 emac.BUF_RECV: np.full(count * itemsize, 0xAB, dtype=np.uint8),
                 emac.BUF_STAGE: np.zeros(max(stage, 1), dtype=np.uint8)}
         desc = emac.plan_describe(R, count, code, copyin, 0)
         _run_leg(ops, LEG_RS, bufs)
         _fold([f[:3] for f in folds if f[3] == emac.LEG_FOLD], bufs, code, desc)
-        _run_leg(ops, emac.LEG_NODES_RS, bufs)
-        for off, n, leaves, leg in folds:
-            if leg != emac.LEG_NODES_FOLD:
-                continue
-            (b0, o0), (b1, o1) = leaves
-            x0 = bufs[b0][o0:o0 + n * itemsize].view(dt)
-            x1 = bufs[b1][o1:o1 + n * itemsize].view(dt)
-            with np.errstate(over="ignore"):
-                bufs[emac.BUF_RECV][off:off + n * itemsize].view(dt)[:] = x0 + x1
-        _run_leg(ops, emac.LEG_NODES_AG, bufs)
+        for st in range(k):
+            _run_leg(ops, emac.LEG_NODES_RS | st << SH, bufs)
+            for off, n, leaves, leg in folds:
+                if leg != emac.LEG_NODES_FOLD | st << SH:
+                    continue
+                (b0, o0), (b1, o1) = leaves
+                x0 = bufs[b0][o0:o0 + n * itemsize].view(dt)
+                x1 = bufs[b1][o1:o1 + n * itemsize].view(dt)
+                with np.errstate(over="ignore"):
+                    bufs[emac.BUF_RECV][off:off + n * itemsize].view(dt)[:] = x0 + x1
+        for st in reversed(range(k)):
+            _run_leg(ops, emac.LEG_NODES_AG | st << SH, bufs)
         _run_leg(ops, LEG_AG, bufs)
-        want = oracle.allreduce_nodes(sends, copyin, 2)[rank]
+        want = oracle.allreduce_nodes(sends, copyin, nodes)[rank]
         if not np.array_equal(bufs[emac.BUF_RECV], want.view(np.uint8)):
             failures.append((rank, code, count, copyin))
     q.put(failures)
@@ -140,6 +145,26 @@ def test_two_node_program_over_gloo(world, cases):
     q = ctx.Queue()
     port = 29800 + world * 7 + os.getpid() % 200
     procs = [ctx.Process(target=_nodes_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert [f for r in results for f in r] == []
+
+
+@pytest.mark.parametrize("world,nodes,cases", [
+    (4, 4, [(emac.FLOAT, 100003, "6;1 -1 1"), (emac.DOUBLE, 7, "6;1 -1 1")]),
+    (8, 4, [(emac.FLOAT, 65539, "6;1 -2 2"), (emac.INT, 4099, "6;3 -2 2"), (emac.DOUBLE, 1001, "7;1 -2 2")]),
+    (8, 8, [(emac.FLOAT, 30011, "6;1 -1 1"), (emac.LONG, 999, "6;1 -1 1")]),
+])
+def test_many_node_program_over_gloo(world, nodes, cases):
+    """2^k nodes, one port per step: emac_comm_program_nodes over gloo equals the oracle bitwise."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29900 + world * 7 + nodes + os.getpid() % 200
+    procs = [ctx.Process(target=_nodes_worker, args=(r, world, port, cases, q, nodes)) for r in range(world)]
     for p in procs:
         p.start()
     results = [q.get(timeout=240) for _ in procs]

@@ -367,7 +367,7 @@ def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=Non
     """COMM form (one rank per communicator) on the in-process loopback transport: the legs run
     on every rank in lock-step -- stage-in, reduce-scatter, fold, [the two-node legs,] all-gather,
     stage-out -- so the staging slots, fold buckets and leg programs of the multi-GPU path execute
-    on one GPU. nodes=2: ranks [0, R/2) and [R/2, R) are two nodes (ext_mpi_amd_comm_set_nodes)."""
+    on one GPU. nodes=2^k: consecutive blocks of R/nodes ranks are nodes (ext_mpi_amd_comm_set_nodes)."""
     R, count = len(sends), sends[0].size
     comms = emac.comm_init_loopback(R)
     if nodes > 1:
@@ -397,7 +397,7 @@ def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=Non
                 for t in rbufs:
                     t.fill_(-1)
             torch.cuda.synchronize()
-            for leg in emac.LEG_ORDER:
+            for leg in emac.lockstep_legs(nodes):
                 for h in hs:
                     emac.start_legs(h, leg)
                 for h in hs:
@@ -437,6 +437,20 @@ def test_comm_two_nodes_loopback_vs_oracle(oracle, R, copyin, code):
         want = oracle.allreduce_nodes(sends, copyin, 2)
         got = run_comm_loopback(sends, code, copyin, phase=[(r * 3) % 4 for r in range(R)], nodes=2)
         assert_bitwise(got, want, f"two nodes R={R} {copyin} code={code} n={count}")
+
+
+@pytest.mark.parametrize("R,nodes,copyin", [(4, 4, "6;1 -1 1"), (8, 4, "6;1 -2 2"), (16, 4, "6;1 -2 -2 2 2"),
+                                             (8, 8, "6;1 -1 1"), (16, 8, "7;1 -2 2"), (16, 16, "6;1 -1 1"),
+                                             (12, 4, "5;1 -3 3")])
+@pytest.mark.parametrize("code", [emac.FLOAT, emac.DOUBLE, emac.INT])
+def test_comm_many_nodes_loopback_vs_oracle(oracle, R, nodes, copyin, code):
+    """2^k nodes, one port per step: the node-pair swaps and folds step by step (pairs by the
+    lowest node bit first), the ranges back in reverse order -- bitwise vs the oracle."""
+    for count in (0, 5, 1031, 65536 + 7):
+        sends = xorshift_inputs(R, count, code, seed_base=0x4D0E0000 + count)
+        want = oracle.allreduce_nodes(sends, copyin, nodes)
+        got = run_comm_loopback(sends, code, copyin, phase=[(r * 3) % 4 for r in range(R)], nodes=nodes)
+        assert_bitwise(got, want, f"{nodes} nodes R={R} {copyin} code={code} n={count}")
 
 
 def test_comm_two_nodes_loopback_in_place_host_repeats(oracle):

@@ -298,3 +298,17 @@ def test_two_nodes_fold_is_one_reduction_of_the_node_partials(oracle, dt):
     p1 = oracle.allreduce(sends[R:], "6;1 -4 4")[0]
     for out in oracle.allreduce_nodes(sends, "6;1 -4 4", 2):
         assert np.array_equal(out, (p0 + p1).astype(dt)) and np.array_equal(out, (p1 + p0).astype(dt))
+
+
+def test_many_nodes_pairwise_tree(oracle):
+    # 4 nodes, one port per step: ((P0 + P1) + (P2 + P3)) -- the reference's radix-2 steps in its
+    # bit-reversed node order (allreduce_recursive.c:261-284, reduce_copyin.c:375-394)
+    rng = np.random.default_rng(9)
+    sends = [((rng.random(517) * 2 - 1) * 10.0 ** rng.integers(-4, 5, 517)).astype(np.float32) for _ in range(8)]
+    p = [oracle.allreduce(sends[2 * n:2 * n + 2], "6;1 -2 2")[0] for n in range(4)]
+    want = ((p[0] + p[1]).astype(np.float32) + (p[2] + p[3]).astype(np.float32)).astype(np.float32)
+    other = ((p[0] + p[2]).astype(np.float32) + (p[1] + p[3]).astype(np.float32)).astype(np.float32)
+    assert not np.array_equal(want, other)  # the pairing is observable
+    for out in oracle.allreduce_nodes(sends, "6;1 -2 2", 4):
+        assert np.array_equal(out, want)
+    assert oracle.rank_order(4, [2, 2]) == [0, 2, 1, 3]  # the node permutation behind the pairing
