@@ -15,8 +15,8 @@
  * broadcasts): EXT_MPI_COPYIN, EXT_MPI_VERBOSE, EXT_MPI_DEBUG (default 1: the known-answer
  * self-test of debug_persistent.c:393-568 runs inside every Allreduce_init),
  * EXT_MPI_NUM_TASKS_PER_SOCKET (ranks per socket: with the sockets, the node size -- a physical
- * node may hold several logical ones), EXT_MPI_NUM_PORTS (several nodes: one port per step, every
- * entry +-1, log2(nodes) reduce-scatter steps),
+ * node may hold several logical ones), EXT_MPI_NUM_PORTS (the reference's "nodes(ports)" grammar,
+ * ports_groups.c:55-110; several nodes: one port per step, log2(nodes) steps of -1 then of +1),
  * EXT_MPI_NUM_SOCKETS_PER_NODE (any divisor of the node size: sockets change the reference's
  * partner encoding and barrier scope, and the tree method's last-step roots -- the one place
  * they reach the fold arithmetic, ext_mpi_amd_set_num_sockets). MPI_Info
@@ -29,7 +29,9 @@
  * through a per-communicator cache of handles keyed on (buffers, count, type, parameter row).
  * The copy-in factors come from the reference's parameter file
  * ext_mpi_allreduce_blocking_<nodes>_<cores>.txt (/dev/shm first, then the working directory):
- * one row per message-size threshold, host rows then device rows (README "blocking").
+ * one row per message-size threshold, host rows then device rows (README "blocking"); a row whose
+ * ports column names another inter-node schedule than the one-port one over the communicator's
+ * nodes goes to PMPI_Allreduce.
  *
  * Transport (EXT_MPI_AMD_TRANSPORT): "ipc" (default) maps every rank's device buffers into every
  * other rank with hipIpc, as the reference maps them with cudaIpc (src/gpu/cuda_shmem.c:218-299),
@@ -60,6 +62,7 @@ static int cfg_num_sockets = -1;
 static int cfg_tasks_per_socket = -1; /* EXT_MPI_NUM_TASKS_PER_SOCKET: ranks of a (logical) socket */
 static int cfg_ports_ok = 1;          /* EXT_MPI_NUM_PORTS names the one-port schedule (or is unset) */
 static int cfg_ports_steps = -1;      /* ... with this many reduce-scatter steps (-1: unset) */
+static int cfg_ports_nodes = 0;       /* ... over a group of this many nodes (0: no group given) */
 static int cfg_blocking = 0;
 static int cfg_rccl = 0; /* EXT_MPI_AMD_TRANSPORT=rccl: legs over RCCL instead of hipIpc mappings */
 static int initialised = 0;
@@ -76,6 +79,61 @@ static int env_int(const char *name, int *out) {
   return 0;
 }
 
+/* EXT_MPI_NUM_PORTS and the ports column of a blocking parameter row, in the grammar of
+   ext_mpi_scan_ports_groups (ports_groups.c:55-110; README: "4(-1 -1 1 1)", "1(-1)"):
+   "G(p0 p1 ...)" with G the nodes of the group and p the ports of each inter-node step
+   (negative: reduce-scatter, positive: allgather; radix |p| + 1). ' ', ',' and '_' separate.
+   The inter-node schedule here is the one-port one over one group: "1(...)" (one node, no
+   inter-node step) or "2^k(-1 ... -1 1 ... 1)" with k entries of each sign. A bare port list
+   (which the reference's scanner runs past the end of) is read as the ports of one group of
+   unstated size. Returns the group's nodes (0: not stated) and *steps (the reduce-scatter
+   steps, -1 for an empty string), or -1 when the string names anything else: several ports per
+   step, several groups, unequal step counts, a group size other than 2^steps. */
+static int parse_ports(const char *s, int *steps) {
+  int groups = 0, bare = 0, nodes = 0, neg = 0, pos = 0, tokens = 0, in_group = 0, ok = 1;
+  const char *p = s;
+  *steps = -1;
+  while (p && *p) {
+    char *end;
+    long v;
+    if (*p == ' ' || *p == ',' || *p == '_') {
+      p++;
+      continue;
+    }
+    if (*p == ')') {
+      if (!in_group) ok = 0;
+      in_group = 0;
+      p++;
+      continue;
+    }
+    v = strtol(p, &end, 10);
+    if (end == p) return -1;
+    p = end;
+    tokens++;
+    while (*p == ' ' || *p == '_') p++;
+    if (*p == '(') { /* the group's node count */
+      if (in_group || ++groups > 1 || v < 1) ok = 0;
+      nodes = (int)v;
+      in_group = 1;
+      p++;
+      continue;
+    }
+    if (!in_group) bare = 1;
+    if (v == -1 && !pos)
+      neg++;
+    else if (v == 1)
+      pos++;
+    else
+      ok = 0; /* several ports per step, or a reduce-scatter step after an allgather step */
+  }
+  if (!tokens) return 0;
+  if (!ok || in_group || (bare && groups)) return -1;
+  *steps = neg;
+  if (nodes == 1) return 1; /* one node: its ports name no inter-node step */
+  if (neg != pos || (nodes > 1 && nodes != 1 << neg)) return -1;
+  return nodes;
+}
+
 static void read_env(void) {
   int rank, len = 0;
   PMPI_Comm_rank(MPI_COMM_WORLD, &rank);
@@ -86,28 +144,8 @@ static void read_env(void) {
     env_int("EXT_MPI_DEBUG", &cfg_debug);
     env_int("EXT_MPI_NUM_SOCKETS_PER_NODE", &cfg_num_sockets);
     env_int("EXT_MPI_NUM_TASKS_PER_SOCKET", &cfg_tasks_per_socket);
-    {
-      /* EXT_MPI_NUM_PORTS "p0 p1 ..." (ports_groups.c:37-74, "(groups)" parts ignored): the
-         inter-node schedule here is the one-port one, radix 2 per step -- every entry +-1 */
-      const char *pp = getenv("EXT_MPI_NUM_PORTS");
-      while (pp && *pp) {
-        char *end;
-        long v;
-        if (*pp == '(') {
-          while (*pp && *pp != ')') pp++;
-          if (*pp) pp++;
-          continue;
-        }
-        v = strtol(pp, &end, 10);
-        if (end == pp) {
-          pp++;
-          continue;
-        }
-        if (v != 1 && v != -1) cfg_ports_ok = 0;
-        if (v == -1) cfg_ports_steps = cfg_ports_steps < 0 ? 1 : cfg_ports_steps + 1;
-        pp = end;
-      }
-    }
+    cfg_ports_nodes = parse_ports(getenv("EXT_MPI_NUM_PORTS"), &cfg_ports_steps); /* ext_mpi.c:124-157 */
+    cfg_ports_ok = cfg_ports_nodes >= 0;
     cfg_rccl = getenv("EXT_MPI_AMD_TRANSPORT") && !strcmp(getenv("EXT_MPI_AMD_TRANSPORT"), "rccl");
     if (c) {
       strncpy(cfg_copyin, c, sizeof(cfg_copyin) - 1);
@@ -121,6 +159,7 @@ static void read_env(void) {
   PMPI_Bcast(&cfg_tasks_per_socket, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_ports_ok, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_ports_steps, 1, MPI_INT, 0, MPI_COMM_WORLD);
+  PMPI_Bcast(&cfg_ports_nodes, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_rccl, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&len, 1, MPI_INT, 0, MPI_COMM_WORLD);
   if (len > 0) PMPI_Bcast(cfg_copyin, len, MPI_CHAR, 0, MPI_COMM_WORLD);
@@ -222,10 +261,40 @@ static int comm_attr_delete(MPI_Comm comm, int keyval, void *attr, void *extra) 
   return MPI_SUCCESS;
 }
 
-static int node_comm(MPI_Comm comm, const void *devbuf, int *ext_comm) {
-  comm_attr *a;
-  int flag, size, rank, nsize, nrank, device, ndev, rc, nodes;
+/* The communicator's node layout (collective): *nodes = 1 (one node) or 2^k (<= 16) nodes of
+   equal size in node-major rank order (the reference's row layout, ext_mpi_native.c:879-960),
+   0 for any other shape; *nsize = ranks per node, *nrank = rank in the node. The reference's node
+   is EXT_MPI_NUM_TASKS_PER_SOCKET x sockets consecutive ranks when that is set (ext_mpi.c:195-215,
+   :638): a physical node may hold several logical ones. */
+static void comm_topology(MPI_Comm comm, int *nodes, int *nsize, int *nrank) {
+  int size, rank, v[2], k = 0;
   MPI_Comm node;
+  PMPI_Comm_size(comm, &size);
+  PMPI_Comm_rank(comm, &rank);
+  PMPI_Comm_split_type(comm, MPI_COMM_TYPE_SHARED, rank, MPI_INFO_NULL, &node);
+  PMPI_Comm_size(node, nsize);
+  PMPI_Comm_rank(node, nrank);
+  PMPI_Comm_free(&node);
+  if (cfg_tasks_per_socket > 0) {
+    const int lsize = cfg_tasks_per_socket * (cfg_num_sockets > 0 ? cfg_num_sockets : 1);
+    if (lsize <= *nsize && *nsize % lsize == 0) {
+      *nsize = lsize;
+      *nrank = rank % lsize;
+    }
+  }
+  *nodes = *nsize > 0 && size % *nsize == 0 ? size / *nsize : 0;
+  while ((1 << k) < *nodes) k++;
+  v[0] = *nsize == size;
+  v[1] = *nodes >= 2 && *nodes <= 16 && (1 << k) == *nodes && *nrank == rank % *nsize;
+  PMPI_Allreduce(MPI_IN_PLACE, v, 2, MPI_INT, MPI_MIN, comm);
+  *nodes = v[0] ? 1 : v[1] ? *nodes : 0;
+}
+
+/* `env_ports`: EXT_MPI_NUM_PORTS governs the inter-node schedule (not when a blocking parameter
+   row, already checked by the caller, names it) */
+static int node_comm(MPI_Comm comm, const void *devbuf, int env_ports, int *ext_comm) {
+  comm_attr *a;
+  int flag, size, rank, nsize, nrank, device, ndev, rc, nodes, k = 0;
   unsigned char id[EXT_MPI_AMD_UNIQUE_ID_BYTES];
   if (comm_keyval == MPI_KEYVAL_INVALID) return EXT_MPI_AMD_ERROR_ARG;
   PMPI_Comm_get_attr(comm, comm_keyval, &a, &flag);
@@ -235,34 +304,14 @@ static int node_comm(MPI_Comm comm, const void *devbuf, int *ext_comm) {
   }
   PMPI_Comm_size(comm, &size);
   PMPI_Comm_rank(comm, &rank);
-  PMPI_Comm_split_type(comm, MPI_COMM_TYPE_SHARED, rank, MPI_INFO_NULL, &node);
-  PMPI_Comm_size(node, &nsize);
-  PMPI_Comm_rank(node, &nrank);
-  PMPI_Comm_free(&node);
-  if (cfg_tasks_per_socket > 0) {
-    /* the reference's node = EXT_MPI_NUM_TASKS_PER_SOCKET x sockets consecutive ranks
-       (ext_mpi.c:195-215, :638): a physical node may hold several logical ones */
-    const int lsize = cfg_tasks_per_socket * (cfg_num_sockets > 0 ? cfg_num_sockets : 1);
-    if (lsize <= nsize && nsize % lsize == 0) {
-      nsize = lsize;
-      nrank = rank % lsize;
-    }
-  }
-  {
-    /* one node, or 2^k nodes of equal size in node-major rank order (the reference's row layout,
-       ext_mpi_native.c:879-960): those run the one-port inter-node schedule over RCCL */
-    int v[2], k = 0;
-    nodes = nsize > 0 && size % nsize == 0 ? size / nsize : 0;
-    while ((1 << k) < nodes) k++;
-    v[0] = nsize == size;
-    v[1] = nodes >= 2 && nodes <= 16 && (1 << k) == nodes && nrank == rank % nsize;
-    PMPI_Allreduce(MPI_IN_PLACE, v, 2, MPI_INT, MPI_MIN, comm);
-    if (!v[0] && !v[1]) return EXT_MPI_AMD_ERROR_UNSUPPORTED; /* other inter-node shapes: out of scope */
-    if (v[0]) nodes = 1;
-    /* several ports per step are not built, nor a step count other than log2(nodes) */
-    if (nodes > 1 && (!cfg_ports_ok || (cfg_ports_steps >= 0 && cfg_ports_steps != k)))
-      return EXT_MPI_AMD_ERROR_UNSUPPORTED;
-  }
+  comm_topology(comm, &nodes, &nsize, &nrank);
+  if (!nodes) return EXT_MPI_AMD_ERROR_UNSUPPORTED; /* other inter-node shapes: out of scope */
+  while ((1 << k) < nodes) k++;
+  /* several ports per step are not built, nor a step count other than log2(nodes), nor a group
+     of another size than the communicator's */
+  if (nodes > 1 && env_ports &&
+      (!cfg_ports_ok || (cfg_ports_steps >= 0 && cfg_ports_steps != k) || (cfg_ports_nodes && cfg_ports_nodes != nodes)))
+    return EXT_MPI_AMD_ERROR_UNSUPPORTED;
   ndev = ext_mpi_amd_gpu_device_count();
   device = ext_mpi_amd_gpu_device_of(devbuf);
   if (device < 0) device = ndev > 0 ? nrank % ndev : -1;
@@ -379,7 +428,8 @@ out:
 typedef struct {
   long msize;  /* message size in bytes from which the row applies */
   int sockets; /* logical sockets per node */
-  int nodes;   /* "<nodes>(ports)" field: 1 = single node */
+  int nodes;   /* "<nodes>(<ports>)" field, parse_ports: nodes (0 unstated, -1 not this path) */
+  int steps;   /* ... its reduce-scatter steps */
   char copyin[256];
 } brow;
 
@@ -395,6 +445,7 @@ typedef struct {
 typedef struct {
   int status; /* 0 not yet bound, 1 bound to ext_comm, <0 engine error, 2 not for this path */
   int ext_comm;
+  int nodes, nsize; /* comm_topology (nodes 0: a shape this path does not take); nodes < 0: not yet */
   int loaded, nrow[2]; /* [0] host rows, [1] device rows */
   brow row[2][BROWS];
   bentry cache[BCACHE];
@@ -436,24 +487,24 @@ static void blocking_register(MPI_Comm comm, int any_size) {
   b = (bcomm *)calloc(1, sizeof(bcomm));
   if (!b) return;
   for (i = 0; i < BCACHE; i++) b->cache[i].handle = -1;
+  b->nodes = -1;
   PMPI_Comm_set_attr(comm, blocking_keyval, b);
 }
 
 /* init_blocking_native (ext_mpi_native_blocking.c:189-290): "<bytes> <sockets> <ports>
-   <copyin>" per line, '_' standing for ' '; a non-increasing size starts the device rows. */
+   <copyin>" per line, '_' standing for ' '; a non-increasing size starts the device rows. The
+   file is ext_mpi_allreduce_blocking_<nodes>_<cores per node>.txt (:225-230). */
 static void blocking_load_rows(bcomm *b, MPI_Comm comm) {
   char fname[256], ports[1000], cf[1000];
   long ms, prev = -1;
-  int so, size, rank, side = 0, i;
+  int so, rank, side = 0, i;
   FILE *f;
-  PMPI_Comm_size(comm, &size);
   PMPI_Comm_rank(comm, &rank);
   b->loaded = 1;
-  /* single node: <nodes> = 1, <cores> = every rank of the communicator */
-  snprintf(fname, sizeof(fname), "/dev/shm/ext_mpi_allreduce_blocking_%d_%d.txt", 1, size);
+  snprintf(fname, sizeof(fname), "/dev/shm/ext_mpi_allreduce_blocking_%d_%d.txt", b->nodes, b->nsize);
   f = fopen(fname, "r");
   if (!f) {
-    snprintf(fname, sizeof(fname), "ext_mpi_allreduce_blocking_%d_%d.txt", 1, size);
+    snprintf(fname, sizeof(fname), "ext_mpi_allreduce_blocking_%d_%d.txt", b->nodes, b->nsize);
     f = fopen(fname, "r");
   }
   if (!f) {
@@ -468,7 +519,7 @@ static void blocking_load_rows(bcomm *b, MPI_Comm comm) {
     r = &b->row[side][b->nrow[side]++];
     r->msize = ms;
     r->sockets = so;
-    r->nodes = atoi(ports);
+    r->nodes = parse_ports(ports, &r->steps);
     for (i = 0; cf[i]; i++)
       if (cf[i] == '_') cf[i] = ' ';
     snprintf(r->copyin, sizeof(r->copyin), "%.255s", cf);
@@ -497,25 +548,31 @@ static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int
   bentry *e;
   if (sendbuf == MPI_IN_PLACE) sendbuf = recvbuf; /* ext_mpi_blocking.c:427-429 */
   in_place = sendbuf == recvbuf;
-  if (b->status == 0) {
-    rc = node_comm(comm, recvbuf, &b->ext_comm);
-    b->status = rc == 0 ? 1 : rc == EXT_MPI_AMD_ERROR_UNSUPPORTED ? 2 : rc;
+  if (b->nodes < 0) {
+    int nrank;
+    comm_topology(comm, &b->nodes, &b->nsize, &nrank); /* collective: every rank, first call */
   }
-  if (b->status != 1) return b->status == 2 ? 1 : b->status;
+  if (!b->nodes) return 1; /* an inter-node shape this path does not take */
   if (!b->loaded) blocking_load_rows(b, comm);
   on_dev = ext_mpi_amd_gpu_is_device_pointer(recvbuf) && ext_mpi_amd_gpu_is_device_pointer(sendbuf);
   side = on_dev && b->nrow[1] ? 1 : 0;
   row = blocking_select_row(b, side, (long)bytes);
   if (row >= 0) {
-    int size;
-    PMPI_Comm_size(comm, &size);
-    if (b->row[side][row].nodes != 1) return 1; /* inter-node row: not this path */
-    if (b->row[side][row].sockets < 1 || size % b->row[side][row].sockets) return 1;
-    copyin = b->row[side][row].copyin;
-    row_sockets = b->row[side][row].sockets;
+    const brow *w = &b->row[side][row];
+    /* the row's inter-node schedule must be the one-port one over this communicator's nodes */
+    if (w->nodes < 0 || (w->nodes ? w->nodes != b->nodes : b->nodes > 1 && (w->steps < 0 || 1 << w->steps != b->nodes)))
+      return 1;
+    if (w->sockets < 1 || b->nsize % w->sockets) return 1;
+    copyin = w->copyin;
+    row_sockets = w->sockets;
   } else if (cfg_has_copyin) {
     copyin = cfg_copyin;
   }
+  if (b->status == 0) {
+    rc = node_comm(comm, recvbuf, row < 0, &b->ext_comm);
+    b->status = rc == 0 ? 1 : rc == EXT_MPI_AMD_ERROR_UNSUPPORTED ? 2 : rc;
+  }
+  if (b->status != 1) return b->status == 2 ? 1 : b->status;
   if (on_dev) {
     s = sendbuf;
     r = recvbuf;
@@ -655,7 +712,7 @@ int EXT_MPI_Allreduce_init(const void *sendbuf, void *recvbuf, int count, MPI_Da
     PMPI_Info_get(info, "ext_mpi_copyin", (int)sizeof(info_copyin) - 1, info_copyin, &flag);
     if (flag) copyin = info_copyin;
   }
-  if ((rc = node_comm(comm, recvbuf, &ext_comm))) return rc;
+  if ((rc = node_comm(comm, recvbuf, 1, &ext_comm))) return rc;
   PMPI_Type_size(datatype, &tsize);
   if (cfg_debug && (rc = known_answer_test(recvbuf, sendbuf == recvbuf, count, tsize, comm, ext_comm, copyin)))
     return rc;

@@ -2,8 +2,8 @@
  * (tests/benchmark.c shape): only MPI calls plus the MPI-4 prototype from ext_mpi_interface.h.
  * argv: count dtype(f|d|i|l) mem(dev|host) [inplace] [blocking] [min|max]. "blocking" drives MPI_Allreduce
  * (run with EXT_MPI_BLOCKING set) instead of MPI_Allreduce_init. Prints "RESULT ok" / "RESULT no-device"
- * / "RESULT fail ...". Integer inputs are checked exactly against PMPI_Allreduce; float inputs
- * are integer-valued (exact in any order) so the same comparison applies. */
+ * / "RESULT pmpi" (no GPU; a blocking call handed to PMPI_Allreduce, exact) / "RESULT fail ...".
+ * Integer inputs are checked exactly against PMPI_Allreduce; float inputs are integer-valued (exact in any order) so the same comparison applies. */
 #include <mpi.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -55,7 +55,11 @@ int main(int argc, char **argv) {
   if (ext_mpi_amd_gpu_device_count() <= 0) {
     if (blocking) rc = MPI_Allreduce(hs, hr, count, dt, op, MPI_COMM_WORLD) == MPI_SUCCESS ? 0 : -5;
     else rc = MPI_Allreduce_init(hs, hr, count, dt, op, MPI_COMM_WORLD, MPI_INFO_NULL, &req);
-    if (rank == 0) printf("RESULT %s rc=%d\n", (rc == -5 && !bad) ? "no-device" : "fail", rc);
+    /* a blocking call this path does not take goes to PMPI_Allreduce: "pmpi" when exact */
+    if (blocking && rc == 0 && memcmp(hr, ref, bytes)) bad |= 2;
+    MPI_Allreduce(MPI_IN_PLACE, &bad, 1, MPI_INT, MPI_BOR, MPI_COMM_WORLD);
+    if (rank == 0)
+      printf("RESULT %s rc=%d\n", bad ? "fail" : rc == -5 ? "no-device" : blocking && rc == 0 ? "pmpi" : "fail", rc);
     MPI_Finalize();
     return 0;
   }
