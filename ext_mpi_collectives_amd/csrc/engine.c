@@ -750,7 +750,9 @@ typedef struct {
    every peer's block through its mapping and checks that its own block shows every peer's flip.
    The runtime places small allocations side by side in shared chunks, and a second
    communicator's block mapped by a process that already maps the first one's was measured to
-   miss (8 processes on one MI355X: one rank never saw a peer's flags). A failed round keeps the
+   miss (8 processes on one MI355X: one rank never saw a peer's flags), and the runtime may refuse
+   to export a fresh block (an allocation placed where a freed one a peer still maps lay; measured
+   on a third communicator of 3 processes after 1200 handle lifetimes). A failed round keeps the
    blocks it allocated (peers may map them; freed with the communicator) and retries with a fresh,
    larger allocation. Collective: every rank runs every round whatever failed locally (`rc`). */
 #define EMAC_SYNC_ATTEMPTS 4
@@ -768,8 +770,17 @@ static int ipc_sync_exchange(emac_comm *cm, int rc, ipc_export *all) {
       cm->sync = NULL;
     }
     if (!rc) rc = emac_gpu_malloc_uncached(&cm->sync, sizeof(emac_sync) << attempt);
-    if (!rc) rc = emac_gpu_ipc_export(cm->sync, mine.handle, &mine.offset);
     if (!rc) {
+      const int er = emac_gpu_ipc_export(cm->sync, mine.handle, &mine.offset);
+      if (er == EMAC_ERR_TRANSPORT) {
+        mine.refused = 1; /* no peer maps it: this rank misses every flip and the round repeats */
+        if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
+          fprintf(stderr, "ipc rank %d: export of my synchronisation block refused (attempt %d)\n", cm->rank, attempt);
+      } else {
+        rc = er;
+      }
+    }
+    if (!rc && !mine.refused) {
       void *b0;
       mine.extent = emac_gpu_alloc_extent(cm->sync, &b0);
       mine.buf_id = emac_gpu_buffer_id(b0);
@@ -783,7 +794,7 @@ static int ipc_sync_exchange(emac_comm *cm, int rc, ipc_export *all) {
         cm->peer_sync[r] = cm->sync;
         continue;
       }
-      cm->peer_sync_base[r] = ipc_map_peer(all[r].handle, all[r].buf_id, all[r].extent);
+      cm->peer_sync_base[r] = all[r].refused ? NULL : ipc_map_peer(all[r].handle, all[r].buf_id, all[r].extent);
       if (!cm->peer_sync_base[r]) {
         /* not fatal: the exporter misses this rank's flip below and the round is repeated with
            fresh blocks (measured: an open refused for a second communicator's block, 4 processes) */
