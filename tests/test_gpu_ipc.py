@@ -40,6 +40,26 @@ def _need_gpu():
 WORLDS = [int(w) for w in os.environ.get("IPC_TEST_WORLDS", "2,3,4,8").split(",")]
 
 
+def _digest(outs, codes, keep=40):
+    """Per rank: its exit code, every line that is not a passing case (set-up retries, errors,
+    tracebacks) -- repeated lines counted once -- and its last lines; bounded, so a failing run's
+    report stays readable."""
+    parts = []
+    for r, (out, code) in enumerate(zip(outs, codes)):
+        lines = out.splitlines()
+        seen, odd = {}, []
+        for l in lines:
+            if l.endswith(": ok"):
+                continue
+            if l not in seen:
+                odd.append(l)
+            seen[l] = seen.get(l, 0) + 1
+        odd = [f"{l}  (x{seen[l]})" if seen[l] > 1 else l for l in odd[:keep]]
+        parts.append(f"--- rank {r}: exit {code}, {len(lines)} lines\n" + "\n".join(odd) +
+                     "\n... last lines:\n" + "\n".join(lines[-8:]))
+    return "\n".join(parts)
+
+
 @pytest.mark.parametrize("world", WORLDS)
 def test_ipc_ranks_share_one_gpu(world):
     port = _port()
@@ -49,6 +69,7 @@ def test_ipc_ranks_share_one_gpu(world):
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), IPC_DEVICE="0", EXT_MPI_AMD_BARRIER_TIMEOUT="20")
+        env.setdefault("EXT_MPI_AMD_DEBUG_IPC", "1")  # set-up retries are reported (silent when none)
         env.setdefault("IPC_FUZZ", "16")  # seeded random cases beside the fixed ones (ipc_worker.fuzz_cases)
         logs.append(tempfile.TemporaryFile(mode="w+"))
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "ipc_worker.py")], env=env,
@@ -69,8 +90,8 @@ def test_ipc_ranks_share_one_gpu(world):
         outs.append(f.read())
         f.close()
     report = "\n".join(outs)
-    print(report)
-    assert codes == [0] * world, report
+    print(_digest(outs, codes))
+    assert codes == [0] * world, _digest(outs, codes)
     lines = [l for l in report.splitlines() if l.startswith("IPC rank")]
-    assert lines and all(l.endswith(": ok") for l in lines), report
-    assert len(lines) == world * sum(1 for l in lines if l.startswith("IPC rank 0/")), report
+    assert lines and all(l.endswith(": ok") for l in lines), _digest(outs, codes)
+    assert len(lines) == world * sum(1 for l in lines if l.startswith("IPC rank 0/")), _digest(outs, codes)
