@@ -1010,7 +1010,7 @@ static int ipc_exchange(emac_handle *h, emac_comm *cm, int rc, int empty, ipc_ex
         (t ? precv : psend)[r] = (char *)base + e->offset;
         pk[n] = (char *)base + e->offset + cm->rank;
         vals[n++] = e->probe[cm->rank] ^ EMAC_PROBE_FLIP;
-        if (getenv("EXT_MPI_AMD_DEBUG_IPC")) {
+        if (getenv("EXT_MPI_AMD_DEBUG_IPC") && atoi(getenv("EXT_MPI_AMD_DEBUG_IPC")) >= 2) { /* every mapping */
           char hex[2 * EMAC_IPC_HANDLE_BYTES + 1];
           for (q = 0; q < EMAC_IPC_HANDLE_BYTES; q++) sprintf(hex + 2 * q, "%02x", e->handle[q]);
           fprintf(stderr, "ipc rank %d: peer %d %s handle %s id %llu base %p extent %ld offset %ld bytes %zu\n",
@@ -1150,10 +1150,10 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
     const long fused_max = fm ? atol(fm) : (1L << 20);
     h->fused = R > 1 && (long)h->bytes <= fused_max;
   }
-  if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
+  if (getenv("EXT_MPI_AMD_DEBUG_IPC") && (attempt > 0 || atoi(getenv("EXT_MPI_AMD_DEBUG_IPC")) >= 2))
     fprintf(stderr, "ipc rank %d: own send %p recv %p bytes %zu, %d buckets, slot %d, %d attempt(s)\n", cm->rank,
             h->dsend[0], h->drecv[0], h->bytes, nb, slot, attempt + 1);
-  if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
+  if (getenv("EXT_MPI_AMD_DEBUG_IPC") && atoi(getenv("EXT_MPI_AMD_DEBUG_IPC")) >= 2)
     for (t = 0; t < nb; t++)
       fprintf(stderr, "ipc rank %d: bucket %d: src0 %p dst0 %p head %ld nvec %ld tail %ld scalar %d count %ld\n", cm->rank,
               t, b[t].src[0], b[t].dst[0], b[t].head, b[t].nvec, b[t].tail, b[t].scalar, b[t].count);
