@@ -78,7 +78,7 @@ typedef struct {
   ext_mpi_amd_allgather_fn ag;
   void *ag_ctx;
   void *sync;                      /* this rank's emac_sync block (uncached device memory) */
-  void *stale_sync[4];             /* blocks of failed set-up rounds (freed with the communicator) */
+  void *stale_sync[8];             /* blocks of failed set-up rounds (freed with the communicator) */
   int nstale_sync;
   void *peer_sync[EMAC_MAX_RANKS]; /* every rank's block as mapped here (own at [rank]) */
   void *peer_sync_base[EMAC_MAX_RANKS]; /* the mappings (shared table, ipc_map_peer) */
@@ -755,7 +755,7 @@ typedef struct {
    on a third communicator of 3 processes after 1200 handle lifetimes). A failed round keeps the
    blocks it allocated (peers may map them; freed with the communicator) and retries with a fresh,
    larger allocation. Collective: every rank runs every round whatever failed locally (`rc`). */
-#define EMAC_SYNC_ATTEMPTS 4
+#define EMAC_SYNC_ATTEMPTS 8
 static int ipc_sync_exchange(emac_comm *cm, int rc, ipc_export *all) {
   ipc_export mine;
   const int R = cm->size;
@@ -903,7 +903,7 @@ int ext_mpi_amd_comm_init_ipc(int rank, int size, ext_mpi_amd_allgather_fn allga
    The probe touches the first R bytes of each buffer during set-up only: the buffers must not be
    written by the device while the set-up runs. */
 #define EMAC_PROBE_FLIP 0x5A
-#define EMAC_IPC_ATTEMPTS 8
+#define EMAC_IPC_ATTEMPTS 16 /* 8 processes re-placing a freed-and-reused 64 MiB buffer took up to 4 */
 
 static void ipc_mirror_poison(emac_comm *cm, void *p) {
   int i;
