@@ -658,17 +658,17 @@ def _rccl_allreduce_baseline(rank, world, dist, torch):
         return {"error": str(e)[:200]}
 
 
-def _two_node_point(emac, rank, world, dev, count, tdtype, code, dname, dist, torch):
-    """§8(f3): the same ranks as two logical nodes of world/2 (ext_mpi_amd_comm_set_nodes; the
-    reference's one-port inter-node schedule between the node legs) on a second RCCL communicator,
-    at the run's size; checked against the float64 sum like the headline."""
-    R = world // 2
+def _node_point(emac, rank, world, dev, count, tdtype, code, dname, dist, torch, nodes=2):
+    """§8(f3): the same ranks as `nodes` logical nodes of world/nodes (ext_mpi_amd_comm_set_nodes;
+    the reference's one-port inter-node schedule between the node legs) on a second RCCL
+    communicator, at the run's size; checked against the float64 sum like the headline."""
+    R = world // nodes
     try:
         uid = [emac.get_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         comm2 = emac.comm_init(rank, world, uid[0], dev)
         try:
-            emac.comm_set_nodes(comm2, 2)
+            emac.comm_set_nodes(comm2, nodes)
             st = 20
             h2, sb, rb, _, el, ok = _comm_run(emac, comm2, count, tdtype, code, dname, f"6;1 -{R} {R}", st, 3, rank,
                                               world, dist, torch)
@@ -677,12 +677,12 @@ def _two_node_point(emac, rank, world, dev, count, tdtype, code, dname, dist, to
             rb.free()
         finally:
             emac.comm_free(comm2)
-        log(f"rank {rank}: two nodes of {R}: {el * 1e6 / st:.2f} us, checked {ok}")
-        return {"nodes": 2, "ranks_per_node": R, "copyin": f"6;1 -{R} {R}", "bytes_per_rank": count * tdtype.itemsize,
+        log(f"rank {rank}: {nodes} nodes of {R}: {el * 1e6 / st:.2f} us, checked {ok}")
+        return {"nodes": nodes, "ranks_per_node": R, "copyin": f"6;1 -{R} {R}", "bytes_per_rank": count * tdtype.itemsize,
                 "us_per_allreduce": round(el * 1e6 / st, 2),
                 "algbw_gbps": round(count * tdtype.itemsize * st / el / 1e9, 2), "checked": ok}
     except Exception as e:  # noqa: BLE001 -- an extra point, never the headline
-        log(f"rank {rank}: two-node schedule failed: {e}")
+        log(f"rank {rank}: {nodes}-node schedule failed: {e}")
         return {"error": str(e)[:200]}
 
 
@@ -753,8 +753,11 @@ def transport_child(args):
         if transport == "rccl":
             res["rccl_allreduce_baseline"] = _rccl_allreduce_baseline(rank, world, dist, torch)
             if world >= 2 and world % 2 == 0:
-                res["two_node_schedule"] = _two_node_point(emac, rank, world, dev, count, tdtype, code, dname, dist,
-                                                           torch)
+                res["two_node_schedule"] = _node_point(emac, rank, world, dev, count, tdtype, code, dname, dist,
+                                                       torch)
+            if world >= 4 and world % 4 == 0:  # two radix-2 node steps (4 nodes)
+                res["four_node_schedule"] = _node_point(emac, rank, world, dev, count, tdtype, code, dname, dist,
+                                                        torch, nodes=4)
         if full:
             # BASELINE configs[3] (double, 256 MiB per rank) and a configs[4]-style size sweep
             points = [(args.dtype, n) for n in (8, 64 << 10, 1 << 20, 16 << 20, 64 << 20, 256 << 20, 512 << 20)]
@@ -872,8 +875,9 @@ def multi_gpu(args):
                 "value": round(world * S * args.steps / r["wall"] / 1e9, 2), "checked": r["checked"]}
         if "rccl_allreduce_baseline" in results[t]:  # whichever role RCCL had
             extras["rccl_allreduce_baseline"] = results[t]["rccl_allreduce_baseline"]
-        if "two_node_schedule" in results[t]:
-            extras["two_node_schedule"] = results[t]["two_node_schedule"]
+        for key in ("two_node_schedule", "four_node_schedule"):
+            if key in results[t]:
+                extras[key] = results[t][key]
     if rank == 0 and primary is None:
         emit(({"metric": "device-resident GB/s reduced (float32 MPI_SUM) per GPU; % HBM3E roofline",
                           "value": 0.0, "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
