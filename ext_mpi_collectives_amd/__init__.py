@@ -105,7 +105,11 @@ def lib():
                                                P(P2P), c_int, P(c_int), P(FoldDesc), c_int, P(c_int), P(c_long)]
         L.ext_mpi_amd_comm_program_nodes.argtypes = [c_int, c_int, c_int, c_long, c_int, ctypes.c_char_p, c_long,
                                                      P(P2P), c_int, P(c_int), P(FoldDesc), c_int, P(c_int), P(c_long)]
+        L.ext_mpi_amd_comm_program_node_ports.argtypes = [c_int, P(c_int), c_int, c_int, c_long, c_int,
+                                                          ctypes.c_char_p, c_long, P(P2P), c_int, P(c_int),
+                                                          P(FoldDesc), c_int, P(c_int), P(c_long)]
         L.ext_mpi_amd_comm_set_nodes.argtypes = [c_int, c_int]
+        L.ext_mpi_amd_comm_set_node_ports.argtypes = [c_int, c_int, P(c_int)]
         L.ext_mpi_amd_set_num_sockets.argtypes = [c_int]
         L.ext_mpi_amd_set_num_sockets.restype = c_int
         L.ext_mpi_amd_version.restype = ctypes.c_char_p
@@ -252,11 +256,17 @@ def LEG_STEP(s):
     return (s + 1) << LEG_STEP_SHIFT
 
 
-def lockstep_legs(nodes=1):
+def lockstep_legs(nodes=1, ports=None):
     """The legs of one Start in the order a lock-step driver runs them on every rank: stage-in,
-    reduce-scatter, fold, per node step the pair exchange and its fold, the exchanges back in
-    reverse step order, allgather, stage-out."""
-    k = max(0, (nodes - 1).bit_length())
+    reduce-scatter, fold, per node step the line exchange and its fold, the exchanges back in
+    reverse step order, allgather, stage-out. `ports`: the inter-node list (None: one port per
+    step for a power of two, else one step)."""
+    if ports is not None:
+        k = sum(1 for p in ports if p < 0)
+    elif nodes > 1 and nodes & (nodes - 1):
+        k = 1
+    else:
+        k = max(0, (nodes - 1).bit_length())
     legs = [LEG_STAGE_IN, LEG_REDUCE_SCATTER, LEG_FOLD]
     for st in range(k):
         legs += [LEG_NODES_RS | LEG_STEP(st), LEG_NODES_FOLD | LEG_STEP(st)]
@@ -307,27 +317,35 @@ def comm_program(nranks, rank, count, dtype, copyin=None, send_phase=0, max_ops=
     return o, [(off, n, leaves) for off, n, leaves, _ in f], stage
 
 
+def _ports(ports):
+    """The reference's 0-terminated num_ports list (None: NULL, the default schedule)."""
+    return None if ports is None else (ctypes.c_int * (len(ports) + 1))(*ports, 0)
+
+
 def comm_program_nodes(nodes, ranks_per_node, rank, count, dtype, copyin=None, send_phase=0, max_ops=65536,
-                       max_folds=4096):
-    """comm_program over ``nodes`` (1 or 2) nodes; ``rank`` is global (node-major). Folds are
-    (offset, count, [(buf, leaf_offset)], leg) with leg LEG_FOLD (the node's fold) or
-    LEG_NODES_FOLD (this node's partial, then the other node's)."""
+                       max_folds=4096, ports=None):
+    """comm_program over ``nodes`` nodes under the inter-node ports list ``ports`` (None: one port
+    per step, 2^k nodes); ``rank`` is global (node-major). Folds are (offset, count,
+    [(buf, leaf_offset)], leg) with leg LEG_FOLD (the node's fold) or LEG_NODES_FOLD | step << 8
+    (the kept lines' partials in the reference's accumulator order)."""
     ops = (P2P * max_ops)()
     folds = (FoldDesc * max_folds)()
     nops, nf, stage = ctypes.c_int(), ctypes.c_int(), ctypes.c_long()
-    _check("ext_mpi_amd_comm_program_nodes",
-           lib().ext_mpi_amd_comm_program_nodes(nodes, ranks_per_node, rank, count, dtype, _enc(copyin), send_phase,
-                                                ops, max_ops, ctypes.byref(nops), folds, max_folds, ctypes.byref(nf),
-                                                ctypes.byref(stage)))
+    _check("ext_mpi_amd_comm_program_node_ports",
+           lib().ext_mpi_amd_comm_program_node_ports(nodes, _ports(ports), ranks_per_node, rank, count, dtype,
+                                                     _enc(copyin), send_phase, ops, max_ops, ctypes.byref(nops), folds,
+                                                     max_folds, ctypes.byref(nf), ctypes.byref(stage)))
     o = [(x.leg, x.peer, x.is_send, x.buf, x.offset, x.bytes) for x in ops[:nops.value]]
     f = [(x.offset, x.count, [(x.buf[t], x.leaf_offset[t]) for t in range(x.nleaf)], x.leg) for x in folds[:nf.value]]
     return o, f, stage.value
 
 
-def comm_set_nodes(comm, nodes):
-    """Declare the ranks of an RCCL / loopback communicator `nodes` (a power of two) nodes of
-    size / nodes consecutive ranks each."""
-    return _check("ext_mpi_amd_comm_set_nodes", lib().ext_mpi_amd_comm_set_nodes(comm, nodes))
+def comm_set_nodes(comm, nodes, ports=None):
+    """Declare the ranks of an RCCL / loopback communicator `nodes` nodes of size / nodes
+    consecutive ranks each, under the inter-node ports list `ports` (the reference's
+    EXT_MPI_NUM_PORTS, e.g. [-2, 2] for 3 nodes; None: one port per step for a power of two,
+    else one step of radix `nodes`)."""
+    return _check("ext_mpi_amd_comm_set_node_ports", lib().ext_mpi_amd_comm_set_node_ports(comm, nodes, _ports(ports)))
 
 
 def set_num_sockets(sockets):

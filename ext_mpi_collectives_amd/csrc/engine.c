@@ -71,6 +71,7 @@ typedef struct {
   int used;
   int rank, size, device;
   int nodes; /* COMM form: ranks [n * size / nodes, (n + 1) * size / nodes) form node n (0: one node) */
+  emac_node_sched ns; /* ... and their inter-node schedule (ext_mpi_amd_comm_set_node_ports) */
   ncclComm_t nccl;
   int loop_group; /* >= 0: in-process loopback communicator (testing transport), no RCCL */
   /* peer-mapped transport (ext_mpi_amd_comm_init_ipc) */
@@ -167,8 +168,9 @@ typedef struct {
   int fused; /* whole Allreduce in one launch (emac_gpu_fold_fused) */
   void *ev_release; /* system-scope release recorded before every phase-0 barrier */
   emac_launch pull; /* every other owner's result copied into this rank's receive buffer */
-  int nodes;            /* COMM form over 2^k nodes: the node-pair legs run (emac_comm_program_nodes) */
-  emac_launch xfold[4]; /* ... and, per step, fold this node's partial with the partner node's */
+  int nodes;            /* COMM form over several nodes: the node legs run (emac_comm_program_nodes) */
+  emac_node_sched ns;   /* ... under this inter-node schedule */
+  emac_launch xfold[EMAC_MAX_NODE_STEPS]; /* ... and, per step, the fold of the kept lines' partials */
   void *graph[EXT_MPI_AMD_LEG_ALL + 1]; /* COMM form: captured legs, per subset of EXT_MPI_AMD_LEG_* */
   unsigned char graph_failed[EXT_MPI_AMD_LEG_ALL + 1];
   emac_pipe *pipe; /* pipelined host staging (NODE form), or NULL */
@@ -217,7 +219,7 @@ static void release(emac_handle *h) {
   emac_gpu_free(h->d_edges);
   emac_gpu_free(h->pull.d_buckets);
   emac_gpu_free(h->pull.d_edges);
-  for (r = 0; r < 4; r++) {
+  for (r = 0; r < EMAC_MAX_NODE_STEPS; r++) {
     emac_gpu_free(h->xfold[r].d_buckets);
     emac_gpu_free(h->xfold[r].d_edges);
   }
@@ -1207,6 +1209,8 @@ int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, i
     h->me_pos = h->plan.rank_pos[h->me % R];
     h->bytes = (size_t)count * (size_t)h->plan.tsize;
     h->nodes = cm->size / R;
+    h->ns = cm->ns;
+    if (h->nodes > 1 && h->ns.nodes != h->nodes) rc = EMAC_ERR_ARG;
   }
   h->nbuf = 1;
   h->nsrc = R;
@@ -1222,14 +1226,14 @@ int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, i
     emac_fold *folds = NULL;
     int nf = 0, f;
     emac_bucket *xb = NULL;
-    int nxb[4] = {0, 0, 0, 0}, st, nsteps = 0;
-    while ((1 << nsteps) < h->nodes) nsteps++;
-    if ((rc = emac_comm_program_nodes(&h->plan, h->nodes, h->me / R, h->me % R,
+    int nxb[EMAC_MAX_NODE_STEPS] = {0}, st;
+    const int nsteps = h->nodes > 1 ? h->ns.nsteps : 0;
+    if ((rc = emac_comm_program_nodes(&h->plan, h->nodes > 1 ? &h->ns : NULL, h->me / R, h->me % R,
                                       (long)((unsigned long)h->dsend[0] & 15ul), &h->ops, &h->nops, &folds, &nf,
                                       &stage_total)))
       goto fail;
     b = (emac_bucket *)calloc((size_t)nf + 1, sizeof(emac_bucket));
-    xb = (emac_bucket *)calloc(4 * ((size_t)nf + 1), sizeof(emac_bucket));
+    xb = (emac_bucket *)calloc(EMAC_MAX_NODE_STEPS * ((size_t)nf + 1), sizeof(emac_bucket));
     if (!b || !xb || (rc = emac_gpu_malloc(&h->staging, (size_t)(stage_total > 0 ? stage_total : 16)))) {
       free(folds);
       free(xb);
@@ -1251,7 +1255,8 @@ int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, i
     }
     free(folds);
     for (st = 0; st < nsteps; st++)
-      if (nxb[st] && (rc = upload_launch_as(h, &h->xfold[st], xb + (size_t)st * ((size_t)nf + 1), nxb[st], 2, 0))) {
+      if (nxb[st] &&
+          (rc = upload_launch_as(h, &h->xfold[st], xb + (size_t)st * ((size_t)nf + 1), nxb[st], h->ns.radix[st], 0))) {
         free(xb);
         goto fail;
       }
@@ -1469,21 +1474,26 @@ static int enqueue_legs(emac_handle *h, int legs) {
                           h->tiles_per_bucket, h->all_full, h->d_edges, h->nedges, h->stream)))
     return rc;
   if (h->kind == KIND_COMM && h->nodes > 1) {
-    /* 2^k nodes: per step the node-pair exchange of the owned range's halves and their two-leaf
-       fold, then the exchanges back in reverse step order (emac_comm_program_nodes). A step
+    /* several nodes: per step the exchange of the lines with the column peers and the fold of
+       the kept lines' partials (a left fold of radix leaves in the order the program lists
+       them), then the exchanges back in reverse step order (emac_comm_program_nodes). A step
        selector in the legs' high bits (EXT_MPI_AMD_LEG_STEP) runs that step's legs alone. */
-    static const emac_codes pair = {{1, 0}, {0, 1}, 1, 2};
-    int st, nsteps = 0;
-    const int only = (legs >> EMAC_LEG_STEP_SHIFT) & 31;
-    while ((1 << nsteps) < h->nodes) nsteps++;
+    int st;
+    const int nsteps = h->ns.nsteps, only = (legs >> EMAC_LEG_STEP_SHIFT) & 31;
     for (st = 0; st < nsteps; st++) {
       const emac_launch *X = &h->xfold[st];
+      emac_codes lin;
+      memset(&lin, 0, sizeof(lin));
+      lin.first[0] = 1; /* one level: a left fold */
+      lin.close[h->ns.radix[st] - 1] = 1;
+      lin.nlev = 1;
+      lin.nleaf = h->ns.radix[st];
       if (only && st != only - 1) continue;
       if ((legs & EXT_MPI_AMD_LEG_NODES_RS) && (rc = run_leg(h, EMAC_LEG_NODES_RS | st << EMAC_LEG_STEP_SHIFT)))
         return rc;
       if ((legs & EXT_MPI_AMD_LEG_NODES_FOLD) && X->nb &&
-          (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, 2, 0, X->unroll, &pair, X->d_buckets, X->nb, X->ntiles,
-                              X->tiles_per_bucket, X->all_full, X->d_edges, X->nedges, h->stream)))
+          (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->ns.radix[st], 0, X->unroll, &lin, X->d_buckets, X->nb,
+                              X->ntiles, X->tiles_per_bucket, X->all_full, X->d_edges, X->nedges, h->stream)))
         return rc;
     }
     for (st = nsteps - 1; st >= 0; st--) {
@@ -1634,17 +1644,36 @@ int ext_mpi_amd_comm_program(int nranks, int rank, long count, int dtype, const 
                                         max_folds, nfolds, staging_bytes);
 }
 
-int ext_mpi_amd_comm_set_nodes(int comm, int nodes) {
+int ext_mpi_amd_comm_set_node_ports(int comm, int nodes, const int *ports) {
+  emac_node_sched ns;
+  int rc;
   if (comm < 0 || comm >= MAX_COMMS || !comms[comm].used) return EMAC_ERR_ARG;
-  if (nodes < 1 || comms[comm].size % nodes || (nodes & (nodes - 1))) return EMAC_ERR_ARG;
+  if (nodes < 1 || comms[comm].size % nodes) return EMAC_ERR_ARG;
   if (nodes > EMAC_MAX_NODES || (nodes > 1 && comms[comm].ipc)) return EMAC_ERR_UNSUPPORTED;
+  if ((rc = emac_node_sched_build(&ns, nodes, ports))) return rc;
   comms[comm].nodes = nodes;
+  comms[comm].ns = ns;
   return 0;
+}
+
+int ext_mpi_amd_comm_set_nodes(int comm, int nodes) {
+  if (nodes > 1 && (nodes & (nodes - 1))) return EMAC_ERR_ARG; /* one port per step: a power of two */
+  return ext_mpi_amd_comm_set_node_ports(comm, nodes, NULL);
 }
 
 int ext_mpi_amd_comm_program_nodes(int nodes, int ranks_per_node, int rank, long count, int dtype, const char *copyin,
                                    long send_phase, ext_mpi_amd_p2p *ops, int max_ops, int *nops,
                                    ext_mpi_amd_fold *folds, int max_folds, int *nfolds, long *staging_bytes) {
+  if (nodes > 1 && (nodes & (nodes - 1))) return EMAC_ERR_ARG; /* one port per step: a power of two */
+  return ext_mpi_amd_comm_program_node_ports(nodes, NULL, ranks_per_node, rank, count, dtype, copyin, send_phase, ops,
+                                             max_ops, nops, folds, max_folds, nfolds, staging_bytes);
+}
+
+int ext_mpi_amd_comm_program_node_ports(int nodes, const int *ports, int ranks_per_node, int rank, long count,
+                                        int dtype, const char *copyin, long send_phase, ext_mpi_amd_p2p *ops,
+                                        int max_ops, int *nops, ext_mpi_amd_fold *folds, int max_folds, int *nfolds,
+                                        long *staging_bytes) {
+  emac_node_sched ns;
   emac_plan p;
   emac_copyin cfg;
   emac_p2p *o = NULL;
@@ -1653,9 +1682,12 @@ int ext_mpi_amd_comm_program_nodes(int nodes, int ranks_per_node, int rank, long
   int rc, i, t, no = 0, nf = 0;
   if (R < 1 || R > EMAC_MAX_RANKS || nodes < 1 || nodes > EMAC_MAX_NODES || rank < 0 || rank >= nodes * R)
     return EMAC_ERR_ARG;
+  if ((rc = emac_node_sched_build(&ns, nodes, ports))) return rc;
   if ((rc = parse_cfg(copyin, R, &cfg))) return rc;
   if ((rc = emac_plan_build(&p, R, count, dtype, EMAC_SUM, &cfg))) return rc;
-  if ((rc = emac_comm_program_nodes(&p, nodes, rank / R, rank % R, send_phase, &o, &no, &f, &nf, staging_bytes))) goto out;
+  if ((rc = emac_comm_program_nodes(&p, nodes > 1 ? &ns : NULL, rank / R, rank % R, send_phase, &o, &no, &f, &nf,
+                                    staging_bytes)))
+    goto out;
   if (no > max_ops || nf > max_folds) {
     rc = EMAC_ERR_ARG;
     goto out;

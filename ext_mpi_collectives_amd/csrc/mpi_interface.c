@@ -16,7 +16,7 @@
  * self-test of debug_persistent.c:393-568 runs inside every Allreduce_init),
  * EXT_MPI_NUM_TASKS_PER_SOCKET (ranks per socket: with the sockets, the node size -- a physical
  * node may hold several logical ones), EXT_MPI_NUM_PORTS (the reference's "nodes(ports)" grammar,
- * ports_groups.c:55-110; several nodes: one port per step, log2(nodes) steps of -1 then of +1),
+ * ports_groups.c:55-110: the reduce-scatter ports, then the allgather ports, of allreduce_core),
  * EXT_MPI_NUM_SOCKETS_PER_NODE (any divisor of the node size: sockets change the reference's
  * partner encoding and barrier scope, and the tree method's last-step roots -- the one place
  * they reach the fold arithmetic, ext_mpi_amd_set_num_sockets). MPI_Info
@@ -29,18 +29,19 @@
  * through a per-communicator cache of handles keyed on (buffers, count, type, parameter row).
  * The copy-in factors come from the reference's parameter file
  * ext_mpi_allreduce_blocking_<nodes>_<cores>.txt (/dev/shm first, then the working directory):
- * one row per message-size threshold, host rows then device rows (README "blocking"); a row whose
- * ports column names another inter-node schedule than the one-port one over the communicator's
- * nodes goes to PMPI_Allreduce.
+ * one row per message-size threshold, host rows then device rows (README "blocking"); a row's
+ * ports column sets the inter-node schedule of the handles made for it, and a row naming another
+ * node count or a schedule this path does not take goes to PMPI_Allreduce.
  *
  * Transport (EXT_MPI_AMD_TRANSPORT): "ipc" (default) maps every rank's device buffers into every
  * other rank with hipIpc, as the reference maps them with cudaIpc (src/gpu/cuda_shmem.c:218-299),
  * bootstrapped with PMPI_Allgather; "rccl" runs the legs as RCCL point-to-point rounds,
  * bootstrapped with PMPI_Bcast of the unique id. One engine communicator per MPI communicator,
  * cached as an MPI attribute and destroyed with it. The communicator lies within one node, or
- * spans 2^k nodes (<= 16) of equal size in node-major rank order: then the legs run over RCCL with
- * the reference's one-port inter-node schedule (ext_mpi_amd_comm_set_nodes); other inter-node
- * shapes return EXT_MPI_AMD_ERROR_UNSUPPORTED (the blocking front end hands them to PMPI).
+ * spans up to 16 nodes of equal size in node-major rank order: then the legs run over RCCL with
+ * the reference's inter-node schedule (EXT_MPI_NUM_PORTS; unset: one port per step for a power of
+ * two, else one step; ext_mpi_amd_comm_set_node_ports); other inter-node shapes return
+ * EXT_MPI_AMD_ERROR_UNSUPPORTED (the blocking front end hands them to PMPI).
  */
 #include <mpi.h>
 #include <stdio.h>
@@ -60,9 +61,8 @@ static int cfg_verbose = 0;
 static int cfg_debug = 1;
 static int cfg_num_sockets = -1;
 static int cfg_tasks_per_socket = -1; /* EXT_MPI_NUM_TASKS_PER_SOCKET: ranks of a (logical) socket */
-static int cfg_ports_ok = 1;          /* EXT_MPI_NUM_PORTS names the one-port schedule (or is unset) */
-static int cfg_ports_steps = -1;      /* ... with this many reduce-scatter steps (-1: unset) */
-static int cfg_ports_nodes = 0;       /* ... over a group of this many nodes (0: no group given) */
+static int cfg_ports_nodes = 0;      /* EXT_MPI_NUM_PORTS: its nodes (0 unset, -1 not this path) */
+static int cfg_ports[16];             /* ... its 0-terminated port list (parse_ports) */
 static int cfg_blocking = 0;
 static int cfg_rccl = 0; /* EXT_MPI_AMD_TRANSPORT=rccl: legs over RCCL instead of hipIpc mappings */
 static int initialised = 0;
@@ -83,16 +83,19 @@ static int env_int(const char *name, int *out) {
    ext_mpi_scan_ports_groups (ports_groups.c:55-110; README: "4(-1 -1 1 1)", "1(-1)"):
    "G(p0 p1 ...)" with G the nodes of the group and p the ports of each inter-node step
    (negative: reduce-scatter, positive: allgather; radix |p| + 1). ' ', ',' and '_' separate.
-   The inter-node schedule here is the one-port one over one group: "1(...)" (one node, no
-   inter-node step) or "2^k(-1 ... -1 1 ... 1)" with k entries of each sign. A bare port list
-   (which the reference's scanner runs past the end of) is read as the ports of one group of
-   unstated size. Returns the group's nodes (0: not stated) and *steps (the reduce-scatter
-   steps, -1 for an empty string), or -1 when the string names anything else: several ports per
-   step, several groups, unequal step counts, a group size other than 2^steps. */
-static int parse_ports(const char *s, int *steps) {
-  int groups = 0, bare = 0, nodes = 0, neg = 0, pos = 0, tokens = 0, in_group = 0, ok = 1;
+   Taken here: one group, "1(...)" (one node, no inter-node step) or the reduce-scatter ports
+   then the allgather ports, each part's radices multiplying to G (allreduce_core,
+   allreduce_recursive.c:222-453; e.g. "4(-1 -1 1 1)", "3(-2 2)", "6(-1 -2 2 1)"). A bare port
+   list (which the reference's scanner runs past the end of) is read as the ports of one group of
+   that many nodes. Returns the group's nodes and the 0-terminated list in ports[] (EMAC_PORTS_MAX
+   entries at most), 0 for an empty string, or -1 when the string names anything else: several
+   groups, a list without reduce-scatter ports or ending in one (reduce_scatter_core / reduction
+   inside the allgather steps), radices that do not multiply to G. */
+#define EMAC_PORTS_MAX 9
+static int parse_ports(const char *s, int *ports) {
+  int groups = 0, bare = 0, nodes = 0, n = 0, in_group = 0, ok = 1, i, prs = 1, pag = 1, seen_ag = 0;
   const char *p = s;
-  *steps = -1;
+  ports[0] = 0;
   while (p && *p) {
     char *end;
     long v;
@@ -109,7 +112,6 @@ static int parse_ports(const char *s, int *steps) {
     v = strtol(p, &end, 10);
     if (end == p) return -1;
     p = end;
-    tokens++;
     while (*p == ' ' || *p == '_') p++;
     if (*p == '(') { /* the group's node count */
       if (in_group || ++groups > 1 || v < 1) ok = 0;
@@ -119,19 +121,27 @@ static int parse_ports(const char *s, int *steps) {
       continue;
     }
     if (!in_group) bare = 1;
-    if (v == -1 && !pos)
-      neg++;
-    else if (v == 1)
-      pos++;
-    else
-      ok = 0; /* several ports per step, or a reduce-scatter step after an allgather step */
+    if (n == EMAC_PORTS_MAX - 1 || v == 0 || v < -16 || v > 16) {
+      ok = 0;
+      continue;
+    }
+    ports[n++] = (int)v;
+    ports[n] = 0;
   }
-  if (!tokens) return 0;
+  if (!n && !groups) return 0;
   if (!ok || in_group || (bare && groups)) return -1;
-  *steps = neg;
   if (nodes == 1) return 1; /* one node: its ports name no inter-node step */
-  if (neg != pos || (nodes > 1 && nodes != 1 << neg)) return -1;
-  return nodes;
+  for (i = 0; i < n; i++) {
+    if (ports[i] < 0) {
+      if (seen_ag) return -1; /* a reduce-scatter step after an allgather step */
+      prs *= 1 - ports[i];
+    } else {
+      seen_ag = 1;
+      pag *= 1 + ports[i];
+    }
+  }
+  if (prs == 1 || !seen_ag || prs != pag || (nodes && nodes != prs) || prs > 16) return -1;
+  return prs;
 }
 
 static void read_env(void) {
@@ -144,8 +154,7 @@ static void read_env(void) {
     env_int("EXT_MPI_DEBUG", &cfg_debug);
     env_int("EXT_MPI_NUM_SOCKETS_PER_NODE", &cfg_num_sockets);
     env_int("EXT_MPI_NUM_TASKS_PER_SOCKET", &cfg_tasks_per_socket);
-    cfg_ports_nodes = parse_ports(getenv("EXT_MPI_NUM_PORTS"), &cfg_ports_steps); /* ext_mpi.c:124-157 */
-    cfg_ports_ok = cfg_ports_nodes >= 0;
+    cfg_ports_nodes = parse_ports(getenv("EXT_MPI_NUM_PORTS"), cfg_ports); /* ext_mpi.c:124-157 */
     cfg_rccl = getenv("EXT_MPI_AMD_TRANSPORT") && !strcmp(getenv("EXT_MPI_AMD_TRANSPORT"), "rccl");
     if (c) {
       strncpy(cfg_copyin, c, sizeof(cfg_copyin) - 1);
@@ -157,9 +166,8 @@ static void read_env(void) {
   PMPI_Bcast(&cfg_debug, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_num_sockets, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_tasks_per_socket, 1, MPI_INT, 0, MPI_COMM_WORLD);
-  PMPI_Bcast(&cfg_ports_ok, 1, MPI_INT, 0, MPI_COMM_WORLD);
-  PMPI_Bcast(&cfg_ports_steps, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_ports_nodes, 1, MPI_INT, 0, MPI_COMM_WORLD);
+  PMPI_Bcast(cfg_ports, 16, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_rccl, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&len, 1, MPI_INT, 0, MPI_COMM_WORLD);
   if (len > 0) PMPI_Bcast(cfg_copyin, len, MPI_CHAR, 0, MPI_COMM_WORLD);
@@ -240,6 +248,7 @@ static int request_handle(const MPI_Request *r) {
    destroyed with it. The communicator must lie within one node. */
 typedef struct {
   int ext_comm;
+  int nodes;     /* comm_topology: 1, or the nodes of an RCCL communicator over several */
   MPI_Comm boot; /* private duplicate the IPC bootstrap exchanges run on */
 } comm_attr;
 
@@ -261,13 +270,13 @@ static int comm_attr_delete(MPI_Comm comm, int keyval, void *attr, void *extra) 
   return MPI_SUCCESS;
 }
 
-/* The communicator's node layout (collective): *nodes = 1 (one node) or 2^k (<= 16) nodes of
-   equal size in node-major rank order (the reference's row layout, ext_mpi_native.c:879-960),
-   0 for any other shape; *nsize = ranks per node, *nrank = rank in the node. The reference's node
+/* The communicator's node layout (collective): *nodes = 1 (one node) or up to 16 nodes of equal
+   size in node-major rank order (the reference's row layout, ext_mpi_native.c:879-960), 0 for
+   any other shape; *nsize = ranks per node, *nrank = rank in the node. The reference's node
    is EXT_MPI_NUM_TASKS_PER_SOCKET x sockets consecutive ranks when that is set (ext_mpi.c:195-215,
    :638): a physical node may hold several logical ones. */
 static void comm_topology(MPI_Comm comm, int *nodes, int *nsize, int *nrank) {
-  int size, rank, v[2], k = 0;
+  int size, rank, v[2];
   MPI_Comm node;
   PMPI_Comm_size(comm, &size);
   PMPI_Comm_rank(comm, &rank);
@@ -283,18 +292,29 @@ static void comm_topology(MPI_Comm comm, int *nodes, int *nsize, int *nrank) {
     }
   }
   *nodes = *nsize > 0 && size % *nsize == 0 ? size / *nsize : 0;
-  while ((1 << k) < *nodes) k++;
   v[0] = *nsize == size;
-  v[1] = *nodes >= 2 && *nodes <= 16 && (1 << k) == *nodes && *nrank == rank % *nsize;
+  v[1] = *nodes >= 2 && *nodes <= 16 && *nrank == rank % *nsize;
   PMPI_Allreduce(MPI_IN_PLACE, v, 2, MPI_INT, MPI_MIN, comm);
   *nodes = v[0] ? 1 : v[1] ? *nodes : 0;
 }
 
-/* `env_ports`: EXT_MPI_NUM_PORTS governs the inter-node schedule (not when a blocking parameter
-   row, already checked by the caller, names it) */
-static int node_comm(MPI_Comm comm, const void *devbuf, int env_ports, int *ext_comm) {
+/* EXT_MPI_NUM_PORTS for a communicator of `nodes` nodes: *ports = its list, or NULL for the
+   default (one port per step for a power of two, else one step of radix `nodes`); -1 when it
+   names a schedule this path does not take or another node count */
+static int env_ports(int nodes, const int **ports) {
+  *ports = NULL;
+  if (nodes <= 1 || cfg_ports_nodes == 0) return 0;
+  if (cfg_ports_nodes != nodes) return -1; /* not this path (-1), or a group of another size */
+  *ports = cfg_ports;
+  return 0;
+}
+
+/* `use_env`: EXT_MPI_NUM_PORTS governs the inter-node schedule (not when a blocking parameter
+   row, already checked by the caller, names it per handle) */
+static int node_comm(MPI_Comm comm, const void *devbuf, int use_env, int *ext_comm) {
   comm_attr *a;
-  int flag, size, rank, nsize, nrank, device, ndev, rc, nodes, k = 0;
+  const int *ports = NULL;
+  int flag, size, rank, nsize, nrank, device, ndev, rc, nodes;
   unsigned char id[EXT_MPI_AMD_UNIQUE_ID_BYTES];
   if (comm_keyval == MPI_KEYVAL_INVALID) return EXT_MPI_AMD_ERROR_ARG;
   PMPI_Comm_get_attr(comm, comm_keyval, &a, &flag);
@@ -306,18 +326,14 @@ static int node_comm(MPI_Comm comm, const void *devbuf, int env_ports, int *ext_
   PMPI_Comm_rank(comm, &rank);
   comm_topology(comm, &nodes, &nsize, &nrank);
   if (!nodes) return EXT_MPI_AMD_ERROR_UNSUPPORTED; /* other inter-node shapes: out of scope */
-  while ((1 << k) < nodes) k++;
-  /* several ports per step are not built, nor a step count other than log2(nodes), nor a group
-     of another size than the communicator's */
-  if (nodes > 1 && env_ports &&
-      (!cfg_ports_ok || (cfg_ports_steps >= 0 && cfg_ports_steps != k) || (cfg_ports_nodes && cfg_ports_nodes != nodes)))
-    return EXT_MPI_AMD_ERROR_UNSUPPORTED;
+  if (use_env && env_ports(nodes, &ports)) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
   ndev = ext_mpi_amd_gpu_device_count();
   device = ext_mpi_amd_gpu_device_of(devbuf);
   if (device < 0) device = ndev > 0 ? nrank % ndev : -1;
   a = (comm_attr *)calloc(1, sizeof(comm_attr));
   if (!a) return EXT_MPI_AMD_ERROR_MALLOC;
   a->boot = MPI_COMM_NULL;
+  a->nodes = nodes;
   if (!cfg_rccl && nodes == 1) { /* peer mappings reach the ranks of one node only */
     PMPI_Comm_dup(comm, &a->boot);
     /* collective even without a device: every rank reaches the same verdict */
@@ -331,7 +347,8 @@ static int node_comm(MPI_Comm comm, const void *devbuf, int env_ports, int *ext_
     if (rank == 0 && (rc = ext_mpi_amd_get_unique_id(id))) memset(id, 0, sizeof(id));
     PMPI_Bcast(id, EXT_MPI_AMD_UNIQUE_ID_BYTES, MPI_BYTE, 0, comm);
     rc = ndev > 0 ? ext_mpi_amd_comm_init(rank, size, id, device, ext_comm) : EXT_MPI_AMD_ERROR_DEVICE;
-    if (rc == 0 && nodes > 1 && (rc = ext_mpi_amd_comm_set_nodes(*ext_comm, nodes))) ext_mpi_amd_comm_free(*ext_comm);
+    if (rc == 0 && nodes > 1 && (rc = ext_mpi_amd_comm_set_node_ports(*ext_comm, nodes, ports)))
+      ext_mpi_amd_comm_free(*ext_comm);
     flag = rc == 0;
     PMPI_Allreduce(MPI_IN_PLACE, &flag, 1, MPI_INT, MPI_MIN, comm);
     if (!flag) {
@@ -428,8 +445,8 @@ out:
 typedef struct {
   long msize;  /* message size in bytes from which the row applies */
   int sockets; /* logical sockets per node */
-  int nodes;   /* "<nodes>(<ports>)" field, parse_ports: nodes (0 unstated, -1 not this path) */
-  int steps;   /* ... its reduce-scatter steps */
+  int nodes;   /* "<nodes>(<ports>)" field, parse_ports: its nodes (-1: not this path) */
+  int ports[EMAC_PORTS_MAX]; /* ... its 0-terminated port list */
   char copyin[256];
 } brow;
 
@@ -519,7 +536,7 @@ static void blocking_load_rows(bcomm *b, MPI_Comm comm) {
     r = &b->row[side][b->nrow[side]++];
     r->msize = ms;
     r->sockets = so;
-    r->nodes = parse_ports(ports, &r->steps);
+    r->nodes = parse_ports(ports, r->ports);
     for (i = 0; cf[i]; i++)
       if (cf[i] == '_') cf[i] = ' ';
     snprintf(r->copyin, sizeof(r->copyin), "%.255s", cf);
@@ -559,9 +576,8 @@ static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int
   row = blocking_select_row(b, side, (long)bytes);
   if (row >= 0) {
     const brow *w = &b->row[side][row];
-    /* the row's inter-node schedule must be the one-port one over this communicator's nodes */
-    if (w->nodes < 0 || (w->nodes ? w->nodes != b->nodes : b->nodes > 1 && (w->steps < 0 || 1 << w->steps != b->nodes)))
-      return 1;
+    /* the row's inter-node schedule must be one this path takes, over this communicator's nodes */
+    if (w->nodes != b->nodes) return 1;
     if (w->sockets < 1 || b->nsize % w->sockets) return 1;
     copyin = w->copyin;
     row_sockets = w->sockets;
@@ -628,10 +644,23 @@ static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int
     }
     bcomm_drop(b, slot);
     e = &b->cache[slot];
-    /* a parameter-file row names its own socket count (ext_mpi_native_blocking.c:189-290) */
+    /* a parameter-file row names its own socket count (ext_mpi_native_blocking.c:189-290) and
+       inter-node ports; a handle keeps the schedule it was made with */
     const int prev_sockets = row_sockets > 0 ? ext_mpi_amd_set_num_sockets(row_sockets) : 0;
+    const int *hp = NULL;
+    if (b->nodes > 1) {
+      if (row >= 0)
+        hp = b->row[side][row].ports;
+      else if (env_ports(b->nodes, &hp))
+        return 1;
+      if ((rc = ext_mpi_amd_comm_set_node_ports(b->ext_comm, b->nodes, hp))) return rc;
+    }
     rc = ext_mpi_amd_allreduce_init(s, r, count, dtype, op, b->ext_comm, copyin, &e->handle);
     if (prev_sockets > 0) ext_mpi_amd_set_num_sockets(prev_sockets);
+    if (b->nodes > 1) { /* back to the communicator's own (EXT_MPI_NUM_PORTS or the default) */
+      if (env_ports(b->nodes, &hp)) hp = NULL;
+      ext_mpi_amd_comm_set_node_ports(b->ext_comm, b->nodes, hp);
+    }
     if (rc) {
       e->handle = -1;
       return rc;

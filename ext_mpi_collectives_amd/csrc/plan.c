@@ -377,33 +377,104 @@ void emac_plan_free(emac_plan *p) {
    each owned chunk, one 16-byte aligned slot per peer. */
 int emac_comm_program(const emac_plan *p, int me, long send_phase, emac_p2p **ops_out, int *nops_out,
                       emac_fold **folds_out, int *nfolds_out, long *staging_bytes) {
-  return emac_comm_program_nodes(p, 1, 0, me, send_phase, ops_out, nops_out, folds_out, nfolds_out, staging_bytes);
+  return emac_comm_program_nodes(p, NULL, 0, me, send_phase, ops_out, nops_out, folds_out, nfolds_out, staging_bytes);
 }
 
-/* log2 of a power of two, -1 otherwise */
-static int log2_exact(int n) {
-  int k = 0;
-  if (n < 1) return -1;
-  while ((1 << k) < n) k++;
-  return (1 << k) == n ? k : -1;
+int emac_node_sched_build(emac_node_sched *s, int nodes, const int *ports) {
+  int def[2 * EMAC_MAX_NODE_STEPS + 1], ag[EMAC_MAX_NODE_STEPS], nag = 0, i, prod_rs = 1, prod_ag = 1;
+  if (!s || nodes < 1 || nodes > EMAC_MAX_NODES) return EMAC_ERR_ARG;
+  memset(s, 0, sizeof(*s));
+  s->nodes = nodes;
+  for (i = 0; i < nodes; i++) s->task_node[i] = s->node_task[i] = i;
+  if (nodes == 1) return EMAC_OK; /* one node: no inter-node step, whatever the ports say */
+  if (!ports) {
+    int k = 0;
+    while ((1 << k) < nodes) k++;
+    if ((1 << k) == nodes && k <= EMAC_MAX_NODE_STEPS) { /* one port per step */
+      for (i = 0; i < k; i++) {
+        def[i] = -1;
+        def[k + i] = 1;
+      }
+      def[2 * k] = 0;
+    } else { /* one step of radix `nodes` */
+      def[0] = -(nodes - 1);
+      def[1] = nodes - 1;
+      def[2] = 0;
+    }
+    ports = def;
+  }
+  /* allreduce_core (allreduce_recursive.c:222-453): the reduce-scatter ports first (negative),
+     then the allgather ports (positive); a list ending in a negative port is reduce_scatter_core,
+     one without reduce-scatter ports reduces inside the allgather steps -- neither is this path */
+  for (i = 0; ports[i] < 0; i++) {
+    if (s->nsteps == EMAC_MAX_NODE_STEPS) return EMAC_ERR_UNSUPPORTED;
+    s->radix[s->nsteps++] = 1 - ports[i];
+    prod_rs *= 1 - ports[i];
+  }
+  for (; ports[i] > 0; i++) {
+    if (nag == EMAC_MAX_NODE_STEPS) return EMAC_ERR_UNSUPPORTED;
+    ag[nag++] = ports[i] + 1;
+    prod_ag *= ports[i] + 1;
+  }
+  if (ports[i] != 0 || !s->nsteps || !nag) return EMAC_ERR_UNSUPPORTED;
+  if (prod_rs != nodes || prod_ag != nodes) return EMAC_ERR_ARG;
+  /* ext_mpi_native.c:879-912: ext_mpi_rank_order over the allgather radices; the algorithm runs
+     on task = the position of the node in that order (rank_permutation.c:133-139) */
+  position_order(nodes, nag, ag, s->task_node);
+  for (i = 0; i < nodes; i++) s->node_task[s->task_node[i]] = i;
+  return EMAC_OK;
 }
 
-int emac_comm_program_nodes(const emac_plan *p, int nodes, int node, int me, long send_phase, emac_p2p **ops_out,
-                            int *nops_out, emac_fold **folds_out, int *nfolds_out, long *staging_bytes) {
-  const int k = log2_exact(nodes);
-  int R = p->nranks, me_pos, pc, q, t, nops = 0, nf = 0, leg, g0, st;
-  long ts = p->tsize, total = 0;
+/* the element range [*lo, *hi) of the lines (tasks) [a, b) in the message of `count` elements:
+   one line per node (ext_mpi_native.c:768-786: count / nodes, the remainder to the low nodes),
+   laid out in task order (raw_code.c:238-356 addresses line n at the sizes of lines 0..n-1,
+   mmsizes of each line's node after rank_permutation_backward) */
+static void task_lines(const emac_node_sched *ns, long count, int a, int b, long *lo, long *hi) {
+  const int N = ns->nodes;
+  long off = 0;
+  int k;
+  *lo = 0;
+  for (k = 0; k < b; k++) {
+    const int n = ns->task_node[k];
+    const long sz = count / N + (n < count % N);
+    if (k == a) *lo = off;
+    off += sz;
+  }
+  *hi = off;
+  if (a >= b) *lo = off;
+}
+
+/* intersection of [a, b) and [c, d) as (offset, length) */
+static void clip(long a, long b, long c, long d, long *off, long *len) {
+  const long lo = a > c ? a : c, hi = b < d ? b : d;
+  *off = lo;
+  *len = hi > lo ? hi - lo : 0;
+}
+
+int emac_comm_program_nodes(const emac_plan *p, const emac_node_sched *ns, int node, int me, long send_phase,
+                            emac_p2p **ops_out, int *nops_out, emac_fold **folds_out, int *nfolds_out,
+                            long *staging_bytes) {
+  const int K = ns ? ns->nsteps : 0, nodes = ns ? ns->nodes : 1, task = ns ? ns->node_task[node] : 0;
+  int R = p->nranks, me_pos, pc, q, t, nops = 0, nf = 0, leg, g0, st, i, nx = 0, G, Gn;
+  long ts = p->tsize, total = 0, count = 0;
   long *slot0, *stride, *xslot;
   emac_p2p *ops;
   emac_fold *folds;
-  if (k < 0 || nodes > EMAC_MAX_NODES || node < 0 || node >= nodes || me < 0 || me >= R) return EMAC_ERR_ARG;
+  int halving = K > 0;
+  if (nodes < 1 || nodes > EMAC_MAX_NODES || node < 0 || node >= nodes || me < 0 || me >= R) return EMAC_ERR_ARG;
+  for (st = 0; st < K; st++) {
+    nx += ns->radix[st] - 1;
+    halving &= ns->radix[st] == 2;
+  }
+  for (pc = 0; pc < p->npieces; pc++) /* the message's elements: the pieces' chunks tile it */
+    for (q = 0; q < R; q++) count += p->chunk_len[(size_t)pc * R + q];
   me_pos = p->rank_pos[me];
   g0 = node * R; /* global rank of this node's first rank */
   slot0 = (long *)malloc(sizeof(long) * (size_t)p->npieces);
   stride = (long *)malloc(sizeof(long) * (size_t)p->npieces);
-  xslot = (long *)malloc(sizeof(long) * (size_t)p->npieces * (size_t)(k > 0 ? k : 1));
-  ops = (emac_p2p *)malloc(sizeof(emac_p2p) * (size_t)(4 * p->npieces * R + 4 * k * p->npieces + 1));
-  folds = (emac_fold *)calloc((size_t)((1 + k) * p->npieces) + 1, sizeof(emac_fold));
+  xslot = (long *)malloc(sizeof(long) * (size_t)p->npieces * (size_t)(nx > 0 ? nx : 1));
+  ops = (emac_p2p *)malloc(sizeof(emac_p2p) * (size_t)(4 * p->npieces * R + 4 * nx * p->npieces + 1));
+  folds = (emac_fold *)calloc((size_t)((1 + K) * p->npieces) + 1, sizeof(emac_fold));
   if (!slot0 || !stride || !xslot || !ops || !folds) {
     free(slot0);
     free(stride);
@@ -419,18 +490,31 @@ int emac_comm_program_nodes(const emac_plan *p, int nodes, int node, int me, lon
     slot0[pc] = total + phase;
     total += (long)(R - 1) * stride[pc];
   }
-  /* node steps: one slot per piece and step for the partner node's partial of the half this rank
-     keeps, at the 16-byte phase that half has in the receive buffer (send_phase stands for it) */
+  /* node steps: one slot per piece, step and column peer for that peer's partial of the lines this
+     task keeps (inside this rank's chunk), at the 16-byte phase those lines have in the receive
+     buffer (send_phase stands for it) */
   for (pc = 0; pc < p->npieces; pc++) {
-    long lo = p->chunk_off[(size_t)pc * R + me_pos], n = p->chunk_len[(size_t)pc * R + me_pos];
-    for (st = 0; st < k; st++) {
-      const int bit = (node >> st) & 1;
-      const long h0 = (n + 1) / 2;
-      if (bit) lo += h0;
-      n = bit ? n - h0 : h0;
-      total = (total + 15) / 16 * 16;
-      xslot[(size_t)pc * k + st] = total + ((send_phase + lo * ts) & 15);
-      total += ((n * ts + 15) / 16) * 16 + 16;
+    const long off = p->chunk_off[(size_t)pc * R + me_pos], len = p->chunk_len[(size_t)pc * R + me_pos];
+    int x = 0;
+    long hlo = off, hn = len;
+    for (G = nodes, st = 0; st < K; G /= ns->radix[st], st++) {
+      long a, b, ko, kl;
+      Gn = G / ns->radix[st];
+      task_lines(ns, count, task / Gn * Gn, task / Gn * Gn + Gn, &a, &b);
+      clip(a, b, off, off + len, &ko, &kl);
+      if (halving) { /* the half of the current range this node keeps (see below) */
+        const int bit = (node >> st) & 1;
+        const long h0 = (hn + 1) / 2;
+        if (bit) hlo += h0;
+        hn = bit ? hn - h0 : h0;
+        ko = hlo;
+        kl = hn;
+      }
+      for (i = 0; i < ns->radix[st] - 1; i++) {
+        total = (total + 15) / 16 * 16;
+        xslot[(size_t)pc * nx + x++] = total + ((send_phase + ko * ts) & 15);
+        total += ((kl * ts + 15) / 16) * 16 + 16;
+      }
     }
   }
 #define SLOT(pc, q) (slot0[pc] + (long)(((q) - me - 1 + R) % R) * stride[pc])
@@ -469,12 +553,22 @@ int emac_comm_program_nodes(const emac_plan *p, int nodes, int node, int me, lon
     nf++;
   }
 #undef SLOT
-  /* 2^k nodes, one port (allreduce_recursive.c:222-453): step st pairs this node with node ^ 2^st
-     (the reference's radix-2 steps in its permuted node order, ext_mpi_native.c:879-912, pair
-     tasks by their highest bit first, i.e. nodes by their lowest); the owned range halves at
-     every step -- the node with bit st clear keeps the lower half -- and the ranges come back in
-     the reverse order. Each step's fold is one two-operand reduction: own partial, partner's. */
-  for (st = 0; st < k; st++)
+  /* the inter-node steps (allreduce_recursive.c:248-347). Step st splits each task group of G
+     tasks into radix sub-groups of Gn; task `task` keeps the lines of its sub-group and trades
+     with its column peers (task + Gn * (i + 1)) % G in its group, i = 0 .. radix - 2 (:261-316),
+     which are nodes task_node[] (same rank `me` there). The kept lines' fold follows the
+     accumulator order raw_code.c:270-340 gives allreduce_core's lines (r_i = column peer i's
+     partial, own = this node's):
+       a middle step:            own, r_0, ..., r_{p-1}   (reducefrom line+3lb.. into 2lb, :283-293)
+       the first (not last):     r_0, own, r_1, ...       (r_0 received into 2lb, then the own line)
+       the last:                 r_{p-1}, own, r_0, ..., r_{p-2}  (r_{p-1} received into lb, :318-343)
+     -- for SUM only the association matters (a + b == b + a). */
+  /* One port per step over 2^k nodes: every value is a balanced pairwise tree (a + b == b + a at
+     each step), the same whichever node of a pair computes it, so the lines need not be followed:
+     the owned range halves at every step (the node with bit st clear keeps the lower half) and
+     every rank of a node carries an equal share. Task order is the bit reversal here, so step st
+     pairs nodes n and n ^ 2^st. */
+  for (st = 0; halving && st < K; st++)
     for (pc = 0; pc < p->npieces; pc++) {
       long lo = p->chunk_off[(size_t)pc * R + me_pos], n = p->chunk_len[(size_t)pc * R + me_pos];
       long hoff[2], hlen[2];
@@ -493,22 +587,83 @@ int emac_comm_program_nodes(const emac_plan *p, int nodes, int node, int me, lon
         ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, partner, 1, EMAC_BUF_RECV, hoff[1 - bit] * ts, hlen[1 - bit] * ts};
       if (hlen[bit] > 0) {
         emac_fold *f = &folds[nf++];
-        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, partner, 0, EMAC_BUF_STAGE, xslot[(size_t)pc * k + st],
+        /* raw_code.c's accumulator: the partner's partial first at the first and the last step,
+           the own one in between */
+        const int own = st > 0 && st < K - 1 ? 0 : 1;
+        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, partner, 0, EMAC_BUF_STAGE, xslot[(size_t)pc * nx + st],
                                  hlen[bit] * ts};
         f->piece = pc;
         f->offset = hoff[bit] * ts;
         f->count = hlen[bit];
         f->nleaf = 2;
         f->leg = EMAC_LEG_NODES_FOLD | lg;
-        f->buf[0] = EMAC_BUF_RECV; /* this node's partial first */
-        f->loff[0] = hoff[bit] * ts;
-        f->buf[1] = EMAC_BUF_STAGE;
-        f->loff[1] = xslot[(size_t)pc * k + st];
+        f->buf[own] = EMAC_BUF_RECV;
+        f->loff[own] = hoff[bit] * ts;
+        f->buf[1 - own] = EMAC_BUF_STAGE;
+        f->loff[1 - own] = xslot[(size_t)pc * nx + st];
         ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | lg, partner, 1, EMAC_BUF_RECV, hoff[bit] * ts, hlen[bit] * ts};
       }
       if (hlen[1 - bit] > 0)
         ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | lg, partner, 0, EMAC_BUF_RECV, hoff[1 - bit] * ts, hlen[1 - bit] * ts};
     }
+  /* otherwise the lines are followed as the reference lays them out */
+  for (G = nodes, st = 0; !halving && st < K; G /= ns->radix[st], st++) {
+    const int rad = ns->radix[st], lg = st << EMAC_LEG_STEP_SHIFT, last = st == K - 1;
+    int xs = 0, s2;
+    Gn = G / rad;
+    for (s2 = 0; s2 < st; s2++) xs += ns->radix[s2] - 1; /* this step's first staging slot */
+    for (pc = 0; pc < p->npieces; pc++) {
+      const long off = p->chunk_off[(size_t)pc * R + me_pos], len = p->chunk_len[(size_t)pc * R + me_pos];
+      long a, b, ko, kl;
+      int peer_task[EMAC_MAX_NODES];
+      task_lines(ns, count, task / Gn * Gn, task / Gn * Gn + Gn, &a, &b);
+      clip(a, b, off, off + len, &ko, &kl);
+      for (i = 0; i < rad - 1; i++) peer_task[i] = (task + Gn * (i + 1)) % G + task / G * G;
+      for (i = 0; i < rad - 1; i++) { /* the peer's sub-group's lines to it, its partial of mine from it */
+        const int gp = ns->task_node[peer_task[i]] * R + me;
+        long po, pl;
+        task_lines(ns, count, peer_task[i] / Gn * Gn, peer_task[i] / Gn * Gn + Gn, &a, &b);
+        clip(a, b, off, off + len, &po, &pl);
+        if (pl > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, gp, 1, EMAC_BUF_RECV, po * ts, pl * ts};
+        if (kl > 0)
+          ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, gp, 0, EMAC_BUF_STAGE, xslot[(size_t)pc * nx + xs + i], kl * ts};
+      }
+      if (kl > 0) {
+        emac_fold *f = &folds[nf++];
+        int order[EMAC_MAX_NODES], n = 0;
+        /* leaf order: -1 = own, i = column peer i */
+        if (last) {
+          order[n++] = rad - 2;
+          order[n++] = -1;
+          for (i = 0; i < rad - 2; i++) order[n++] = i;
+        } else if (st == 0) {
+          order[n++] = 0;
+          order[n++] = -1;
+          for (i = 1; i < rad - 1; i++) order[n++] = i;
+        } else {
+          order[n++] = -1;
+          for (i = 0; i < rad - 1; i++) order[n++] = i;
+        }
+        f->piece = pc;
+        f->offset = ko * ts;
+        f->count = kl;
+        f->nleaf = rad;
+        f->leg = EMAC_LEG_NODES_FOLD | lg;
+        for (t = 0; t < rad; t++) {
+          f->buf[t] = order[t] < 0 ? EMAC_BUF_RECV : EMAC_BUF_STAGE;
+          f->loff[t] = order[t] < 0 ? ko * ts : xslot[(size_t)pc * nx + xs + order[t]];
+        }
+      }
+      for (i = 0; i < rad - 1; i++) { /* back (run in the reverse step order): mine to it, its to me */
+        const int gp = ns->task_node[peer_task[i]] * R + me;
+        long po, pl;
+        task_lines(ns, count, peer_task[i] / Gn * Gn, peer_task[i] / Gn * Gn + Gn, &a, &b);
+        clip(a, b, off, off + len, &po, &pl);
+        if (kl > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | lg, gp, 1, EMAC_BUF_RECV, ko * ts, kl * ts};
+        if (pl > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | lg, gp, 0, EMAC_BUF_RECV, po * ts, pl * ts};
+      }
+    }
+  }
   free(slot0);
   free(stride);
   free(xslot);

@@ -117,8 +117,26 @@ enum {
   EMAC_LEG_NODES_FOLD = 64,
   EMAC_LEG_NODES_AG = 128
 };
-#define EMAC_MAX_NODES 16    /* a power of two: one radix-2 step per factor */
-#define EMAC_LEG_STEP_SHIFT 8 /* node-pair legs and folds carry their step: leg | step << 8 */
+#define EMAC_MAX_NODES 16
+#define EMAC_MAX_NODE_STEPS 4 /* inter-node reduce-scatter steps */
+#define EMAC_LEG_STEP_SHIFT 8 /* node legs and folds carry their step: leg | step << 8 */
+
+/* The inter-node schedule of several nodes (src/core/allreduce_recursive.c:222-453, the
+   EXT_MPI_NUM_PORTS list): reduce-scatter steps of radix |port| + 1 over the tasks, the tasks
+   being the nodes in the order ext_mpi_rank_order gives them over the allgather radices
+   (ext_mpi_native.c:879-912, rank_permutation.c:89-228). */
+typedef struct {
+  int nodes;
+  int nsteps;                     /* reduce-scatter steps between the nodes */
+  int radix[EMAC_MAX_NODE_STEPS]; /* their radices, first step first */
+  int task_node[EMAC_MAX_NODES];  /* task -> node */
+  int node_task[EMAC_MAX_NODES];  /* node -> task */
+} emac_node_sched;
+/* `ports`: the reference's list (0-terminated: every reduce-scatter port, negative, then every
+   allgather port, positive; the radices of each part multiply to `nodes`), or NULL for the
+   default: one port per step ("-1 ... 1 ...") when `nodes` is a power of two, else one step of
+   radix `nodes`. 0 or EMAC_ERR_ARG / EMAC_ERR_UNSUPPORTED. */
+int emac_node_sched_build(emac_node_sched *s, int nodes, const int *ports);
 
 typedef struct {
   int leg;     /* EMAC_LEG_RS or EMAC_LEG_AG */
@@ -135,8 +153,8 @@ typedef struct {
   long count;                    /* elements */
   int buf[EMAC_MAX_RANKS];       /* per leaf (plan leaf order): EMAC_BUF_SEND, _RECV or _STAGE */
   long loff[EMAC_MAX_RANKS];     /* per leaf: byte offset of the first element */
-  int nleaf;                     /* the node's R, or 2 for the two nodes' partials */
-  int leg;                       /* EMAC_LEG_FOLD or EMAC_LEG_NODES_FOLD */
+  int nleaf;                     /* the node's R, or a node step's radix */
+  int leg;                       /* EMAC_LEG_FOLD or EMAC_LEG_NODES_FOLD | step << 8 */
 } emac_fold;
 
 /* Program of node rank `me`: ops (reduce-scatter ops first, then allgather ops), one fold per
@@ -144,17 +162,19 @@ typedef struct {
    so they share the 16-byte phase of the send buffer. Caller frees *ops and *folds. */
 int emac_comm_program(const emac_plan *p, int me, long send_phase, emac_p2p **ops, int *nops, emac_fold **folds,
                       int *nfolds, long *staging_bytes);
-/* The same for rank `me` of node `node` out of `nodes` (a power of two, 1..16) nodes of p->nranks
-   ranks each (global rank = node * p->nranks + me, the peers in *ops are global ranks). One port
-   per step (EXT_MPI_NUM_PORTS "-1 ... 1 ...", src/core/allreduce_recursive.c:222-453 as
-   ext_mpi_native.c:879-960 composes it): after the node's reduce-scatter and fold each owner
-   chunk holds the node's partial; at step st the owners of the same chunk on nodes n and
-   n ^ 2^st (same rank in their node) swap halves of their current range (NODES_RS | st << 8),
-   fold the half they keep -- own partial, then the partner's: one two-operand reduction --
-   (NODES_FOLD | st << 8), and after the last step the finished ranges are swapped back in the
-   reverse step order (NODES_AG | st << 8); the node's allgather then distributes the chunk. */
-int emac_comm_program_nodes(const emac_plan *p, int nodes, int node, int me, long send_phase, emac_p2p **ops,
-                            int *nops, emac_fold **folds, int *nfolds, long *staging_bytes);
+/* The same for rank `me` of node `node` under the inter-node schedule `ns` (NULL: one node), nodes
+   of p->nranks ranks each (global rank = node * p->nranks + me, the peers in *ops are global
+   ranks), as ext_mpi_native.c:879-1000 composes it: after the node's reduce-scatter and fold
+   each owner chunk holds the node's partial of its elements; the message is cut into one line per
+   node (ext_mpi_native.c:768-786), laid out in task order; at step st every task keeps the lines
+   of its sub-group, sends each other sub-group's lines to the task of the same column there and
+   receives its own lines' partials from those (NODES_RS | st << 8, only the part inside this
+   rank's chunk: the same rank of each node carries it), folds them in the order raw_code.c:
+   270-340 replays allreduce_core's reducefrom lists (NODES_FOLD | st << 8), and after the last
+   step the finished lines go back in the reverse step order (NODES_AG | st << 8); the node's
+   allgather then distributes the chunk. */
+int emac_comm_program_nodes(const emac_plan *p, const emac_node_sched *ns, int node, int me, long send_phase,
+                            emac_p2p **ops, int *nops, emac_fold **folds, int *nfolds, long *staging_bytes);
 
 /* Build the plan of an nranks-rank Allreduce of `count` elements. 0 or an EMAC_ERR_* code. */
 int emac_plan_build(emac_plan *p, int nranks, long count, int dtype, int op, const emac_copyin *cfg);

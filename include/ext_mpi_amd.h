@@ -120,10 +120,10 @@ int ext_mpi_amd_set_stream(int handle, void *hip_stream);
 #define EXT_MPI_AMD_LEG_ALLGATHER 8      /* COMM form: owned chunk to every peer (reduce_copyout) */
 #define EXT_MPI_AMD_LEG_STAGE_OUT 16     /* D2H of host receive buffers */
 #define EXT_MPI_AMD_LEG_STAGE 17         /* both staging copies */
-/* COMM form over 2^k nodes (ext_mpi_amd_comm_set_nodes), between the fold and the allgather: */
-#define EXT_MPI_AMD_LEG_NODES_RS 32      /* per step: owned range's halves swapped with the partner node's owner */
-#define EXT_MPI_AMD_LEG_NODES_FOLD 64    /* per step: kept half = this node's partial + the partner's */
-#define EXT_MPI_AMD_LEG_NODES_AG 128     /* finished ranges swapped back, last step first */
+/* COMM form over several nodes (ext_mpi_amd_comm_set_node_ports), between the fold and the allgather: */
+#define EXT_MPI_AMD_LEG_NODES_RS 32      /* per step: lines traded with the column peers of the other nodes */
+#define EXT_MPI_AMD_LEG_NODES_FOLD 64    /* per step: the kept lines' partials folded */
+#define EXT_MPI_AMD_LEG_NODES_AG 128     /* finished lines sent back, last step first */
 #define EXT_MPI_AMD_LEG_ALL 255
 /* legs | EXT_MPI_AMD_LEG_STEP(s): the node legs of step s alone (a testing transport driving the
    steps in lock-step); without it every step runs, in order */
@@ -154,27 +154,37 @@ typedef struct {
   long count;  /* elements */
   int buf[EXT_MPI_AMD_MAX_RANKS];
   long leaf_offset[EXT_MPI_AMD_MAX_RANKS];
-  int nleaf; /* leaves used: nranks (the node's fold) or 2 (two nodes' partials) */
+  int nleaf; /* leaves used: nranks (the node's fold) or a node step's radix */
   int leg;   /* EXT_MPI_AMD_LEG_FOLD, or EXT_MPI_AMD_LEG_NODES_FOLD | step << 8 */
 } ext_mpi_amd_fold;
 int ext_mpi_amd_comm_program(int nranks, int rank, long count, int dtype, const char *copyin, long send_phase,
                              ext_mpi_amd_p2p *ops, int max_ops, int *nops, ext_mpi_amd_fold *folds, int max_folds,
                              int *nfolds, long *staging_bytes);
-/* The same for `nodes` (a power of two, 1..16) nodes of ranks_per_node ranks; `rank` is global
-   (node-major); node legs and folds carry their step in leg >> 8. */
+/* The same for `nodes` (1..16) nodes of ranks_per_node ranks under the inter-node ports `ports`
+   (as ext_mpi_amd_comm_set_node_ports); `rank` is global (node-major); node legs and folds carry
+   their step in leg >> 8. _nodes: the one-port schedule of a power of two. */
+int ext_mpi_amd_comm_program_node_ports(int nodes, const int *ports, int ranks_per_node, int rank, long count,
+                                        int dtype, const char *copyin, long send_phase, ext_mpi_amd_p2p *ops,
+                                        int max_ops, int *nops, ext_mpi_amd_fold *folds, int max_folds, int *nfolds,
+                                        long *staging_bytes);
 int ext_mpi_amd_comm_program_nodes(int nodes, int ranks_per_node, int rank, long count, int dtype, const char *copyin,
                                    long send_phase, ext_mpi_amd_p2p *ops, int max_ops, int *nops,
                                    ext_mpi_amd_fold *folds, int max_folds, int *nfolds, long *staging_bytes);
 
-/* ---- several nodes (§8f row 3, the inter-node ports schedule, one port per step) ----
+/* ---- several nodes (§8f row 3, the inter-node ports schedule) ----
  * The reference runs an Allreduce over several nodes as: the node's copy-in (the same
  * reduce_copies_* emission as one node, into shared memory), the inter-node algorithm of
- * src/core/allreduce_recursive.c:222-453 over the node partials (EXT_MPI_NUM_PORTS, here one
- * port per step: "-1 ... 1 ..."), the node's copy-out (src/mpi/ext_mpi_native.c:879-1000). On an
- * RCCL (or loopback) communicator whose ranks [n * size/nodes, (n + 1) * size/nodes) form node n,
- * nodes a power of two up to 16, set before ext_mpi_amd_allreduce_init; copyin then describes
- * ONE node (its ranks_per_node positions). Peer-mapped communicators are single-node
- * (EXT_MPI_AMD_ERROR_UNSUPPORTED). */
+ * src/core/allreduce_recursive.c:222-453 over the node partials (EXT_MPI_NUM_PORTS), the node's
+ * copy-out (src/mpi/ext_mpi_native.c:879-1000). On an RCCL (or loopback) communicator whose ranks
+ * [n * size/nodes, (n + 1) * size/nodes) form node n, nodes <= 16, set before
+ * ext_mpi_amd_allreduce_init; copyin then describes ONE node (its ranks_per_node positions).
+ * `ports` is the reference's num_ports list, 0-terminated: the reduce-scatter ports (negative,
+ * radix |p| + 1 each), then the allgather ports (positive), each part's radices multiplying to
+ * `nodes` -- e.g. {-1, -1, 1, 1, 0} for 4 nodes, one port per step; {-2, 2, 0} for 3 nodes;
+ * NULL: one port per step for a power of two, else one step of radix `nodes`. _set_nodes: the
+ * one-port schedule of a power of two. Peer-mapped communicators are single-node
+ * (EXT_MPI_AMD_ERROR_UNSUPPORTED), as are lists without reduce-scatter ports or ending in one. */
+int ext_mpi_amd_comm_set_node_ports(int comm, int nodes, const int *ports);
 int ext_mpi_amd_comm_set_nodes(int comm, int nodes);
 
 /* EXT_MPI_NUM_SOCKETS_PER_NODE (src/mpi/ext_mpi.c:43-187, a process-wide parameter): sockets per

@@ -86,6 +86,10 @@ def lib():
         _lib.ref_emulate_nodes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                                            ctypes.POINTER(ctypes.c_void_p)]
+        _lib.ref_emulate_node_ports.restype = ctypes.c_int
+        _lib.ref_emulate_node_ports.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_long,
+                                                ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                                ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p)]
         _lib.ref_get_rank_cyclic.restype = ctypes.c_int
         _lib.ref_get_rank_cyclic.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int,
                                              ctypes.c_int]
@@ -159,17 +163,23 @@ def allreduce(sends, copyin, in_place=False, op=SUM, num_sockets=1):
     return recvs
 
 
-def allreduce_nodes(sends, copyin, nodes=2, in_place=False, op=SUM, num_sockets=1):
-    """Reference result over `nodes` (1 or 2) nodes of len(sends) // nodes ranks each (node-major):
-    each node's copy-in, the node partials reduced once per element (one port), the copy-out."""
+def allreduce_nodes(sends, copyin, nodes=2, in_place=False, op=SUM, num_sockets=1, ports=None):
+    """Reference result over `nodes` nodes of len(sends) // nodes ranks each (node-major): each
+    node's copy-in, allreduce_core over the node partials under `ports` (the EXT_MPI_NUM_PORTS
+    list, e.g. [-2, 2] for 3 nodes; None: one port per step, 2^k nodes), the copy-out."""
     W = len(sends)
     a0 = np.ascontiguousarray(sends[0])
     code = {np.dtype(np.float64): DOUBLE, np.dtype(np.int64): LONG, np.dtype(np.float32): FLOAT,
             np.dtype(np.int32): INT}[a0.dtype]
     sends = [np.ascontiguousarray(s) for s in sends]
     recvs = [s.copy() for s in sends] if in_place else [np.full_like(s, -1) for s in sends]
-    rc = lib().ref_emulate_nodes(nodes, W // nodes, a0.size, code, op, copyin.encode(), int(in_place), num_sockets,
-                                 _ptrs(sends), _ptrs(recvs))
+    if ports is None:
+        rc = lib().ref_emulate_nodes(nodes, W // nodes, a0.size, code, op, copyin.encode(), int(in_place),
+                                     num_sockets, _ptrs(sends), _ptrs(recvs))
+    else:
+        pl = (ctypes.c_int * (len(ports) + 1))(*ports, 0)
+        rc = lib().ref_emulate_node_ports(nodes, pl, W // nodes, a0.size, code, op, copyin.encode(), int(in_place),
+                                          num_sockets, _ptrs(sends), _ptrs(recvs))
     if rc != 0:
         raise ValueError(f"oracle rejected copyin {copyin!r} for {nodes} x {W // nodes}")
     return recvs

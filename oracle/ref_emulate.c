@@ -93,34 +93,127 @@ done:
   return rc;
 }
 
-/* Several nodes, one port per step (EXT_MPI_NUM_PORTS "-1 1", "-1 -1 1 1", ...). ext_mpi_native.c:879-1000 composes: the node's
-   copy-in -- reduce_copies_one_socket with in_out = 1 and one_node = 0 (reduce_copyin.c:1497-1500):
-   the same reduce-scatter emission as one node, into shared memory -- then the inter-node
-   algorithm of allreduce_recursive.c:222-453 over the node partials: with one port a single
-   radix-2 step, each line reduced from the two nodes' partials of it (:248-347, reducefrom of the
-   own line and the line received from the partner node), the lines exchanged back (:406-437), then
-   the node's copy-out. Every element thus ends as ONE two-operand reduction of the two node
-   partials; a two-operand SUM is commutative, so which partial is the accumulator changes no bit
-   (MIN / MAX with NaNs or signed zeros would depend on it: node 0's partial is taken first here,
-   parity for those inputs is unpinned). Ranks [0, R) are node 0, [R, 2R) node 1. */
-int ref_emulate_nodes(int nodes, int R, long count, int dtype, int red, const char *copyin, int in_place,
-                      int num_sockets, void *const *sendbufs, void *const *recvbufs) {
-  int n, r, b, rc;
-  const size_t bytes = (size_t)count * (size_t)ref_type_size(dtype);
-  if (nodes < 1 || nodes > 16 || (nodes & (nodes - 1)) || R < 1 || ref_type_size(dtype) <= 0) return -1;
+/* Several nodes (EXT_MPI_NUM_PORTS "N(-p0 -p1 ... q0 q1 ...)"). ext_mpi_native.c:879-1000 composes:
+   the node's copy-in -- reduce_copies_one_socket with in_out = 1 and one_node = 0
+   (reduce_copyin.c:1497-1500): the same reduce-scatter emission as one node, into shared memory --
+   then the inter-node algorithm of allreduce_recursive.c:222-453 (allreduce_core) over the node
+   partials, then the node's copy-out. Restated here as the reference runs it, task by task:
+   * the message is cut into one line per node (ext_mpi_native.c:768-786: count / N elements, the
+     remainder to the low nodes), the algorithm runs on tasks = the nodes in ext_mpi_rank_order
+     over the allgather radices (ext_mpi_native.c:879-912; rank_permutation.c:89-228 maps node n
+     to task t with ranks[t] = n, and each task's line t back to node ranks[t]'s line size), and
+     raw_code.c:238-356 lays the lines out in task order (line k at the sizes of lines 0..k-1);
+   * reduce-scatter step s (ports[s] < 0, radix p + 1 = |ports[s]| + 1) splits each group of G
+     tasks into p + 1 sub-groups of Gn = G / (p + 1); every task keeps the lines of its sub-group,
+     receiving from its column peers i = 0..p-1, (t + Gn (i + 1)) mod G in the group (:248-316),
+     their partial of them, and reduces them in the order raw_code.c:270-340 replays the
+     reducefrom lists: the first step (not the last) r_0 (received into line 2lb) += own,
+     += r_1 .. r_{p-1}; a middle step own (2lb) += r_0 .. r_{p-1}; the last step r_{p-1}
+     (received into lb) += own, += r_0 .. r_{p-2};
+   * the allgather steps (:347-437) copy the finished lines back: every rank ends with line k as
+     task k computed it.
+   Only lists whose reduce-scatter part covers every node are restated (the allgather steps then
+   copy); one ending in a reduce-scatter port, or reducing inside the allgather steps, is refused.
+   Ranks [n R, (n + 1) R) are node n. */
+int ref_emulate_node_ports(int nodes, const int *ports, int R, long count, int dtype, int red, const char *copyin,
+                           int in_place, int num_sockets, void *const *sendbufs, void *const *recvbufs) {
+  const int ts = ref_type_size(dtype);
+  int rad[8], ag[8], nrs = 0, nag = 0, task_node[16], n, r, t, k, s, i, G, rc = 0, prod_rs = 1, prod_ag = 1;
+  long lo[17];
+  char **cur = NULL, **nxt = NULL;
+  const size_t bytes = (size_t)count * (size_t)ts;
+  if (nodes < 1 || nodes > 16 || R < 1 || ts <= 0) return -1;
   for (n = 0; n < nodes; n++)
     if ((rc = ref_emulate_op_s(R, count, dtype, red, copyin, in_place, num_sockets, sendbufs + n * R, recvbufs + n * R)))
       return rc;
-  /* 2^k nodes: k radix-2 steps. allreduce_core pairs task t with t ^ 2^(k-1-s) at step s
-     (:261-284, highest bit first), and ext_mpi_native.c:879-912 runs it on tasks permuted by
-     ext_mpi_rank_order over the factors (2, ..., 2) -- a bit reversal, task t = node bitrev(t)
-     (rank_permutation.c:133-139, :176-200) -- so in node order step s pairs n with n ^ 2^s: the
-     partials combine as a balanced pairwise tree, lowest node bit first, each combination one
-     two-operand reduction (node n's partial first here; commutative for SUM) */
-  for (b = 1; b < nodes; b <<= 1)
-    for (n = 0; n < nodes; n += 2 * b) ref_reduction_op(red, dtype, recvbufs[n * R], recvbufs[(n + b) * R], count);
-  for (r = 1; r < nodes * R; r++) memcpy(recvbufs[r], recvbufs[0], bytes);
-  return 0;
+  if (nodes == 1) return 0;
+  for (i = 0; ports[i] < 0; i++) {
+    if (nrs == 8) return -1;
+    rad[nrs++] = 1 - ports[i];
+    prod_rs *= 1 - ports[i];
+  }
+  for (; ports[i] > 0; i++) {
+    if (nag == 8) return -1;
+    ag[nag++] = ports[i] + 1;
+    prod_ag *= ports[i] + 1;
+  }
+  if (ports[i] || !nrs || !nag || prod_rs != nodes || prod_ag != nodes) return -1;
+  for (t = 0; t < nodes; t++) task_node[t] = t;
+  ref_rank_order(nodes, nag, ag, task_node);
+  lo[0] = 0;
+  for (k = 0; k < nodes; k++) {
+    const int m = task_node[k];
+    lo[k + 1] = lo[k] + count / nodes + (m < count % nodes);
+  }
+  cur = (char **)calloc((size_t)nodes, sizeof(char *));
+  nxt = (char **)calloc((size_t)nodes, sizeof(char *));
+  if (!cur || !nxt) {
+    rc = -1;
+    goto out;
+  }
+  for (t = 0; t < nodes; t++) {
+    cur[t] = (char *)malloc(bytes ? bytes : 1);
+    nxt[t] = (char *)malloc(bytes ? bytes : 1);
+    if (!cur[t] || !nxt[t]) {
+      rc = -1;
+      goto out;
+    }
+    memcpy(cur[t], recvbufs[task_node[t] * R], bytes); /* task t's node partial */
+  }
+  for (G = nodes, s = 0; s < nrs; G /= rad[s], s++) {
+    const int p = rad[s] - 1, Gn = G / rad[s], last = s == nrs - 1;
+    for (t = 0; t < nodes; t++) {
+      int peer[16];
+      const long a = lo[t / Gn * Gn], b = lo[t / Gn * Gn + Gn];
+      char *acc = nxt[t] + a * ts;
+      const long len = b - a;
+      for (i = 0; i < p; i++) peer[i] = (t + Gn * (i + 1)) % G + t / G * G;
+      if (len <= 0) continue;
+      if (last) {
+        memcpy(acc, cur[peer[p - 1]] + a * ts, (size_t)(len * ts));
+        ref_reduction_op(red, dtype, acc, cur[t] + a * ts, len);
+        for (i = 0; i < p - 1; i++) ref_reduction_op(red, dtype, acc, cur[peer[i]] + a * ts, len);
+      } else if (s == 0) {
+        memcpy(acc, cur[peer[0]] + a * ts, (size_t)(len * ts));
+        ref_reduction_op(red, dtype, acc, cur[t] + a * ts, len);
+        for (i = 1; i < p; i++) ref_reduction_op(red, dtype, acc, cur[peer[i]] + a * ts, len);
+      } else {
+        memcpy(acc, cur[t] + a * ts, (size_t)(len * ts));
+        for (i = 0; i < p; i++) ref_reduction_op(red, dtype, acc, cur[peer[i]] + a * ts, len);
+      }
+    }
+    for (t = 0; t < nodes; t++) { /* the kept lines move on; the rest is dead */
+      char *x = cur[t];
+      cur[t] = nxt[t];
+      nxt[t] = x;
+    }
+  }
+  /* the allgather steps: line k as task k finished it, to every rank */
+  for (r = 0; r < nodes * R; r++)
+    for (k = 0; k < nodes; k++)
+      if (lo[k + 1] > lo[k]) memcpy((char *)recvbufs[r] + lo[k] * ts, cur[k] + lo[k] * ts, (size_t)((lo[k + 1] - lo[k]) * ts));
+out:
+  for (t = 0; t < nodes && cur && nxt; t++) {
+    free(cur[t]);
+    free(nxt[t]);
+  }
+  free(cur);
+  free(nxt);
+  return rc;
+}
+
+/* one port per step over 2^k nodes ("-1 ... -1 1 ... 1") */
+int ref_emulate_nodes(int nodes, int R, long count, int dtype, int red, const char *copyin, int in_place,
+                      int num_sockets, void *const *sendbufs, void *const *recvbufs) {
+  int ports[17], k = 0, i;
+  if (nodes < 1 || nodes > 16 || (nodes & (nodes - 1))) return -1;
+  while ((1 << k) < nodes) k++;
+  for (i = 0; i < k; i++) {
+    ports[i] = -1;
+    ports[k + i] = 1;
+  }
+  ports[2 * k] = 0;
+  return ref_emulate_node_ports(nodes, ports, R, count, dtype, red, copyin, in_place, num_sockets, sendbufs, recvbufs);
 }
 
 /* debug_persistent.c:491-497 (host pattern, add = 73) and :426-432 (device pattern, add = 0) */

@@ -21,7 +21,7 @@
  *   src/mpi/ext_mpi_native_exec.c:21-84      node barriers (as phases)     -> ref_emulate.c
  *   src/mpi/debug_persistent.c:426-497       known-answer input pattern    -> ref_emulate.c
  *   src/mpi/ext_mpi_native.c:879-1000,
- *   src/core/allreduce_recursive.c:222-453   two nodes, one port           -> ref_emulate.c
+ *   src/core/allreduce_recursive.c:222-453   several nodes (ports)         -> ref_emulate.c
  *
  * Parity pinning: the reference's own known-answer test pattern (debug_persistent.c) and the
  * method-6 schedules captured from the reference generators, both
@@ -104,9 +104,13 @@ int ref_emulate_op(int R, long count, int dtype, int op, const char *copyin, int
 int ref_emulate_op_s(int R, long count, int dtype, int op, const char *copyin, int in_place, int num_sockets,
                      void *const *sendbufs, void *const *recvbufs);
 
-/* nodes (a power of two, <= 16) nodes of R ranks, one port per step (src/mpi/ext_mpi_native.c:879-1000
-   with src/core/allreduce_recursive.c:222-453 and rank_permutation.c): each node's copy-in, the node
-   partials combined pairwise (lowest node bit first), the copy-out. nodes * R buffers, node-major. */
+/* nodes (<= 16) nodes of R ranks under the inter-node ports list `ports` (0-terminated, the
+   reference's EXT_MPI_NUM_PORTS: reduce-scatter ports, negative, then allgather ports;
+   src/mpi/ext_mpi_native.c:879-1000 with src/core/allreduce_recursive.c:222-453, raw_code.c and
+   rank_permutation.c): each node's copy-in, allreduce_core over the node partials task by task,
+   the copy-out. nodes * R buffers, node-major. ref_emulate_nodes: one port per step, 2^k nodes. */
+int ref_emulate_node_ports(int nodes, const int *ports, int R, long count, int dtype, int red, const char *copyin,
+                           int in_place, int num_sockets, void *const *sendbufs, void *const *recvbufs);
 int ref_emulate_nodes(int nodes, int R, long count, int dtype, int red, const char *copyin, int in_place,
                       int num_sockets, void *const *sendbufs, void *const *recvbufs);
 

@@ -90,7 +90,7 @@ def test_comm_program_over_gloo(world, cases):
     assert [f for r in results for f in r] == []
 
 
-def _nodes_worker(rank, world, port, cases, q, nodes=2):
+def _nodes_worker(rank, world, port, cases, q, nodes=2, ports=None):
     """`nodes` nodes of world // nodes ranks: the node legs, per step the node-pair legs and
     their fold, the exchanges back in reverse step order"""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -98,13 +98,13 @@ def _nodes_worker(rank, world, port, cases, q, nodes=2):
     from oracle import oracle
     failures = []
     R = world // nodes
-    k = (nodes - 1).bit_length()
+    k = (nodes - 1).bit_length() if ports is None else sum(1 for p in ports if p < 0)
     SH = emac.LEG_STEP_SHIFT
     for code, count, copyin in cases:
         sends = xorshift_inputs(world, count, code, seed_base=0x2A0DE000 + count)
         dt = NP[code]
         itemsize = np.dtype(dt).itemsize
-        ops, folds, stage = emac.comm_program_nodes(nodes, R, rank, count, code, copyin)
+        ops, folds, stage = emac.comm_program_nodes(nodes, R, rank, count, code, copyin, ports=ports)
         bufs = {emac.BUF_SEND: sends[rank].view(np.uint8).copy(),
                 emac.BUF_RECV: np.full(count * itemsize, 0xAB, dtype=np.uint8),
                 emac.BUF_STAGE: np.zeros(max(stage, 1), dtype=np.uint8)}
@@ -116,15 +116,16 @@ def _nodes_worker(rank, world, port, cases, q, nodes=2):
             for off, n, leaves, leg in folds:
                 if leg != emac.LEG_NODES_FOLD | st << SH:
                     continue
-                (b0, o0), (b1, o1) = leaves
-                x0 = bufs[b0][o0:o0 + n * itemsize].view(dt)
-                x1 = bufs[b1][o1:o1 + n * itemsize].view(dt)
+                xs = [bufs[b][o:o + n * itemsize].view(dt).copy() for b, o in leaves]
+                acc = xs[0]
                 with np.errstate(over="ignore"):
-                    bufs[emac.BUF_RECV][off:off + n * itemsize].view(dt)[:] = x0 + x1
+                    for x in xs[1:]:  # a left fold in the listed order
+                        acc = acc + x
+                bufs[emac.BUF_RECV][off:off + n * itemsize].view(dt)[:] = acc
         for st in reversed(range(k)):
             _run_leg(ops, emac.LEG_NODES_AG | st << SH, bufs)
         _run_leg(ops, LEG_AG, bufs)
-        want = oracle.allreduce_nodes(sends, copyin, nodes)[rank]
+        want = oracle.allreduce_nodes(sends, copyin, nodes, ports=ports)[rank]
         if not np.array_equal(bufs[emac.BUF_RECV], want.view(np.uint8)):
             failures.append((rank, code, count, copyin))
     q.put(failures)
@@ -184,7 +185,8 @@ def test_two_node_program_shape():
     assert len(node_folds) == 1
     off, n, leaves, _ = node_folds[0]
     assert (off, n) == ((1000 + 500) * 4, 500)  # node 1 finishes the second half of chunk 1
-    assert leaves[0] == (emac.BUF_RECV, off) and leaves[1][0] == emac.BUF_STAGE
+    # raw_code.c's accumulator at the last step: the partner's partial (received), then the own
+    assert leaves[1] == (emac.BUF_RECV, off) and leaves[0][0] == emac.BUF_STAGE
 
 
 def test_comm_program_shape():
@@ -237,3 +239,28 @@ def test_ipc_bootstrap_over_gloo_without_gpu(world):
     assert all(p.exitcode == 0 for p in procs)
     assert [r[1] for r in results] == [-5] * world
     assert len({tuple(r[2]) for r in results}) == 1 and results[0][2]  # same exchanges on every rank
+
+
+@pytest.mark.parametrize("world,nodes,ports,cases", [
+    (3, 3, [-2, 2], [(emac.FLOAT, 100003, "6;1 -1 1"), (emac.DOUBLE, 7, "6;1 -1 1"), (emac.FLOAT, 2, "6;1 -1 1")]),
+    (6, 3, [-2, 2], [(emac.FLOAT, 65539, "6;1 -2 2"), (emac.INT, 4099, "6;3 -2 2"), (emac.DOUBLE, 1001, "7;1 -2 2")]),
+    (4, 4, [-3, 3], [(emac.FLOAT, 30011, "6;1 -1 1"), (emac.LONG, 999, "6;1 -1 1")]),
+    (6, 6, [-1, -2, 2, 1], [(emac.FLOAT, 40009, "6;1 -1 1"), (emac.DOUBLE, 6007, "6;1 -1 1")]),
+    (8, 8, [-3, -1, 1, 3], [(emac.FLOAT, 40009, "6;1 -1 1")]),
+    (8, 4, [-1, -1, 1, 1], [(emac.FLOAT, 20011, "6;1 -2 2")]),
+])
+def test_node_ports_program_over_gloo(world, nodes, ports, cases):
+    """Several ports per step (EXT_MPI_NUM_PORTS "N(-p ... p ...)", radix-3/4 node steps, mixed
+    radices): the program of emac_comm_program_nodes over gloo equals the oracle's task-by-task
+    restatement of allreduce_core bitwise."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30100 + world * 7 + nodes * 3 + len(ports) + os.getpid() % 200
+    procs = [ctx.Process(target=_nodes_worker, args=(r, world, port, cases, q, nodes, ports)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert [f for r in results for f in r] == []

@@ -363,16 +363,18 @@ def test_fold_handle_and_copy_reduce(code, nsrc, ndst):
             assert np.array_equal(d.cpu().numpy().view(np.uint8), want.view(np.uint8)), (how, nsrc, ndst)
 
 
-def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=None, op=emac.SUM, repeats=1, nodes=1):
+def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=None, op=emac.SUM, repeats=1, nodes=1,
+                      ports=None):
     """COMM form (one rank per communicator) on the in-process loopback transport: the legs run
     on every rank in lock-step -- stage-in, reduce-scatter, fold, [the two-node legs,] all-gather,
     stage-out -- so the staging slots, fold buckets and leg programs of the multi-GPU path execute
-    on one GPU. nodes=2^k: consecutive blocks of R/nodes ranks are nodes (ext_mpi_amd_comm_set_nodes)."""
+    on one GPU. nodes > 1: consecutive blocks of R/nodes ranks are nodes, under the inter-node
+    ports list `ports` (ext_mpi_amd_comm_set_node_ports; None: one port per step)."""
     R, count = len(sends), sends[0].size
     comms = emac.comm_init_loopback(R)
     if nodes > 1:
         for c in comms:
-            emac.comm_set_nodes(c, nodes)
+            emac.comm_set_nodes(c, nodes, ports)
     phase = phase or [0] * R
     keep = []
     if host:
@@ -397,7 +399,7 @@ def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=Non
                 for t in rbufs:
                     t.fill_(-1)
             torch.cuda.synchronize()
-            for leg in emac.lockstep_legs(nodes):
+            for leg in emac.lockstep_legs(nodes, ports):
                 for h in hs:
                     emac.start_legs(h, leg)
                 for h in hs:
@@ -451,6 +453,37 @@ def test_comm_many_nodes_loopback_vs_oracle(oracle, R, nodes, copyin, code):
         want = oracle.allreduce_nodes(sends, copyin, nodes)
         got = run_comm_loopback(sends, code, copyin, phase=[(r * 3) % 4 for r in range(R)], nodes=nodes)
         assert_bitwise(got, want, f"{nodes} nodes R={R} {copyin} code={code} n={count}")
+
+
+@pytest.mark.parametrize("R,nodes,ports,copyin", [(3, 3, [-2, 2], "6;1 -1 1"), (6, 3, [-2, 2], "6;1 -2 2"),
+                                                   (12, 3, [-2, 2], "7;1 -2 -2 2 2"), (8, 4, [-3, 3], "6;1 -2 2"),
+                                                   (6, 6, [-1, -2, 2, 1], "6;1 -1 1"),
+                                                   (12, 6, [-2, -1, 1, 2], "5;1 -2 2"),
+                                                   (16, 8, [-3, -1, 1, 3], "6;1 -2 2"), (9, 9, [-2, -2, 2, 2], "6;1 -1 1"),
+                                                   (10, 5, [-4, 4], "6;1 -2 2")])
+@pytest.mark.parametrize("code", [emac.FLOAT, emac.DOUBLE, emac.INT])
+def test_comm_node_ports_loopback_vs_oracle(oracle, R, nodes, ports, copyin, code):
+    """Several ports per step (radix 3-5 node steps, mixed radices): every task trades its
+    sub-group's lines with its column peers and folds them in the reference's accumulator order
+    (raw_code.c over allreduce_core's reducefrom lists) -- bitwise vs the oracle's restatement."""
+    for count in (0, 5, 1031, 65536 + 7):
+        sends = xorshift_inputs(R, count, code, seed_base=0x4D0F0000 + count)
+        want = oracle.allreduce_nodes(sends, copyin, nodes, ports=ports)
+        got = run_comm_loopback(sends, code, copyin, phase=[(r * 3) % 4 for r in range(R)], nodes=nodes, ports=ports)
+        assert_bitwise(got, want, f"{nodes} nodes {ports} R={R} {copyin} code={code} n={count}")
+
+
+def test_comm_node_ports_in_place_host_min(oracle):
+    sends = xorshift_inputs(9, 100003, emac.FLOAT, seed_base=0x20DE8000)
+    want = oracle.allreduce_nodes(sends, "6;1 -3 3", 3, in_place=True, ports=[-2, 2])
+    assert_bitwise(run_comm_loopback(sends, emac.FLOAT, "6;1 -3 3", in_place=True, nodes=3, ports=[-2, 2]), want,
+                   "three nodes in place")
+    want = oracle.allreduce_nodes(sends, "6;1 -3 3", 3, ports=[-2, 2])
+    assert_bitwise(run_comm_loopback(sends, emac.FLOAT, "6;1 -3 3", host=True, nodes=3, ports=[-2, 2]), want,
+                   "three nodes host buffers")
+    want = oracle.allreduce_nodes(sends, "6;1 -3 3", 3, op=oracle.MIN, ports=[-2, 2])
+    assert_bitwise(run_comm_loopback(sends, emac.FLOAT, "6;1 -3 3", nodes=3, ports=[-2, 2], op=emac.MIN), want,
+                   "three nodes MIN")
 
 
 def test_comm_two_nodes_loopback_in_place_host_repeats(oracle):

@@ -58,22 +58,29 @@ def test_mpi_layer_single_rank_gpu(tmp_path, args):
     assert res and res[0].startswith("RESULT ok"), out
 
 
-@pytest.mark.parametrize("ports,want", [
-    (None, "RESULT no-device"),               # two logical nodes of 1: the one-port schedule
-    ("2(-1 1)", "RESULT no-device"),          # the reference's grammar (README, ports_groups.c:55-110)
-    ("2(-1,1)", "RESULT no-device"),
-    ("-1 1", "RESULT no-device"),             # a bare port list: one group of unstated size
-    ("2(-2 2)", "RESULT fail rc=-4"),         # several ports per step: not built
-    ("4(-1 -1 1 1)", "RESULT fail rc=-4"),    # a group of 4 nodes over a communicator of 2
-    ("-1 -1 1 1", "RESULT fail rc=-4"),       # two steps over 2 nodes
-    ("2(-1 1) 2(-1 1)", "RESULT fail rc=-4"),  # several groups
-    ("2(3)", "RESULT fail rc=-4"),
+@pytest.mark.parametrize("n,ports,want", [
+    (2, None, "RESULT no-device"),               # two logical nodes of 1: the one-port schedule
+    (2, "2(-1 1)", "RESULT no-device"),          # the reference's grammar (README, ports_groups.c:55-110)
+    (2, "2(-1,1)", "RESULT no-device"),
+    (2, "-1 1", "RESULT no-device"),             # a bare port list: one group of that many nodes
+    (3, "3(-2 2)", "RESULT no-device"),          # two ports, one radix-3 step
+    (3, None, "RESULT no-device"),               # 3 nodes, no list: one radix-3 step
+    (4, "4(-3 3)", "RESULT no-device"),
+    (4, "4(-1 -1 1 1)", "RESULT no-device"),
+    (2, "2(-2 2)", "RESULT fail rc=-4"),         # radix 3 over 2 nodes
+    (2, "4(-1 -1 1 1)", "RESULT fail rc=-4"),    # a group of 4 nodes over a communicator of 2
+    (2, "-1 -1 1 1", "RESULT fail rc=-4"),       # two steps over 2 nodes
+    (2, "2(-1 1) 2(-1 1)", "RESULT fail rc=-4"),  # several groups
+    (2, "2(1)", "RESULT fail rc=-4"),            # reduction inside the allgather steps: not this path
+    (4, "4(3)", "RESULT fail rc=-4"),
+    (3, "3(-1 1)", "RESULT fail rc=-4"),
 ])
-def test_mpi_logical_nodes_without_gpu(tmp_path, ports, want):
-    """EXT_MPI_NUM_TASKS_PER_SOCKET splits the ranks into logical nodes (ext_mpi.c:195-215): two of
-    them take the two-node schedule over RCCL (no device here: ERROR_DEVICE on every rank);
-    EXT_MPI_NUM_PORTS in the reference's "nodes(ports)" grammar names it, anything else (several
-    ports per step, another node count) is refused (ERROR_UNSUPPORTED) instead of computed otherwise."""
+def test_mpi_logical_nodes_without_gpu(tmp_path, n, ports, want):
+    """EXT_MPI_NUM_TASKS_PER_SOCKET splits the ranks into logical nodes (ext_mpi.c:195-215): several
+    of them take the inter-node schedule over RCCL (no device here: ERROR_DEVICE on every rank);
+    EXT_MPI_NUM_PORTS in the reference's "nodes(ports)" grammar names it, anything else (another
+    node count, several groups, reduction inside the allgather steps) is refused
+    (ERROR_UNSUPPORTED) instead of computed otherwise."""
     import torch
     if torch.cuda.is_available():
         pytest.skip("GPU present")
@@ -81,14 +88,14 @@ def test_mpi_logical_nodes_without_gpu(tmp_path, ports, want):
     env = {"EXT_MPI_NUM_TASKS_PER_SOCKET": "1"}
     if ports is not None:
         env["EXT_MPI_NUM_PORTS"] = ports
-    res, out = _run(exe, 2, [1000, "i", "dev"], env=env)
+    res, out = _run(exe, n, [1000, "i", "dev"], env=env)
     assert res and res[0].startswith(want), out
 
 
 @pytest.mark.parametrize("ports,want", [
     ("2(-1_1)", "RESULT no-device"),          # the one-port schedule over the 2 nodes: the engine
     ("-1_1", "RESULT no-device"),
-    ("2(-2_2)", "RESULT pmpi"),               # several ports per step: PMPI_Allreduce
+    ("2(-2_2)", "RESULT pmpi"),               # radix 3 over 2 nodes: PMPI_Allreduce
     ("4(-1_-1_1_1)", "RESULT pmpi"),          # another node count: PMPI_Allreduce
     ("1(-1)", "RESULT pmpi"),                 # a one-node row on a two-node communicator
 ])

@@ -312,3 +312,97 @@ def test_many_nodes_pairwise_tree(oracle):
     for out in oracle.allreduce_nodes(sends, "6;1 -2 2", 4):
         assert np.array_equal(out, want)
     assert oracle.rank_order(4, [2, 2]) == [0, 2, 1, 3]  # the node permutation behind the pairing
+
+
+def _rank_order(size, factors, ranks):
+    """ext_mpi_rank_order (reduce_copyin.c:375-394), literally."""
+    if not factors:
+        return ranks
+    f0, blk = abs(factors[0]), size // abs(factors[0])
+    new = [0] * size
+    for i in range(blk):
+        for j in range(f0):
+            new[i + j * blk] = ranks[i * f0 + j]
+    if len(factors) > 1:
+        for j in range(f0):
+            new[j * blk:(j + 1) * blk] = _rank_order(blk, factors[1:], new[j * blk:(j + 1) * blk])
+    return new
+
+
+def _allreduce_core_literal(partials, ports):
+    """Independent statement of the inter-node reduce-scatter for the oracle's check: the line
+    tables of allreduce_core's reduce-scatter loop (allreduce_recursive.c:248-347) built as the
+    reference builds them -- recvfrom node/line per slot, the reducefrom list of the output slot --
+    and replayed the way raw_code.c:221-356 executes a block: a received line is copied into its
+    slot, then the output slot accumulates its reducefrom slots in list order; tasks are the nodes
+    in ext_mpi_rank_order over the allgather factors, lines laid out in task order with node
+    ranks[k]'s size (ext_mpi_native.c:768-786, rank_permutation.c). Returns the reduced message."""
+    N, count = len(partials), partials[0].size
+    rs = [p for p in ports if p < 0]
+    ag = [p + 1 for p in ports if p > 0]
+    ranks = _rank_order(N, ag, list(range(N)))  # task -> node
+    lb = 1
+    for p in ag:
+        lb *= p
+    assert lb == N
+    sizes = [count // N + (ranks[k] < count % N) for k in range(N)]
+    lo = np.concatenate([[0], np.cumsum(sizes)]).astype(int)
+    line = lambda arr, l: arr[lo[l]:lo[l + 1]]  # noqa: E731
+    # slots[t][n] = task t's data in slot n (lines n mod lb), block 0: the own partial in 0..lb-1
+    slots = [{n: line(partials[ranks[t]], n).copy() for n in range(lb)} for t in range(N)]
+    gbstep = lb
+    for step, port in enumerate(rs):
+        p = abs(port)
+        last = step == len(rs) - 1
+        gnext = gbstep // (p + 1)
+        recv, red = [dict() for _ in range(N)], [dict() for _ in range(N)]
+        for t in range(N):
+            for ln in range(t // gbstep * gbstep, t // gbstep * gbstep + gbstep):
+                if ln // gnext == t // gnext:
+                    src = lambda i: (t + gnext * (i + 1)) % gbstep + t // gbstep * gbstep  # noqa: E731
+                    if not last:
+                        base = 3 if step > 0 else 2
+                        for i in range(p):
+                            recv[t][ln + (base + i) * lb] = (src(i), ln)
+                        red[t][ln + 2 * lb] = ([ln + (3 + i) * lb for i in range(p)] if step > 0 else
+                                               [ln] + [ln + (2 + i) * lb for i in range(1, p)])
+                    else:
+                        recv[t][ln + lb] = (src(p - 1), ln)
+                        for i in range(p - 1):
+                            recv[t][ln + (3 + i) * lb] = (src(i), ln)
+                        red[t][ln + lb] = ([ln + (2 + i) * lb for i in range(p)] if step > 0 else
+                                           [ln] + [ln + (2 + i) * lb for i in range(1, p)])
+        # the sender's copy of line `ln`: its accumulator slot of the previous block
+        held = lambda q, ln: slots[q][ln + 2 * lb] if step > 0 else slots[q][ln]  # noqa: E731
+        new = [dict(s) for s in slots]
+        for t in range(N):
+            for n, (q, ln) in recv[t].items():
+                new[t][n] = held(q, ln).copy()
+        for t in range(N):
+            for n, lst in red[t].items():
+                acc = new[t][n].copy()
+                for r in lst:
+                    acc = acc + new[t][r]
+                new[t][n] = acc
+        slots = new
+        gbstep = gnext
+    return np.concatenate([slots[k][k + lb] for k in range(N)]) if N > 1 else partials[0]
+
+
+@pytest.mark.parametrize("nodes,ports", [(2, [-1, 1]), (4, [-1, -1, 1, 1]), (3, [-2, 2]), (4, [-3, 3]),
+                                         (6, [-1, -2, 2, 1]), (6, [-2, -1, 1, 2]), (8, [-3, -1, 1, 3]),
+                                         (9, [-2, -2, 2, 2]), (8, [-1, -1, -1, 1, 1, 1]), (5, [-4, 4])])
+def test_node_ports_against_literal_line_tables(oracle, nodes, ports):
+    """The oracle's inter-node restatement (ref_emulate_node_ports) against an independent,
+    literal replay of allreduce_core's line tables: bitwise for float (association observable)."""
+    rng = np.random.default_rng(nodes * 31 + len(ports))
+    for count in (1, 7, 1000 + nodes, 4099):
+        sends = [((rng.random(count) * 2 - 1) * 10.0 ** rng.integers(-4, 5, count)).astype(np.float32)
+                 for _ in range(nodes)]
+        want = _allreduce_core_literal(sends, ports)
+        got = oracle.allreduce_nodes(sends, "6;1 -1 1", nodes, ports=ports)
+        for out in got:
+            assert np.array_equal(out, want), (nodes, ports, count)
+    if nodes == 3:  # the association differs per line: observable, so pinned by the statement
+        s = [np.float32([1e8]), np.float32([1.0]), np.float32([-1e8])]
+        assert oracle.allreduce_nodes(s, "6;1 -1 1", 3, ports=ports)[0][0] == _allreduce_core_literal(s, ports)[0]
