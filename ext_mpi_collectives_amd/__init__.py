@@ -256,23 +256,38 @@ def LEG_STEP(s):
     return (s + 1) << LEG_STEP_SHIFT
 
 
+def node_steps(nodes, ports=None):
+    """(exchange steps, copying allgather steps) of the inter-node schedule (plan.h
+    emac_node_sched): the reduce-scatter steps and the allgather steps that still reduce inside
+    the groups they leave, then the allgather steps that copy. ports None: one port per step
+    for a power of two, else one step of radix `nodes`."""
+    if nodes <= 1:
+        return 0, 0
+    if ports is None:
+        k = (nodes - 1).bit_length()
+        ports = [-1] * k + [1] * k if 1 << k == nodes else [-(nodes - 1), nodes - 1]
+    rs = [1 - p for p in ports if p < 0]
+    ag = [p + 1 for p in ports if p > 0]
+    gm = nodes
+    for r in rs:
+        gm //= r
+    g, nred = 1, 0
+    while g < gm:
+        g *= ag[nred]
+        nred += 1
+    return len(rs) + nred, len(ag) - nred
+
+
 def lockstep_legs(nodes=1, ports=None):
     """The legs of one Start in the order a lock-step driver runs them on every rank: stage-in,
-    reduce-scatter, fold, per node step the line exchange and its fold, the exchanges back in
-    reverse step order, allgather, stage-out. `ports`: the inter-node list (None: one port per
-    step for a power of two, else one step)."""
-    if ports is not None:
-        k = sum(1 for p in ports if p < 0)
-    elif nodes > 1 and nodes & (nodes - 1):
-        k = 1
-    else:
-        k = max(0, (nodes - 1).bit_length())
+    reduce-scatter, fold, per node exchange step the line exchange and its fold, the copying
+    allgather steps, allgather, stage-out. `ports`: the inter-node list (see node_steps)."""
+    nx, na = node_steps(nodes, ports)
     legs = [LEG_STAGE_IN, LEG_REDUCE_SCATTER, LEG_FOLD]
-    for st in range(k):
+    for st in range(nx):
         legs += [LEG_NODES_RS | LEG_STEP(st), LEG_NODES_FOLD | LEG_STEP(st)]
-    legs += [LEG_NODES_AG | LEG_STEP(st) for st in reversed(range(k))]
+    legs += [LEG_NODES_AG | LEG_STEP(j) for j in range(na)]
     return legs + [LEG_ALLGATHER, LEG_STAGE_OUT]
-
 
 
 def start_legs(h, legs):

@@ -170,7 +170,7 @@ typedef struct {
   emac_launch pull; /* every other owner's result copied into this rank's receive buffer */
   int nodes;            /* COMM form over several nodes: the node legs run (emac_comm_program_nodes) */
   emac_node_sched ns;   /* ... under this inter-node schedule */
-  emac_launch xfold[EMAC_MAX_NODE_STEPS]; /* ... and, per step, the fold of the kept lines' partials */
+  emac_launch xfold[2 * EMAC_MAX_NODE_STEPS]; /* ... and, per exchange step, the fold of the lines' partials */
   void *graph[EXT_MPI_AMD_LEG_ALL + 1]; /* COMM form: captured legs, per subset of EXT_MPI_AMD_LEG_* */
   unsigned char graph_failed[EXT_MPI_AMD_LEG_ALL + 1];
   emac_pipe *pipe; /* pipelined host staging (NODE form), or NULL */
@@ -219,7 +219,7 @@ static void release(emac_handle *h) {
   emac_gpu_free(h->d_edges);
   emac_gpu_free(h->pull.d_buckets);
   emac_gpu_free(h->pull.d_edges);
-  for (r = 0; r < EMAC_MAX_NODE_STEPS; r++) {
+  for (r = 0; r < 2 * EMAC_MAX_NODE_STEPS; r++) {
     emac_gpu_free(h->xfold[r].d_buckets);
     emac_gpu_free(h->xfold[r].d_edges);
   }
@@ -718,6 +718,7 @@ int ext_mpi_amd_comm_mfree(int comm, void *p) {
 
 static int ipc_agree(emac_comm *cm, int ok_local);
 static char *leg_base(const emac_handle *h, int buf);
+static int node_radix(const emac_node_sched *ns, int st);
 
 /* Collective: every rank first closes its mappings of the others' memory, then all agree, and
    only then is this rank's exported memory (synchronisation block, mirror pool) freed. */
@@ -1226,14 +1227,14 @@ int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, i
     emac_fold *folds = NULL;
     int nf = 0, f;
     emac_bucket *xb = NULL;
-    int nxb[EMAC_MAX_NODE_STEPS] = {0}, st;
-    const int nsteps = h->nodes > 1 ? h->ns.nsteps : 0;
+    int nxb[2 * EMAC_MAX_NODE_STEPS] = {0}, st;
+    const int nsteps = h->nodes > 1 ? h->ns.nsteps + h->ns.nred : 0; /* exchange steps with a fold */
     if ((rc = emac_comm_program_nodes(&h->plan, h->nodes > 1 ? &h->ns : NULL, h->me / R, h->me % R,
                                       (long)((unsigned long)h->dsend[0] & 15ul), &h->ops, &h->nops, &folds, &nf,
                                       &stage_total)))
       goto fail;
     b = (emac_bucket *)calloc((size_t)nf + 1, sizeof(emac_bucket));
-    xb = (emac_bucket *)calloc(EMAC_MAX_NODE_STEPS * ((size_t)nf + 1), sizeof(emac_bucket));
+    xb = (emac_bucket *)calloc(2 * EMAC_MAX_NODE_STEPS * ((size_t)nf + 1), sizeof(emac_bucket));
     if (!b || !xb || (rc = emac_gpu_malloc(&h->staging, (size_t)(stage_total > 0 ? stage_total : 16)))) {
       free(folds);
       free(xb);
@@ -1256,7 +1257,8 @@ int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, i
     free(folds);
     for (st = 0; st < nsteps; st++)
       if (nxb[st] &&
-          (rc = upload_launch_as(h, &h->xfold[st], xb + (size_t)st * ((size_t)nf + 1), nxb[st], h->ns.radix[st], 0))) {
+          (rc = upload_launch_as(h, &h->xfold[st], xb + (size_t)st * ((size_t)nf + 1), nxb[st], node_radix(&h->ns, st),
+                                 0))) {
         free(xb);
         goto fail;
       }
@@ -1281,6 +1283,11 @@ fail:
   free(b);
   release(h);
   return rc;
+}
+
+/* radix of exchange step st: the reduce-scatter steps, then the allgather steps that reduce */
+static int node_radix(const emac_node_sched *ns, int st) {
+  return st < ns->nsteps ? ns->radix[st] : ns->red_radix[st - ns->nsteps];
 }
 
 static char *leg_base(const emac_handle *h, int buf) {
@@ -1479,24 +1486,25 @@ static int enqueue_legs(emac_handle *h, int legs) {
        them), then the exchanges back in reverse step order (emac_comm_program_nodes). A step
        selector in the legs' high bits (EXT_MPI_AMD_LEG_STEP) runs that step's legs alone. */
     int st;
-    const int nsteps = h->ns.nsteps, only = (legs >> EMAC_LEG_STEP_SHIFT) & 31;
+    const int nsteps = h->ns.nsteps + h->ns.nred, only = (legs >> EMAC_LEG_STEP_SHIFT) & 31;
     for (st = 0; st < nsteps; st++) {
       const emac_launch *X = &h->xfold[st];
+      const int rad = node_radix(&h->ns, st);
       emac_codes lin;
       memset(&lin, 0, sizeof(lin));
       lin.first[0] = 1; /* one level: a left fold */
-      lin.close[h->ns.radix[st] - 1] = 1;
+      lin.close[rad - 1] = 1;
       lin.nlev = 1;
-      lin.nleaf = h->ns.radix[st];
+      lin.nleaf = rad;
       if (only && st != only - 1) continue;
       if ((legs & EXT_MPI_AMD_LEG_NODES_RS) && (rc = run_leg(h, EMAC_LEG_NODES_RS | st << EMAC_LEG_STEP_SHIFT)))
         return rc;
       if ((legs & EXT_MPI_AMD_LEG_NODES_FOLD) && X->nb &&
-          (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->ns.radix[st], 0, X->unroll, &lin, X->d_buckets, X->nb,
+          (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, rad, 0, X->unroll, &lin, X->d_buckets, X->nb,
                               X->ntiles, X->tiles_per_bucket, X->all_full, X->d_edges, X->nedges, h->stream)))
         return rc;
     }
-    for (st = nsteps - 1; st >= 0; st--) {
+    for (st = 0; st < h->ns.nagp; st++) { /* the copying allgather steps, block growing */
       if (only && st != only - 1) continue;
       if ((legs & EXT_MPI_AMD_LEG_NODES_AG) && (rc = run_leg(h, EMAC_LEG_NODES_AG | st << EMAC_LEG_STEP_SHIFT)))
         return rc;

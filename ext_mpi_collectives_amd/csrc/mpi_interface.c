@@ -83,14 +83,14 @@ static int env_int(const char *name, int *out) {
    ext_mpi_scan_ports_groups (ports_groups.c:55-110; README: "4(-1 -1 1 1)", "1(-1)"):
    "G(p0 p1 ...)" with G the nodes of the group and p the ports of each inter-node step
    (negative: reduce-scatter, positive: allgather; radix |p| + 1). ' ', ',' and '_' separate.
-   Taken here: one group, "1(...)" (one node, no inter-node step) or the reduce-scatter ports
-   then the allgather ports, each part's radices multiplying to G (allreduce_core,
-   allreduce_recursive.c:222-453; e.g. "4(-1 -1 1 1)", "3(-2 2)", "6(-1 -2 2 1)"). A bare port
-   list (which the reference's scanner runs past the end of) is read as the ports of one group of
-   that many nodes. Returns the group's nodes and the 0-terminated list in ports[] (EMAC_PORTS_MAX
+   Taken here: one group, "1(...)" (one node, no inter-node step) or allreduce_core's list
+   (allreduce_recursive.c:222-453): the reduce-scatter ports, then the allgather ports whose
+   radices multiply to G -- "4(-1 -1 1 1)", "3(-2 2)", "6(-1 -2 2 1)", and with fewer
+   reduce-scatter steps the first allgather steps reduce: "4(3)", "4(-1 1 1)". A bare port list
+   (which the reference's scanner runs past the end of) is read as the ports of one group of that
+   many nodes. Returns the group's nodes and the 0-terminated list in ports[] (EMAC_PORTS_MAX
    entries at most), 0 for an empty string, or -1 when the string names anything else: several
-   groups, a list without reduce-scatter ports or ending in one (reduce_scatter_core / reduction
-   inside the allgather steps), radices that do not multiply to G. */
+   groups, a list ending in a reduce-scatter port (reduce_scatter_core), radices that do not fit G. */
 #define EMAC_PORTS_MAX 9
 static int parse_ports(const char *s, int *ports) {
   int groups = 0, bare = 0, nodes = 0, n = 0, in_group = 0, ok = 1, i, prs = 1, pag = 1, seen_ag = 0;
@@ -140,8 +140,10 @@ static int parse_ports(const char *s, int *ports) {
       pag *= 1 + ports[i];
     }
   }
-  if (prs == 1 || !seen_ag || prs != pag || (nodes && nodes != prs) || prs > 16) return -1;
-  return prs;
+  /* the allgather radices multiply to the nodes, the reduce-scatter ones to a divisor of it
+     (the first allgather steps then reduce inside the groups left, emac_node_sched_build) */
+  if (!seen_ag || pag > 16 || pag % prs || (nodes && nodes != pag)) return -1;
+  return pag;
 }
 
 static void read_env(void) {

@@ -381,7 +381,7 @@ int emac_comm_program(const emac_plan *p, int me, long send_phase, emac_p2p **op
 }
 
 int emac_node_sched_build(emac_node_sched *s, int nodes, const int *ports) {
-  int def[2 * EMAC_MAX_NODE_STEPS + 1], ag[EMAC_MAX_NODE_STEPS], nag = 0, i, prod_rs = 1, prod_ag = 1;
+  int def[2 * EMAC_MAX_NODE_STEPS + 1], ag[2 * EMAC_MAX_NODE_STEPS], nag = 0, i, j, g, prod_rs = 1, prod_ag = 1;
   if (!s || nodes < 1 || nodes > EMAC_MAX_NODES) return EMAC_ERR_ARG;
   memset(s, 0, sizeof(*s));
   s->nodes = nodes;
@@ -405,19 +405,31 @@ int emac_node_sched_build(emac_node_sched *s, int nodes, const int *ports) {
   }
   /* allreduce_core (allreduce_recursive.c:222-453): the reduce-scatter ports first (negative),
      then the allgather ports (positive); a list ending in a negative port is reduce_scatter_core,
-     one without reduce-scatter ports reduces inside the allgather steps -- neither is this path */
+     not this path. The reduce-scatter steps leave groups of gm = nodes / prod_rs tasks holding
+     the same lines; the allgather steps whose block is still smaller than gm reduce inside it
+     (:348-403), the others copy (:404-437). */
   for (i = 0; ports[i] < 0; i++) {
     if (s->nsteps == EMAC_MAX_NODE_STEPS) return EMAC_ERR_UNSUPPORTED;
     s->radix[s->nsteps++] = 1 - ports[i];
     prod_rs *= 1 - ports[i];
   }
   for (; ports[i] > 0; i++) {
-    if (nag == EMAC_MAX_NODE_STEPS) return EMAC_ERR_UNSUPPORTED;
+    if (nag == 2 * EMAC_MAX_NODE_STEPS) return EMAC_ERR_UNSUPPORTED;
     ag[nag++] = ports[i] + 1;
     prod_ag *= ports[i] + 1;
   }
-  if (ports[i] != 0 || !s->nsteps || !nag) return EMAC_ERR_UNSUPPORTED;
-  if (prod_rs != nodes || prod_ag != nodes) return EMAC_ERR_ARG;
+  if (ports[i] != 0 || !nag) return EMAC_ERR_UNSUPPORTED;
+  if (prod_ag != nodes || nodes % prod_rs) return EMAC_ERR_ARG;
+  s->gm = nodes / prod_rs;
+  for (j = 0, g = 1; g < s->gm; g *= ag[j], j++) {
+    if (s->nred == EMAC_MAX_NODE_STEPS) return EMAC_ERR_UNSUPPORTED;
+    s->red_radix[s->nred++] = ag[j];
+  }
+  if (g != s->gm) return EMAC_ERR_UNSUPPORTED; /* an allgather step across the group boundary */
+  for (; j < nag; j++) {
+    if (s->nagp == EMAC_MAX_NODE_STEPS) return EMAC_ERR_UNSUPPORTED;
+    s->agp_radix[s->nagp++] = ag[j];
+  }
   /* ext_mpi_native.c:879-912: ext_mpi_rank_order over the allgather radices; the algorithm runs
      on task = the position of the node in that order (rank_permutation.c:133-139) */
   position_order(nodes, nag, ag, s->task_node);
@@ -455,17 +467,20 @@ int emac_comm_program_nodes(const emac_plan *p, const emac_node_sched *ns, int n
                             emac_p2p **ops_out, int *nops_out, emac_fold **folds_out, int *nfolds_out,
                             long *staging_bytes) {
   const int K = ns ? ns->nsteps : 0, nodes = ns ? ns->nodes : 1, task = ns ? ns->node_task[node] : 0;
-  int R = p->nranks, me_pos, pc, q, t, nops = 0, nf = 0, leg, g0, st, i, nx = 0, G, Gn;
+  const int KR = ns ? ns->nred : 0, KA = ns ? ns->nagp : 0, gm = ns ? ns->gm : 1;
+  int R = p->nranks, me_pos, pc, q, t, nops = 0, nf = 0, leg, g0, st, i, nx = 0, G, Gn, j, g;
   long ts = p->tsize, total = 0, count = 0;
   long *slot0, *stride, *xslot;
   emac_p2p *ops;
   emac_fold *folds;
-  int halving = K > 0;
+  int halving = K > 0 && KR == 0;
   if (nodes < 1 || nodes > EMAC_MAX_NODES || node < 0 || node >= nodes || me < 0 || me >= R) return EMAC_ERR_ARG;
   for (st = 0; st < K; st++) {
     nx += ns->radix[st] - 1;
     halving &= ns->radix[st] == 2;
   }
+  for (j = 0; j < KR; j++) nx += ns->red_radix[j] - 1;
+  for (j = 0; j < KA; j++) nx += ns->agp_radix[j] - 1; /* (bounds the copy ops below) */
   for (pc = 0; pc < p->npieces; pc++) /* the message's elements: the pieces' chunks tile it */
     for (q = 0; q < R; q++) count += p->chunk_len[(size_t)pc * R + q];
   me_pos = p->rank_pos[me];
@@ -474,7 +489,7 @@ int emac_comm_program_nodes(const emac_plan *p, const emac_node_sched *ns, int n
   stride = (long *)malloc(sizeof(long) * (size_t)p->npieces);
   xslot = (long *)malloc(sizeof(long) * (size_t)p->npieces * (size_t)(nx > 0 ? nx : 1));
   ops = (emac_p2p *)malloc(sizeof(emac_p2p) * (size_t)(4 * p->npieces * R + 4 * nx * p->npieces + 1));
-  folds = (emac_fold *)calloc((size_t)((1 + K) * p->npieces) + 1, sizeof(emac_fold));
+  folds = (emac_fold *)calloc((size_t)((1 + K + KR) * p->npieces) + 1, sizeof(emac_fold));
   if (!slot0 || !stride || !xslot || !ops || !folds) {
     free(slot0);
     free(stride);
@@ -511,6 +526,16 @@ int emac_comm_program_nodes(const emac_plan *p, const emac_node_sched *ns, int n
         kl = hn;
       }
       for (i = 0; i < ns->radix[st] - 1; i++) {
+        total = (total + 15) / 16 * 16;
+        xslot[(size_t)pc * nx + x++] = total + ((send_phase + ko * ts) & 15);
+        total += ((kl * ts + 15) / 16) * 16 + 16;
+      }
+    }
+    for (j = 0; j < KR; j++) { /* the allgather steps that reduce: every line of the gm group */
+      long a, b, ko, kl;
+      task_lines(ns, count, task / gm * gm, task / gm * gm + gm, &a, &b);
+      clip(a, b, off, off + len, &ko, &kl);
+      for (i = 0; i < ns->red_radix[j] - 1; i++) {
         total = (total + 15) / 16 * 16;
         xslot[(size_t)pc * nx + x++] = total + ((send_phase + ko * ts) & 15);
         total += ((kl * ts + 15) / 16) * 16 + 16;
@@ -573,6 +598,7 @@ int emac_comm_program_nodes(const emac_plan *p, const emac_node_sched *ns, int n
       long lo = p->chunk_off[(size_t)pc * R + me_pos], n = p->chunk_len[(size_t)pc * R + me_pos];
       long hoff[2], hlen[2];
       const int partner = (node ^ (1 << st)) * R + me, bit = (node >> st) & 1, lg = st << EMAC_LEG_STEP_SHIFT;
+      const int la = (K - 1 - st) << EMAC_LEG_STEP_SHIFT; /* its allgather step: the reverse order */
       int s2;
       for (s2 = 0; s2 < st; s2++) { /* this step's range */
         const long h0 = (n + 1) / 2;
@@ -601,10 +627,10 @@ int emac_comm_program_nodes(const emac_plan *p, const emac_node_sched *ns, int n
         f->loff[own] = hoff[bit] * ts;
         f->buf[1 - own] = EMAC_BUF_STAGE;
         f->loff[1 - own] = xslot[(size_t)pc * nx + st];
-        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | lg, partner, 1, EMAC_BUF_RECV, hoff[bit] * ts, hlen[bit] * ts};
+        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | la, partner, 1, EMAC_BUF_RECV, hoff[bit] * ts, hlen[bit] * ts};
       }
       if (hlen[1 - bit] > 0)
-        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | lg, partner, 0, EMAC_BUF_RECV, hoff[1 - bit] * ts, hlen[1 - bit] * ts};
+        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | la, partner, 0, EMAC_BUF_RECV, hoff[1 - bit] * ts, hlen[1 - bit] * ts};
     }
   /* otherwise the lines are followed as the reference lays them out */
   for (G = nodes, st = 0; !halving && st < K; G /= ns->radix[st], st++) {
@@ -654,12 +680,70 @@ int emac_comm_program_nodes(const emac_plan *p, const emac_node_sched *ns, int n
           f->loff[t] = order[t] < 0 ? ko * ts : xslot[(size_t)pc * nx + xs + order[t]];
         }
       }
-      for (i = 0; i < rad - 1; i++) { /* back (run in the reverse step order): mine to it, its to me */
+    }
+  }
+  /* the allgather steps that still reduce (allreduce_recursive.c:348-403): while the block g of
+     an allgather radix is smaller than gm, every task sends all lines of its gm group to the
+     tasks (t + g (i + 1)) mod gnext of its block and folds what comes back, in its own order --
+     the first step of all (no reduce-scatter step before): r_0, own, r_1, ...; any later one:
+     own, r_0, ... -- so the tasks of a block may keep differently associated sums */
+  for (j = 0, g = 1; !halving && j < KR; g *= ns->red_radix[j], j++) {
+    const int rad = ns->red_radix[j], gnext = g * rad, xst = K + j, lg = xst << EMAC_LEG_STEP_SHIFT;
+    int xs = 0, s2, peer_task[EMAC_MAX_NODES];
+    for (s2 = 0; s2 < K; s2++) xs += ns->radix[s2] - 1;
+    for (s2 = 0; s2 < j; s2++) xs += ns->red_radix[s2] - 1;
+    for (i = 0; i < rad - 1; i++) peer_task[i] = (task + g * (i + 1)) % gnext + task / gnext * gnext;
+    for (pc = 0; pc < p->npieces; pc++) {
+      const long off = p->chunk_off[(size_t)pc * R + me_pos], len = p->chunk_len[(size_t)pc * R + me_pos];
+      long a, b, ho, hl;
+      task_lines(ns, count, task / gm * gm, task / gm * gm + gm, &a, &b);
+      clip(a, b, off, off + len, &ho, &hl);
+      if (hl <= 0) continue;
+      for (i = 0; i < rad - 1; i++) {
         const int gp = ns->task_node[peer_task[i]] * R + me;
+        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, gp, 1, EMAC_BUF_RECV, ho * ts, hl * ts};
+        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, gp, 0, EMAC_BUF_STAGE, xslot[(size_t)pc * nx + xs + i], hl * ts};
+      }
+      {
+        emac_fold *f = &folds[nf++];
+        int order[EMAC_MAX_NODES], n = 0;
+        if (K == 0 && j == 0) {
+          order[n++] = 0;
+          order[n++] = -1;
+          for (i = 1; i < rad - 1; i++) order[n++] = i;
+        } else {
+          order[n++] = -1;
+          for (i = 0; i < rad - 1; i++) order[n++] = i;
+        }
+        f->piece = pc;
+        f->offset = ho * ts;
+        f->count = hl;
+        f->nleaf = rad;
+        f->leg = EMAC_LEG_NODES_FOLD | lg;
+        for (t = 0; t < rad; t++) {
+          f->buf[t] = order[t] < 0 ? EMAC_BUF_RECV : EMAC_BUF_STAGE;
+          f->loff[t] = order[t] < 0 ? ho * ts : xslot[(size_t)pc * nx + xs + order[t]];
+        }
+      }
+    }
+  }
+  /* the allgather steps that copy (:404-437), block g from gm up: every task sends the lines of
+     its g-block to the tasks (t + g (i + 1)) mod gnext of its block and receives from each of
+     them the lines of its g-block -- the task at its own position there (NODES_AG | step << 8,
+     run in this order) */
+  for (j = 0, g = gm; !halving && j < KA; g *= ns->agp_radix[j], j++) {
+    const int rad = ns->agp_radix[j], gnext = g * rad, lg = j << EMAC_LEG_STEP_SHIFT;
+    for (pc = 0; pc < p->npieces; pc++) {
+      const long off = p->chunk_off[(size_t)pc * R + me_pos], len = p->chunk_len[(size_t)pc * R + me_pos];
+      long a, b, mo, ml;
+      task_lines(ns, count, task / g * g, task / g * g + g, &a, &b);
+      clip(a, b, off, off + len, &mo, &ml);
+      for (i = 0; i < rad - 1; i++) {
+        const int pt = (task + g * (i + 1)) % gnext + task / gnext * gnext, gp = ns->task_node[pt] * R + me;
         long po, pl;
-        task_lines(ns, count, peer_task[i] / Gn * Gn, peer_task[i] / Gn * Gn + Gn, &a, &b);
+        task_lines(ns, count, pt / g * g, pt / g * g + g, &a, &b);
         clip(a, b, off, off + len, &po, &pl);
-        if (kl > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | lg, gp, 1, EMAC_BUF_RECV, ko * ts, kl * ts};
+        if (ml > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | lg, gp, 1, EMAC_BUF_RECV, mo * ts, ml * ts};
         if (pl > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | lg, gp, 0, EMAC_BUF_RECV, po * ts, pl * ts};
       }
     }

@@ -127,15 +127,22 @@ enum {
    (ext_mpi_native.c:879-912, rank_permutation.c:89-228). */
 typedef struct {
   int nodes;
-  int nsteps;                     /* reduce-scatter steps between the nodes */
-  int radix[EMAC_MAX_NODE_STEPS]; /* their radices, first step first */
-  int task_node[EMAC_MAX_NODES];  /* task -> node */
-  int node_task[EMAC_MAX_NODES];  /* node -> task */
+  int nsteps;                         /* reduce-scatter steps between the nodes */
+  int radix[EMAC_MAX_NODE_STEPS];     /* their radices, first step first */
+  int gm;                             /* tasks per group holding the same lines after them */
+  int nred;                           /* allgather steps that still reduce, inside a gm group */
+  int red_radix[EMAC_MAX_NODE_STEPS]; /* their radices */
+  int nagp;                           /* allgather steps that copy */
+  int agp_radix[EMAC_MAX_NODE_STEPS]; /* their radices */
+  int task_node[EMAC_MAX_NODES];      /* task -> node */
+  int node_task[EMAC_MAX_NODES];      /* node -> task */
 } emac_node_sched;
 /* `ports`: the reference's list (0-terminated: every reduce-scatter port, negative, then every
-   allgather port, positive; the radices of each part multiply to `nodes`), or NULL for the
-   default: one port per step ("-1 ... 1 ...") when `nodes` is a power of two, else one step of
-   radix `nodes`. 0 or EMAC_ERR_ARG / EMAC_ERR_UNSUPPORTED. */
+   allgather port, positive; the allgather radices multiply to `nodes`, the reduce-scatter ones to
+   a divisor of it -- the first allgather steps then reduce inside the groups the reduce-scatter
+   leaves, e.g. "4(3)", "4(-1 1 1)"), or NULL for the default: one port per step ("-1 ... 1 ...")
+   when `nodes` is a power of two, else one step of radix `nodes`. 0 or EMAC_ERR_ARG /
+   EMAC_ERR_UNSUPPORTED. */
 int emac_node_sched_build(emac_node_sched *s, int nodes, const int *ports);
 
 typedef struct {

@@ -118,7 +118,8 @@ done:
 int ref_emulate_node_ports(int nodes, const int *ports, int R, long count, int dtype, int red, const char *copyin,
                            int in_place, int num_sockets, void *const *sendbufs, void *const *recvbufs) {
   const int ts = ref_type_size(dtype);
-  int rad[8], ag[8], nrs = 0, nag = 0, task_node[16], n, r, t, k, s, i, G, rc = 0, prod_rs = 1, prod_ag = 1;
+  int rad[8], ag[8], nrs = 0, nag = 0, task_node[16], node_task[16], n, r, t, k, s, i, j, G, g, gm, rc = 0, prod_rs = 1,
+      prod_ag = 1;
   long lo[17];
   char **cur = NULL, **nxt = NULL;
   const size_t bytes = (size_t)count * (size_t)ts;
@@ -137,9 +138,16 @@ int ref_emulate_node_ports(int nodes, const int *ports, int R, long count, int d
     ag[nag++] = ports[i] + 1;
     prod_ag *= ports[i] + 1;
   }
-  if (ports[i] || !nrs || !nag || prod_rs != nodes || prod_ag != nodes) return -1;
+  /* the reduce-scatter radices leave groups of gm = nodes / prod_rs tasks holding the same lines;
+     the allgather steps while their block is smaller than gm reduce inside it (:347-403), the rest
+     copy (:404-437) */
+  if (ports[i] || !nag || prod_ag != nodes || nodes % prod_rs) return -1;
+  gm = nodes / prod_rs;
+  for (j = 0, g = 1; g < gm; g *= ag[j], j++);
+  if (g != gm) return -1; /* an allgather step straddling gm: not restated */
   for (t = 0; t < nodes; t++) task_node[t] = t;
   ref_rank_order(nodes, nag, ag, task_node);
+  for (t = 0; t < nodes; t++) node_task[task_node[t]] = t;
   lo[0] = 0;
   for (k = 0; k < nodes; k++) {
     const int m = task_node[k];
@@ -188,10 +196,52 @@ int ref_emulate_node_ports(int nodes, const int *ports, int R, long count, int d
       nxt[t] = x;
     }
   }
-  /* the allgather steps: line k as task k finished it, to every rank */
-  for (r = 0; r < nodes * R; r++)
-    for (k = 0; k < nodes; k++)
-      if (lo[k + 1] > lo[k]) memcpy((char *)recvbufs[r] + lo[k] * ts, cur[k] + lo[k] * ts, (size_t)((lo[k + 1] - lo[k]) * ts));
+  /* the allgather steps. While the block is smaller than gm (:347-403), every task sends all lines
+     of its gm group to the tasks (t + g (i + 1)) mod gnext of its block and reduces what comes
+     back, in its own order -- the first step of the whole algorithm (no reduce-scatter step
+     before) r_0 (into lb) += own, += r_1 ..; any later one own (lb) += r_0 .. -- so the tasks of a
+     block may end with differently associated sums. Then (:404-437) every task receives the lines
+     of the other g-blocks of its gnext-block from the task at its own position in that g-block. */
+  for (j = 0, g = 1; g < gm; g *= ag[j], j++) {
+    const int q = ag[j] - 1, gnext = g * ag[j], first = nrs == 0 && j == 0;
+    for (t = 0; t < nodes; t++) {
+      int peer[16];
+      const long a = lo[t / gm * gm], b = lo[t / gm * gm + gm], len = b - a;
+      char *acc = nxt[t] + a * ts;
+      for (i = 0; i < q; i++) peer[i] = (t + g * (i + 1)) % gnext + t / gnext * gnext;
+      if (len <= 0) continue;
+      if (first) {
+        memcpy(acc, cur[peer[0]] + a * ts, (size_t)(len * ts));
+        ref_reduction_op(red, dtype, acc, cur[t] + a * ts, len);
+        for (i = 1; i < q; i++) ref_reduction_op(red, dtype, acc, cur[peer[i]] + a * ts, len);
+      } else {
+        memcpy(acc, cur[t] + a * ts, (size_t)(len * ts));
+        for (i = 0; i < q; i++) ref_reduction_op(red, dtype, acc, cur[peer[i]] + a * ts, len);
+      }
+    }
+    for (t = 0; t < nodes; t++) {
+      char *x = cur[t];
+      cur[t] = nxt[t];
+      nxt[t] = x;
+    }
+  }
+  for (; j < nag; g *= ag[j], j++) {
+    const int gnext = g * ag[j];
+    for (t = 0; t < nodes; t++) {
+      memcpy(nxt[t], cur[t], bytes);
+      for (k = t / gnext * gnext; k < t / gnext * gnext + gnext; k += g) {
+        const int src = k / g * g + t % g; /* the task at t's position in that g-block */
+        const long a = lo[k], b = lo[k + g];
+        if (k / g != t / g && b > a) memcpy(nxt[t] + a * ts, cur[src] + a * ts, (size_t)((b - a) * ts));
+      }
+    }
+    for (t = 0; t < nodes; t++) {
+      char *x = cur[t];
+      cur[t] = nxt[t];
+      nxt[t] = x;
+    }
+  }
+  for (r = 0; r < nodes * R; r++) memcpy(recvbufs[r], cur[node_task[r / R]], bytes);
 out:
   for (t = 0; t < nodes && cur && nxt; t++) {
     free(cur[t]);

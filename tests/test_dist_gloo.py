@@ -98,7 +98,7 @@ def _nodes_worker(rank, world, port, cases, q, nodes=2, ports=None):
     from oracle import oracle
     failures = []
     R = world // nodes
-    k = (nodes - 1).bit_length() if ports is None else sum(1 for p in ports if p < 0)
+    nx, na = emac.node_steps(nodes, ports)
     SH = emac.LEG_STEP_SHIFT
     for code, count, copyin in cases:
         sends = xorshift_inputs(world, count, code, seed_base=0x2A0DE000 + count)
@@ -111,7 +111,7 @@ def _nodes_worker(rank, world, port, cases, q, nodes=2, ports=None):
         desc = emac.plan_describe(R, count, code, copyin, 0)
         _run_leg(ops, LEG_RS, bufs)
         _fold([f[:3] for f in folds if f[3] == emac.LEG_FOLD], bufs, code, desc)
-        for st in range(k):
+        for st in range(nx):
             _run_leg(ops, emac.LEG_NODES_RS | st << SH, bufs)
             for off, n, leaves, leg in folds:
                 if leg != emac.LEG_NODES_FOLD | st << SH:
@@ -122,8 +122,8 @@ def _nodes_worker(rank, world, port, cases, q, nodes=2, ports=None):
                     for x in xs[1:]:  # a left fold in the listed order
                         acc = acc + x
                 bufs[emac.BUF_RECV][off:off + n * itemsize].view(dt)[:] = acc
-        for st in reversed(range(k)):
-            _run_leg(ops, emac.LEG_NODES_AG | st << SH, bufs)
+        for j in range(na):  # the copying allgather steps, block growing
+            _run_leg(ops, emac.LEG_NODES_AG | j << SH, bufs)
         _run_leg(ops, LEG_AG, bufs)
         want = oracle.allreduce_nodes(sends, copyin, nodes, ports=ports)[rank]
         if not np.array_equal(bufs[emac.BUF_RECV], want.view(np.uint8)):
@@ -248,6 +248,12 @@ def test_ipc_bootstrap_over_gloo_without_gpu(world):
     (6, 6, [-1, -2, 2, 1], [(emac.FLOAT, 40009, "6;1 -1 1"), (emac.DOUBLE, 6007, "6;1 -1 1")]),
     (8, 8, [-3, -1, 1, 3], [(emac.FLOAT, 40009, "6;1 -1 1")]),
     (8, 4, [-1, -1, 1, 1], [(emac.FLOAT, 20011, "6;1 -2 2")]),
+    # allgather steps that reduce (README "4(3)", "4(-1 1 1)", "4(1 1)"): nodes may disagree
+    (4, 4, [3], [(emac.FLOAT, 30011, "6;1 -1 1"), (emac.INT, 77, "6;1 -1 1")]),
+    (8, 4, [-1, 1, 1], [(emac.FLOAT, 20011, "6;1 -2 2")]),
+    (4, 4, [1, 1], [(emac.DOUBLE, 9001, "6;1 -1 1")]),
+    (6, 6, [-1, 2, 1], [(emac.FLOAT, 12001, "6;1 -1 1")]),
+    (6, 3, [2], [(emac.FLOAT, 12001, "6;1 -2 2")]),
 ])
 def test_node_ports_program_over_gloo(world, nodes, ports, cases):
     """Several ports per step (EXT_MPI_NUM_PORTS "N(-p ... p ...)", radix-3/4 node steps, mixed

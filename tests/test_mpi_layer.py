@@ -71,15 +71,18 @@ def test_mpi_layer_single_rank_gpu(tmp_path, args):
     (2, "4(-1 -1 1 1)", "RESULT fail rc=-4"),    # a group of 4 nodes over a communicator of 2
     (2, "-1 -1 1 1", "RESULT fail rc=-4"),       # two steps over 2 nodes
     (2, "2(-1 1) 2(-1 1)", "RESULT fail rc=-4"),  # several groups
-    (2, "2(1)", "RESULT fail rc=-4"),            # reduction inside the allgather steps: not this path
-    (4, "4(3)", "RESULT fail rc=-4"),
+    (2, "2(1)", "RESULT no-device"),             # reduction inside the allgather steps (README)
+    (4, "4(3)", "RESULT no-device"),
+    (4, "4(-1 1 1)", "RESULT no-device"),
+    (4, "4(-1 -1)", "RESULT fail rc=-4"),        # reduce_scatter_core: not this path
+    (4, "4(-1 2 1)", "RESULT fail rc=-4"),       # an allgather step across the reduce-scatter groups
     (3, "3(-1 1)", "RESULT fail rc=-4"),
 ])
 def test_mpi_logical_nodes_without_gpu(tmp_path, n, ports, want):
     """EXT_MPI_NUM_TASKS_PER_SOCKET splits the ranks into logical nodes (ext_mpi.c:195-215): several
     of them take the inter-node schedule over RCCL (no device here: ERROR_DEVICE on every rank);
     EXT_MPI_NUM_PORTS in the reference's "nodes(ports)" grammar names it, anything else (another
-    node count, several groups, reduction inside the allgather steps) is refused
+    node count, several groups, a list ending in a reduce-scatter port) is refused
     (ERROR_UNSUPPORTED) instead of computed otherwise."""
     import torch
     if torch.cuda.is_available():

@@ -330,13 +330,15 @@ def _rank_order(size, factors, ranks):
 
 
 def _allreduce_core_literal(partials, ports):
-    """Independent statement of the inter-node reduce-scatter for the oracle's check: the line
-    tables of allreduce_core's reduce-scatter loop (allreduce_recursive.c:248-347) built as the
-    reference builds them -- recvfrom node/line per slot, the reducefrom list of the output slot --
-    and replayed the way raw_code.c:221-356 executes a block: a received line is copied into its
-    slot, then the output slot accumulates its reducefrom slots in list order; tasks are the nodes
-    in ext_mpi_rank_order over the allgather factors, lines laid out in task order with node
-    ranks[k]'s size (ext_mpi_native.c:768-786, rank_permutation.c). Returns the reduced message."""
+    """Independent statement of the inter-node algorithm for the oracle's check: the line tables
+    of allreduce_core (allreduce_recursive.c:222-453) built as the reference builds them --
+    recvfrom node/line per slot, the reducefrom list of the output slot, for the reduce-scatter
+    steps (:248-347), the allgather steps that still reduce (:348-403) and the copying ones
+    (:404-437) -- and replayed the way raw_code.c:221-356 executes a block: a received line is
+    copied into its slot, then the output slot accumulates its reducefrom slots in list order.
+    Tasks are the nodes in ext_mpi_rank_order over the allgather factors, lines laid out in task
+    order with node ranks[k]'s size (ext_mpi_native.c:768-786, rank_permutation.c). Returns the
+    result of every node (the tasks of a block may disagree when the allgather steps reduce)."""
     N, count = len(partials), partials[0].size
     rs = [p for p in ports if p < 0]
     ag = [p + 1 for p in ports if p > 0]
@@ -350,6 +352,20 @@ def _allreduce_core_literal(partials, ports):
     line = lambda arr, l: arr[lo[l]:lo[l + 1]]  # noqa: E731
     # slots[t][n] = task t's data in slot n (lines n mod lb), block 0: the own partial in 0..lb-1
     slots = [{n: line(partials[ranks[t]], n).copy() for n in range(lb)} for t in range(N)]
+
+    def run_block(recv, red, held):
+        new = [dict(x) for x in slots]
+        for t in range(N):
+            for n, (q, ln) in recv[t].items():
+                new[t][n] = held(q, ln).copy()
+        for t in range(N):
+            for n, lst in red[t].items():
+                acc = new[t][n].copy()
+                for r in lst:
+                    acc = acc + new[t][r]
+                new[t][n] = acc
+        return new
+
     gbstep = lb
     for step, port in enumerate(rs):
         p = abs(port)
@@ -373,25 +389,47 @@ def _allreduce_core_literal(partials, ports):
                         red[t][ln + lb] = ([ln + (2 + i) * lb for i in range(p)] if step > 0 else
                                            [ln] + [ln + (2 + i) * lb for i in range(1, p)])
         # the sender's copy of line `ln`: its accumulator slot of the previous block
-        held = lambda q, ln: slots[q][ln + 2 * lb] if step > 0 else slots[q][ln]  # noqa: E731
-        new = [dict(s) for s in slots]
-        for t in range(N):
-            for n, (q, ln) in recv[t].items():
-                new[t][n] = held(q, ln).copy()
-        for t in range(N):
-            for n, lst in red[t].items():
-                acc = new[t][n].copy()
-                for r in lst:
-                    acc = acc + new[t][r]
-                new[t][n] = acc
-        slots = new
+        slots = run_block(recv, red, lambda q, ln: slots[q][ln + 2 * lb] if step > 0 else slots[q][ln])
         gbstep = gnext
-    return np.concatenate([slots[k][k + lb] for k in range(N)]) if N > 1 else partials[0]
+    middle, step, g = gbstep, len(rs), 1
+    for a in ag:
+        gnext = g * a
+        recv, red = [dict() for _ in range(N)], [dict() for _ in range(N)]
+        for t in range(N):
+            if g < middle:  # the allgather steps that reduce (:348-403)
+                for ln in range(t // middle * middle, t // middle * middle + middle):
+                    for i in range(a - 1):
+                        peer = (t + g * (i + 1)) % gnext + t // gnext * gnext
+                        recv[t][ln + ((i + 1) if step == 0 else (i + 2)) * lb] = (peer, ln)
+                    red[t][ln + lb] = ([ln] + [ln + (i + 1) * lb for i in range(1, a - 1)] if step == 0 else
+                                       [ln + (i + 2) * lb for i in range(a - 1)])
+            else:  # the copying ones (:404-437)
+                for ln in range(t // gnext * gnext, t // gnext * gnext + gnext):
+                    if ln // g != t // g:
+                        if ln // g > t // g:
+                            i = (gnext + ln // g - t // g - 1) % gnext
+                        else:
+                            i = (gnext + ln // g - t // g) % gnext - 1
+                        recv[t][ln + lb] = ((t + g * (i + 1)) % gnext + t // gnext * gnext, ln)
+        if g < middle and step == 0:  # the first step of all sends the own partial (slot ln)
+            held = lambda q, ln: slots[q][ln]  # noqa: E731
+        else:
+            held = lambda q, ln: slots[q][ln + lb]  # noqa: E731
+        slots = run_block(recv, red, held)
+        g, step = gnext, step + 1
+    out = []
+    for n in range(N):  # node n = task ranks.index(n)
+        t = ranks.index(n)
+        out.append(np.concatenate([slots[t][k + lb] for k in range(N)]))
+    return out
 
 
 @pytest.mark.parametrize("nodes,ports", [(2, [-1, 1]), (4, [-1, -1, 1, 1]), (3, [-2, 2]), (4, [-3, 3]),
                                          (6, [-1, -2, 2, 1]), (6, [-2, -1, 1, 2]), (8, [-3, -1, 1, 3]),
-                                         (9, [-2, -2, 2, 2]), (8, [-1, -1, -1, 1, 1, 1]), (5, [-4, 4])])
+                                         (9, [-2, -2, 2, 2]), (8, [-1, -1, -1, 1, 1, 1]), (5, [-4, 4]),
+                                         # allgather steps that reduce (README: 4(3), 4(-1 1 1), 4(1 1))
+                                         (4, [3]), (4, [-1, 1, 1]), (4, [1, 1]), (3, [2]), (6, [-1, 2, 1]),
+                                         (8, [-1, 3, 1]), (6, [2, 1]), (2, [1])])
 def test_node_ports_against_literal_line_tables(oracle, nodes, ports):
     """The oracle's inter-node restatement (ref_emulate_node_ports) against an independent,
     literal replay of allreduce_core's line tables: bitwise for float (association observable)."""
@@ -401,8 +439,8 @@ def test_node_ports_against_literal_line_tables(oracle, nodes, ports):
                  for _ in range(nodes)]
         want = _allreduce_core_literal(sends, ports)
         got = oracle.allreduce_nodes(sends, "6;1 -1 1", nodes, ports=ports)
-        for out in got:
-            assert np.array_equal(out, want), (nodes, ports, count)
+        for n, out in enumerate(got):
+            assert np.array_equal(out, want[n]), (nodes, ports, count, n)
     if nodes == 3:  # the association differs per line: observable, so pinned by the statement
         s = [np.float32([1e8]), np.float32([1.0]), np.float32([-1e8])]
-        assert oracle.allreduce_nodes(s, "6;1 -1 1", 3, ports=ports)[0][0] == _allreduce_core_literal(s, ports)[0]
+        assert oracle.allreduce_nodes(s, "6;1 -1 1", 3, ports=ports)[0][0] == _allreduce_core_literal(s, ports)[0][0]
