@@ -179,11 +179,13 @@ int ext_mpi_amd_comm_program_nodes(int nodes, int ranks_per_node, int rank, long
  * [n * size/nodes, (n + 1) * size/nodes) form node n, nodes <= 16, set before
  * ext_mpi_amd_allreduce_init; copyin then describes ONE node (its ranks_per_node positions).
  * `ports` is the reference's num_ports list, 0-terminated: the reduce-scatter ports (negative,
- * radix |p| + 1 each), then the allgather ports (positive), each part's radices multiplying to
- * `nodes` -- e.g. {-1, -1, 1, 1, 0} for 4 nodes, one port per step; {-2, 2, 0} for 3 nodes;
- * NULL: one port per step for a power of two, else one step of radix `nodes`. _set_nodes: the
- * one-port schedule of a power of two. Peer-mapped communicators are single-node
- * (EXT_MPI_AMD_ERROR_UNSUPPORTED), as are lists without reduce-scatter ports or ending in one. */
+ * radix |p| + 1 each), then the allgather ports (positive) whose radices multiply to `nodes` --
+ * e.g. {-1, -1, 1, 1, 0} for 4 nodes, one port per step; {-2, 2, 0} for 3 nodes; with fewer
+ * reduce-scatter steps ({3, 0}, {-1, 1, 1, 0}) the first allgather steps reduce inside the groups
+ * left, each node in its own order (allreduce_recursive.c:348-403); NULL: one port per step for
+ * a power of two, else one step of radix `nodes`. _set_nodes: the one-port schedule of a power of
+ * two. Peer-mapped communicators are single-node (EXT_MPI_AMD_ERROR_UNSUPPORTED), as are lists
+ * ending in a reduce-scatter port. */
 int ext_mpi_amd_comm_set_node_ports(int comm, int nodes, const int *ports);
 int ext_mpi_amd_comm_set_nodes(int comm, int nodes);
 
