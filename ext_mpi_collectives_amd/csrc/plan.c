@@ -430,11 +430,96 @@ int emac_node_sched_build(emac_node_sched *s, int nodes, const int *ports) {
     if (s->nagp == EMAC_MAX_NODE_STEPS) return EMAC_ERR_UNSUPPORTED;
     s->agp_radix[s->nagp++] = ag[j];
   }
-  /* ext_mpi_native.c:879-912: ext_mpi_rank_order over the allgather radices; the algorithm runs
-     on task = the position of the node in that order (rank_permutation.c:133-139) */
-  position_order(nodes, nag, ag, s->task_node);
-  for (i = 0; i < nodes; i++) s->node_task[s->task_node[i]] = i;
+  /* the task order depends on the message size: node_task_order, per program */
   return EMAC_OK;
+}
+
+/* rank_perm_heuristic (rank_permutation.c:12-87): pairs groups ("colors") of nodes by their
+   summed line sizes, smallest with largest, halving the colors each round; the nodes end in the
+   order perm[task]. The qsort there compares sizes only; ties keep their order here, as glibc's
+   merge-sort qsort leaves them (an introsort qsort may not: parity with such a C library is
+   unpinned where sizes tie). */
+static void node_heuristic(int n, const long *sizes, int *perm) {
+  long value[EMAC_MAX_NODES], cval[EMAC_MAX_NODES];
+  int key[EMAC_MAX_NODES], color[EMAC_MAX_NODES], k2[EMAC_MAX_NODES], c2[EMAC_MAX_NODES], ckey[EMAC_MAX_NODES];
+  long v2[EMAC_MAX_NODES];
+  int ncol = n, i, j, k;
+  for (i = 0; i < n; i++) {
+    value[i] = sizes[i];
+    key[i] = color[i] = i;
+  }
+  while (ncol > 1) {
+    for (i = 0; i < ncol; i++) {
+      cval[i] = 0;
+      ckey[i] = i;
+    }
+    for (i = 0; i < n; i++) cval[color[i]] += value[i];
+    if (ncol % 2) cval[0] = 0;
+    for (i = 1; i < ncol; i++) { /* stable insertion sort by value */
+      const long v = cval[i];
+      const int kk = ckey[i];
+      for (j = i - 1; j >= 0 && cval[j] > v; j--) {
+        cval[j + 1] = cval[j];
+        ckey[j + 1] = ckey[j];
+      }
+      cval[j + 1] = v;
+      ckey[j + 1] = kk;
+    }
+    k = 0;
+    if (!(ncol % 2)) {
+      for (i = 0; i < ncol; i++)
+        for (j = 0; j < n; j++)
+          if (ckey[i % 2 ? ncol - 1 - i / 2 : i / 2] == color[j]) {
+            v2[k] = value[j];
+            k2[k] = key[j];
+            c2[k++] = i / 2;
+          }
+    } else {
+      for (j = 0; j < n; j++)
+        if (color[j] == 0) {
+          v2[k] = value[j];
+          k2[k] = key[j];
+          c2[k++] = 0;
+        }
+      for (i = 0; i < ncol - 1; i++)
+        for (j = 0; j < n; j++)
+          if (ckey[i % 2 ? ncol - 1 - i / 2 : i / 2 + 1] == color[j]) {
+            v2[k] = value[j];
+            k2[k] = key[j];
+            c2[k++] = i / 2 + 1;
+          }
+    }
+    for (i = 0; i < n; i++) {
+      value[i] = v2[i];
+      key[i] = k2[i];
+      color[i] = c2[i];
+    }
+    ncol = (ncol + 1) / 2;
+  }
+  for (i = 0; i < n; i++) perm[i] = key[i];
+}
+
+/* The task order the reference's generators run with, as they run: ext_mpi_native.c:879-897
+   writes ext_mpi_rank_order's permutation as PARAMETER RANK_PERM, but
+   ext_mpi_generate_rank_permutation_forward tests its own still-NULL local rank_perm
+   (rank_permutation.c:90,106) and so always replaces it -- with the identity when every line has
+   the same size, else with rank_perm_heuristic over the line sizes (:111-122); the backward pass
+   maps with that one (:170-200). The line sizes are count / N elements, the remainder to the low
+   nodes (ext_mpi_native.c:768-786), or, for a list without reduce-scatter ports (allreduce_short,
+   :667), the whole message in line 0. */
+static void node_task_order(emac_node_sched *ns, long count) {
+  long sz[EMAC_MAX_NODES];
+  int i, equal = 1;
+  const int N = ns->nodes;
+  for (i = 0; i < N; i++) {
+    sz[i] = ns->nsteps ? count / N + (i < count % N) : (i ? 0 : count);
+    equal &= sz[i] == sz[0];
+  }
+  if (equal)
+    for (i = 0; i < N; i++) ns->task_node[i] = i;
+  else
+    node_heuristic(N, sz, ns->task_node);
+  for (i = 0; i < N; i++) ns->node_task[ns->task_node[i]] = i;
 }
 
 /* the element range [*lo, *hi) of the lines (tasks) [a, b) in the message of `count` elements:
@@ -463,13 +548,33 @@ static void clip(long a, long b, long c, long d, long *off, long *len) {
   *len = hi > lo ? hi - lo : 0;
 }
 
+static int program_nodes(const emac_plan *p, const emac_node_sched *ns, int node, int me, long send_phase, long count,
+                         emac_p2p **ops_out, int *nops_out, emac_fold **folds_out, int *nfolds_out,
+                         long *staging_bytes);
+
 int emac_comm_program_nodes(const emac_plan *p, const emac_node_sched *ns, int node, int me, long send_phase,
                             emac_p2p **ops_out, int *nops_out, emac_fold **folds_out, int *nfolds_out,
                             long *staging_bytes) {
+  emac_node_sched nsl;
+  long count = 0;
+  int pc, q;
+  for (pc = 0; pc < p->npieces; pc++) /* the message's elements: the pieces' chunks tile it */
+    for (q = 0; q < p->nranks; q++) count += p->chunk_len[(size_t)pc * p->nranks + q];
+  if (ns) { /* this message's task order */
+    nsl = *ns;
+    node_task_order(&nsl, count);
+    ns = &nsl;
+  }
+  return program_nodes(p, ns, node, me, send_phase, count, ops_out, nops_out, folds_out, nfolds_out, staging_bytes);
+}
+
+static int program_nodes(const emac_plan *p, const emac_node_sched *ns, int node, int me, long send_phase, long count,
+                         emac_p2p **ops_out, int *nops_out, emac_fold **folds_out, int *nfolds_out,
+                         long *staging_bytes) {
   const int K = ns ? ns->nsteps : 0, nodes = ns ? ns->nodes : 1, task = ns ? ns->node_task[node] : 0;
   const int KR = ns ? ns->nred : 0, KA = ns ? ns->nagp : 0, gm = ns ? ns->gm : 1;
   int R = p->nranks, me_pos, pc, q, t, nops = 0, nf = 0, leg, g0, st, i, nx = 0, G, Gn, j, g;
-  long ts = p->tsize, total = 0, count = 0;
+  long ts = p->tsize, total = 0;
   long *slot0, *stride, *xslot;
   emac_p2p *ops;
   emac_fold *folds;
@@ -481,8 +586,6 @@ int emac_comm_program_nodes(const emac_plan *p, const emac_node_sched *ns, int n
   }
   for (j = 0; j < KR; j++) nx += ns->red_radix[j] - 1;
   for (j = 0; j < KA; j++) nx += ns->agp_radix[j] - 1; /* (bounds the copy ops below) */
-  for (pc = 0; pc < p->npieces; pc++) /* the message's elements: the pieces' chunks tile it */
-    for (q = 0; q < R; q++) count += p->chunk_len[(size_t)pc * R + q];
   me_pos = p->rank_pos[me];
   g0 = node * R; /* global rank of this node's first rank */
   slot0 = (long *)malloc(sizeof(long) * (size_t)p->npieces);
@@ -518,7 +621,7 @@ int emac_comm_program_nodes(const emac_plan *p, const emac_node_sched *ns, int n
       task_lines(ns, count, task / Gn * Gn, task / Gn * Gn + Gn, &a, &b);
       clip(a, b, off, off + len, &ko, &kl);
       if (halving) { /* the half of the current range this node keeps (see below) */
-        const int bit = (node >> st) & 1;
+        const int bit = (task >> (K - 1 - st)) & 1;
         const long h0 = (hn + 1) / 2;
         if (bit) hlo += h0;
         hn = bit ? hn - h0 : h0;
@@ -589,21 +692,22 @@ int emac_comm_program_nodes(const emac_plan *p, const emac_node_sched *ns, int n
        the last:                 r_{p-1}, own, r_0, ..., r_{p-2}  (r_{p-1} received into lb, :318-343)
      -- for SUM only the association matters (a + b == b + a). */
   /* One port per step over 2^k nodes: every value is a balanced pairwise tree (a + b == b + a at
-     each step), the same whichever node of a pair computes it, so the lines need not be followed:
-     the owned range halves at every step (the node with bit st clear keeps the lower half) and
-     every rank of a node carries an equal share. Task order is the bit reversal here, so step st
-     pairs nodes n and n ^ 2^st. */
+     each step), the same whichever task of a pair computes it, so the lines need not be followed:
+     step st pairs task t with t ^ 2^(K-1-st) (allreduce_core, :261-284), the owned range halves
+     at every step (the task with that bit clear keeps the lower half) and every rank of a node
+     carries an equal share. */
   for (st = 0; halving && st < K; st++)
     for (pc = 0; pc < p->npieces; pc++) {
       long lo = p->chunk_off[(size_t)pc * R + me_pos], n = p->chunk_len[(size_t)pc * R + me_pos];
       long hoff[2], hlen[2];
-      const int partner = (node ^ (1 << st)) * R + me, bit = (node >> st) & 1, lg = st << EMAC_LEG_STEP_SHIFT;
+      const int tb = K - 1 - st, partner = ns->task_node[task ^ (1 << tb)] * R + me, bit = (task >> tb) & 1,
+                lg = st << EMAC_LEG_STEP_SHIFT;
       const int la = (K - 1 - st) << EMAC_LEG_STEP_SHIFT; /* its allgather step: the reverse order */
       int s2;
       for (s2 = 0; s2 < st; s2++) { /* this step's range */
-        const long h0 = (n + 1) / 2;
-        if ((node >> s2) & 1) lo += h0;
-        n = ((node >> s2) & 1) ? n - h0 : h0;
+        const long h0 = (n + 1) / 2, b2 = (task >> (K - 1 - s2)) & 1;
+        if (b2) lo += h0;
+        n = b2 ? n - h0 : h0;
       }
       hoff[0] = lo;
       hlen[0] = (n + 1) / 2;

@@ -93,15 +93,83 @@ done:
   return rc;
 }
 
+/* rank_perm_heuristic, rank_permutation.c:12-87 (qsort over equal values taken as stable, as
+   glibc's merge-sort qsort leaves them) */
+static void ref_perm_heuristic(int num_nodes, const long *counts, int *rank_perm) {
+  long value[16], v2[16], aval[16];
+  int key[16], color[16], k2[16], c2[16], akey[16], num_colors = num_nodes, i, j, k;
+  for (i = 0; i < num_nodes; i++) {
+    value[i] = counts[i];
+    key[i] = color[i] = i;
+  }
+  while (num_colors > 1) {
+    for (i = 0; i < num_colors; i++) {
+      aval[i] = 0;
+      akey[i] = i;
+    }
+    for (i = 0; i < num_nodes; i++) aval[color[i]] += value[i];
+    if (num_colors % 2) aval[0] = 0;
+    for (i = 0; i < num_colors; i++) /* a stable (bubble) sort by value */
+      for (j = num_colors - 1; j > i; j--)
+        if (aval[j - 1] > aval[j]) {
+          long tv = aval[j - 1];
+          int tk = akey[j - 1];
+          aval[j - 1] = aval[j];
+          akey[j - 1] = akey[j];
+          aval[j] = tv;
+          akey[j] = tk;
+        }
+    k = 0;
+    if (!(num_colors % 2)) {
+      for (i = 0; i < num_colors; i++)
+        for (j = 0; j < num_nodes; j++) {
+          const int want = (i % 2) ? akey[num_colors - 1 - i / 2] : akey[i / 2];
+          if (want == color[j]) {
+            v2[k] = value[j];
+            k2[k] = key[j];
+            c2[k++] = i / 2;
+          }
+        }
+    } else {
+      for (j = 0; j < num_nodes; j++)
+        if (color[j] == 0) {
+          v2[k] = value[j];
+          k2[k] = key[j];
+          c2[k++] = 0;
+        }
+      for (i = 0; i < num_colors - 1; i++)
+        for (j = 0; j < num_nodes; j++) {
+          const int want = (i % 2) ? akey[num_colors - 1 - i / 2] : akey[i / 2 + 1];
+          if (want == color[j]) {
+            v2[k] = value[j];
+            k2[k] = key[j];
+            c2[k++] = i / 2 + 1;
+          }
+        }
+    }
+    for (i = 0; i < num_nodes; i++) {
+      value[i] = v2[i];
+      key[i] = k2[i];
+      color[i] = c2[i];
+    }
+    num_colors = (num_colors + 1) / 2;
+  }
+  for (i = 0; i < num_nodes; i++) rank_perm[i] = key[i];
+}
+
 /* Several nodes (EXT_MPI_NUM_PORTS "N(-p0 -p1 ... q0 q1 ...)"). ext_mpi_native.c:879-1000 composes:
    the node's copy-in -- reduce_copies_one_socket with in_out = 1 and one_node = 0
    (reduce_copyin.c:1497-1500): the same reduce-scatter emission as one node, into shared memory --
    then the inter-node algorithm of allreduce_recursive.c:222-453 (allreduce_core) over the node
    partials, then the node's copy-out. Restated here as the reference runs it, task by task:
    * the message is cut into one line per node (ext_mpi_native.c:768-786: count / N elements, the
-     remainder to the low nodes), the algorithm runs on tasks = the nodes in ext_mpi_rank_order
-     over the allgather radices (ext_mpi_native.c:879-912; rank_permutation.c:89-228 maps node n
-     to task t with ranks[t] = n, and each task's line t back to node ranks[t]'s line size), and
+     remainder to the low nodes), the algorithm runs on tasks, node n being task t with
+     perm[t] = n (rank_permutation.c:133-139; lines mapped back with perm, :176-200).
+     ext_mpi_native.c:879-897 writes ext_mpi_rank_order's permutation as RANK_PERM, but the
+     forward pass tests its own still-NULL local rank_perm (rank_permutation.c:90,106) and always
+     replaces it: the identity when every line has the same size, else rank_perm_heuristic over
+     the line sizes (:111-122) -- the lines being, for a list without reduce-scatter ports
+     (allreduce_short, ext_mpi_native.c:667,768-788), the whole message in line 0.
      raw_code.c:238-356 lays the lines out in task order (line k at the sizes of lines 0..k-1);
    * reduce-scatter step s (ports[s] < 0, radix p + 1 = |ports[s]| + 1) splits each group of G
      tasks into p + 1 sub-groups of Gn = G / (p + 1); every task keeps the lines of its sub-group,
@@ -118,7 +186,7 @@ done:
 int ref_emulate_node_ports(int nodes, const int *ports, int R, long count, int dtype, int red, const char *copyin,
                            int in_place, int num_sockets, void *const *sendbufs, void *const *recvbufs) {
   const int ts = ref_type_size(dtype);
-  int rad[8], ag[8], nrs = 0, nag = 0, task_node[16], node_task[16], n, r, t, k, s, i, j, G, g, gm, rc = 0, prod_rs = 1,
+  int rad[8], ag[8] = {0}, nrs = 0, nag = 0, task_node[16], node_task[16], n, r, t, k, s, i, j, G, g, gm, rc = 0, prod_rs = 1,
       prod_ag = 1;
   long lo[17];
   char **cur = NULL, **nxt = NULL;
@@ -145,8 +213,16 @@ int ref_emulate_node_ports(int nodes, const int *ports, int R, long count, int d
   gm = nodes / prod_rs;
   for (j = 0, g = 1; g < gm; g *= ag[j], j++);
   if (g != gm) return -1; /* an allgather step straddling gm: not restated */
-  for (t = 0; t < nodes; t++) task_node[t] = t;
-  ref_rank_order(nodes, nag, ag, task_node);
+  {
+    long sz[16];
+    int equal = 1;
+    for (t = 0; t < nodes; t++) {
+      sz[t] = nrs ? count / nodes + (t < count % nodes) : (t ? 0 : count);
+      equal &= sz[t] == sz[0];
+    }
+    for (t = 0; t < nodes; t++) task_node[t] = t;
+    if (!equal) ref_perm_heuristic(nodes, sz, task_node);
+  }
   for (t = 0; t < nodes; t++) node_task[task_node[t]] = t;
   lo[0] = 0;
   for (k = 0; k < nodes; k++) {

@@ -301,17 +301,24 @@ def test_two_nodes_fold_is_one_reduction_of_the_node_partials(oracle, dt):
 
 
 def test_many_nodes_pairwise_tree(oracle):
-    # 4 nodes, one port per step: ((P0 + P1) + (P2 + P3)) -- the reference's radix-2 steps in its
-    # bit-reversed node order (allreduce_recursive.c:261-284, reduce_copyin.c:375-394)
+    # 4 nodes, one port per step: allreduce_core pairs task t with t ^ 2 then t ^ 1
+    # (allreduce_recursive.c:261-284). The tasks are NOT ext_mpi_rank_order's [0, 2, 1, 3]: the
+    # forward permutation pass discards that RANK_PERM (rank_permutation.c:90,106) and runs with
+    # the identity when the 4 lines are equal -- ((P0 + P2) + (P1 + P3)) -- else with
+    # rank_perm_heuristic over the line sizes: 517 = 130 + 3 x 129 gives [2, 3, 1, 0], so
+    # ((P2 + P1) + (P3 + P0)).
     rng = np.random.default_rng(9)
-    sends = [((rng.random(517) * 2 - 1) * 10.0 ** rng.integers(-4, 5, 517)).astype(np.float32) for _ in range(8)]
-    p = [oracle.allreduce(sends[2 * n:2 * n + 2], "6;1 -2 2")[0] for n in range(4)]
-    want = ((p[0] + p[1]).astype(np.float32) + (p[2] + p[3]).astype(np.float32)).astype(np.float32)
-    other = ((p[0] + p[2]).astype(np.float32) + (p[1] + p[3]).astype(np.float32)).astype(np.float32)
-    assert not np.array_equal(want, other)  # the pairing is observable
-    for out in oracle.allreduce_nodes(sends, "6;1 -2 2", 4):
-        assert np.array_equal(out, want)
-    assert oracle.rank_order(4, [2, 2]) == [0, 2, 1, 3]  # the node permutation behind the pairing
+    f32 = np.float32
+    for count, pairs in ((516, ((0, 2), (1, 3))), (517, ((2, 1), (3, 0)))):
+        sends = [((rng.random(count) * 2 - 1) * 10.0 ** rng.integers(-4, 5, count)).astype(f32) for _ in range(8)]
+        p = [oracle.allreduce(sends[2 * n:2 * n + 2], "6;1 -2 2")[0] for n in range(4)]
+        (a, b), (c, d) = pairs
+        want = ((p[a] + p[b]).astype(f32) + (p[c] + p[d]).astype(f32)).astype(f32)
+        other = ((p[0] + p[1]).astype(f32) + (p[2] + p[3]).astype(f32)).astype(f32)
+        assert not np.array_equal(want, other)  # the pairing is observable
+        for out in oracle.allreduce_nodes(sends, "6;1 -2 2", 4):
+            assert np.array_equal(out, want)
+    assert _perm_heuristic(4, [130, 129, 129, 129]) == [2, 3, 1, 0]
 
 
 def _rank_order(size, factors, ranks):
@@ -329,6 +336,58 @@ def _rank_order(size, factors, ranks):
     return new
 
 
+def _perm_heuristic(num_nodes, counts):
+    """rank_perm_heuristic (rank_permutation.c:12-87), literally; its qsort on value taken as a
+    stable sort (glibc's merge-sort qsort)."""
+    org = [dict(value=counts[i], key=i, color=i) for i in range(num_nodes)]
+    num_colors = num_nodes
+    flag = True
+    while flag:
+        arr = [dict(value=0, key=i) for i in range(num_colors)]
+        for o in org:
+            arr[o['color']]['value'] += o['value']
+        if num_colors % 2:
+            arr[0]['value'] = 0
+        arr = sorted(arr, key=lambda a: a['value'])
+        org2 = []
+        if num_colors % 2 == 0:
+            for i in range(num_colors):
+                for o in org:
+                    if i % 2:
+                        if arr[num_colors - 1 - i // 2]['key'] == o['color']:
+                            org2.append(dict(o, color=i // 2))
+                    else:
+                        if arr[i // 2]['key'] == o['color']:
+                            org2.append(dict(o, color=i // 2))
+        else:
+            for o in org:
+                if o['color'] == 0:
+                    org2.append(dict(o))
+            for i in range(num_colors - 1):
+                for o in org:
+                    if i % 2:
+                        if arr[num_colors - 1 - i // 2]['key'] == o['color']:
+                            org2.append(dict(o, color=i // 2 + 1))
+                    else:
+                        if arr[i // 2 + 1]['key'] == o['color']:
+                            org2.append(dict(o, color=i // 2 + 1))
+        org = org2
+        num_colors = (num_colors + 1) // 2
+        flag = num_colors > 1
+    return [o['key'] for o in org]
+
+
+def _task_order(N, count, ports):
+    """The task order the reference runs with (rank_permutation.c:89-160): its forward pass tests
+    its own NULL local rank_perm (:90,106) and so replaces ext_mpi_rank_order's RANK_PERM --
+    identity for equal line sizes, else the heuristic over them; the line sizes are count / N
+    (remainder to the low nodes), or the whole message in line 0 without reduce-scatter ports
+    (allreduce_short, ext_mpi_native.c:667,768-788)."""
+    rs = any(p < 0 for p in ports)
+    sizes = [count // N + (i < count % N) if rs else (count if i == 0 else 0) for i in range(N)]
+    return list(range(N)) if len(set(sizes)) == 1 else _perm_heuristic(N, sizes)
+
+
 def _allreduce_core_literal(partials, ports):
     """Independent statement of the inter-node algorithm for the oracle's check: the line tables
     of allreduce_core (allreduce_recursive.c:222-453) built as the reference builds them --
@@ -336,13 +395,13 @@ def _allreduce_core_literal(partials, ports):
     steps (:248-347), the allgather steps that still reduce (:348-403) and the copying ones
     (:404-437) -- and replayed the way raw_code.c:221-356 executes a block: a received line is
     copied into its slot, then the output slot accumulates its reducefrom slots in list order.
-    Tasks are the nodes in ext_mpi_rank_order over the allgather factors, lines laid out in task
-    order with node ranks[k]'s size (ext_mpi_native.c:768-786, rank_permutation.c). Returns the
-    result of every node (the tasks of a block may disagree when the allgather steps reduce)."""
+    Tasks are the nodes in the order _task_order gives, lines laid out in task order with node
+    ranks[k]'s size (ext_mpi_native.c:768-786, rank_permutation.c). Returns the result of every
+    node (the tasks of a block may disagree when the allgather steps reduce)."""
     N, count = len(partials), partials[0].size
     rs = [p for p in ports if p < 0]
     ag = [p + 1 for p in ports if p > 0]
-    ranks = _rank_order(N, ag, list(range(N)))  # task -> node
+    ranks = _task_order(N, count, ports)  # task -> node
     lb = 1
     for p in ag:
         lb *= p
