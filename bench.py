@@ -658,7 +658,7 @@ def _rccl_allreduce_baseline(rank, world, dist, torch):
         return {"error": str(e)[:200]}
 
 
-def _node_point(emac, rank, world, dev, count, tdtype, code, dname, dist, torch, nodes=2):
+def _node_point(emac, rank, world, dev, count, tdtype, code, dname, dist, torch, nodes=2, ports=None):
     """§8(f3): the same ranks as `nodes` logical nodes of world/nodes (ext_mpi_amd_comm_set_nodes;
     the reference's one-port inter-node schedule between the node legs) on a second RCCL
     communicator, at the run's size; checked against the float64 sum like the headline."""
@@ -668,7 +668,7 @@ def _node_point(emac, rank, world, dev, count, tdtype, code, dname, dist, torch,
         dist.broadcast_object_list(uid, src=0)
         comm2 = emac.comm_init(rank, world, uid[0], dev)
         try:
-            emac.comm_set_nodes(comm2, nodes)
+            emac.comm_set_nodes(comm2, nodes, ports)
             st = 20
             h2, sb, rb, _, el, ok = _comm_run(emac, comm2, count, tdtype, code, dname, f"6;1 -{R} {R}", st, 3, rank,
                                               world, dist, torch)
@@ -678,7 +678,7 @@ def _node_point(emac, rank, world, dev, count, tdtype, code, dname, dist, torch,
         finally:
             emac.comm_free(comm2)
         log(f"rank {rank}: {nodes} nodes of {R}: {el * 1e6 / st:.2f} us, checked {ok}")
-        return {"nodes": nodes, "ranks_per_node": R, "copyin": f"6;1 -{R} {R}", "bytes_per_rank": count * tdtype.itemsize,
+        return {"nodes": nodes, "ports": ports or "one per step", "ranks_per_node": R, "copyin": f"6;1 -{R} {R}", "bytes_per_rank": count * tdtype.itemsize,
                 "us_per_allreduce": round(el * 1e6 / st, 2),
                 "algbw_gbps": round(count * tdtype.itemsize * st / el / 1e9, 2), "checked": ok}
     except Exception as e:  # noqa: BLE001 -- an extra point, never the headline
@@ -755,9 +755,11 @@ def transport_child(args):
             if world >= 2 and world % 2 == 0:
                 res["two_node_schedule"] = _node_point(emac, rank, world, dev, count, tdtype, code, dname, dist,
                                                        torch)
-            if world >= 4 and world % 4 == 0:  # two radix-2 node steps (4 nodes)
+            if world >= 4 and world % 4 == 0:  # two radix-2 node steps (4 nodes), and one radix-4 step
                 res["four_node_schedule"] = _node_point(emac, rank, world, dev, count, tdtype, code, dname, dist,
                                                         torch, nodes=4)
+                res["four_node_three_ports"] = _node_point(emac, rank, world, dev, count, tdtype, code, dname, dist,
+                                                           torch, nodes=4, ports=[-3, 3])
         if full:
             # BASELINE configs[3] (double, 256 MiB per rank) and a configs[4]-style size sweep
             points = [(args.dtype, n) for n in (8, 64 << 10, 1 << 20, 16 << 20, 64 << 20, 256 << 20, 512 << 20)]
@@ -875,7 +877,7 @@ def multi_gpu(args):
                 "value": round(world * S * args.steps / r["wall"] / 1e9, 2), "checked": r["checked"]}
         if "rccl_allreduce_baseline" in results[t]:  # whichever role RCCL had
             extras["rccl_allreduce_baseline"] = results[t]["rccl_allreduce_baseline"]
-        for key in ("two_node_schedule", "four_node_schedule"):
+        for key in ("two_node_schedule", "four_node_schedule", "four_node_three_ports"):
             if key in results[t]:
                 extras[key] = results[t][key]
     if rank == 0 and primary is None:
