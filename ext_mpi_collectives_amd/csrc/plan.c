@@ -578,7 +578,7 @@ static int program_nodes(const emac_plan *p, const emac_node_sched *ns, int node
   long *slot0, *stride, *xslot;
   emac_p2p *ops;
   emac_fold *folds;
-  int halving = K > 0 && KR == 0;
+  int halving = K > 0 && KR == 0, single;
   if (nodes < 1 || nodes > EMAC_MAX_NODES || node < 0 || node >= nodes || me < 0 || me >= R) return EMAC_ERR_ARG;
   for (st = 0; st < K; st++) {
     nx += ns->radix[st] - 1;
@@ -586,13 +586,14 @@ static int program_nodes(const emac_plan *p, const emac_node_sched *ns, int node
   }
   for (j = 0; j < KR; j++) nx += ns->red_radix[j] - 1;
   for (j = 0; j < KA; j++) nx += ns->agp_radix[j] - 1; /* (bounds the copy ops below) */
+  single = !halving && K == 1 && KR == 0; /* one reduce-scatter step over every node */
   me_pos = p->rank_pos[me];
   g0 = node * R; /* global rank of this node's first rank */
   slot0 = (long *)malloc(sizeof(long) * (size_t)p->npieces);
   stride = (long *)malloc(sizeof(long) * (size_t)p->npieces);
   xslot = (long *)malloc(sizeof(long) * (size_t)p->npieces * (size_t)(nx > 0 ? nx : 1));
   ops = (emac_p2p *)malloc(sizeof(emac_p2p) * (size_t)(4 * p->npieces * R + 4 * nx * p->npieces + 1));
-  folds = (emac_fold *)calloc((size_t)((1 + K + KR) * p->npieces) + 1, sizeof(emac_fold));
+  folds = (emac_fold *)calloc((size_t)((1 + K + KR + nodes) * p->npieces) + 1, sizeof(emac_fold));
   if (!slot0 || !stride || !xslot || !ops || !folds) {
     free(slot0);
     free(stride);
@@ -627,6 +628,10 @@ static int program_nodes(const emac_plan *p, const emac_node_sched *ns, int node
         hn = bit ? hn - h0 : h0;
         ko = hlo;
         kl = hn;
+      }
+      if (single) { /* this task's share of the chunk (see below) */
+        ko = off + len * task / nodes;
+        kl = off + len * (task + 1) / nodes - ko;
       }
       for (i = 0; i < ns->radix[st] - 1; i++) {
         total = (total + 15) / 16 * 16;
@@ -736,8 +741,57 @@ static int program_nodes(const emac_plan *p, const emac_node_sched *ns, int node
       if (hlen[1 - bit] > 0)
         ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | la, partner, 0, EMAC_BUF_RECV, hoff[1 - bit] * ts, hlen[1 - bit] * ts};
     }
+  /* One reduce-scatter step over every node (N(-(N-1) ...)): every element's value is ONE fold
+     of the N node partials, in the order its line's task gives (r_{N-2}, own, r_0, ..., r_{N-3}
+     with r_i = task (l + i + 1) mod N, the last-step rule below), whichever node computes it. So
+     the work is shared out evenly instead: task t folds the t-th N-th of every rank's chunk, cut
+     at the line boundaries inside it, each piece with its line's leaf order; the finished shares
+     go to every node in the first copying allgather leg. Every rank sends and receives
+     (N-1)/N of its chunk each way. */
+  for (pc = 0; single && pc < p->npieces; pc++) {
+    const long off = p->chunk_off[(size_t)pc * R + me_pos], len = p->chunk_len[(size_t)pc * R + me_pos];
+    const long mo = off + len * task / nodes, ml = off + len * (task + 1) / nodes - mo;
+    int u, x;
+    for (u = 0, x = 0; u < nodes; u++) { /* the other tasks' shares to them, their partials of mine */
+      const long uo = off + len * u / nodes, ul = off + len * (u + 1) / nodes - uo;
+      const int gp = ns->task_node[u] * R + me;
+      if (u == task) continue;
+      if (ul > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS, gp, 1, EMAC_BUF_RECV, uo * ts, ul * ts};
+      if (ml > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS, gp, 0, EMAC_BUF_STAGE, xslot[(size_t)pc * nx + x], ml * ts};
+      x++;
+    }
+    for (t = 0; t < nodes && ml > 0; t++) { /* my share, line by line */
+      long a, b, so, sl;
+      int order[EMAC_MAX_NODES], n = 0, l;
+      emac_fold *f;
+      task_lines(ns, count, t, t + 1, &a, &b);
+      clip(a, b, mo, mo + ml, &so, &sl);
+      if (sl <= 0) continue;
+      order[n++] = (t + nodes - 1) % nodes;
+      order[n++] = t;
+      for (i = 0; i < nodes - 2; i++) order[n++] = (t + i + 1) % nodes;
+      f = &folds[nf++];
+      f->piece = pc;
+      f->offset = so * ts;
+      f->count = sl;
+      f->nleaf = nodes;
+      f->leg = EMAC_LEG_NODES_FOLD;
+      for (l = 0; l < nodes; l++) {
+        const int u2 = order[l]; /* the task whose partial this leaf is */
+        f->buf[l] = u2 == task ? EMAC_BUF_RECV : EMAC_BUF_STAGE;
+        f->loff[l] = u2 == task ? so * ts : xslot[(size_t)pc * nx + (u2 < task ? u2 : u2 - 1)] + (so - mo) * ts;
+      }
+    }
+    for (u = 0; u < nodes; u++) { /* the finished shares, to and from every node */
+      const long uo = off + len * u / nodes, ul = off + len * (u + 1) / nodes - uo;
+      const int gp = ns->task_node[u] * R + me;
+      if (u == task) continue;
+      if (ml > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG, gp, 1, EMAC_BUF_RECV, mo * ts, ml * ts};
+      if (ul > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG, gp, 0, EMAC_BUF_RECV, uo * ts, ul * ts};
+    }
+  }
   /* otherwise the lines are followed as the reference lays them out */
-  for (G = nodes, st = 0; !halving && st < K; G /= ns->radix[st], st++) {
+  for (G = nodes, st = 0; !halving && !single && st < K; G /= ns->radix[st], st++) {
     const int rad = ns->radix[st], lg = st << EMAC_LEG_STEP_SHIFT, last = st == K - 1;
     int xs = 0, s2;
     Gn = G / rad;
@@ -835,7 +889,7 @@ static int program_nodes(const emac_plan *p, const emac_node_sched *ns, int node
      its g-block to the tasks (t + g (i + 1)) mod gnext of its block and receives from each of
      them the lines of its g-block -- the task at its own position there (NODES_AG | step << 8,
      run in this order) */
-  for (j = 0, g = gm; !halving && j < KA; g *= ns->agp_radix[j], j++) {
+  for (j = 0, g = gm; !halving && !single && j < KA; g *= ns->agp_radix[j], j++) {
     const int rad = ns->agp_radix[j], gnext = g * rad, lg = j << EMAC_LEG_STEP_SHIFT;
     for (pc = 0; pc < p->npieces; pc++) {
       const long off = p->chunk_off[(size_t)pc * R + me_pos], len = p->chunk_len[(size_t)pc * R + me_pos];

@@ -270,3 +270,19 @@ def test_node_ports_program_over_gloo(world, nodes, ports, cases):
         p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs)
     assert [f for r in results for f in r] == []
+
+
+def test_single_step_node_ports_program_is_balanced():
+    """One reduce-scatter step over every node ("3(-2 2)"): each rank trades an equal share of its
+    chunk -- (N-1)/N of it each way -- whatever lines the chunk lies in, and its folds follow the
+    lines inside its share."""
+    nodes, R, count = 3, 4, 3 * 4 * 1000 + 7
+    for rank in range(nodes * R):
+        ops, folds, _ = emac.comm_program_nodes(nodes, R, rank, count, emac.FLOAT, "6;1 -4 4", ports=[-2, 2])
+        chunk = [f for f in folds if f[3] == emac.LEG_FOLD][0][1]
+        sent = sum(o[5] for o in ops if o[0] == emac.LEG_NODES_RS and o[2]) // 4
+        got = sum(o[5] for o in ops if o[0] == emac.LEG_NODES_RS and not o[2]) // 4
+        assert abs(sent - 2 * chunk / 3) <= 2 and abs(got - 2 * chunk / 3) <= 2, (rank, chunk, sent, got)
+        node_folds = [f for f in folds if f[3] == emac.LEG_NODES_FOLD]
+        assert node_folds and all(len(f[2]) == nodes for f in node_folds)
+        assert abs(sum(f[1] for f in node_folds) - chunk / 3) <= 1
