@@ -286,3 +286,20 @@ def test_single_step_node_ports_program_is_balanced():
         node_folds = [f for f in folds if f[3] == emac.LEG_NODES_FOLD]
         assert node_folds and all(len(f[2]) == nodes for f in node_folds)
         assert abs(sum(f[1] for f in node_folds) - chunk / 3) <= 1
+
+
+@pytest.mark.parametrize("nodes,ports,code", [
+    (4, [-1, -1], emac.ERROR_UNSUPPORTED),      # ends in a reduce-scatter port: reduce_scatter_core
+    (4, [-1, 2, 1], emac.ERROR_ARG),            # allgather radices 3 x 2 != 4 nodes
+    (4, [-3, 1, 1, 1], emac.ERROR_ARG),         # allgather radices multiply to 8
+    (6, [-1, 2, 1], None), (4, [3], None), (4, [1, 1], None), (8, [-1, -1, -1, 1, 1, 1], None),
+    (4, [-1, 2, 1, -1], emac.ERROR_UNSUPPORTED),  # a reduce-scatter port after the allgather ports
+])
+def test_node_ports_validation(nodes, ports, code):
+    """The inter-node list is checked as allreduce_core needs it (emac_node_sched_build)."""
+    if code is None:
+        emac.comm_program_nodes(nodes, 2, 0, 1000, emac.FLOAT, "6;1 -2 2", ports=ports)
+        return
+    with pytest.raises(emac.ExtMpiError) as e:
+        emac.comm_program_nodes(nodes, 2, 0, 1000, emac.FLOAT, "6;1 -2 2", ports=ports)
+    assert e.value.code == code
