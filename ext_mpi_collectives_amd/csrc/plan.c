@@ -585,7 +585,11 @@ static int program_nodes(const emac_plan *p, const emac_node_sched *ns, int node
     halving &= ns->radix[st] == 2;
   }
   for (j = 0; j < KR; j++) nx += ns->red_radix[j] - 1;
-  for (j = 0; j < KA; j++) nx += ns->agp_radix[j] - 1; /* (bounds the copy ops below) */
+  for (j = 0; j < KA; j++) {
+    nx += ns->agp_radix[j] - 1; /* (bounds the copy ops below) */
+    halving &= ns->agp_radix[j] == 2;
+  }
+  halving &= KA == K; /* the halves come back in K radix-2 copying steps */
   single = !halving && K == 1 && KR == 0; /* one reduce-scatter step over every node */
   me_pos = p->rank_pos[me];
   g0 = node * R; /* global rank of this node's first rank */

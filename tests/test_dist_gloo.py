@@ -254,6 +254,9 @@ def test_ipc_bootstrap_over_gloo_without_gpu(world):
     (4, 4, [1, 1], [(emac.DOUBLE, 9001, "6;1 -1 1")]),
     (6, 6, [-1, 2, 1], [(emac.FLOAT, 12001, "6;1 -1 1")]),
     (6, 3, [2], [(emac.FLOAT, 12001, "6;1 -2 2")]),
+    # radix-2 reduce-scatter steps with other allgather radices: the lines are followed
+    (4, 4, [-1, -1, 3], [(emac.FLOAT, 20011, "6;1 -1 1")]),
+    (8, 8, [-1, -1, -1, 3, 1], [(emac.FLOAT, 20011, "6;1 -1 1")]),
 ])
 def test_node_ports_program_over_gloo(world, nodes, ports, cases):
     """Several ports per step (EXT_MPI_NUM_PORTS "N(-p ... p ...)", radix-3/4 node steps, mixed

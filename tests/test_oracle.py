@@ -488,7 +488,9 @@ def _allreduce_core_literal(partials, ports):
                                          (9, [-2, -2, 2, 2]), (8, [-1, -1, -1, 1, 1, 1]), (5, [-4, 4]),
                                          # allgather steps that reduce (README: 4(3), 4(-1 1 1), 4(1 1))
                                          (4, [3]), (4, [-1, 1, 1]), (4, [1, 1]), (3, [2]), (6, [-1, 2, 1]),
-                                         (8, [-1, 3, 1]), (6, [2, 1]), (2, [1])])
+                                         (8, [-1, 3, 1]), (6, [2, 1]), (2, [1]),
+                                         # radix-2 reduce-scatter steps, other allgather radices
+                                         (4, [-1, -1, 3]), (8, [-1, -1, -1, 3, 1])])
 def test_node_ports_against_literal_line_tables(oracle, nodes, ports):
     """The oracle's inter-node restatement (ref_emulate_node_ports) against an independent,
     literal replay of allreduce_core's line tables: bitwise for float (association observable)."""
