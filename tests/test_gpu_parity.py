@@ -464,7 +464,10 @@ def test_comm_many_nodes_loopback_vs_oracle(oracle, R, nodes, copyin, code):
                                                    # allgather steps that reduce (README 4(3), 4(-1 1 1))
                                                    (4, 4, [3], "6;1 -1 1"), (8, 4, [-1, 1, 1], "6;1 -2 2"),
                                                    (8, 4, [1, 1], "6;1 -2 2"), (6, 6, [-1, 2, 1], "6;1 -1 1"),
-                                                   (6, 3, [2], "6;1 -2 2")])
+                                                   (6, 3, [2], "6;1 -2 2"),
+                                                   # radix-2 reduce-scatter steps, other allgather radices
+                                                   (4, 4, [-1, -1, 3], "6;1 -1 1"),
+                                                   (16, 8, [-1, -1, -1, 3, 1], "6;1 -2 2")])
 @pytest.mark.parametrize("code", [emac.FLOAT, emac.DOUBLE, emac.INT])
 def test_comm_node_ports_loopback_vs_oracle(oracle, R, nodes, ports, copyin, code):
     """Several ports per step (radix 3-5 node steps, mixed radices): every task trades its
