@@ -467,7 +467,8 @@ def test_comm_many_nodes_loopback_vs_oracle(oracle, R, nodes, copyin, code):
                                                    (6, 3, [2], "6;1 -2 2"),
                                                    # radix-2 reduce-scatter steps, other allgather radices
                                                    (4, 4, [-1, -1, 3], "6;1 -1 1"),
-                                                   (16, 8, [-1, -1, -1, 3, 1], "6;1 -2 2")])
+                                                   (16, 8, [-1, -1, -1, 3, 1], "6;1 -2 2"),
+                                                   (16, 16, [-15, 15], "6;1 -1 1")])  # 16 leaves
 @pytest.mark.parametrize("code", [emac.FLOAT, emac.DOUBLE, emac.INT])
 def test_comm_node_ports_loopback_vs_oracle(oracle, R, nodes, ports, copyin, code):
     """Several ports per step (radix 3-5 node steps, mixed radices): every task trades its
