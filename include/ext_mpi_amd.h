@@ -121,12 +121,14 @@ int ext_mpi_amd_set_stream(int handle, void *hip_stream);
 #define EXT_MPI_AMD_LEG_STAGE_OUT 16     /* D2H of host receive buffers */
 #define EXT_MPI_AMD_LEG_STAGE 17         /* both staging copies */
 /* COMM form over several nodes (ext_mpi_amd_comm_set_node_ports), between the fold and the allgather: */
-#define EXT_MPI_AMD_LEG_NODES_RS 32      /* per step: lines traded with the column peers of the other nodes */
-#define EXT_MPI_AMD_LEG_NODES_FOLD 64    /* per step: the kept lines' partials folded */
-#define EXT_MPI_AMD_LEG_NODES_AG 128     /* finished lines sent back, last step first */
+#define EXT_MPI_AMD_LEG_NODES_RS 32      /* per exchange step: lines traded with the other nodes' column peers */
+#define EXT_MPI_AMD_LEG_NODES_FOLD 64    /* per exchange step: the lines' partials folded */
+#define EXT_MPI_AMD_LEG_NODES_AG 128     /* per copying allgather step: finished lines sent on */
 #define EXT_MPI_AMD_LEG_ALL 255
 /* legs | EXT_MPI_AMD_LEG_STEP(s): the node legs of step s alone (a testing transport driving the
-   steps in lock-step); without it every step runs, in order */
+   steps in lock-step; s counts the exchange steps -- reduce-scatter steps, then allgather steps
+   that reduce -- for NODES_RS / NODES_FOLD, and the copying allgather steps for NODES_AG);
+   without it every step runs, in order */
 #define EXT_MPI_AMD_LEG_STEP(s) (((s) + 1) << 8)
 int ext_mpi_amd_start_legs(int handle, int legs);
 
