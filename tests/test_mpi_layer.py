@@ -95,14 +95,17 @@ def test_mpi_logical_nodes_without_gpu(tmp_path, n, ports, want):
     assert res and res[0].startswith(want), out
 
 
-@pytest.mark.parametrize("ports,want", [
-    ("2(-1_1)", "RESULT no-device"),          # the one-port schedule over the 2 nodes: the engine
-    ("-1_1", "RESULT no-device"),
-    ("2(-2_2)", "RESULT pmpi"),               # radix 3 over 2 nodes: PMPI_Allreduce
-    ("4(-1_-1_1_1)", "RESULT pmpi"),          # another node count: PMPI_Allreduce
-    ("1(-1)", "RESULT pmpi"),                 # a one-node row on a two-node communicator
+@pytest.mark.parametrize("n,ports,want", [
+    (3, "3(-2_2)", "RESULT no-device"),       # one radix-3 step over 3 nodes (ext_mpi_allreduce_blocking_3_1.txt)
+    (3, "3(2)", "RESULT no-device"),          # reduction inside the allgather step
+    (3, "3(-1_1)", "RESULT pmpi"),            # radix 2 over 3 nodes: PMPI_Allreduce
+    (2, "2(-1_1)", "RESULT no-device"),       # the one-port schedule over the 2 nodes: the engine
+    (2, "-1_1", "RESULT no-device"),
+    (2, "2(-2_2)", "RESULT pmpi"),            # radix 3 over 2 nodes: PMPI_Allreduce
+    (2, "4(-1_-1_1_1)", "RESULT pmpi"),       # another node count: PMPI_Allreduce
+    (2, "1(-1)", "RESULT pmpi"),              # a one-node row on a two-node communicator
 ])
-def test_mpi_blocking_two_nodes_without_gpu(tmp_path, ports, want):
+def test_mpi_blocking_two_nodes_without_gpu(tmp_path, n, ports, want):
     """Blocking MPI_Allreduce on two logical nodes of one rank reads
     ext_mpi_allreduce_blocking_2_1.txt (<nodes>_<cores per node>, ext_mpi_native_blocking.c:225-230):
     a row naming the one-port schedule over these nodes goes to the engine (ERROR_DEVICE without a
@@ -111,8 +114,8 @@ def test_mpi_blocking_two_nodes_without_gpu(tmp_path, ports, want):
     if torch.cuda.is_available():
         pytest.skip("GPU present")
     exe = _build(tmp_path)
-    (tmp_path / "ext_mpi_allreduce_blocking_2_1.txt").write_text(f"8 1 {ports} 6;1_-1_1\n")
-    res, out = _run(exe, 2, [1000, "i", "host", "blocking"], cwd=str(tmp_path),
+    (tmp_path / f"ext_mpi_allreduce_blocking_{n}_1.txt").write_text(f"8 1 {ports} 6;1_-1_1\n")
+    res, out = _run(exe, n, [1000, "i", "host", "blocking"], cwd=str(tmp_path),
                     env={"EXT_MPI_BLOCKING": "1", "EXT_MPI_NUM_TASKS_PER_SOCKET": "1"})
     assert res and res[0].startswith(want), out
 
