@@ -505,3 +505,28 @@ def test_node_ports_against_literal_line_tables(oracle, nodes, ports):
     if nodes == 3:  # the association differs per line: observable, so pinned by the statement
         s = [np.float32([1e8]), np.float32([1.0]), np.float32([-1e8])]
         assert oracle.allreduce_nodes(s, "6;1 -1 1", 3, ports=ports)[0][0] == _allreduce_core_literal(s, ports)[0][0]
+
+
+@pytest.mark.parametrize("R,m", [(8, 4), (8, 2), (6, 3), (6, 2), (4, 2), (12, 4), (12, 3), (16, 4)])
+def test_subsplit_fold_order_independent_statement(oracle, R, m):
+    """Independent statement of a two-level sub-split "6;1 -m m 1 m 1 -B B" (B = R / m) from
+    reduce_copies_one_socket (reduce_copyin.c:970-1084), composed of single-level Allreduces
+    (themselves pinned by the reference's printed schedules). ext_mpi_rank_order over the one
+    leading negative factor leaves the positions as node ranks (:375-394 copies its permutation
+    back only when more factors follow), so level 0 folds over the strided ranks {i B + g}
+    (ranks_loc, :976-981), member i ending with chunk i of group g's sum (ext_mpi_sizes_displs
+    over m); level 1 folds, over the contiguous ranks {c B + i} (ranks_loci, :1003-1007) --
+    member c of every group i -- chunk c of those group sums. Bitwise for float and double."""
+    B = R // m
+    copyin = f"6;1 -{m} {m} 1 {m} 1 -{B} {B}"
+    rng = np.random.default_rng(R * 7 + m)
+    for dt in (np.float32, np.float64):
+        for count in (1, 7, 1000 + R, 4099):
+            sends = [((rng.random(count) * 2 - 1) * 10.0 ** rng.integers(-4, 5, count)).astype(dt) for _ in range(R)]
+            blocks = [oracle.allreduce(sends[g::B], f"6;1 -{m} {m}")[0] for g in range(B)]
+            sizes = [count // m + (c < count % m) for c in range(m)]
+            lo = np.concatenate([[0], np.cumsum(sizes)]).astype(int)
+            want = np.concatenate([oracle.allreduce([blk[lo[c]:lo[c + 1]] for blk in blocks], f"6;1 -{B} {B}")[0]
+                                   if lo[c + 1] > lo[c] else blocks[0][lo[c]:lo[c]] for c in range(m)])
+            for out in oracle.allreduce(sends, copyin):
+                assert np.array_equal(out, want), (R, m, dt, count)
