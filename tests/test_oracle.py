@@ -322,17 +322,17 @@ def test_many_nodes_pairwise_tree(oracle):
 
 
 def _rank_order(size, factors, ranks):
-    """ext_mpi_rank_order (reduce_copyin.c:375-394), literally."""
-    if not factors:
-        return ranks
+    """ext_mpi_rank_order (reduce_copyin.c:375-394), literally: the permutation lands in `ranks`
+    only through the recursive copy-back (:383-393), so a single factor leaves `ranks` as it is."""
+    if len(factors) <= 1:
+        return list(ranks)
     f0, blk = abs(factors[0]), size // abs(factors[0])
     new = [0] * size
     for i in range(blk):
         for j in range(f0):
             new[i + j * blk] = ranks[i * f0 + j]
-    if len(factors) > 1:
-        for j in range(f0):
-            new[j * blk:(j + 1) * blk] = _rank_order(blk, factors[1:], new[j * blk:(j + 1) * blk])
+    for j in range(f0):
+        new[j * blk:(j + 1) * blk] = _rank_order(blk, factors[1:], new[j * blk:(j + 1) * blk])
     return new
 
 
@@ -507,26 +507,56 @@ def test_node_ports_against_literal_line_tables(oracle, nodes, ports):
         assert oracle.allreduce_nodes(s, "6;1 -1 1", 3, ports=ports)[0][0] == _allreduce_core_literal(s, ports)[0][0]
 
 
-@pytest.mark.parametrize("R,m", [(8, 4), (8, 2), (6, 3), (6, 2), (4, 2), (12, 4), (12, 3), (16, 4)])
-def test_subsplit_fold_order_independent_statement(oracle, R, m):
-    """Independent statement of a two-level sub-split "6;1 -m m 1 m 1 -B B" (B = R / m) from
+def _level_copyin(radices):
+    return "6;1 " + " ".join(f"-{r}" for r in radices) + " " + " ".join(str(r) for r in reversed(radices))
+
+
+def _nest_statement(oracle, data, levels):
+    """Sum under the sub-split nest `levels` (radix chains, one per level) of the inputs `data`
+    at the positions of one reduce_copies_one_socket call (reduce_copyin.c:970-1084): the level
+    folds the members {i g + j} (ranks_loc, :976-981; g = positions / members) with the
+    single-level schedule of its radices -- a single-level Allreduce whose own rank order puts
+    member q at node rank perm[q] -- and the rest of the nest runs, without a further rank
+    order, over the positions {c g + i} (ranks_loci, :1003-1007) on chunk c of the group sums."""
+    m = int(np.prod(levels[0]))
+    g = len(data) // m
+    perm = _rank_order(m, [-r for r in levels[0]], list(range(m)))
+    blocks = []
+    for j in range(g):
+        arr = [None] * m
+        for q in range(m):
+            arr[perm[q]] = data[q * g + j]
+        blocks.append(oracle.allreduce(arr, _level_copyin(levels[0]))[0])
+    if len(levels) == 1:
+        return blocks[0]
+    count = len(data[0])
+    lo = np.concatenate([[0], np.cumsum([count // m + (c < count % m) for c in range(m)])]).astype(int)
+    return np.concatenate([_nest_statement(oracle, [b[lo[c]:lo[c + 1]] for b in blocks], levels[1:])
+                           if lo[c + 1] > lo[c] else blocks[0][:0] for c in range(m)])
+
+
+@pytest.mark.parametrize("levels", [((4,), (2,)), ((2,), (4,)), ((3,), (2,)), ((2,), (3,)), ((2,), (2,)),
+                                    ((4,), (3,)), ((3,), (4,)), ((4,), (4,)), ((2,), (2,), (2,)),
+                                    ((2,), (3,), (2,)), ((4,), (2,), (2,)), ((2,), (2,), (4,)),
+                                    ((2, 2), (2,)), ((3,), (2, 2)), ((4,), (2, 2)), ((2, 2), (4,)),
+                                    ((3, 2), (2,)), ((2, 3), (2, 2)), ((2, 2), (2,), (2,))])
+def test_subsplit_fold_order_independent_statement(oracle, levels):
+    """Independent statement of a sub-split nest "6;1 <level 0> 1 <members> 1 <level 1> ..." from
     reduce_copies_one_socket (reduce_copyin.c:970-1084), composed of single-level Allreduces
-    (themselves pinned by the reference's printed schedules). ext_mpi_rank_order over the one
-    leading negative factor leaves the positions as node ranks (:375-394 copies its permutation
-    back only when more factors follow), so level 0 folds over the strided ranks {i B + g}
-    (ranks_loc, :976-981), member i ending with chunk i of group g's sum (ext_mpi_sizes_displs
-    over m); level 1 folds, over the contiguous ranks {c B + i} (ranks_loci, :1003-1007) --
-    member c of every group i -- chunk c of those group sums. Bitwise for float and double."""
-    B = R // m
-    copyin = f"6;1 -{m} {m} 1 {m} 1 -{B} {B}"
-    rng = np.random.default_rng(R * 7 + m)
+    (themselves pinned by the reference's printed schedules). The node's positions are
+    ext_mpi_rank_order over level 0's radices (:1495-1504), identity for one radix (:383-393);
+    level 0 folds over the positions {i g + j}, member i ending with chunk i of that group's sum
+    (ext_mpi_sizes_displs over the members); the next level folds, over the positions {c g + i}
+    -- member c of every group -- chunk c of those group sums, and so on. Bitwise for float and
+    double."""
+    R = int(np.prod([np.prod(lv) for lv in levels]))
+    parts = [" ".join(f"-{r}" for r in lv) + " " + " ".join(str(r) for r in reversed(lv)) for lv in levels]
+    copyin = "6;1 " + "".join(f"{p} 1 {int(np.prod(lv))} 1 " for p, lv in zip(parts[:-1], levels[:-1])) + parts[-1]
+    pos = _rank_order(R, [-r for r in levels[0]], list(range(R)))
+    rng = np.random.default_rng(R * 7 + len(levels))
     for dt in (np.float32, np.float64):
         for count in (1, 7, 1000 + R, 4099):
             sends = [((rng.random(count) * 2 - 1) * 10.0 ** rng.integers(-4, 5, count)).astype(dt) for _ in range(R)]
-            blocks = [oracle.allreduce(sends[g::B], f"6;1 -{m} {m}")[0] for g in range(B)]
-            sizes = [count // m + (c < count % m) for c in range(m)]
-            lo = np.concatenate([[0], np.cumsum(sizes)]).astype(int)
-            want = np.concatenate([oracle.allreduce([blk[lo[c]:lo[c + 1]] for blk in blocks], f"6;1 -{B} {B}")[0]
-                                   if lo[c + 1] > lo[c] else blocks[0][lo[c]:lo[c]] for c in range(m)])
+            want = _nest_statement(oracle, [sends[pos[q]] for q in range(R)], levels)
             for out in oracle.allreduce(sends, copyin):
-                assert np.array_equal(out, want), (R, m, dt, count)
+                assert np.array_equal(out, want), (copyin, dt, count)
