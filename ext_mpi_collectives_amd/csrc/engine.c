@@ -90,6 +90,7 @@ typedef struct {
   unsigned long slot_epoch[EMAC_SYNC_SLOTS][2]; /* a slot's epochs continue across its handles */
   ipc_mirror *mirrors;
   int nmirrors;
+  int cross_device; /* some peer runs on another device: release to system scope before phase 0 */
 } emac_comm;
 
 /* Loopback groups: every rank of the communicator lives in this process; the i-th handle a
@@ -167,7 +168,10 @@ typedef struct {
   int nmapped;
   int fused; /* whole Allreduce in one launch (emac_gpu_fold_fused) */
   void *ev_release; /* system-scope release recorded before every phase-0 barrier */
-  emac_launch pull; /* every other owner's result copied into this rank's receive buffer */
+  emac_launch pull; /* every owner's result copied from its outbox into this rank's receive buffer */
+  void *outbox;     /* this rank's owner chunks' results (pool memory, exported to the peers) */
+  size_t outbox_bytes;
+  int done_collective; /* some rank exported caller memory: Done agrees with every peer */
   int nodes;            /* COMM form over several nodes: the node legs run (emac_comm_program_nodes) */
   emac_node_sched ns;   /* ... under this inter-node schedule */
   emac_launch xfold[2 * EMAC_MAX_NODE_STEPS]; /* ... and, per exchange step, the fold of the lines' partials */
@@ -188,6 +192,7 @@ static int new_handle_slot(void) {
 
 static void ipc_unmap(void *base);
 static void mirror_free(emac_handle *h, void *p);
+static void ipc_mirror_put(emac_comm *cm, void *p);
 
 static void pipe_free(emac_pipe *pp) {
   int p;
@@ -232,6 +237,7 @@ static void release(emac_handle *h) {
     if (h->recv_reg[r]) emac_gpu_host_unregister(h->user_recv[r]);
   }
   for (r = 0; r < h->nmapped; r++) ipc_unmap(h->mapped[r]);
+  if (h->outbox) ipc_mirror_put(&comms[h->comm], h->outbox);
   emac_gpu_event_destroy(h->ev_release);
   for (r = 0; r <= EXT_MPI_AMD_LEG_ALL; r++) emac_gpu_graph_destroy(h->graph[r]);
   if (h->kind == KIND_IPC && h->slot_held) {
@@ -246,7 +252,6 @@ static void release(emac_handle *h) {
 }
 
 static int ipc_mirror_get(emac_comm *cm, void **p, size_t bytes);
-static void ipc_mirror_put(emac_comm *cm, void *p);
 
 static int mirror_alloc(emac_handle *h, void **p) {
   if (h->kind == KIND_IPC) return ipc_mirror_get(&comms[h->comm], p, h->bytes);
@@ -260,12 +265,13 @@ static void mirror_free(emac_handle *h, void *p) {
     emac_gpu_free(p);
 }
 
-/* A buffer the handle can use in place: device memory, and in the IPC form also exportable
-   (emac_gpu_ipc_exportable) and long enough for the set-up probe (R bytes). Anything else gets
-   a device mirror. */
-static int in_place_ok(const emac_handle *h, const void *p) {
+/* A buffer the handle can use in place: device memory, and in the IPC form, for a buffer the
+   peers read (the send buffer; in place, the one buffer), also exportable
+   (emac_gpu_ipc_exportable). The receive buffer of the IPC form is never exported: peers never
+   touch it. Anything else gets a device mirror. */
+static int in_place_ok(const emac_handle *h, const void *p, int peers_read) {
   if (!emac_gpu_is_device_pointer(p)) return 0;
-  return h->kind != KIND_IPC || (h->bytes >= (size_t)comms[h->comm].size && emac_gpu_ipc_exportable(p));
+  return h->kind != KIND_IPC || !peers_read || comms[h->comm].size == 1 || emac_gpu_ipc_exportable(p);
 }
 
 /* Page-locking a caller's host buffer is opt-in (EXT_MPI_AMD_HOST_REGISTER=1; never in the IPC
@@ -299,7 +305,7 @@ static int map_buffers(emac_handle *h, int r, const void *send, void *recv) {
   void *dv;
   h->user_send[r] = (void *)send;
   h->user_recv[r] = recv;
-  if (in_place_ok(h, recv)) {
+  if (in_place_ok(h, recv, send == recv)) {
     h->drecv[r] = recv;
   } else if (host_direct(h, recv, &dv)) {
     h->drecv[r] = dv;
@@ -311,7 +317,7 @@ static int map_buffers(emac_handle *h, int r, const void *send, void *recv) {
   }
   if (send == recv) {
     h->dsend[r] = h->drecv[r];
-  } else if (in_place_ok(h, send)) {
+  } else if (in_place_ok(h, send, 1)) {
     h->dsend[r] = (void *)send;
   } else if (host_direct(h, send, &dv)) {
     h->dsend[r] = dv;
@@ -742,9 +748,11 @@ typedef struct {
   long extent; /* bytes of the exported allocation: the importer's mapping must match */
   unsigned long long buf_id; /* the exporter's allocation id (0: unknown) */
   int status;
-  int in_place;  /* [0]: the receive buffer is the send buffer */
   int refused;   /* [0]: the runtime refused to export one of this rank's buffers */
-  unsigned char probe[EMAC_MAX_RANKS]; /* original first R bytes of the buffer (ipc_exchange) */
+  int caller;    /* [0]: the exported send buffer is caller memory (not a library mirror) */
+  long len;      /* bytes the peers access (the sample spans them) */
+  unsigned char sample[EMAC_SAMPLE_BYTES]; /* the exporter's own read of the buffer (ipc_exchange) */
+  unsigned char uuid[16];                  /* communicator set-up: the exporter's device */
   unsigned char free_slots[EMAC_SYNC_SLOTS / 8]; /* handle set-up: slots this rank can use */
 } ipc_export;
 
@@ -789,9 +797,13 @@ static int ipc_sync_exchange(emac_comm *cm, int rc, ipc_export *all) {
       mine.buf_id = emac_gpu_buffer_id(b0);
     }
     mine.status = rc == 0;
+    if (!rc) emac_gpu_device_uuid(mine.uuid);
     if (cm->ag(cm->ag_ctx, &mine, all, (long)sizeof(ipc_export))) return EMAC_ERR_TRANSPORT;
     for (r = 0; r < R; r++)
       if (!all[r].status) rc = rc ? rc : EMAC_ERR_TRANSPORT;
+    cm->cross_device = 0;
+    for (r = 0; !rc && r < R; r++)
+      if (memcmp(all[r].uuid, mine.uuid, 16)) cm->cross_device = 1;
     for (r = 0; !rc && r < R; r++) {
       if (r == cm->rank) {
         cm->peer_sync[r] = cm->sync;
@@ -894,19 +906,31 @@ int ext_mpi_amd_comm_init_ipc(int rank, int size, ext_mpi_amd_allgather_fn allga
   return 0;
 }
 
-/* The runtime's IPC handle of an allocation is a function of the exporter's address and size,
-   and an export can resolve to OLD memory: when a buffer is freed while a peer still maps it and
-   a new one is allocated at the same address, the new handle equals the old one and importing it
-   maps the old (still referenced) memory -- or the export is refused. Measured with 4 processes
-   (stale leaves read, fan-out stores lost); nothing in the handle tells the cases apart. So every
-   mapping is validated with a write probe before it is used: each importer q flips byte q of
-   every peer buffer through its mapping, and each exporter checks that its own buffers show the
-   flips (then restores them). A buffer some peer failed to reach is re-placed in a fresh pooled
-   mirror (new address, staged in and out on the handle's stream) and the exchange repeats.
-   The probe touches the first R bytes of each buffer during set-up only: the buffers must not be
-   written by the device while the set-up runs. */
-#define EMAC_PROBE_FLIP 0x5A
-#define EMAC_IPC_ATTEMPTS 16 /* 8 processes re-placing a freed-and-reused 64 MiB buffer took up to 4 */
+/* Mapping the peers' buffers (the reference: cuda_shmem.c:218-299 opens every peer's cudaIpc
+   handle once at init; EXT_MPI_Done closes them after a node barrier, ext_mpi_native.c:269-387 with
+   cuda_shmem.c:190-216,301-314). What can go wrong, and what rules it out here:
+   * The runtime's IPC handle of an allocation is a function of the exporter's address and size:
+     an allocation freed while a peer still maps it and re-allocated at the same address exports
+     the same handle, and importing it resolves to the OLD memory. The rule of the reference rules
+     it out: a peer-mapped handle's Done is collective (ext_mpi_amd_done: every rank closes its
+     mappings, then the ranks agree), so no caller allocation is freed under a mapping as long as
+     the caller keeps its buffers until Done, and the library's own exported memory (outboxes,
+     mirrors, synchronisation blocks) is pooled per communicator and freed only by the collective
+     communicator free.
+   * Peers never WRITE caller memory, at set-up or later: the send buffer is only read (the fold's
+     leaves), each rank's results go to its own library-owned outbox, and every rank pulls the
+     results into its own receive buffer, which is never exported. A stale mapping could therefore
+     only feed wrong leaves, never overwrite anything.
+   * Every mapping is still validated, read-only: the exporter samples its buffer
+     (emac_gpu_sample: 8 spots of 8 bytes) and publishes the sample with its handle; every importer
+     samples the same spots through its mapping. A mismatch, a mapping the runtime refuses or one
+     shorter than the exporter's allocation sends the buffer to a fresh pooled mirror (send
+     buffer: staged in on the handle's stream; outbox: a new one) and the exchange repeats.
+     EXT_MPI_AMD_IPC_FORCE_MIRROR=1 re-places every exported buffer in the first round, so the
+     mirror path runs deterministically (tests/test_gpu_ipc.py).
+   The set-up reads the caller's send buffer: the device is synchronised first, so a kernel still
+   filling it cannot make the exporter's and the importers' samples differ. */
+#define EMAC_IPC_ATTEMPTS 16
 
 static void ipc_mirror_poison(emac_comm *cm, void *p) {
   int i;
@@ -914,175 +938,199 @@ static void ipc_mirror_poison(emac_comm *cm, void *p) {
     if (cm->mirrors[i].p == p) cm->mirrors[i].busy = 2; /* kept, never handed out again */
 }
 
-/* re-place this rank's send (recv_side 0) or receive buffer in a fresh mirror (in place: both) */
-static int ipc_remirror(emac_handle *h, int recv_side) {
+/* re-place this rank's send buffer (in place: the one buffer) in a fresh mirror; `poison`: the old
+   mirror is kept out of the pool for good (a peer could not map or validate it) */
+static int ipc_remirror_send(emac_handle *h, int poison) {
   emac_comm *cm = &comms[h->comm];
   const int same = h->dsend[0] == h->drecv[0];
-  unsigned char *flag;
-  void **d, *p;
+  unsigned char *flag = same ? &h->recv_mirror[0] : &h->send_mirror[0];
+  void *p;
   int rc;
-  if (same) recv_side = 1; /* in place: one buffer, held as the receive side (stage_in / stage_out) */
-  flag = recv_side ? &h->recv_mirror[0] : &h->send_mirror[0];
-  d = recv_side ? &h->drecv[0] : &h->dsend[0];
-  if (*flag) ipc_mirror_poison(cm, *d);
   if ((rc = ipc_mirror_get(cm, &p, h->bytes))) return rc;
-  *d = p;
+  if (*flag && poison) ipc_mirror_poison(cm, h->dsend[0]);
+  else if (*flag) ipc_mirror_put(cm, h->dsend[0]);
+  h->dsend[0] = p;
+  if (same) h->drecv[0] = p; /* in place: staged in and out through the mirror */
   *flag = 1;
-  if (same) h->dsend[0] = p;
   return 0;
 }
 
-/* own probe bytes: the first R bytes of the send buffer, then of the receive buffer */
-static int ipc_probe_own(emac_handle *h, int R, int in_place, unsigned char *vals, int store) {
-  void *p[EMAC_PROBE_MAX];
-  int t, q, n = 0;
-  for (t = 0; t < (in_place ? 1 : 2); t++)
-    for (q = 0; q < R; q++) p[n++] = (char *)(t ? h->drecv[0] : h->dsend[0]) + q;
-  return store ? emac_gpu_poke(p, vals, n, h->stream) : emac_gpu_peek((const void *const *)p, vals, n, h->stream);
+static int ipc_new_outbox(emac_handle *h, int poison) {
+  emac_comm *cm = &comms[h->comm];
+  void *old = h->outbox;
+  int rc = ipc_mirror_get(cm, &h->outbox, h->outbox_bytes);
+  if (old && poison) ipc_mirror_poison(cm, old);
+  else if (old) ipc_mirror_put(cm, old);
+  return rc;
 }
 
+/* Byte offset of every piece of position `pos`'s owner chunk inside that rank's outbox: pieces
+   back to back, each at the 16-byte phase its elements have in the message (so the fold's leaves,
+   the outbox and the receive buffer agree on vector alignment). Returns the outbox bytes. */
+static long outbox_layout(const emac_plan *p, int pos, long *at) {
+  const int R = p->nranks;
+  long cur = 0;
+  int pc;
+  for (pc = 0; pc < p->npieces; pc++) {
+    const long off = p->chunk_off[(size_t)pc * R + pos], len = p->chunk_len[(size_t)pc * R + pos];
+    const long a = ((cur + 15) & ~15L) + ((off * p->tsize) & 15);
+    if (at) at[pc] = a;
+    if (len > 0) cur = a + len * p->tsize;
+  }
+  return cur;
+}
+
+enum { IPC_SEND = 0, IPC_OUTBOX = 1, IPC_NBUF = 2 };
+
 /* One exchange of the IPC set-up (collective whatever failed locally before: `rc`). On return
-   psend/precv hold the validated peer mappings, all[] the exports, and stale[t] tells that this
-   rank's buffer t (0 send, 1 receive) was refused for export or missed by some peer. */
-static int ipc_exchange(emac_handle *h, emac_comm *cm, int rc, int empty, ipc_export *all, void **psend, void **precv,
-                        int *stale) {
-  ipc_export mine[2];
-  unsigned char orig[2 * EMAC_MAX_RANKS], seen[2 * EMAC_MAX_RANKS];
-  int R = cm->size, r, t, q, any_refused = 0, agreed;
-  const int in_place = h->dsend[0] == h->drecv[0];
+   peer[t][r] holds the validated mapping of rank r's buffer t (send, outbox), all[] the exports,
+   and miss[t] a bit per exporter whose buffer t this rank could not map or validate. */
+static int ipc_exchange(emac_handle *h, emac_comm *cm, int rc, int empty, ipc_export *all, void *(*peer)[EMAC_MAX_RANKS],
+                        unsigned *miss) {
+  ipc_export mine[IPC_NBUF];
+  const int R = cm->size;
+  void *own[IPC_NBUF] = {h->dsend[0], h->outbox};
+  const long len[IPC_NBUF] = {(long)h->bytes, (long)h->outbox_bytes};
+  int r, t, any_refused = 0;
   memset(mine, 0, sizeof(mine));
-  stale[0] = stale[1] = 0;
-  if (!rc && !empty) rc = ipc_probe_own(h, R, in_place, orig, 0);
-  for (t = 0; t < 2 && !rc && !empty; t++) {
-    void *d = t ? h->drecv[0] : h->dsend[0], *b0;
-    const int er = emac_gpu_ipc_export(d, mine[t].handle, &mine[t].offset);
+  miss[0] = miss[1] = 0;
+  for (t = 0; t < IPC_NBUF && !rc && !empty; t++) {
+    void *b0;
+    const int er = emac_gpu_ipc_export(own[t], mine[t].handle, &mine[t].offset);
     if (er == EMAC_ERR_TRANSPORT)
-      stale[t] = 1; /* refused by the runtime: re-place it */
+      mine[0].refused = 1; /* refused by the runtime: this round is void, the buffer is re-placed */
     else
       rc = er;
-    mine[t].extent = emac_gpu_alloc_extent(d, &b0);
+    mine[t].extent = emac_gpu_alloc_extent(own[t], &b0);
     mine[t].buf_id = emac_gpu_buffer_id(b0);
-    memcpy(mine[t].probe, orig + (in_place ? 0 : t) * R, (size_t)R);
+    mine[t].len = len[t];
   }
-  if (in_place) stale[0] = stale[1] = stale[0] | stale[1];
-  mine[0].in_place = in_place;
-  mine[0].refused = stale[0] | stale[1];
+  if (!rc && !empty) {
+    unsigned char smp[IPC_NBUF * EMAC_SAMPLE_BYTES];
+    rc = emac_gpu_sample((const void *const *)own, len, IPC_NBUF, smp, h->stream);
+    for (t = 0; !rc && t < IPC_NBUF; t++) memcpy(mine[t].sample, smp + t * EMAC_SAMPLE_BYTES, EMAC_SAMPLE_BYTES);
+  }
   for (r = 0; r < EMAC_SYNC_SLOTS; r++)
     if (!cm->slot_used[r]) mine[0].free_slots[r >> 3] |= (unsigned char)(1u << (r & 7));
   mine[0].status = rc == 0;
+  mine[0].caller = !empty && !h->send_mirror[0] && !(h->dsend[0] == h->drecv[0] && h->recv_mirror[0]);
   if (cm->ag(cm->ag_ctx, mine, all, (long)sizeof(mine))) return EMAC_ERR_TRANSPORT;
   for (r = 0; r < R; r++) {
-    if (!all[2 * r].status && !rc) rc = EMAC_ERR_TRANSPORT;
-    any_refused |= all[2 * r].refused;
+    if (!all[IPC_NBUF * r].status && !rc) rc = EMAC_ERR_TRANSPORT;
+    any_refused |= all[IPC_NBUF * r].refused;
   }
-  if (empty || any_refused) return rc; /* nothing to map, or this attempt is void on every rank */
-  /* map every peer buffer; one that cannot be mapped whole is left unprobed, so that its
-     exporter sees the miss and re-places it */
+  if (rc || empty) return rc;
+  if (any_refused) { /* void on every rank: the refusing exporter re-places its buffers */
+    if (mine[0].refused) miss[0] = miss[1] = 1u << cm->rank;
+    return 0;
+  }
   {
-    void *pk[EMAC_PROBE_MAX];
-    unsigned char vals[EMAC_PROBE_MAX];
-    int n = 0;
-    for (r = 0; r < R; r++) {
-      psend[r] = precv[r] = NULL;
-      if (r == cm->rank) {
-        psend[r] = h->dsend[0];
-        precv[r] = h->drecv[0];
-        continue;
-      }
-      for (t = 0; t < 2 && !rc; t++) {
-        const ipc_export *e = &all[2 * r + t];
+    const void *pk[IPC_NBUF * EMAC_MAX_RANKS];
+    long pl[IPC_NBUF * EMAC_MAX_RANKS];
+    int who[IPC_NBUF * EMAC_MAX_RANKS], n = 0;
+    unsigned char seen[IPC_NBUF * EMAC_MAX_RANKS * EMAC_SAMPLE_BYTES];
+    for (r = 0; r < R; r++)
+      for (t = 0; t < IPC_NBUF; t++) {
+        const ipc_export *e = &all[IPC_NBUF * r + t];
         void *base, *ext_base;
         long extent;
-        if (t == 1 && all[2 * r].in_place) {
-          precv[r] = psend[r];
+        peer[t][r] = NULL;
+        if (r == cm->rank) {
+          peer[t][r] = own[t];
           continue;
         }
-        base = ipc_map_peer(e->handle, e->buf_id, e->extent);
-        if (!base) continue;
+        miss[t] |= 1u << r; /* until validated below */
+        if (!(base = ipc_map_peer(e->handle, e->buf_id, e->extent))) continue;
         h->mapped[h->nmapped++] = base;
-        /* a mapping the runtime can describe must hold the peer's whole buffer (one it cannot
-           describe is taken at the exporter's word; the probe still checks it is reachable) */
+        /* a mapping the runtime can describe must hold the peer's whole allocation (one it cannot
+           describe is taken at the exporter's word; the sample still checks it) */
         extent = emac_gpu_alloc_extent(base, &ext_base);
         if (extent < 0) {
           extent = e->extent;
           ext_base = base;
         }
-        if (ext_base != base || extent != e->extent || e->offset < 0 || e->offset + (long)h->bytes > extent ||
-            e->offset + R > extent)
-          continue; /* short mapping: never launched over */
-        (t ? precv : psend)[r] = (char *)base + e->offset;
-        pk[n] = (char *)base + e->offset + cm->rank;
-        vals[n++] = e->probe[cm->rank] ^ EMAC_PROBE_FLIP;
-        if (getenv("EXT_MPI_AMD_DEBUG_IPC") && atoi(getenv("EXT_MPI_AMD_DEBUG_IPC")) >= 2) { /* every mapping */
-          char hex[2 * EMAC_IPC_HANDLE_BYTES + 1];
-          for (q = 0; q < EMAC_IPC_HANDLE_BYTES; q++) sprintf(hex + 2 * q, "%02x", e->handle[q]);
-          fprintf(stderr, "ipc rank %d: peer %d %s handle %s id %llu base %p extent %ld offset %ld bytes %zu\n",
-                  cm->rank, r, t ? "recv" : "send", hex, e->buf_id, base, extent, e->offset, h->bytes);
-        }
+        if (ext_base != base || extent != e->extent || e->offset < 0 || e->offset + e->len > extent) continue;
+        peer[t][r] = (char *)base + e->offset;
+        pk[n] = peer[t][r];
+        pl[n] = e->len;
+        who[n++] = IPC_NBUF * r + t;
       }
+    if ((rc = emac_gpu_sample(pk, pl, n, seen, h->stream))) return rc;
+    for (t = 0; t < n; t++) {
+      const int q = who[t] / IPC_NBUF, b = who[t] % IPC_NBUF;
+      if (!memcmp(seen + t * EMAC_SAMPLE_BYTES, all[who[t]].sample, EMAC_SAMPLE_BYTES))
+        miss[b] &= ~(1u << q);
+      else
+        peer[b][q] = NULL;
     }
-    if (!rc) rc = emac_gpu_poke(pk, vals, n, h->stream);
+    if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
+      for (r = 0; r < R; r++)
+        for (t = 0; t < IPC_NBUF; t++)
+          if ((miss[t] >> r) & 1)
+            fprintf(stderr, "ipc rank %d: cannot map or validate peer %d's %s\n", cm->rank, r, t ? "outbox" : "send buffer");
   }
-  /* every rank's flips have landed */
-  agreed = ipc_agree(cm, rc == 0);
-  if (!rc) rc = agreed;
-  if (rc) return rc;
-  if ((rc = ipc_probe_own(h, R, in_place, seen, 0))) return rc;
-  for (t = 0; t < (in_place ? 1 : 2); t++)
-    for (q = 0; q < R; q++)
-      if (q != cm->rank && seen[t * R + q] != (orig[t * R + q] ^ EMAC_PROBE_FLIP)) {
-        stale[t] = 1;
-        if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
-          fprintf(stderr, "ipc rank %d: peer %d does not reach my %s buffer\n", cm->rank, q, t ? "recv" : "send");
-      }
-  if (in_place) stale[1] = stale[0];
-  return ipc_probe_own(h, R, in_place, orig, 1); /* restore */
+  return 0;
 }
 
 /* Collective: every rank runs the same exchanges whatever failed locally before (`rc`), so that
    a local failure cannot unmatch the sequence. */
 static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf, void *recvbuf, int rc) {
-  ipc_export all[2 * EMAC_MAX_RANKS];
-  void *psend[EMAC_MAX_RANKS], *precv[EMAC_MAX_RANKS];
+  ipc_export all[IPC_NBUF * EMAC_MAX_RANKS];
+  void *peer[IPC_NBUF][EMAC_MAX_RANKS];
+  long *at = NULL;
   emac_bucket *b = NULL;
   int R = cm->size, r, t, pc, nb = 0, c, slot, attempt;
-  const int empty = h->bytes == 0; /* same count on every rank: nothing to map or fold */
-  /* The write probe below reads, flips and restores the first R bytes of this rank's buffers: work
-     the application still has in flight on them (e.g. the kernel filling the send buffer on its
-     own stream, legal before a persistent init) must have landed first, or the restore would
-     write back bytes read before it (measured: the first two elements of a freshly filled send
-     buffer stayed wrong for the handle's lifetime, 8 processes on one MI355X). */
+  const int empty = h->bytes == 0 || R == 1; /* same on every rank: nothing to map */
+  const char *fe = getenv("EXT_MPI_AMD_IPC_FORCE_MIRROR");
+  const int force = fe && atoi(fe) > 0;
+  /* the samples read the send buffer: work the application still has in flight on it must have
+     landed (the reference synchronises the device before every barrier, ext_mpi_native_exec.c:556-558) */
   if (!rc && !empty) rc = emac_gpu_device_sync();
-  if (!rc && !empty) rc = map_buffers(h, 0, sendbuf, recvbuf);
+  if (!rc && h->bytes) rc = map_buffers(h, 0, sendbuf, recvbuf);
+  if (!rc && !empty) {
+    h->outbox_bytes = (size_t)outbox_layout(&h->plan, h->me_pos, NULL);
+    if (h->outbox_bytes < 16) h->outbox_bytes = 16;
+    rc = ipc_new_outbox(h, 0);
+  }
   for (attempt = 0;; attempt++) {
-    int stale[2], v[3], allv[3 * EMAC_MAX_RANKS], again = 0;
-    rc = ipc_exchange(h, cm, rc, empty, all, psend, precv, stale);
+    unsigned miss[IPC_NBUF], v[1 + IPC_NBUF], allv[(1 + IPC_NBUF) * EMAC_MAX_RANKS], stale[IPC_NBUF] = {0, 0};
+    int again = 0;
+    rc = ipc_exchange(h, cm, rc, empty, all, peer, miss);
+    if (!rc && force && attempt == 0 && !empty) miss[0] = miss[1] = 1u << cm->rank; /* re-place mine */
     v[0] = rc == 0;
-    v[1] = stale[0];
-    v[2] = stale[1];
+    v[1] = miss[0];
+    v[2] = miss[1];
     if (cm->ag(cm->ag_ctx, v, allv, (long)sizeof(v))) return EMAC_ERR_TRANSPORT;
     for (r = 0; r < R; r++) {
-      if (!allv[3 * r]) return rc ? rc : EMAC_ERR_TRANSPORT;
-      again |= allv[3 * r + 1] | allv[3 * r + 2];
+      if (!allv[(1 + IPC_NBUF) * r]) return rc ? rc : EMAC_ERR_TRANSPORT;
+      for (t = 0; t < IPC_NBUF; t++) {
+        const unsigned m = allv[(1 + IPC_NBUF) * r + 1 + t];
+        again |= m != 0;
+        stale[t] |= (m >> cm->rank) & 1u;
+      }
     }
     if (!again) break;
     if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
       fprintf(stderr, "ipc rank %d: attempt %d: re-placing%s%s\n", cm->rank, attempt, stale[0] ? " send" : "",
-              stale[1] ? " recv" : "");
+              stale[1] ? " outbox" : "");
     if (attempt == EMAC_IPC_ATTEMPTS - 1) {
       fprintf(stderr, "ext_mpi_amd: rank %d: peer mappings still unreachable after %d set-up rounds (%s%s)\n",
-              cm->rank, EMAC_IPC_ATTEMPTS, stale[0] ? "send " : "", stale[1] ? "recv" : "");
+              cm->rank, EMAC_IPC_ATTEMPTS, stale[0] ? "send " : "", stale[1] ? "outbox" : "");
       return EMAC_ERR_TRANSPORT;
     }
     for (r = 0; r < h->nmapped; r++) ipc_unmap(h->mapped[r]);
     h->nmapped = 0;
-    if (stale[0]) rc = ipc_remirror(h, 0);
-    if (!rc && stale[1] && h->dsend[0] != h->drecv[0]) rc = ipc_remirror(h, 1);
+    /* a forced round's buffers were fine: they go back to the pool */
+    if (stale[0]) rc = ipc_remirror_send(h, !(force && attempt == 0));
+    if (!rc && stale[1]) rc = ipc_new_outbox(h, !(force && attempt == 0));
   }
+  /* Done is collective iff some rank's exported send buffer is caller memory (the same verdict on
+     every rank): library memory is never freed under a mapping anyway (ext_mpi_amd_done) */
+  for (r = 0; r < R; r++) h->done_collective |= all[IPC_NBUF * r].caller;
   /* the synchronisation slot: the lowest one free on every rank (ranks may have released
      their handles in different orders) */
   for (slot = 0; slot < EMAC_SYNC_SLOTS; slot++) {
-    for (r = 0; r < R && (all[2 * r].free_slots[slot >> 3] >> (slot & 7)) & 1; r++);
+    for (r = 0; r < R && (all[IPC_NBUF * r].free_slots[slot >> 3] >> (slot & 7)) & 1; r++);
     if (r == R) break;
   }
   if (slot == EMAC_SYNC_SLOTS) return EMAC_ERR_MALLOC; /* same verdict on every rank */
@@ -1091,33 +1139,39 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
   h->slot_held = 1;
   cm->err[slot] = 0; /* a failure of the slot's previous handle that nobody waited for */
   {
-    /* EXT_MPI_AMD_IPC_RELEASE=1: an explicit system-scope release (command processor, every XCD)
-       before each phase-0 barrier. Off by default: the packet boundary between the application's
-       producer kernel and the barrier launch already writes back every XCD's L2 (device memory
-       only is ever exported), and the event cost 5 us per Start with 2 processes, 9 us with 4
-       (profiles/r02_ipc_latency_release.json). */
+    /* A system-scope release (command processor, every XCD's L2) before each phase-0 barrier,
+       by default when some peer sits on another device: its loads of this rank's send buffer go
+       over xGMI to HBM and see nothing an L2 still holds. Ranks sharing one device read through
+       the same L2s and the packet boundary after the producer kernel suffices, so the release
+       (5 us per Start with 2 processes, 9 us with 4: profiles/r02_ipc_latency_release.json) is
+       off there. EXT_MPI_AMD_IPC_RELEASE=1 / 0 forces it on / off. */
     const char *e = getenv("EXT_MPI_AMD_IPC_RELEASE");
-    if (R > 1 && e && atoi(e) > 0 && (rc = emac_gpu_event_create_release(&h->ev_release))) return rc;
+    const int rel = e ? atoi(e) > 0 : cm->cross_device;
+    if (R > 1 && rel && (rc = emac_gpu_event_create_release(&h->ev_release))) return rc;
   }
   h->epoch[0] = cm->slot_epoch[slot][0];
   h->epoch[1] = cm->slot_epoch[slot][1];
-  if (empty) return 0;
+  if (!h->bytes) return 0;
   /* this rank's owner chunks (reduce_copyin): leaves from the peers' send buffers in the plan's
-     fold order, the result into this rank's own receive buffer. Then (reduce_copyout) every
-     other owner's result is PULLED from that owner's receive buffer into this rank's: a receive
-     buffer is only ever written by its own rank. A peer's stores into it through the peer's
-     mapping did not invalidate copies of its lines in the owner's L2s (measured: stale -1s read
-     by the owner's next kernel after filling the buffer, 8 processes on one MI355X), whereas
-     every remote access of the pull is a system-coherent load. */
+     fold order, the result into this rank's outbox (its receive buffer when alone). Then
+     (reduce_copyout) every owner's result is PULLED from that owner's outbox into this rank's
+     receive buffer, this rank's own last: each rank writes only memory it owns. */
   c = h->me_pos;
-  b = (emac_bucket *)calloc((size_t)h->plan.npieces * (size_t)R, sizeof(emac_bucket));
-  if (!b) return EMAC_ERR_MALLOC;
+  b = (emac_bucket *)calloc((size_t)h->plan.npieces * (size_t)(R + 1), sizeof(emac_bucket));
+  at = (long *)calloc((size_t)h->plan.npieces, sizeof(long));
+  if (!b || !at) {
+    free(b);
+    free(at);
+    return EMAC_ERR_MALLOC;
+  }
+  if (R > 1) outbox_layout(&h->plan, c, at);
   for (pc = 0; pc < h->plan.npieces; pc++) {
     long off = h->plan.chunk_off[(size_t)pc * R + c], len = h->plan.chunk_len[(size_t)pc * R + c];
     emac_bucket *bk = &b[nb];
     if (len <= 0) continue;
-    for (t = 0; t < R; t++) bk->src[t] = psend[h->plan.leaf_rank[c][t]];
-    bk->dst[0] = precv[cm->rank];
+    for (t = 0; t < R; t++) bk->src[t] = R > 1 ? peer[IPC_SEND][h->plan.leaf_rank[c][t]] : h->dsend[0];
+    /* place_bucket moves every pointer by the chunk's message offset */
+    bk->dst[0] = R > 1 ? (char *)h->outbox + at[pc] - off * h->plan.tsize : (char *)h->drecv[0];
     bk->ndst = 1;
     place_bucket(bk, R, off, len, h->plan.tsize);
     nb++;
@@ -1126,40 +1180,39 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
   h->fan = R > 1 ? 2 : 0; /* peer-mapped: system-coherent launch */
   if (R > 1) {
     /* the pull, owners in the order after this rank (next owner first), so that at any moment
-       the ranks' loads head for different GPUs' links */
+       the ranks' loads head for different GPUs' links; this rank's own chunk (local) last */
     emac_bucket *pb = b + nb;
     int np = 0, k;
-    for (pc = 0; pc < h->plan.npieces; pc++)
-      for (k = 1; k < R; k++) {
-        const int q = (cm->rank + k) % R, cq = h->plan.rank_pos[q];
+    for (k = 1; k <= R; k++) {
+      const int q = (cm->rank + k) % R, cq = h->plan.rank_pos[q];
+      outbox_layout(&h->plan, cq, at);
+      for (pc = 0; pc < h->plan.npieces; pc++) {
         long off = h->plan.chunk_off[(size_t)pc * R + cq], len = h->plan.chunk_len[(size_t)pc * R + cq];
         if (len <= 0) continue;
-        pb[np].src[0] = precv[q];
-        pb[np].dst[0] = precv[cm->rank];
+        pb[np].src[0] = (char *)peer[IPC_OUTBOX][q] + at[pc] - off * h->plan.tsize;
+        pb[np].dst[0] = h->drecv[0];
         pb[np].ndst = 1;
         place_bucket(&pb[np], 1, off, len, h->plan.tsize);
         np++;
       }
+    }
     if ((rc = upload_launch_as(h, &h->pull, pb, np, 1, 0))) { /* a copy: the schedule of nsrc 1 for every op */
       free(b);
+      free(at);
       return rc;
     }
   }
-
+  free(at);
   {
-    /* small messages: barrier, fold and barrier in one launch (EXT_MPI_AMD_IPC_FUSED_MAX bytes
-       per rank, default 1 MiB; 0 disables) */
+    /* small messages: barrier, fold, barrier and pull in one launch (EXT_MPI_AMD_IPC_FUSED_MAX
+       bytes per rank, default 1 MiB; 0 disables) */
     const char *fm = getenv("EXT_MPI_AMD_IPC_FUSED_MAX");
     const long fused_max = fm ? atol(fm) : (1L << 20);
     h->fused = R > 1 && (long)h->bytes <= fused_max;
   }
   if (getenv("EXT_MPI_AMD_DEBUG_IPC") && (attempt > 0 || atoi(getenv("EXT_MPI_AMD_DEBUG_IPC")) >= 2))
-    fprintf(stderr, "ipc rank %d: own send %p recv %p bytes %zu, %d buckets, slot %d, %d attempt(s)\n", cm->rank,
-            h->dsend[0], h->drecv[0], h->bytes, nb, slot, attempt + 1);
-  if (getenv("EXT_MPI_AMD_DEBUG_IPC") && atoi(getenv("EXT_MPI_AMD_DEBUG_IPC")) >= 2)
-    for (t = 0; t < nb; t++)
-      fprintf(stderr, "ipc rank %d: bucket %d: src0 %p dst0 %p head %ld nvec %ld tail %ld scalar %d count %ld\n", cm->rank,
-              t, b[t].src[0], b[t].dst[0], b[t].head, b[t].nvec, b[t].tail, b[t].scalar, b[t].count);
+    fprintf(stderr, "ipc rank %d: own send %p recv %p outbox %p bytes %zu, %d buckets, slot %d, %d attempt(s)\n",
+            cm->rank, h->dsend[0], h->drecv[0], h->outbox, h->bytes, nb, slot, attempt + 1);
   rc = upload_buckets(h, b, nb);
   free(b);
   return rc;
@@ -1606,12 +1659,22 @@ int ext_mpi_amd_wait(int handle) {
   return rc ? rc : ipc_status(h);
 }
 
+/* Done of a peer-mapped handle over caller memory is collective over the communicator, as the
+   reference's (EXT_MPI_Done_native -> ext_mpi_gpu_destroy_shared_memory's node barrier,
+   cuda_shmem.c:190-216, then cudaIpcCloseMemHandle, :301-314): every rank closes its mappings of
+   the peers' buffers, then the ranks agree, so when Done returns no peer maps this rank's buffers
+   any more and the caller may free them (ipc_exchange). A handle whose exported buffers are all
+   library memory (mirrors, the MPI layer's scratch) is released locally: that memory returns to
+   the communicator's pool and is only freed by the collective communicator free. */
 int ext_mpi_amd_done(int handle) {
   emac_handle *h = get(handle);
+  int comm, collective;
   if (!h) return EMAC_ERR_ARG;
   handles[handle] = NULL;
+  comm = h->comm;
+  collective = h->kind == KIND_IPC && h->done_collective && comms[comm].used && comms[comm].size > 1;
   release(h);
-  return 0;
+  return collective ? ipc_agree(&comms[comm], 1) : 0;
 }
 
 void *ext_mpi_amd_stream(int handle) {

@@ -308,11 +308,13 @@ extern "C" {
 
 int ext_mpi_amd_gpu_malloc(void **p, size_t bytes) { return emac_gpu_malloc(p, bytes); }
 int ext_mpi_amd_gpu_free(void *p) { return emac_gpu_free(p); }
+// hipMemcpyDefault: the direction follows the pointers (unified addressing), so the MPI layer's
+// staging through device scratch also takes device-resident caller buffers
 int ext_mpi_amd_gpu_memcpy_hd(void *dst, const void *src, size_t bytes) {
-  return bytes ? ok(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice)) : 0;
+  return bytes ? ok(hipMemcpy(dst, src, bytes, hipMemcpyDefault)) : 0;
 }
 int ext_mpi_amd_gpu_memcpy_dh(void *dst, const void *src, size_t bytes) {
-  return bytes ? ok(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost)) : 0;
+  return bytes ? ok(hipMemcpy(dst, src, bytes, hipMemcpyDefault)) : 0;
 }
 int ext_mpi_amd_gpu_is_device_pointer(const void *p) { return emac_gpu_is_device_pointer(p); }
 int ext_mpi_amd_gpu_synchronize(void) { return emac_gpu_device_sync(); }

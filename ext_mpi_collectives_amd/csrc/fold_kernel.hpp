@@ -490,15 +490,16 @@ __device__ __forceinline__ void run_remote(const Work &w, const emac_codes &code
 //  phase 0 (ipc_sync.hpp): workgroup 0's first wave signals every peer, the first wave of EVERY
 //          workgroup waits for them (a workgroup folds only after it has seen every peer ready);
 //  fold:   this rank's owner chunks, leaves loaded from the peers' send buffers, the result
-//          stored (write-through) into this rank's own receive buffer only;
+//          stored (write-through) into this rank's own outbox only;
 //  phase 1: each workgroup drains its stores and counts itself in arrive[slot]; the last one
-//          signals the peers; every workgroup waits for every peer's signal;
-//  pull:   every other owner's result loaded from that owner's receive buffer and stored into
-//          this rank's own. The receive buffer is only ever written by its own rank: lines of it
-//          that this rank's L2s hold stay coherent with what the application reads next
-//          (measured: a peer's write into them through its mapping left stale lines in the
-//          reader's L2, 8 processes on one MI355X). The next Start's phase 0 keeps every owner
-//          from overwriting its result before the peers have pulled it.
+//          signals the peers and this rank itself (its own flag: every own chunk has landed);
+//          every workgroup waits for every peer's signal and for its own rank's;
+//  pull:   every owner's result (this rank's own too) loaded from that owner's outbox and stored
+//          into this rank's receive buffer. The receive buffer is only ever written by its own
+//          rank: lines of it that this rank's L2s hold stay coherent with what the application
+//          reads next (measured: a peer's write into them through its mapping left stale lines in
+//          the reader's L2, 8 processes on one MI355X). The next Start's phase 0 keeps every owner
+//          from overwriting its outbox before the peers have pulled it.
 // The grid never exceeds one workgroup per CU, so every workgroup is resident while any waits.
 template <typename T, int OP, int N, int U, int CH>
 __global__ __launch_bounds__(EMAC_BLOCK) void ipc_fused_kernel(Work fold, Work pull, emac_codes codes, NodeSync ns,
@@ -521,9 +522,9 @@ __global__ __launch_bounds__(EMAC_BLOCK) void ipc_fused_kernel(Work fold, Work p
     if (arrived == gridDim.x - 1) {  // the last workgroup: every owner chunk of this rank has landed
       // the next launch on this slot is stream-ordered behind this one
       if (threadIdx.x == 0) __hip_atomic_store(&ns.self->arrive[ns.slot], 0ul, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      wave_signal(ns, 1, epoch1);
+      wave_signal(ns, 1, epoch1, true);
     }
-    const bool in_time = wave_wait(ns, 1, epoch1);
+    const bool in_time = wave_wait(ns, 1, epoch1, true);
     const bool gave_up = peer_gave_up(ns);
     wave_report(ns, (in_time ? 0 : EMAC_SYNC_ERR_TIMEOUT) | (gave_up ? EMAC_SYNC_ERR_ABORTED : 0));
     if (threadIdx.x == 0) verdict = ok && in_time && !gave_up;

@@ -104,6 +104,13 @@ int emac_gpu_malloc_uncached(void **p, size_t bytes); /* zeroed, rounded up to E
 #define EMAC_PROBE_MAX (2 * EMAC_MAX_RANKS)
 int emac_gpu_poke(void *const *ptrs, const unsigned char *vals, int n, void *stream);
 int emac_gpu_peek(const void *const *ptrs, unsigned char *vals, int n, void *stream);
+/* read-only samples (IPC set-up): EMAC_SAMPLE_BYTES bytes of each of n buffers of lens[i] bytes
+   into out[i * EMAC_SAMPLE_BYTES ...] -- EMAC_SAMPLE_SPOTS spots of 8 bytes spread over the buffer
+   (the whole buffer, zero-padded, when shorter) -- system-coherent, complete on return */
+#define EMAC_SAMPLE_SPOTS 8
+#define EMAC_SAMPLE_BYTES (8 * EMAC_SAMPLE_SPOTS)
+int emac_gpu_sample(const void *const *ptrs, const long *lens, int n, unsigned char *out, void *stream);
+int emac_gpu_device_uuid(unsigned char *uuid); /* 16 bytes identifying the current device */
 int emac_gpu_host_alloc_mapped(void **p, size_t bytes); /* pinned, device-visible, zeroed */
 int emac_gpu_host_free(void *p);
 long emac_gpu_wallclock_hz(void);

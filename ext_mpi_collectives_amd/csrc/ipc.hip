@@ -9,18 +9,23 @@
 // launches on the rank's own stream and never returns to the host (one launch for small
 // messages: fold_kernel.hpp ipc_fused_kernel):
 //
-//   node_barrier(in)  -> fold over peer-mapped leaves, fan-out into every peer's recv -> node_barrier(out)
+//   node_barrier(in) -> fold of the owner chunks over the peers' mapped send buffers into this
+//   rank's library-owned result buffer ("outbox") -> node_barrier(out) -> pull of every owner's
+//   result from its outbox into this rank's receive buffer
 //
+// Peers only ever READ caller memory (the send buffers); nothing of the set-up or of a Start
+// writes through a mapping into memory the caller owns (engine.c ipc_exchange).
 // Visibility across GPUs: every XCD of a gfx950 has its own L2, and the L2 is neither written
 // back nor invalidated for other agents by plain stores/loads. Nothing here relies on where a
-// workgroup lands: the application's writes to this rank's buffers are released to system scope
-// by the command processor on every XCD before the phase-0 barrier (emac_gpu_event_create_release,
-// recorded by engine.c), the fold between the barriers is system-coherent by itself (sc0 sc1
-// loads, write-through stores drained before the phase-1 signal), and the flags live in
-// uncached device memory, written and polled with system-scope atomics: one 8-byte word per
-// (handle slot, phase, peer), holding the last epoch that peer signalled (ipc_sync.hpp). Every
-// wait is bounded by a wall-clock timeout that sets the slot's error word in pinned host memory
-// and lets the kernel end; a phase-0 timeout also cancels this rank's fold (emac_sync.go).
+// workgroup lands: when a peer sits on another device the application's writes to this rank's
+// send buffer are released to system scope by the command processor on every XCD before the
+// phase-0 barrier (emac_gpu_event_create_release, recorded by engine.c), the fold and the pull
+// are system-coherent by themselves (sc0 sc1 loads, write-through stores drained before the
+// next signal), and the flags live in uncached device memory, written and polled with
+// system-scope atomics: one 8-byte word per (handle slot, phase, peer), holding the last epoch
+// that peer signalled (ipc_sync.hpp). Every wait is bounded by a wall-clock timeout that sets the
+// slot's error word in pinned host memory and lets the kernel end; a phase-0 timeout also cancels
+// this rank's fold (the go[slot] word of ipc_sync.hpp).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -83,6 +88,28 @@ __global__ __launch_bounds__(64) void peek_kernel(ProbeSet a, unsigned char *out
   if (i < a.n) out[i] = *reinterpret_cast<volatile const unsigned char *>(a.p[i]);
 }
 
+// Read-only samples of the IPC set-up (engine.c ipc_exchange): workgroup j reads
+// EMAC_SAMPLE_BYTES bytes of buffer j -- EMAC_SAMPLE_SPOTS spots of 8 bytes spread evenly over
+// its `len` bytes (all of it when shorter) -- after a system-scope acquire, so an importer and
+// the exporter read the same memory whatever either process's L2s held before. Nothing is written
+// to the sampled memory.
+struct SampleSet {
+  const unsigned char *p[EMAC_PROBE_MAX];
+  long len[EMAC_PROBE_MAX];
+};
+
+__global__ __launch_bounds__(EMAC_SAMPLE_BYTES) void sample_kernel(SampleSet a, unsigned char *out) {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const int j = blockIdx.x, i = threadIdx.x;
+  const long len = a.len[j];
+  long at;
+  if (len <= EMAC_SAMPLE_BYTES)
+    at = i < len ? i : -1;
+  else
+    at = (len - 8) * (long)(i >> 3) / (EMAC_SAMPLE_SPOTS - 1) + (i & 7);
+  out[j * EMAC_SAMPLE_BYTES + i] = at >= 0 ? *reinterpret_cast<volatile const unsigned char *>(a.p[j] + at) : 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -118,6 +145,38 @@ int emac_gpu_peek(const void *const *ptrs, unsigned char *vals, int n, void *str
   if (!rc) rc = ok(hipStreamSynchronize(s));
   (void)hipFree(d);
   return rc;
+}
+
+int emac_gpu_sample(const void *const *ptrs, const long *lens, int n, unsigned char *out, void *stream) {
+  SampleSet a;
+  unsigned char *d = nullptr;
+  if (n < 0 || n > EMAC_PROBE_MAX) return EMAC_ERR_ARG;
+  if (!n) return 0;
+  memset(&a, 0, sizeof(a));
+  for (int i = 0; i < n; ++i) {
+    a.p[i] = static_cast<const unsigned char *>(ptrs[i]);
+    a.len[i] = lens[i];
+  }
+  if (hipMalloc(&d, (size_t)EMAC_SAMPLE_BYTES * EMAC_PROBE_MAX) != hipSuccess) return EMAC_ERR_MALLOC;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(sample_kernel, dim3((unsigned)n), dim3(EMAC_SAMPLE_BYTES), 0, s, a, d);
+  int rc = ok(hipGetLastError());
+  if (!rc) rc = ok(hipMemcpyAsync(out, d, (size_t)n * EMAC_SAMPLE_BYTES, hipMemcpyDeviceToHost, s));
+  if (!rc) rc = ok(hipStreamSynchronize(s));
+  (void)hipFree(d);
+  return rc;
+}
+
+int emac_gpu_device_uuid(unsigned char *uuid) {
+  int dev = 0;
+  hipUUID u;
+  memset(uuid, 0, 16);
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetUuid(&u, dev) != hipSuccess) {
+    clear_error("emac_gpu_device_uuid");
+    return EMAC_ERR_DEVICE;
+  }
+  memcpy(uuid, u.bytes, 16);
+  return 0;
 }
 
 int emac_gpu_ipc_export(const void *p, void *handle, long *offset) {

@@ -40,18 +40,20 @@ struct NodeSync {
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
-// lane q < nranks, q != me: store `epoch` into peer q's flag for this rank
-__device__ __forceinline__ void wave_signal(const NodeSync &s, int phase, unsigned long epoch) {
+// lane q < nranks, q != me: store `epoch` into peer q's flag for this rank (self_too: lane me
+// also into this rank's own flag for itself -- the fused launch's "every own chunk has landed")
+__device__ __forceinline__ void wave_signal(const NodeSync &s, int phase, unsigned long epoch, bool self_too = false) {
   const int q = lane_id();
-  if (q < s.nranks && q != s.me)
+  if (q < s.nranks && (q != s.me || self_too))
     __hip_atomic_store(&s.peers[q]->flags[s.slot][phase][s.me], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// lane q waits for peer q's flag to reach `epoch`; true (on every lane) iff every peer arrived in time
-__device__ __forceinline__ bool wave_wait(const NodeSync &s, int phase, unsigned long epoch) {
+// lane q waits for peer q's flag to reach `epoch` (self_too: lane me for this rank's own flag);
+// true (on every lane) iff every one arrived in time
+__device__ __forceinline__ bool wave_wait(const NodeSync &s, int phase, unsigned long epoch, bool self_too = false) {
   const int q = lane_id();
   int late = 0;
-  if (q < s.nranks && q != s.me) {
+  if (q < s.nranks && (q != s.me || self_too)) {
     const unsigned long *f = &s.self->flags[s.slot][phase][q];
     const long t0 = wall_clock64();
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {

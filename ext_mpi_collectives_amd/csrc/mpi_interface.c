@@ -251,6 +251,7 @@ static int request_handle(const MPI_Request *r) {
 typedef struct {
   int ext_comm;
   int nodes;     /* comm_topology: 1, or the nodes of an RCCL communicator over several */
+  int nsize;     /* ranks per node */
   MPI_Comm boot; /* private duplicate the IPC bootstrap exchanges run on */
 } comm_attr;
 
@@ -311,24 +312,33 @@ static int env_ports(int nodes, const int **ports) {
   return 0;
 }
 
-/* `use_env`: EXT_MPI_NUM_PORTS governs the inter-node schedule (not when a blocking parameter
-   row, already checked by the caller, names it per handle) */
-static int node_comm(MPI_Comm comm, const void *devbuf, int use_env, int *ext_comm) {
+/* The engine communicator of `comm` (collective at its first use): *nodes / *nsize its node layout.
+   Over several nodes it starts with the default inter-node schedule; every handle sets its own
+   (EXT_MPI_NUM_PORTS or a blocking parameter row, ext_mpi_amd_comm_set_node_ports) before it is
+   made, so the first message size cannot decide the communicator's fate. `check_env`: refuse
+   (ERROR_UNSUPPORTED, nothing created) when EXT_MPI_NUM_PORTS names a schedule this path does not
+   take over these nodes -- the persistent path's verdict; the blocking path checks per call. */
+static int node_comm(MPI_Comm comm, const void *devbuf, int check_env, int *ext_comm, int *nodes_out,
+                     int *nsize_out) {
   comm_attr *a;
-  const int *ports = NULL;
   int flag, size, rank, nsize, nrank, device, ndev, rc, nodes;
   unsigned char id[EXT_MPI_AMD_UNIQUE_ID_BYTES];
   if (comm_keyval == MPI_KEYVAL_INVALID) return EXT_MPI_AMD_ERROR_ARG;
   PMPI_Comm_get_attr(comm, comm_keyval, &a, &flag);
   if (flag && a) {
     *ext_comm = a->ext_comm;
+    if (nodes_out) *nodes_out = a->nodes;
+    if (nsize_out) *nsize_out = a->nsize;
     return 0;
   }
   PMPI_Comm_size(comm, &size);
   PMPI_Comm_rank(comm, &rank);
   comm_topology(comm, &nodes, &nsize, &nrank);
   if (!nodes) return EXT_MPI_AMD_ERROR_UNSUPPORTED; /* other inter-node shapes: out of scope */
-  if (use_env && env_ports(nodes, &ports)) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
+  if (check_env && nodes > 1) {
+    const int *hp;
+    if (env_ports(nodes, &hp)) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
+  }
   ndev = ext_mpi_amd_gpu_device_count();
   device = ext_mpi_amd_gpu_device_of(devbuf);
   if (device < 0) device = ndev > 0 ? nrank % ndev : -1;
@@ -336,6 +346,7 @@ static int node_comm(MPI_Comm comm, const void *devbuf, int use_env, int *ext_co
   if (!a) return EXT_MPI_AMD_ERROR_MALLOC;
   a->boot = MPI_COMM_NULL;
   a->nodes = nodes;
+  a->nsize = nsize;
   if (!cfg_rccl && nodes == 1) { /* peer mappings reach the ranks of one node only */
     PMPI_Comm_dup(comm, &a->boot);
     /* collective even without a device: every rank reaches the same verdict */
@@ -349,7 +360,7 @@ static int node_comm(MPI_Comm comm, const void *devbuf, int use_env, int *ext_co
     if (rank == 0 && (rc = ext_mpi_amd_get_unique_id(id))) memset(id, 0, sizeof(id));
     PMPI_Bcast(id, EXT_MPI_AMD_UNIQUE_ID_BYTES, MPI_BYTE, 0, comm);
     rc = ndev > 0 ? ext_mpi_amd_comm_init(rank, size, id, device, ext_comm) : EXT_MPI_AMD_ERROR_DEVICE;
-    if (rc == 0 && nodes > 1 && (rc = ext_mpi_amd_comm_set_node_ports(*ext_comm, nodes, ports)))
+    if (rc == 0 && nodes > 1 && (rc = ext_mpi_amd_comm_set_node_ports(*ext_comm, nodes, NULL)))
       ext_mpi_amd_comm_free(*ext_comm);
     flag = rc == 0;
     PMPI_Allreduce(MPI_IN_PLACE, &flag, 1, MPI_INT, MPI_MIN, comm);
@@ -361,6 +372,8 @@ static int node_comm(MPI_Comm comm, const void *devbuf, int use_env, int *ext_co
   }
   a->ext_comm = *ext_comm;
   PMPI_Comm_set_attr(comm, comm_keyval, a);
+  if (nodes_out) *nodes_out = nodes;
+  if (nsize_out) *nsize_out = nsize;
   return 0;
 }
 
@@ -560,7 +573,7 @@ static int blocking_select_row(const bcomm *b, int side, long bytes) {
 static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int dtype, int op, int tsize, bcomm *b,
                               MPI_Comm comm) {
   size_t bytes = (size_t)count * (size_t)tsize, need, stride;
-  int on_dev, side, row, i, rc, slot = -1, in_place, rank, row_sockets = 0;
+  int on_dev, side, row, i, rc, slot = -1, in_place, rank, row_sockets = 0, staged;
   const char *copyin = NULL;
   const void *s;
   void *r;
@@ -586,17 +599,27 @@ static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int
   } else if (cfg_has_copyin) {
     copyin = cfg_copyin;
   }
+  /* without a row the communicator's own EXT_MPI_NUM_PORTS governs; one naming another node
+     count or a list this path does not take goes to PMPI (same verdict on every rank) */
+  if (row < 0 && b->nodes > 1) {
+    const int *hp;
+    if (env_ports(b->nodes, &hp)) return 1;
+  }
   if (b->status == 0) {
-    rc = node_comm(comm, recvbuf, row < 0, &b->ext_comm);
+    rc = node_comm(comm, recvbuf, 0, &b->ext_comm, NULL, NULL);
     b->status = rc == 0 ? 1 : rc == EXT_MPI_AMD_ERROR_UNSUPPORTED ? 2 : rc;
   }
   if (b->status != 1) return b->status == 2 ? 1 : b->status;
-  if (on_dev) {
+  /* Host buffers go through device scratch (no page-locking of caller memory that may be freed
+     between calls), and so do device buffers on the peer-mapped transport: a cached handle must
+     not keep mappings of caller allocations the application may free and re-allocate between two
+     calls (the reference hooks cudaFree for that, cuda_shmem.c); the scratch is library memory,
+     so dropping a cached handle is local on every rank (ext_mpi_amd_done). */
+  staged = !on_dev || !cfg_rccl;
+  if (!staged) {
     s = sendbuf;
     r = recvbuf;
   } else {
-    /* host buffers go through device scratch (no page-locking of caller memory that may be
-       freed between calls) */
     stride = (bytes + 255) & ~(size_t)255;
     need = in_place ? stride : 2 * stride;
     if (need < 256) need = 256;
@@ -647,25 +670,28 @@ static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int
     bcomm_drop(b, slot);
     e = &b->cache[slot];
     /* a parameter-file row names its own socket count (ext_mpi_native_blocking.c:189-290) and
-       inter-node ports; a handle keeps the schedule it was made with */
+       inter-node ports; a handle keeps the schedule it was made with. Both are restored on every
+       exit; a row whose ports the engine refuses (e.g. an allgather step crossing the
+       reduce-scatter groups) goes to PMPI like any row this path does not take. */
     const int prev_sockets = row_sockets > 0 ? ext_mpi_amd_set_num_sockets(row_sockets) : 0;
     const int *hp = NULL;
+    int pmpi = 0;
     if (b->nodes > 1) {
       if (row >= 0)
         hp = b->row[side][row].ports;
       else if (env_ports(b->nodes, &hp))
-        return 1;
-      if ((rc = ext_mpi_amd_comm_set_node_ports(b->ext_comm, b->nodes, hp))) return rc;
+        pmpi = 1;
+      if (!pmpi && ext_mpi_amd_comm_set_node_ports(b->ext_comm, b->nodes, hp)) pmpi = 1;
     }
-    rc = ext_mpi_amd_allreduce_init(s, r, count, dtype, op, b->ext_comm, copyin, &e->handle);
+    rc = pmpi ? 0 : ext_mpi_amd_allreduce_init(s, r, count, dtype, op, b->ext_comm, copyin, &e->handle);
     if (prev_sockets > 0) ext_mpi_amd_set_num_sockets(prev_sockets);
     if (b->nodes > 1) { /* back to the communicator's own (EXT_MPI_NUM_PORTS or the default) */
       if (env_ports(b->nodes, &hp)) hp = NULL;
       ext_mpi_amd_comm_set_node_ports(b->ext_comm, b->nodes, hp);
     }
-    if (rc) {
+    if (pmpi || rc) {
       e->handle = -1;
-      return rc;
+      return pmpi ? 1 : rc;
     }
     e->send = s;
     e->recv = r;
@@ -685,7 +711,7 @@ static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int
   e = &b->cache[slot];
   e->used = ++b->clock;
   if ((rc = ext_mpi_amd_start(e->handle)) || (rc = ext_mpi_amd_wait(e->handle))) return rc;
-  if (!on_dev && bytes && (rc = ext_mpi_amd_gpu_memcpy_dh(recvbuf, r, bytes))) return rc;
+  if (staged && bytes && (rc = ext_mpi_amd_gpu_memcpy_dh(recvbuf, r, bytes))) return rc;
   return 0;
 }
 
@@ -724,26 +750,28 @@ int EXT_MPI_Finalize(void) {
 
 int EXT_MPI_Allreduce_init(const void *sendbuf, void *recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
                            MPI_Comm comm, MPI_Info info, int *handle) {
-  int dtype = map_type(datatype), eop = map_op(op), ext_comm, rc, flag = 0, rank, tsize;
+  int dtype = map_type(datatype), eop = map_op(op), ext_comm, rc, flag = 0, rank, tsize, nodes = 1, nsize = 1;
   const char *copyin = NULL;
   char info_copyin[1024];
   *handle = -1;
   if (!initialised) EXT_MPI_Init();
   if (dtype < 0 || eop < 0 || count < 0) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
   if (sendbuf == MPI_IN_PLACE) sendbuf = recvbuf; /* ext_mpi.c:651-653 */
-  /* sockets change the partner encoding and the tree method's last roots (plan.h) */
-  if (cfg_num_sockets > 1) {
-    int size;
-    PMPI_Comm_size(comm, &size);
-    if (size % cfg_num_sockets) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
-  }
   if (cfg_has_copyin) {
     copyin = cfg_copyin;
   } else if (info != MPI_INFO_NULL) {
     PMPI_Info_get(info, "ext_mpi_copyin", (int)sizeof(info_copyin) - 1, info_copyin, &flag);
     if (flag) copyin = info_copyin;
   }
-  if ((rc = node_comm(comm, recvbuf, 1, &ext_comm))) return rc;
+  if ((rc = node_comm(comm, recvbuf, 1, &ext_comm, &nodes, &nsize))) return rc;
+  /* sockets change the partner encoding and the tree method's last roots (plan.h): they must
+     divide the ranks of a node */
+  if (cfg_num_sockets > 1 && nsize % cfg_num_sockets) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
+  if (nodes > 1) { /* this handle's inter-node schedule: EXT_MPI_NUM_PORTS or the default */
+    const int *hp;
+    if (env_ports(nodes, &hp)) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
+    if ((rc = ext_mpi_amd_comm_set_node_ports(ext_comm, nodes, hp))) return rc;
+  }
   PMPI_Type_size(datatype, &tsize);
   if (cfg_debug && (rc = known_answer_test(recvbuf, sendbuf == recvbuf, count, tsize, comm, ext_comm, copyin)))
     return rc;

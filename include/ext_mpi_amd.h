@@ -83,13 +83,15 @@ int ext_mpi_amd_comm_free(int comm);
  * device; point-to-point ops become device copies executed by the receiving rank. Run each leg
  * on every rank before the next one (ext_mpi_amd_start_legs). Not for production. */
 int ext_mpi_amd_comm_init_loopback(int size, int *comm_of_rank);
-/* Peer-mapped communicator: one rank per GPU, every rank's device send/recv buffers mapped into
- * every other rank with hipIpc (the reference's src/gpu/cuda_shmem.c:218-299 cudaIpc mapping),
- * the fold reading the peers' chunks over xGMI and storing the result into every peer's receive
- * buffer, node barriers as stream-ordered kernels. `allgather` is called collectively (same
- * order on every rank) at communicator and handle set-up only: it must gather `bytes` bytes from
- * every rank into `recv` in rank order (as PMPI_Allgather(send, bytes, MPI_BYTE, recv, bytes,
- * MPI_BYTE, comm)) and return 0; it must stay callable while the communicator lives. */
+/* Peer-mapped communicator: one rank per GPU, every rank's device send buffer mapped into every
+ * other rank with hipIpc (the reference's src/gpu/cuda_shmem.c:218-299 cudaIpc mapping), the
+ * owner's fold reading the peers' chunks over xGMI into a library-owned result buffer that every
+ * rank then pulls from into its own receive buffer (peers never write caller memory), node
+ * barriers as stream-ordered kernels. `allgather` is called collectively (same order on every
+ * rank) at communicator and handle set-up and at a handle's ext_mpi_amd_done: it must gather
+ * `bytes` bytes from every rank into `recv` in rank order (as PMPI_Allgather(send, bytes,
+ * MPI_BYTE, recv, bytes, MPI_BYTE, comm)) and return 0; it must stay callable while the
+ * communicator lives. */
 typedef int (*ext_mpi_amd_allgather_fn)(void *ctx, const void *send, void *recv, long bytes);
 int ext_mpi_amd_comm_init_ipc(int rank, int size, ext_mpi_amd_allgather_fn allgather, void *ctx, int device,
                               int *comm);
@@ -108,6 +110,12 @@ int ext_mpi_amd_comm_mfree(int comm, void *p);
 int ext_mpi_amd_start(int handle);
 int ext_mpi_amd_test(int handle); /* 1 complete, 0 in flight, <0 error */
 int ext_mpi_amd_wait(int handle);
+/* Release a handle. On a peer-mapped communicator of more than one rank whose handle maps some
+ * rank's caller-owned device send buffer this is collective, like the reference's EXT_MPI_Done (a
+ * node barrier, src/gpu/cuda_shmem.c:190-216): every rank must call it, in the same order as its
+ * other collective Done calls on that communicator, and once it returns no peer maps this rank's
+ * buffers -- they may be freed. Handles over library memory only (host buffers, staged through
+ * device mirrors) are released locally. */
 int ext_mpi_amd_done(int handle);
 void *ext_mpi_amd_stream(int handle); /* hipStream_t the handle runs on */
 /* Run later Starts on a caller-owned hipStream_t (e.g. to serialise several handles). */

@@ -1,4 +1,4 @@
-"""One rank of the peer-mapped (IPC) form, run as its own process by test_gpu_ipc.py.
+"""One rank of the peer-mapped (IPC) form, run as its own process by test_gpu_peer_mapped.py.
 
 Every rank runs the same cases in the same order; for each it regenerates every rank's input
 (seeded per rank), checks its own receive buffer bit for bit against the CPU oracle and prints
@@ -75,6 +75,17 @@ def fuzz_cases(R, n):
         in_place = in_place and host is not True  # the host branch below has no in-place form
         out.append((code, count, variants[int(rng.integers(len(variants)))], in_place, host, int(rng.integers(1, 3)), op))
     return out
+
+
+def _report_mismatch(rank, world, k, got, want):
+    """stderr: how many elements differ, the first few (index, got, want) and the owner chunks
+    (equal split) they fall in -- enough to tell a stale leaf from a lost pull"""
+    g, w = got.view(np.uint8).reshape(-1, got.itemsize), want.view(np.uint8).reshape(-1, want.itemsize)
+    bad = np.nonzero(np.any(g != w, axis=1))[0]
+    n = got.size
+    chunks = sorted({int(i * world // max(n, 1)) for i in bad[:1000]})
+    print(f"rank {rank}: case {k}: {bad.size} of {n} differ; first {bad[:6].tolist()} got {got[bad[:6]].tolist()} "
+          f"want {want[bad[:6]].tolist()}; owner chunks {chunks[:8]}", file=sys.stderr, flush=True)
 
 
 def timeout_recovery(rank, world):
@@ -176,7 +187,10 @@ def main():
                 assert L.ext_mpi_amd_gpu_memcpy_dh(got.ctypes.data, drecv, nbytes) == 0
             else:
                 got = hrecv if host else recv.cpu().numpy()
-            ok &= bool(np.array_equal(got.view(np.uint8), want.view(np.uint8)))
+            good = bool(np.array_equal(got.view(np.uint8), want.view(np.uint8)))
+            if not good and ok:
+                _report_mismatch(rank, world, k, got, want)
+            ok &= good
         emac.done(h)
         if os.environ.get("IPC_SYNC_AFTER_DONE"):  # diagnosis: surface an asynchronous fault at its case
             torch.cuda.synchronize()
@@ -187,6 +201,7 @@ def main():
         failures += not ok
         print(f"IPC rank {rank}/{world} case {k} code {code} op {op} count {count} '{copyin}' in_place={in_place} "
               f"host={host} x{repeats}: {'ok' if ok else 'MISMATCH'}", flush=True)
+    sections = os.environ.get("IPC_SECTIONS", "realloc,newdata,concurrent,recycle,recovery").split(",")
     if os.environ.get("IPC_CASES_ONLY"):
         emac.comm_free(comm)
         dist.barrier()
@@ -198,7 +213,7 @@ def main():
     # dropped its old mapping would import the old memory (stale leaves, lost fan-out).
     L, n = emac.lib(), 16 << 20
     ok = True
-    for it in range(4):
+    for it in range(4 if "realloc" in sections else 0):
         bufs = []
         for _ in range(2):
             p = ctypes.c_void_p()
@@ -226,7 +241,7 @@ def main():
     print(f"IPC rank {rank}/{world} re-allocated buffers: {'ok' if ok else 'MISMATCH'}", flush=True)
     # new send data before every Start (the fold must never see a previous iteration's lines)
     ok = True
-    for in_place in (False, True):
+    for in_place in ((False, True) if "newdata" in sections else ()):
         x = torch.empty(100003, device="cuda")
         y = x if in_place else torch.empty_like(x)
         h = emac.allreduce_init(x.data_ptr(), y.data_ptr(), x.numel(), emac.FLOAT, comm)
@@ -241,7 +256,7 @@ def main():
     print(f"IPC rank {rank}/{world} new data every Start: {'ok' if ok else 'MISMATCH'}", flush=True)
     # several handles in flight on separate streams, started in the same order on every rank
     hs, bufs = [], []
-    for j in range(3):
+    for j in range(3 if "concurrent" in sections else 0):
         s = torch.full((4099,), float(rank + 1 + j), device="cuda")
         r = torch.empty_like(s)
         bufs.append((s, r))
@@ -252,7 +267,14 @@ def main():
     for h in hs:
         emac.wait(h)
     tri = world * (world + 1) / 2
-    ok = all(bool(torch.all(r == tri + world * j).item()) for j, (_, r) in enumerate(bufs))
+    ok = True
+    for j, (_, r) in enumerate(bufs):
+        good = bool(torch.all(r == tri + world * j).item())
+        if not good:
+            bad = (r != tri + world * j).nonzero().flatten()
+            print(f"rank {rank}: concurrent handle {j}: {bad.numel()} of {r.numel()} wrong, first {bad[:6].tolist()} "
+                  f"values {r[bad[:6]].tolist()} want {tri + world * j}", file=sys.stderr, flush=True)
+        ok &= good
     for h in hs:
         emac.done(h)
     failures += not ok
@@ -262,7 +284,7 @@ def main():
     ok = True
     x = torch.full((64,), float(rank + 1), device="cuda")
     y = torch.empty_like(x)
-    for it in range(600):
+    for it in range(600 if "recycle" in sections else 0):
         pair = [emac.allreduce_init(x.data_ptr(), y.data_ptr(), 64, emac.FLOAT, comm) for _ in range(2)]
         for h in pair:
             emac.start(h)
@@ -276,7 +298,8 @@ def main():
             emac.done(h)
     failures += not ok
     print(f"IPC rank {rank}/{world} slot recycling (1200 handles): {'ok' if ok else 'MISMATCH'}", flush=True)
-    failures += not timeout_recovery(rank, world)
+    if "recovery" in sections:
+        failures += not timeout_recovery(rank, world)
     emac.comm_free(comm)
     dist.barrier()
     dist.destroy_process_group()

@@ -226,7 +226,7 @@ def test_ipc_bootstrap_over_gloo_without_gpu(world):
     takes part in the same bootstrap exchanges (no rank left waiting) and all fail loudly with
     ERROR_DEVICE instead of falling back to the CPU."""
     if torch.cuda.is_available():
-        pytest.skip("GPU present: tests/test_gpu_ipc.py covers the working path")
+        pytest.skip("GPU present: tests/test_gpu_peer_mapped.py covers the working path")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29700 + world * 7 + os.getpid() % 200

@@ -1,12 +1,14 @@
 """Peer-mapped (IPC) form on the GPU box: R processes, one rank each, sharing the one MI355X.
 
 Each rank is a separate process (tests/ipc_worker.py) with its own HIP context; the ranks
-exchange hipIpc handles through a gloo bootstrap, map each other's send/receive buffers, and
-run the persistent Allreduce: barrier kernel -> fold over the peers' leaves with the fan-out
-stored into every peer's receive buffer -> barrier kernel. Every rank checks its result bit for
-bit against the CPU oracle (float, double, int, long; repeats, in place, host buffers, empty and
-one-element messages, -k fractions, pieces, radix chains, a sub-split) and several handles
-in flight on separate streams.
+exchange hipIpc handles through a gloo bootstrap, map each other's send buffers and result
+buffers ("outboxes"), and run the persistent Allreduce: barrier -> fold of the owner chunks over
+the peers' leaves into the outbox -> barrier -> pull of every owner's result into the own receive
+buffer. Every rank checks its result bit for bit against the CPU oracle (float, double, int,
+long; repeats, in place, host buffers, empty and one-element messages, -k fractions, pieces,
+radix chains, a sub-split), freed and re-allocated buffers, and several handles in flight on
+separate streams. (Named to sort after test_gpu_parity.py: the single-process parity suite runs
+first under `pytest -x`.)
 """
 import os
 import socket
@@ -40,28 +42,29 @@ def _need_gpu():
 WORLDS = [int(w) for w in os.environ.get("IPC_TEST_WORLDS", "2,3,4,8").split(",")]
 
 
-def _digest(outs, codes, keep=40):
-    """Per rank: its exit code, every line that is not a passing case (set-up retries, errors,
-    tracebacks) -- repeated lines counted once -- and its last lines; bounded, so a failing run's
-    report stays readable."""
-    parts = []
+def _digest(outs, codes, keep=12):
+    """First every rank's exit code and failing cases (so a truncated report still names every
+    rank that failed), then per rank every other line that is not a passing case (set-up retries,
+    errors, tracebacks) -- repeated lines counted once -- and its last lines."""
+    head, parts = [], []
     for r, (out, code) in enumerate(zip(outs, codes)):
         lines = out.splitlines()
+        bad = [l for l in lines if l.startswith("IPC rank") and not l.endswith(": ok")]
+        head.append(f"rank {r}: exit {code}, {len(bad)} failing case(s)" + "".join("\n  " + l for l in bad[:6]))
         seen, odd = {}, []
         for l in lines:
-            if l.endswith(": ok"):
+            if l.endswith(": ok") or l in bad:
                 continue
             if l not in seen:
                 odd.append(l)
             seen[l] = seen.get(l, 0) + 1
         odd = [f"{l}  (x{seen[l]})" if seen[l] > 1 else l for l in odd[:keep]]
         parts.append(f"--- rank {r}: exit {code}, {len(lines)} lines\n" + "\n".join(odd) +
-                     "\n... last lines:\n" + "\n".join(lines[-8:]))
-    return "\n".join(parts)
+                     "\n... last lines:\n" + "\n".join(lines[-4:]))
+    return "\n".join(head) + "\n" + "\n".join(parts)
 
 
-@pytest.mark.parametrize("world", WORLDS)
-def test_ipc_ranks_share_one_gpu(world):
+def _run_world(world, extra_env=None, budget=150):
     port = _port()
     procs, logs = [], []
     # each rank writes to its own file: pipes read one after the other would fill up and block a
@@ -71,10 +74,11 @@ def test_ipc_ranks_share_one_gpu(world):
                    MASTER_PORT=str(port), IPC_DEVICE="0", EXT_MPI_AMD_BARRIER_TIMEOUT="20")
         env.setdefault("EXT_MPI_AMD_DEBUG_IPC", "1")  # set-up retries are reported (silent when none)
         env.setdefault("IPC_FUZZ", "16")  # seeded random cases beside the fixed ones (ipc_worker.fuzz_cases)
+        env.update(extra_env or {})
         logs.append(tempfile.TemporaryFile(mode="w+"))
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "ipc_worker.py")], env=env,
                                       stdout=logs[-1], stderr=subprocess.STDOUT, text=True))
-    deadline = time.monotonic() + 150
+    deadline = time.monotonic() + budget
     codes = []
     for p in procs:
         try:
@@ -95,3 +99,18 @@ def test_ipc_ranks_share_one_gpu(world):
     lines = [l for l in report.splitlines() if l.startswith("IPC rank")]
     assert lines and all(l.endswith(": ok") for l in lines), _digest(outs, codes)
     assert len(lines) == world * sum(1 for l in lines if l.startswith("IPC rank 0/")), _digest(outs, codes)
+    return report
+
+
+@pytest.mark.parametrize("world", WORLDS)
+def test_ipc_ranks_share_one_gpu(world):
+    _run_world(world)
+
+
+@pytest.mark.parametrize("world", [3, 8])
+def test_ipc_forced_mirror(world):
+    """EXT_MPI_AMD_IPC_FORCE_MIRROR=1: every exported buffer (send buffer, outbox) is re-placed in
+    the first set-up round of every handle, so the mirror path -- staged send buffers, a second
+    exchange, re-validated mappings -- runs on every case, bitwise against the oracle."""
+    report = _run_world(world, {"EXT_MPI_AMD_IPC_FORCE_MIRROR": "1", "IPC_FUZZ": "4"})
+    assert "re-placing send outbox" in report  # the forced round was taken (EXT_MPI_AMD_DEBUG_IPC)
