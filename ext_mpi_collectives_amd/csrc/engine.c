@@ -67,6 +67,23 @@ typedef struct {
   int busy;
 } ipc_mirror;
 
+/* The arena of a peer-mapped communicator: per rank a few large device segments, each exported and
+   mapped by every peer once, when it is added, and validated then (a nonce in its head); handles
+   carve their outboxes and send-buffer mirrors out of them (first fit, free list per segment). */
+#define EMAC_ARENA_SEGS 32
+#define EMAC_ARENA_HEAD 256            /* the nonce */
+#define EMAC_ARENA_ALIGN 256
+#define EMAC_ARENA_MIN (64L << 20)     /* first segment */
+typedef struct {
+  long off, len;
+} arena_free;
+typedef struct {
+  void *base;
+  long bytes;
+  arena_free *fr; /* free blocks, ascending offsets, coalesced */
+  int nfr, capfr;
+} arena_seg;
+
 typedef struct {
   int used;
   int rank, size, device;
@@ -91,6 +108,13 @@ typedef struct {
   ipc_mirror *mirrors;
   int nmirrors;
   int cross_device; /* some peer runs on another device: release to system scope before phase 0 */
+  /* the arena (library memory the peers read: outboxes, send-buffer mirrors), ipc_allreduce_init */
+  arena_seg seg[EMAC_ARENA_SEGS]; /* this rank's segments */
+  int nseg;
+  void *peer_seg[EMAC_MAX_RANKS][EMAC_ARENA_SEGS]; /* every rank's segment k as reachable here */
+  int peer_nseg[EMAC_MAX_RANKS];
+  void *bad_seg[EMAC_ARENA_SEGS]; /* own segments some peer could not validate */
+  int nbad;
 } emac_comm;
 
 /* Loopback groups: every rank of the communicator lives in this process; the i-th handle a
@@ -172,6 +196,8 @@ typedef struct {
   void *outbox;     /* this rank's owner chunks' results (pool memory, exported to the peers) */
   size_t outbox_bytes;
   int done_collective; /* some rank exported caller memory: Done agrees with every peer */
+  unsigned char send_arena; /* dsend[0] is an arena block of `bytes` (a send mirror, or in place the one buffer) */
+  unsigned char send_local; /* dsend[0] is a plain device mirror (a communicator of one rank) */
   int nodes;            /* COMM form over several nodes: the node legs run (emac_comm_program_nodes) */
   emac_node_sched ns;   /* ... under this inter-node schedule */
   emac_launch xfold[2 * EMAC_MAX_NODE_STEPS]; /* ... and, per exchange step, the fold of the lines' partials */
@@ -192,7 +218,7 @@ static int new_handle_slot(void) {
 
 static void ipc_unmap(void *base);
 static void mirror_free(emac_handle *h, void *p);
-static void ipc_mirror_put(emac_comm *cm, void *p);
+static void arena_release(emac_comm *cm, void *p, long bytes);
 
 static void pipe_free(emac_pipe *pp) {
   int p;
@@ -230,14 +256,20 @@ static void release(emac_handle *h) {
   }
   emac_gpu_free(h->staging);
   for (r = 0; r < h->nbuf; r++) {
-    int same = h->dsend[r] == h->drecv[r];
-    if (h->send_mirror[r]) mirror_free(h, h->dsend[r]);
-    if (h->recv_mirror[r] && !(same && h->send_mirror[r])) mirror_free(h, h->drecv[r]);
+    const int same = h->dsend[r] == h->drecv[r];
+    const int own = r == 0 && (h->send_arena || h->send_local); /* send side allocated by the IPC set-up */
+    if (r == 0 && h->send_arena)
+      arena_release(&comms[h->comm], h->dsend[0], (long)h->bytes);
+    else if (r == 0 && h->send_local)
+      emac_gpu_free(h->dsend[0]);
+    else if (h->send_mirror[r])
+      mirror_free(h, h->dsend[r]);
+    if (h->recv_mirror[r] && h->drecv[r] && !(same && (h->send_mirror[r] || own))) mirror_free(h, h->drecv[r]);
     if (h->send_reg[r]) emac_gpu_host_unregister(h->user_send[r]);
     if (h->recv_reg[r]) emac_gpu_host_unregister(h->user_recv[r]);
   }
   for (r = 0; r < h->nmapped; r++) ipc_unmap(h->mapped[r]);
-  if (h->outbox) ipc_mirror_put(&comms[h->comm], h->outbox);
+  if (h->outbox) arena_release(&comms[h->comm], h->outbox, (long)h->outbox_bytes);
   emac_gpu_event_destroy(h->ev_release);
   for (r = 0; r <= EXT_MPI_AMD_LEG_ALL; r++) emac_gpu_graph_destroy(h->graph[r]);
   if (h->kind == KIND_IPC && h->slot_held) {
@@ -251,19 +283,11 @@ static void release(emac_handle *h) {
   free(h);
 }
 
-static int ipc_mirror_get(emac_comm *cm, void **p, size_t bytes);
+/* device mirrors the peers never touch (every receive-side mirror; IPC send mirrors come from
+   the communicator's arena, ipc_allreduce_init) */
+static int mirror_alloc(emac_handle *h, void **p) { return emac_gpu_malloc(p, h->bytes); }
 
-static int mirror_alloc(emac_handle *h, void **p) {
-  if (h->kind == KIND_IPC) return ipc_mirror_get(&comms[h->comm], p, h->bytes);
-  return emac_gpu_malloc(p, h->bytes);
-}
-
-static void mirror_free(emac_handle *h, void *p) {
-  if (h->kind == KIND_IPC)
-    ipc_mirror_put(&comms[h->comm], p);
-  else
-    emac_gpu_free(p);
-}
+static void mirror_free(emac_handle *h, void *p) { emac_gpu_free(p); }
 
 /* A buffer the handle can use in place: device memory, and in the IPC form, for a buffer the
    peers read (the send buffer; in place, the one buffer), also exportable
@@ -311,7 +335,9 @@ static int map_buffers(emac_handle *h, int r, const void *send, void *recv) {
     h->drecv[r] = dv;
     h->host_direct = 1;
   } else {
-    if ((rc = mirror_alloc(h, &h->drecv[r]))) return rc;
+    /* IPC form, in place: the one buffer is read by the peers -- its mirror comes from the arena
+       (ipc_allreduce_init; NULL until then) */
+    if (!(h->kind == KIND_IPC && send == recv) && (rc = mirror_alloc(h, &h->drecv[r]))) return rc;
     h->recv_mirror[r] = 1;
     h->recv_reg[r] = host_register(h, recv);
   }
@@ -323,7 +349,8 @@ static int map_buffers(emac_handle *h, int r, const void *send, void *recv) {
     h->dsend[r] = dv;
     h->host_direct = 1;
   } else {
-    if ((rc = mirror_alloc(h, &h->dsend[r]))) return rc;
+    /* IPC form: from the arena (ipc_allreduce_init; NULL until then) */
+    if (h->kind != KIND_IPC && (rc = mirror_alloc(h, &h->dsend[r]))) return rc;
     h->send_mirror[r] = 1;
     h->send_reg[r] = host_register(h, send);
   }
@@ -704,6 +731,14 @@ static void ipc_mirror_put(emac_comm *cm, void *p) {
     if (cm->mirrors[i].p == p && cm->mirrors[i].busy == 1) cm->mirrors[i].busy = 0; /* poisoned ones stay out */
 }
 
+static int ipc_pool_owns(const emac_comm *cm, const void *p) {
+  int i;
+  for (i = 0; i < cm->nmirrors; i++)
+    if ((const char *)p >= (const char *)cm->mirrors[i].p && (const char *)p < (const char *)cm->mirrors[i].p + cm->mirrors[i].bytes)
+      return 1;
+  return 0;
+}
+
 int ext_mpi_amd_comm_malloc(int comm, void **p, unsigned long bytes) {
   if (!p || comm < 0 || comm >= MAX_COMMS || !comms[comm].used) return EMAC_ERR_ARG;
   *p = NULL;
@@ -729,10 +764,17 @@ static int node_radix(const emac_node_sched *ns, int st);
 /* Collective: every rank first closes its mappings of the others' memory, then all agree, and
    only then is this rank's exported memory (synchronisation block, mirror pool) freed. */
 static void ipc_comm_release(emac_comm *cm) {
-  int r;
-  for (r = 0; r < cm->size; r++)
+  int r, k;
+  for (r = 0; r < cm->size; r++) {
     if (r != cm->rank && cm->peer_sync_base[r]) ipc_unmap(cm->peer_sync_base[r]);
+    for (k = 0; r != cm->rank && k < cm->peer_nseg[r]; k++) ipc_unmap(cm->peer_seg[r][k]);
+  }
   if (cm->ag && cm->size > 1) ipc_agree(cm, 1);
+  for (k = 0; k < cm->nseg; k++) {
+    emac_gpu_free(cm->seg[k].base);
+    free(cm->seg[k].fr);
+  }
+  for (k = 0; k < cm->nbad; k++) emac_gpu_free(cm->bad_seg[k]);
   for (r = 0; r < cm->nmirrors; r++) emac_gpu_free(cm->mirrors[r].p);
   free(cm->mirrors);
   emac_gpu_free(cm->d_peer_sync);
@@ -750,6 +792,7 @@ typedef struct {
   int status;
   int refused;   /* [0]: the runtime refused to export one of this rank's buffers */
   int caller;    /* [0]: the exported send buffer is caller memory (not a library mirror) */
+  int seg;       /* >= 0: an arena block, in the exporter's segment `seg` at `offset` (nothing exported) */
   long len;      /* bytes the peers access (the sample spans them) */
   unsigned char sample[EMAC_SAMPLE_BYTES]; /* the exporter's own read of the buffer (ipc_exchange) */
   unsigned char uuid[16];                  /* communicator set-up: the exporter's device */
@@ -912,55 +955,233 @@ int ext_mpi_amd_comm_init_ipc(int rank, int size, ext_mpi_amd_allgather_fn allga
    * The runtime's IPC handle of an allocation is a function of the exporter's address and size:
      an allocation freed while a peer still maps it and re-allocated at the same address exports
      the same handle, and importing it resolves to the OLD memory. The rule of the reference rules
-     it out: a peer-mapped handle's Done is collective (ext_mpi_amd_done: every rank closes its
-     mappings, then the ranks agree), so no caller allocation is freed under a mapping as long as
-     the caller keeps its buffers until Done, and the library's own exported memory (outboxes,
-     mirrors, synchronisation blocks) is pooled per communicator and freed only by the collective
+     it out for caller memory: a peer-mapped handle's Done is collective (ext_mpi_amd_done: every
+     rank closes its mappings, then the ranks agree), so no caller allocation is freed under a
+     mapping as long as the caller keeps its buffers until Done.
+   * Library memory the peers read -- outboxes, mirrors of send buffers -- lives in the
+     communicator's ARENA: a few large segments per rank, each exported and mapped ONCE (when it is
+     added) and validated then with a random nonce the owner wrote into its head, so a mapping of
+     any other memory cannot pass. Handles carve blocks out of the segments; nothing library-owned
+     is exported, imported or closed per handle, and segments are freed only by the collective
      communicator free.
    * Peers never WRITE caller memory, at set-up or later: the send buffer is only read (the fold's
-     leaves), each rank's results go to its own library-owned outbox, and every rank pulls the
-     results into its own receive buffer, which is never exported. A stale mapping could therefore
-     only feed wrong leaves, never overwrite anything.
-   * Every mapping is still validated, read-only: the exporter samples its buffer
-     (emac_gpu_sample: 8 spots of 8 bytes) and publishes the sample with its handle; every importer
-     samples the same spots through its mapping. A mismatch, a mapping the runtime refuses or one
-     shorter than the exporter's allocation sends the buffer to a fresh pooled mirror (send
-     buffer: staged in on the handle's stream; outbox: a new one) and the exchange repeats.
-     EXT_MPI_AMD_IPC_FORCE_MIRROR=1 re-places every exported buffer in the first round, so the
-     mirror path runs deterministically (tests/test_gpu_ipc.py).
+     leaves), each rank's results go to its own outbox, and every rank pulls the results into its
+     own receive buffer, which is never exported. A stale mapping could therefore only feed wrong
+     leaves, never overwrite anything.
+   * Every mapping of a caller's send buffer is still validated, read-only: the exporter samples
+     its buffer (emac_gpu_sample: 8 spots of 8 bytes) and publishes the sample with its handle;
+     every importer samples the same spots through its mapping. A mismatch, a mapping the runtime
+     refuses or one shorter than the exporter's allocation re-places that send buffer in an arena
+     mirror (staged in on the handle's stream) and the exchange repeats.
+     EXT_MPI_AMD_IPC_FORCE_MIRROR=1 re-places every rank's send buffer in the first round, so the
+     mirror path runs deterministically (tests/test_gpu_peer_mapped.py).
    The set-up reads the caller's send buffer: the device is synchronised first, so a kernel still
    filling it cannot make the exporter's and the importers' samples differ. */
-#define EMAC_IPC_ATTEMPTS 16
+#define EMAC_IPC_ATTEMPTS 8
 
-static void ipc_mirror_poison(emac_comm *cm, void *p) {
-  int i;
-  for (i = 0; i < cm->nmirrors; i++)
-    if (cm->mirrors[i].p == p) cm->mirrors[i].busy = 2; /* kept, never handed out again */
+/* ---- the arena ---- */
+
+static int arena_alloc(emac_comm *cm, long bytes, void **p) {
+  int k, i;
+  bytes = (bytes + EMAC_ARENA_ALIGN - 1) / EMAC_ARENA_ALIGN * EMAC_ARENA_ALIGN;
+  if (bytes <= 0) bytes = EMAC_ARENA_ALIGN;
+  for (k = 0; k < cm->nseg; k++) {
+    arena_seg *s = &cm->seg[k];
+    for (i = 0; i < s->nfr; i++)
+      if (s->fr[i].len >= bytes) {
+        *p = (char *)s->base + s->fr[i].off;
+        s->fr[i].off += bytes;
+        s->fr[i].len -= bytes;
+        if (!s->fr[i].len) {
+          memmove(&s->fr[i], &s->fr[i + 1], sizeof(arena_free) * (size_t)(s->nfr - i - 1));
+          s->nfr--;
+        }
+        return 0;
+      }
+  }
+  return EMAC_ERR_MALLOC;
 }
 
-/* re-place this rank's send buffer (in place: the one buffer) in a fresh mirror; `poison`: the old
-   mirror is kept out of the pool for good (a peer could not map or validate it) */
-static int ipc_remirror_send(emac_handle *h, int poison) {
-  emac_comm *cm = &comms[h->comm];
-  const int same = h->dsend[0] == h->drecv[0];
-  unsigned char *flag = same ? &h->recv_mirror[0] : &h->send_mirror[0];
-  void *p;
-  int rc;
-  if ((rc = ipc_mirror_get(cm, &p, h->bytes))) return rc;
-  if (*flag && poison) ipc_mirror_poison(cm, h->dsend[0]);
-  else if (*flag) ipc_mirror_put(cm, h->dsend[0]);
-  h->dsend[0] = p;
-  if (same) h->drecv[0] = p; /* in place: staged in and out through the mirror */
-  *flag = 1;
+static int arena_owns(const emac_comm *cm, const void *p, int *seg) {
+  int k;
+  for (k = 0; k < cm->nseg; k++)
+    if ((const char *)p >= (const char *)cm->seg[k].base && (const char *)p < (const char *)cm->seg[k].base + cm->seg[k].bytes) {
+      if (seg) *seg = k;
+      return 1;
+    }
   return 0;
 }
 
-static int ipc_new_outbox(emac_handle *h, int poison) {
-  emac_comm *cm = &comms[h->comm];
-  void *old = h->outbox;
-  int rc = ipc_mirror_get(cm, &h->outbox, h->outbox_bytes);
-  if (old && poison) ipc_mirror_poison(cm, old);
-  else if (old) ipc_mirror_put(cm, old);
+static void arena_release(emac_comm *cm, void *p, long bytes) {
+  arena_seg *s;
+  long off;
+  int k, i;
+  if (!p || !cm->used || !arena_owns(cm, p, &k)) return;
+  bytes = (bytes + EMAC_ARENA_ALIGN - 1) / EMAC_ARENA_ALIGN * EMAC_ARENA_ALIGN;
+  if (bytes <= 0) bytes = EMAC_ARENA_ALIGN;
+  s = &cm->seg[k];
+  off = (long)((char *)p - (char *)s->base);
+  for (i = 0; i < s->nfr && s->fr[i].off < off; i++);
+  if (s->nfr == s->capfr) {
+    arena_free *f = (arena_free *)realloc(s->fr, sizeof(arena_free) * (size_t)(2 * s->capfr + 8));
+    if (!f) return; /* the block stays allocated */
+    s->fr = f;
+    s->capfr = 2 * s->capfr + 8;
+  }
+  memmove(&s->fr[i + 1], &s->fr[i], sizeof(arena_free) * (size_t)(s->nfr - i));
+  s->fr[i].off = off;
+  s->fr[i].len = bytes;
+  s->nfr++;
+  if (i + 1 < s->nfr && s->fr[i].off + s->fr[i].len == s->fr[i + 1].off) { /* merge with the next */
+    s->fr[i].len += s->fr[i + 1].len;
+    memmove(&s->fr[i + 1], &s->fr[i + 2], sizeof(arena_free) * (size_t)(s->nfr - i - 2));
+    s->nfr--;
+  }
+  if (i > 0 && s->fr[i - 1].off + s->fr[i - 1].len == s->fr[i].off) { /* and the previous */
+    s->fr[i - 1].len += s->fr[i].len;
+    memmove(&s->fr[i], &s->fr[i + 1], sizeof(arena_free) * (size_t)(s->nfr - i - 1));
+    s->nfr--;
+  }
+}
+
+typedef struct {
+  int status, grow;
+  unsigned char handle[EMAC_IPC_HANDLE_BYTES];
+  long offset, extent;
+  unsigned long long buf_id;
+  unsigned char nonce[EMAC_SAMPLE_BYTES];
+} arena_export;
+
+static unsigned long long g_nonce_state;
+
+/* Collective: ranks that lack `need` bytes (0: none) add a segment of at least that size (and at
+   least their arena's size so far, EMAC_ARENA_MIN at first); every rank maps every new segment
+   and checks the nonce in its head through the mapping. A segment some rank cannot map or
+   validate is set aside (freed with the communicator) and its owner tries a fresh one. */
+static int arena_grow(emac_comm *cm, int rc, long need) {
+  const int R = cm->size;
+  int attempt, r;
+  for (attempt = 0; attempt < EMAC_IPC_ATTEMPTS; attempt++) {
+    arena_export mine, all[EMAC_MAX_RANKS];
+    void *nb = NULL, *mapped[EMAC_MAX_RANKS];
+    unsigned bad = 0, allbad[EMAC_MAX_RANKS], badall = 0;
+    long sz = 0;
+    int any = 0;
+    memset(&mine, 0, sizeof(mine));
+    if (!rc && need > 0) {
+      long have = 0;
+      int i;
+      for (i = 0; i < cm->nseg; i++) have += cm->seg[i].bytes;
+      sz = need + EMAC_ARENA_HEAD;
+      if (sz < have) sz = have;
+      if (sz < EMAC_ARENA_MIN) sz = EMAC_ARENA_MIN;
+      sz = (long)((sz + (long)EMAC_IPC_GRANULE - 1) / (long)EMAC_IPC_GRANULE * (long)EMAC_IPC_GRANULE);
+      if (cm->nseg == EMAC_ARENA_SEGS || cm->nbad == EMAC_ARENA_SEGS) rc = EMAC_ERR_MALLOC;
+      if (!rc) rc = emac_gpu_malloc(&nb, (size_t)sz);
+      if (!rc) {
+        void *b0;
+        unsigned long long x = g_nonce_state ^ ((unsigned long long)(size_t)nb * 0x9E3779B97F4A7C15ull) ^
+                               ((unsigned long long)cm->rank << 40) ^ (unsigned long long)attempt;
+        for (i = 0; i < EMAC_SAMPLE_BYTES; i++) { /* xorshift64* */
+          x ^= x >> 12;
+          x ^= x << 25;
+          x ^= x >> 27;
+          mine.nonce[i] = (unsigned char)((x * 0x2545F4914F6CDD1Dull) >> 56);
+        }
+        g_nonce_state = x + 0x9E3779B97F4A7C15ull;
+        /* the nonce is the head's first EMAC_SAMPLE_BYTES bytes: sampled whole (len = that size) */
+        rc = emac_gpu_memcpy(nb, mine.nonce, EMAC_SAMPLE_BYTES);
+        if (!rc) rc = emac_gpu_device_sync();
+        if (!rc) rc = emac_gpu_ipc_export(nb, mine.handle, &mine.offset);
+        mine.extent = emac_gpu_alloc_extent(nb, &b0);
+        mine.buf_id = emac_gpu_buffer_id(b0);
+        if (rc == EMAC_ERR_TRANSPORT) { /* export refused: set aside, try another */
+          rc = 0;
+          bad = 1u << cm->rank;
+        }
+      }
+      mine.grow = 1;
+    }
+    mine.status = rc == 0;
+    if (cm->ag(cm->ag_ctx, &mine, all, (long)sizeof(mine))) return EMAC_ERR_TRANSPORT;
+    for (r = 0; r < R; r++) {
+      if (!all[r].status) rc = rc ? rc : EMAC_ERR_TRANSPORT;
+      any |= all[r].grow;
+    }
+    if (rc) {
+      if (nb) emac_gpu_free(nb); /* nobody maps it: every rank stops here */
+      return rc;
+    }
+    if (!any) return 0;
+    {
+      const void *pk[EMAC_MAX_RANKS];
+      long pl[EMAC_MAX_RANKS];
+      int who[EMAC_MAX_RANKS], n = 0;
+      unsigned char seen[EMAC_MAX_RANKS * EMAC_SAMPLE_BYTES];
+      for (r = 0; r < R; r++) {
+        void *ext_base;
+        mapped[r] = NULL;
+        if (!all[r].grow || r == cm->rank) continue;
+        if (!(mapped[r] = ipc_map_peer(all[r].handle, all[r].buf_id, all[r].extent)) || all[r].offset != 0 ||
+            emac_gpu_alloc_extent(mapped[r], &ext_base) != all[r].extent) {
+          bad |= 1u << r;
+          continue;
+        }
+        pk[n] = mapped[r];
+        pl[n] = EMAC_SAMPLE_BYTES;
+        who[n++] = r;
+      }
+      if (n && (rc = emac_gpu_sample(pk, pl, n, seen, NULL))) return rc;
+      for (r = 0; r < n; r++)
+        if (memcmp(seen + r * EMAC_SAMPLE_BYTES, all[who[r]].nonce, EMAC_SAMPLE_BYTES)) bad |= 1u << who[r];
+    }
+    if (cm->ag(cm->ag_ctx, &bad, allbad, (long)sizeof(unsigned))) return EMAC_ERR_TRANSPORT;
+    for (r = 0; r < R; r++) badall |= allbad[r];
+    for (r = 0; r < R; r++) {
+      if (!all[r].grow) continue;
+      if ((badall >> r) & 1) {
+        if (r == cm->rank) {
+          cm->bad_seg[cm->nbad++] = nb; /* a peer may map it: freed with the communicator */
+        } else if (mapped[r]) {
+          ipc_unmap(mapped[r]);
+        }
+        if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
+          fprintf(stderr, "ipc rank %d: rank %d's new arena segment failed validation (attempt %d)\n", cm->rank, r,
+                  attempt);
+        continue;
+      }
+      if (r == cm->rank) {
+        arena_seg *s = &cm->seg[cm->nseg];
+        memset(s, 0, sizeof(*s));
+        s->base = nb;
+        s->bytes = sz;
+        s->fr = (arena_free *)malloc(sizeof(arena_free) * 8);
+        s->capfr = 8;
+        if (s->fr) {
+          s->fr[0].off = EMAC_ARENA_HEAD;
+          s->fr[0].len = sz - EMAC_ARENA_HEAD;
+          s->nfr = 1;
+        }
+        cm->peer_seg[r][cm->nseg++] = nb;
+        cm->peer_nseg[r] = cm->nseg;
+        need = 0;
+      } else {
+        cm->peer_seg[r][cm->peer_nseg[r]++] = mapped[r];
+      }
+    }
+    if (!badall) return 0;
+  }
+  fprintf(stderr, "ext_mpi_amd: rank %d: arena segments still unreachable after %d set-up rounds\n", cm->rank,
+          EMAC_IPC_ATTEMPTS);
+  return EMAC_ERR_TRANSPORT;
+}
+
+/* Collective: the blocks this rank still lacks (`lack` bytes in total), carved after the arena
+   has grown if any rank needed it. */
+static int arena_get(emac_comm *cm, int rc, void **p, long bytes) {
+  const int miss = !rc && bytes > 0 && arena_alloc(cm, bytes, p) != 0;
+  rc = arena_grow(cm, rc, miss ? bytes : 0);
+  if (!rc && miss) rc = arena_alloc(cm, bytes, p);
   return rc;
 }
 
@@ -982,53 +1203,52 @@ static long outbox_layout(const emac_plan *p, int pos, long *at) {
 
 enum { IPC_SEND = 0, IPC_OUTBOX = 1, IPC_NBUF = 2 };
 
-/* One exchange of the IPC set-up (collective whatever failed locally before: `rc`). On return
-   peer[t][r] holds the validated mapping of rank r's buffer t (send, outbox), all[] the exports,
-   and miss[t] a bit per exporter whose buffer t this rank could not map or validate. */
-static int ipc_exchange(emac_handle *h, emac_comm *cm, int rc, int empty, ipc_export *all, void *(*peer)[EMAC_MAX_RANKS],
+/* One exchange of the IPC set-up (collective whatever failed locally before: `rc`). Every rank
+   publishes its send buffer (an exported caller allocation with a sample of it, or an arena block)
+   and its outbox (an arena block). On return peer[t][r] holds rank r's buffer t as reachable here,
+   all[] the exports, and *miss a bit per rank whose send buffer this rank could not map or validate. */
+static int ipc_exchange(emac_handle *h, emac_comm *cm, int rc, ipc_export *all, void *(*peer)[EMAC_MAX_RANKS],
                         unsigned *miss) {
   ipc_export mine[IPC_NBUF];
   const int R = cm->size;
   void *own[IPC_NBUF] = {h->dsend[0], h->outbox};
   const long len[IPC_NBUF] = {(long)h->bytes, (long)h->outbox_bytes};
-  int r, t, any_refused = 0;
+  int r, t, k;
   memset(mine, 0, sizeof(mine));
-  miss[0] = miss[1] = 0;
-  for (t = 0; t < IPC_NBUF && !rc && !empty; t++) {
-    void *b0;
-    const int er = emac_gpu_ipc_export(own[t], mine[t].handle, &mine[t].offset);
-    if (er == EMAC_ERR_TRANSPORT)
-      mine[0].refused = 1; /* refused by the runtime: this round is void, the buffer is re-placed */
-    else
-      rc = er;
-    mine[t].extent = emac_gpu_alloc_extent(own[t], &b0);
-    mine[t].buf_id = emac_gpu_buffer_id(b0);
+  *miss = 0;
+  for (t = 0; t < IPC_NBUF && !rc; t++) {
     mine[t].len = len[t];
-  }
-  if (!rc && !empty) {
-    unsigned char smp[IPC_NBUF * EMAC_SAMPLE_BYTES];
-    rc = emac_gpu_sample((const void *const *)own, len, IPC_NBUF, smp, h->stream);
-    for (t = 0; !rc && t < IPC_NBUF; t++) memcpy(mine[t].sample, smp + t * EMAC_SAMPLE_BYTES, EMAC_SAMPLE_BYTES);
+    if (arena_owns(cm, own[t], &k)) {
+      mine[t].seg = k;
+      mine[t].offset = (long)((char *)own[t] - (char *)cm->seg[k].base);
+    } else if (t == IPC_SEND) {
+      void *b0;
+      const int er = emac_gpu_ipc_export(own[t], mine[t].handle, &mine[t].offset);
+      mine[t].seg = -1;
+      if (er == EMAC_ERR_TRANSPORT)
+        mine[0].refused = 1; /* refused by the runtime: this rank's send buffer is re-placed */
+      else
+        rc = er;
+      mine[t].extent = emac_gpu_alloc_extent(own[t], &b0);
+      mine[t].buf_id = emac_gpu_buffer_id(b0);
+      if (!rc) rc = emac_gpu_sample((const void *const *)&own[t], &len[t], 1, mine[t].sample, h->stream);
+    } else {
+      rc = EMAC_ERR_ARG; /* an outbox outside the arena */
+    }
   }
   for (r = 0; r < EMAC_SYNC_SLOTS; r++)
     if (!cm->slot_used[r]) mine[0].free_slots[r >> 3] |= (unsigned char)(1u << (r & 7));
   mine[0].status = rc == 0;
-  mine[0].caller = !empty && !h->send_mirror[0] && !(h->dsend[0] == h->drecv[0] && h->recv_mirror[0]);
+  mine[0].caller = mine[0].seg < 0 && !ipc_pool_owns(cm, h->dsend[0]);
   if (cm->ag(cm->ag_ctx, mine, all, (long)sizeof(mine))) return EMAC_ERR_TRANSPORT;
-  for (r = 0; r < R; r++) {
+  for (r = 0; r < R; r++)
     if (!all[IPC_NBUF * r].status && !rc) rc = EMAC_ERR_TRANSPORT;
-    any_refused |= all[IPC_NBUF * r].refused;
-  }
-  if (rc || empty) return rc;
-  if (any_refused) { /* void on every rank: the refusing exporter re-places its buffers */
-    if (mine[0].refused) miss[0] = miss[1] = 1u << cm->rank;
-    return 0;
-  }
+  if (rc) return rc;
   {
-    const void *pk[IPC_NBUF * EMAC_MAX_RANKS];
-    long pl[IPC_NBUF * EMAC_MAX_RANKS];
-    int who[IPC_NBUF * EMAC_MAX_RANKS], n = 0;
-    unsigned char seen[IPC_NBUF * EMAC_MAX_RANKS * EMAC_SAMPLE_BYTES];
+    const void *pk[EMAC_MAX_RANKS];
+    long pl[EMAC_MAX_RANKS];
+    int who[EMAC_MAX_RANKS], n = 0;
+    unsigned char seen[EMAC_MAX_RANKS * EMAC_SAMPLE_BYTES];
     for (r = 0; r < R; r++)
       for (t = 0; t < IPC_NBUF; t++) {
         const ipc_export *e = &all[IPC_NBUF * r + t];
@@ -1039,8 +1259,13 @@ static int ipc_exchange(emac_handle *h, emac_comm *cm, int rc, int empty, ipc_ex
           peer[t][r] = own[t];
           continue;
         }
-        miss[t] |= 1u << r; /* until validated below */
-        if (!(base = ipc_map_peer(e->handle, e->buf_id, e->extent))) continue;
+        if (e->seg >= 0) { /* an arena block: the segment was validated when it was added */
+          if (e->seg < cm->peer_nseg[r]) peer[t][r] = (char *)cm->peer_seg[r][e->seg] + e->offset;
+          if (!peer[t][r]) *miss |= 1u << r;
+          continue;
+        }
+        *miss |= 1u << r; /* until validated below */
+        if (all[IPC_NBUF * r].refused || !(base = ipc_map_peer(e->handle, e->buf_id, e->extent))) continue;
         h->mapped[h->nmapped++] = base;
         /* a mapping the runtime can describe must hold the peer's whole allocation (one it cannot
            describe is taken at the exporter's word; the sample still checks it) */
@@ -1053,21 +1278,18 @@ static int ipc_exchange(emac_handle *h, emac_comm *cm, int rc, int empty, ipc_ex
         peer[t][r] = (char *)base + e->offset;
         pk[n] = peer[t][r];
         pl[n] = e->len;
-        who[n++] = IPC_NBUF * r + t;
+        who[n++] = r;
       }
     if ((rc = emac_gpu_sample(pk, pl, n, seen, h->stream))) return rc;
     for (t = 0; t < n; t++) {
-      const int q = who[t] / IPC_NBUF, b = who[t] % IPC_NBUF;
-      if (!memcmp(seen + t * EMAC_SAMPLE_BYTES, all[who[t]].sample, EMAC_SAMPLE_BYTES))
-        miss[b] &= ~(1u << q);
+      if (!memcmp(seen + t * EMAC_SAMPLE_BYTES, all[IPC_NBUF * who[t]].sample, EMAC_SAMPLE_BYTES))
+        *miss &= ~(1u << who[t]);
       else
-        peer[b][q] = NULL;
+        peer[IPC_SEND][who[t]] = NULL;
     }
     if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
       for (r = 0; r < R; r++)
-        for (t = 0; t < IPC_NBUF; t++)
-          if ((miss[t] >> r) & 1)
-            fprintf(stderr, "ipc rank %d: cannot map or validate peer %d's %s\n", cm->rank, r, t ? "outbox" : "send buffer");
+        if ((*miss >> r) & 1) fprintf(stderr, "ipc rank %d: cannot map or validate peer %d's send buffer\n", cm->rank, r);
   }
   return 0;
 }
@@ -1080,53 +1302,95 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
   long *at = NULL;
   emac_bucket *b = NULL;
   int R = cm->size, r, t, pc, nb = 0, c, slot, attempt;
-  const int empty = h->bytes == 0 || R == 1; /* same on every rank: nothing to map */
   const char *fe = getenv("EXT_MPI_AMD_IPC_FORCE_MIRROR");
   const int force = fe && atoi(fe) > 0;
-  /* the samples read the send buffer: work the application still has in flight on it must have
-     landed (the reference synchronises the device before every barrier, ext_mpi_native_exec.c:556-558) */
-  if (!rc && !empty) rc = emac_gpu_device_sync();
   if (!rc && h->bytes) rc = map_buffers(h, 0, sendbuf, recvbuf);
-  if (!rc && !empty) {
-    h->outbox_bytes = (size_t)outbox_layout(&h->plan, h->me_pos, NULL);
-    if (h->outbox_bytes < 16) h->outbox_bytes = 16;
-    rc = ipc_new_outbox(h, 0);
-  }
-  for (attempt = 0;; attempt++) {
-    unsigned miss[IPC_NBUF], v[1 + IPC_NBUF], allv[(1 + IPC_NBUF) * EMAC_MAX_RANKS], stale[IPC_NBUF] = {0, 0};
-    int again = 0;
-    rc = ipc_exchange(h, cm, rc, empty, all, peer, miss);
-    if (!rc && force && attempt == 0 && !empty) miss[0] = miss[1] = 1u << cm->rank; /* re-place mine */
-    v[0] = rc == 0;
-    v[1] = miss[0];
-    v[2] = miss[1];
-    if (cm->ag(cm->ag_ctx, v, allv, (long)sizeof(v))) return EMAC_ERR_TRANSPORT;
-    for (r = 0; r < R; r++) {
-      if (!allv[(1 + IPC_NBUF) * r]) return rc ? rc : EMAC_ERR_TRANSPORT;
-      for (t = 0; t < IPC_NBUF; t++) {
-        const unsigned m = allv[(1 + IPC_NBUF) * r + 1 + t];
-        again |= m != 0;
-        stale[t] |= (m >> cm->rank) & 1u;
+  if (R == 1 || !h->bytes) { /* nothing to map: this rank folds alone (no peers), or nothing at all */
+    if (!rc && h->bytes && !h->dsend[0]) { /* a send mirror map_buffers left to the arena */
+      if (!(rc = emac_gpu_malloc(&h->dsend[0], h->bytes))) h->send_local = 1;
+      if (h->recv_mirror[0] && !h->drecv[0]) h->drecv[0] = h->dsend[0];
+    }
+    attempt = 0;
+    {
+      ipc_export mine;
+      memset(&mine, 0, sizeof(mine));
+      for (r = 0; r < EMAC_SYNC_SLOTS; r++)
+        if (!cm->slot_used[r]) mine.free_slots[r >> 3] |= (unsigned char)(1u << (r & 7));
+      mine.status = rc == 0;
+      for (r = 0; r < R; r++) all[IPC_NBUF * r] = mine;
+      if (R > 1) { /* empty message: agree on the slot only */
+        ipc_export g[EMAC_MAX_RANKS];
+        if (cm->ag(cm->ag_ctx, &mine, g, (long)sizeof(mine))) return EMAC_ERR_TRANSPORT;
+        for (r = 0; r < R; r++) {
+          all[IPC_NBUF * r] = g[r];
+          if (!g[r].status) rc = rc ? rc : EMAC_ERR_TRANSPORT;
+        }
+      }
+      if (rc) return rc;
+    }
+  } else {
+    /* the samples read the send buffer: work the application still has in flight on it must have
+       landed (the reference synchronises the device before every barrier, ext_mpi_native_exec.c:556-558) */
+    if (!rc) rc = emac_gpu_device_sync();
+    if (!rc) {
+      h->outbox_bytes = (size_t)outbox_layout(&h->plan, h->me_pos, NULL);
+      if (h->outbox_bytes < 16) h->outbox_bytes = 16;
+    }
+    /* the outbox, and a send mirror map_buffers left to the arena (host or non-exportable memory) */
+    rc = arena_get(cm, rc, &h->outbox, (long)h->outbox_bytes);
+    {
+      void *p = NULL;
+      const int want = !rc && !h->dsend[0];
+      rc = arena_get(cm, rc, &p, want ? (long)h->bytes : 0);
+      if (!rc && want) {
+        h->dsend[0] = p;
+        h->send_arena = 1;
+        if (h->recv_mirror[0] && !h->drecv[0]) h->drecv[0] = p; /* in place */
       }
     }
-    if (!again) break;
-    if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
-      fprintf(stderr, "ipc rank %d: attempt %d: re-placing%s%s\n", cm->rank, attempt, stale[0] ? " send" : "",
-              stale[1] ? " outbox" : "");
-    if (attempt == EMAC_IPC_ATTEMPTS - 1) {
-      fprintf(stderr, "ext_mpi_amd: rank %d: peer mappings still unreachable after %d set-up rounds (%s%s)\n",
-              cm->rank, EMAC_IPC_ATTEMPTS, stale[0] ? "send " : "", stale[1] ? "outbox" : "");
-      return EMAC_ERR_TRANSPORT;
+    for (attempt = 0;; attempt++) {
+      unsigned miss, allmiss[EMAC_MAX_RANKS], stale = 0;
+      int again = 0;
+      rc = ipc_exchange(h, cm, rc, all, peer, &miss);
+      if (!rc && force && attempt == 0 && !h->send_arena) miss |= 1u << cm->rank; /* re-place mine */
+      if (rc) miss = ~0u; /* a failed rank: the verdict below stops every rank */
+      if (cm->ag(cm->ag_ctx, &miss, allmiss, (long)sizeof(miss))) return EMAC_ERR_TRANSPORT;
+      for (r = 0; r < R; r++) {
+        if (allmiss[r] == ~0u) return rc ? rc : EMAC_ERR_TRANSPORT;
+        again |= allmiss[r] != 0;
+        stale |= (allmiss[r] >> cm->rank) & 1u;
+      }
+      if (!again) break;
+      if (getenv("EXT_MPI_AMD_DEBUG_IPC"))
+        fprintf(stderr, "ipc rank %d: attempt %d: re-placing%s\n", cm->rank, attempt, stale ? " send" : "");
+      if (attempt == EMAC_IPC_ATTEMPTS - 1 || (stale && h->send_arena)) {
+        fprintf(stderr, "ext_mpi_amd: rank %d: peer mappings still unreachable after %d set-up rounds\n", cm->rank,
+                attempt + 1);
+        return EMAC_ERR_TRANSPORT;
+      }
+      for (r = 0; r < h->nmapped; r++) ipc_unmap(h->mapped[r]);
+      h->nmapped = 0;
+      {
+        /* this rank's send buffer into an arena mirror, staged in on the handle's stream (in place:
+           the one buffer, staged in and out) */
+        void *p = NULL;
+        rc = arena_get(cm, rc, &p, stale ? (long)h->bytes : 0);
+        if (!rc && stale) {
+          if (h->dsend[0] == h->drecv[0]) {
+            h->recv_mirror[0] = 1;
+            h->drecv[0] = p;
+          } else {
+            h->send_mirror[0] = 1;
+          }
+          h->dsend[0] = p;
+          h->send_arena = 1;
+        }
+      }
     }
-    for (r = 0; r < h->nmapped; r++) ipc_unmap(h->mapped[r]);
-    h->nmapped = 0;
-    /* a forced round's buffers were fine: they go back to the pool */
-    if (stale[0]) rc = ipc_remirror_send(h, !(force && attempt == 0));
-    if (!rc && stale[1]) rc = ipc_new_outbox(h, !(force && attempt == 0));
   }
   /* Done is collective iff some rank's exported send buffer is caller memory (the same verdict on
      every rank): library memory is never freed under a mapping anyway (ext_mpi_amd_done) */
-  for (r = 0; r < R; r++) h->done_collective |= all[IPC_NBUF * r].caller;
+  for (r = 0; R > 1 && h->bytes && r < R; r++) h->done_collective |= all[IPC_NBUF * r].caller;
   /* the synchronisation slot: the lowest one free on every rank (ranks may have released
      their handles in different orders) */
   for (slot = 0; slot < EMAC_SYNC_SLOTS; slot++) {

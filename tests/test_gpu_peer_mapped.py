@@ -109,8 +109,8 @@ def test_ipc_ranks_share_one_gpu(world):
 
 @pytest.mark.parametrize("world", [3, 8])
 def test_ipc_forced_mirror(world):
-    """EXT_MPI_AMD_IPC_FORCE_MIRROR=1: every exported buffer (send buffer, outbox) is re-placed in
-    the first set-up round of every handle, so the mirror path -- staged send buffers, a second
+    """EXT_MPI_AMD_IPC_FORCE_MIRROR=1: every rank's exported send buffer is re-placed in
+    the first set-up round of every handle (an arena mirror), so the mirror path -- staged send buffers, a second
     exchange, re-validated mappings -- runs on every case, bitwise against the oracle."""
     report = _run_world(world, {"EXT_MPI_AMD_IPC_FORCE_MIRROR": "1", "IPC_FUZZ": "4"})
-    assert "re-placing send outbox" in report  # the forced round was taken (EXT_MPI_AMD_DEBUG_IPC)
+    assert "re-placing send" in report  # the forced round was taken (EXT_MPI_AMD_DEBUG_IPC)
