@@ -98,6 +98,7 @@ def lib():
         L.ext_mpi_amd_start_legs.argtypes = [c_int, c_int]
         L.ext_mpi_amd_stream.argtypes = [c_int]
         L.ext_mpi_amd_stream.restype = c_void_p
+        L.ext_mpi_amd_handle_schedule.argtypes = [c_int, P(c_int), P(c_int), P(c_int)]
         L.ext_mpi_amd_plan_describe.argtypes = [c_int, c_long, c_int, ctypes.c_char_p, c_int, P(c_long),
                                                 P(c_long), c_int, P(c_int), P(c_int), P(ctypes.c_ubyte),
                                                 P(ctypes.c_ubyte), P(c_int)]
@@ -301,6 +302,15 @@ def set_stream(h, stream_ptr):
 def stream(h):
     """hipStream_t (as int) the handle's work runs on."""
     return lib().ext_mpi_amd_stream(h)
+
+
+def handle_schedule(h):
+    """The fold's launch schedule: dict(unroll, issue, tuned) -- tuned 1 when the handle's first
+    Starts measured the candidates and kept the fastest, 0 while measuring, -1 untuned."""
+    u, i, t = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    _check("ext_mpi_amd_handle_schedule", lib().ext_mpi_amd_handle_schedule(h, ctypes.byref(u), ctypes.byref(i),
+                                                                           ctypes.byref(t)))
+    return {"unroll": u.value, "issue": i.value, "tuned": t.value}
 
 
 def plan_describe(nranks, count, dtype, copyin, pos, max_pieces=4096):

@@ -140,6 +140,26 @@ typedef struct {
   int unroll;
 } emac_launch;
 
+/* Launch-schedule tuning of a handle's fold (NODE form, and the COMM form's local fold): the
+   first Start runs the static pick (emac_gpu_pick_unroll) and warms the buffers, the next Starts
+   run one candidate schedule each between timing events, and the Start after them keeps the
+   fastest for the handle's lifetime. Every schedule folds in the same order -- the bits do not
+   depend on the choice. Measured on MI355X leases (tools/schedbench.hip,
+   profiles/r03_schedbench_*.txt): the fastest schedule of a shape moves between leases by more
+   than the spread within one (16 MiB x 8 node fold: U 2 48.1 us, U 4 51.8, U 4 staggered 54.1 on
+   one lease, where round 2's A/B leases had ranked the staggered one first), so no fixed
+   threshold table picks it everywhere. EXT_MPI_AMD_AUTOTUNE=0 keeps the static pick. */
+#define EMAC_TUNE_MAX 3
+#define EMAC_TUNE_MIN_BYTES (16L << 20) /* algorithmic bytes per launch: smaller launches keep the static pick */
+typedef struct {
+  int n;      /* candidates (0: no tuning) */
+  int chosen; /* index of the kept candidate, -1 while measuring */
+  int starts;
+  emac_launch L[EMAC_TUNE_MAX];
+  void *ev[EMAC_TUNE_MAX][2];
+  float us[EMAC_TUNE_MAX];
+} emac_tune;
+
 /* NODE form with host buffers: the message is staged in EMAC_PIPE_PARTS element ranges so that
    the H2D copies of part p+1, the fold of part p and the D2H copies of part p-1 overlap
    (three streams, events between them) */
@@ -204,6 +224,7 @@ typedef struct {
   void *graph[EXT_MPI_AMD_LEG_ALL + 1]; /* COMM form: captured legs, per subset of EXT_MPI_AMD_LEG_* */
   unsigned char graph_failed[EXT_MPI_AMD_LEG_ALL + 1];
   emac_pipe *pipe; /* pipelined host staging (NODE form), or NULL */
+  emac_tune tune;  /* launch-schedule tuning of the fold */
 } emac_handle;
 
 static emac_handle *handles[MAX_HANDLES];
@@ -250,6 +271,12 @@ static void release(emac_handle *h) {
   emac_gpu_free(h->d_edges);
   emac_gpu_free(h->pull.d_buckets);
   emac_gpu_free(h->pull.d_edges);
+  for (r = 0; r < h->tune.n; r++) {
+    if (h->tune.L[r].d_buckets != h->d_buckets) emac_gpu_free(h->tune.L[r].d_buckets);
+    if (h->tune.L[r].d_edges != h->d_edges) emac_gpu_free(h->tune.L[r].d_edges);
+    emac_gpu_event_destroy(h->tune.ev[r][0]);
+    emac_gpu_event_destroy(h->tune.ev[r][1]);
+  }
   for (r = 0; r < 2 * EMAC_MAX_NODE_STEPS; r++) {
     emac_gpu_free(h->xfold[r].d_buckets);
     emac_gpu_free(h->xfold[r].d_edges);
@@ -385,9 +412,25 @@ static int upload_launch(const emac_handle *h, emac_launch *L, emac_bucket *b, i
   return upload_launch_as(h, L, b, nb, h->nsrc, emac_tree_kind(&h->plan.codes, h->plan.op) == 1);
 }
 
+/* the candidates of emac_tune for a fold of nsrc leaves, fan-out `fan` (0 / 1), or 0 */
+static int tune_candidates(const emac_handle *h, int *sched) {
+  const char *e = getenv("EXT_MPI_AMD_AUTOTUNE");
+  const char *g = getenv("EXT_MPI_AMD_GRAPH"); /* captured Starts replay one schedule */
+  if ((e && atoi(e) <= 0) || (h->kind == KIND_COMM && g && atoi(g) > 0) || h->plan.op != EMAC_SUM || h->nsrc < 2 ||
+      h->nsrc > 8 || h->host_direct ||
+      emac_tree_kind(&h->plan.codes, h->plan.op) == 1 || (h->fan != 0 && h->fan != 1))
+    return 0;
+  sched[0] = 2 | 1 << 4; /* fold_kernel.hpp instantiation policy: (U 2, burst), (U 4, burst) */
+  sched[1] = 4 | 1 << 4;
+  if (!h->fan) return 2;
+  sched[2] = 4 | 5 << 4; /* node fan-out: (U 4, s_sleep 2 every 4 loads) too */
+  return 3;
+}
+
 static int upload_buckets(emac_handle *h, emac_bucket *b, int nb) {
   emac_edge *edges = NULL;
-  int rc;
+  int rc, sched[EMAC_TUNE_MAX], nc, k, i;
+  long vec = 0;
   /* (fan | EMAC_FAN_HOST: the schedule for buffers across PCIe, emac_gpu_pick_unroll) */
   if ((rc = emac_layout(b, nb, h->plan.op, h->nsrc, emac_tree_kind(&h->plan.codes, h->plan.op) == 1,
                         h->fan | (h->host_direct ? EMAC_FAN_HOST : 0),
@@ -399,7 +442,107 @@ static int upload_buckets(emac_handle *h, emac_bucket *b, int nb) {
   if (!rc && h->nedges && (rc = emac_gpu_malloc((void **)&h->d_edges, sizeof(emac_edge) * (size_t)h->nedges)) == 0)
     rc = emac_gpu_memcpy(h->d_edges, edges, sizeof(emac_edge) * (size_t)h->nedges);
   free(edges);
+  for (i = 0; i < nb; i++) vec += b[i].nvec;
+  nc = rc ? 0 : tune_candidates(h, sched);
+  if (!nc || vec * 16 * (h->nsrc + (h->fan ? h->nsrc : 1)) < EMAC_TUNE_MIN_BYTES) return rc;
+  {
+    emac_bucket *tb = (emac_bucket *)malloc(sizeof(emac_bucket) * (size_t)nb);
+    if (!tb) return EMAC_ERR_MALLOC;
+    h->tune.chosen = -1;
+    for (k = 0; k < nc && !rc; k++) {
+      emac_launch *L = &h->tune.L[k];
+      memcpy(tb, b, sizeof(emac_bucket) * (size_t)nb);
+      h->tune.n = k + 1; /* freed by release() from here on */
+      if (sched[k] == h->unroll) { /* the static pick: its upload is reused */
+        L->d_buckets = h->d_buckets;
+        L->nb = nb;
+        L->ntiles = h->ntiles;
+        L->tiles_per_bucket = h->tiles_per_bucket;
+        L->all_full = h->all_full;
+        L->d_edges = h->d_edges;
+        L->nedges = h->nedges;
+        L->unroll = h->unroll;
+      } else {
+        rc = emac_layout_as(tb, nb, h->plan.op, h->nsrc, 0, h->fan, sched[k], &edges, &L->nedges, &L->ntiles,
+                            &L->tiles_per_bucket, &L->all_full, &L->unroll);
+        if (!rc) {
+          L->nb = nb;
+          if ((rc = emac_gpu_malloc((void **)&L->d_buckets, sizeof(emac_bucket) * (size_t)nb)) == 0)
+            rc = emac_gpu_memcpy(L->d_buckets, tb, sizeof(emac_bucket) * (size_t)nb);
+          if (!rc && L->nedges && (rc = emac_gpu_malloc((void **)&L->d_edges, sizeof(emac_edge) * (size_t)L->nedges)) == 0)
+            rc = emac_gpu_memcpy(L->d_edges, edges, sizeof(emac_edge) * (size_t)L->nedges);
+          free(edges);
+        }
+      }
+      if (!rc) rc = emac_gpu_event_create_timed(&h->tune.ev[k][0]);
+      if (!rc) rc = emac_gpu_event_create_timed(&h->tune.ev[k][1]);
+    }
+    free(tb);
+  }
   return rc;
+}
+
+/* The handle's fold launch (fan 0 / 1), with the schedule tuning of emac_tune. */
+static int fold_launch(emac_handle *h) {
+  emac_tune *t = &h->tune;
+  int rc, k;
+  if (t->n && t->chosen < 0) {
+    const int s = t->starts++;
+    if (s >= 1 && s <= t->n) { /* candidate s - 1, timed */
+      const emac_launch *L = &t->L[s - 1];
+      if ((rc = emac_gpu_event_record(t->ev[s - 1][0], h->stream))) return rc;
+      if ((rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, h->fan, L->unroll, &h->plan.codes, L->d_buckets, L->nb,
+                              L->ntiles, L->tiles_per_bucket, L->all_full, L->d_edges, L->nedges, h->stream)))
+        return rc;
+      return emac_gpu_event_record(t->ev[s - 1][1], h->stream);
+    }
+    if (s == t->n + 1) { /* keep the fastest: it becomes the handle's launch */
+      int best = 0;
+      for (k = 0; k < t->n; k++) {
+        if ((rc = emac_gpu_event_elapsed_us(t->ev[k][0], t->ev[k][1], &t->us[k]))) return rc;
+        if (t->us[k] < t->us[best]) best = k;
+      }
+      void *old_b = h->d_buckets, *old_e = h->d_edges; /* the static pick's upload */
+      if (t->L[best].d_buckets != h->d_buckets) {
+        h->d_buckets = t->L[best].d_buckets;
+        h->d_edges = t->L[best].d_edges;
+        h->nb = t->L[best].nb;
+        h->ntiles = t->L[best].ntiles;
+        h->tiles_per_bucket = t->L[best].tiles_per_bucket;
+        h->all_full = t->L[best].all_full;
+        h->nedges = t->L[best].nedges;
+        h->unroll = t->L[best].unroll;
+      }
+      for (k = 0; k < t->n; k++) /* every upload but the kept one; the static pick's may be a candidate's */
+        if (k != best && t->L[k].d_buckets != old_b) {
+          emac_gpu_free(t->L[k].d_buckets);
+          emac_gpu_free(t->L[k].d_edges);
+        }
+      if (old_b != h->d_buckets) {
+        emac_gpu_free(old_b);
+        emac_gpu_free(old_e);
+      }
+      for (k = 0; k < t->n; k++) { /* release() frees the kept launch once, as the handle's */
+        t->L[k].d_buckets = h->d_buckets;
+        t->L[k].d_edges = h->d_edges;
+      }
+      t->chosen = best;
+      if (getenv("EXT_MPI_AMD_DEBUG_TUNE"))
+        fprintf(stderr, "ext_mpi_amd: fold schedule kept: U %d issue %d (%.1f us; %d candidates)\n", h->unroll & 15,
+                h->unroll >> 4, t->us[best], t->n);
+    }
+  }
+  return emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, h->fan, h->unroll, &h->plan.codes, h->d_buckets, h->nb, h->ntiles,
+                       h->tiles_per_bucket, h->all_full, h->d_edges, h->nedges, h->stream);
+}
+
+int ext_mpi_amd_handle_schedule(int handle, int *unroll, int *issue, int *tuned) {
+  const emac_handle *h = (handle >= 0 && handle < MAX_HANDLES) ? handles[handle] : NULL;
+  if (!h) return EMAC_ERR_ARG;
+  if (unroll) *unroll = h->unroll & 15;
+  if (issue) *issue = h->unroll >> 4;
+  if (tuned) *tuned = h->tune.n ? (h->tune.chosen >= 0 ? 1 : 0) : -1;
+  return 0;
 }
 
 /* EXT_MPI_NUM_SOCKETS_PER_NODE as the reference keeps it: one process-wide parameter read at
@@ -1793,10 +1936,7 @@ static int enqueue_legs(emac_handle *h, int legs) {
       (rc = emac_gpu_fold_remote(h->plan.dtype, h->plan.op, h->nsrc, h->unroll, &h->plan.codes, h->d_buckets, h->nb,
                                  h->ntiles, h->tiles_per_bucket, h->all_full, h->d_edges, h->nedges, ipc_go(h), h->stream)))
     return rc;
-  if ((legs & EXT_MPI_AMD_LEG_FOLD) && h->fan != 2 &&
-      (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, h->fan, h->unroll, &h->plan.codes, h->d_buckets, h->nb, h->ntiles,
-                          h->tiles_per_bucket, h->all_full, h->d_edges, h->nedges, h->stream)))
-    return rc;
+  if ((legs & EXT_MPI_AMD_LEG_FOLD) && h->fan != 2 && (rc = fold_launch(h))) return rc;
   if (h->kind == KIND_COMM && h->nodes > 1) {
     /* several nodes: per step the exchange of the lines with the column peers and the fold of
        the kept lines' partials (a left fold of radix leaves in the order the program lists

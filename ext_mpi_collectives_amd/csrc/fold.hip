@@ -272,6 +272,19 @@ int emac_gpu_event_create(void **ev) {
   *ev = e;
   return 0;
 }
+int emac_gpu_event_create_timed(void **ev) {
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return EMAC_ERR_DEVICE;
+  *ev = e;
+  return 0;
+}
+int emac_gpu_event_elapsed_us(void *a, void *b, float *us) {
+  float ms = 0.f;
+  int rc = ok(hipEventSynchronize(static_cast<hipEvent_t>(b)));
+  if (!rc) rc = ok(hipEventElapsedTime(&ms, static_cast<hipEvent_t>(a), static_cast<hipEvent_t>(b)));
+  *us = ms * 1000.f;
+  return rc;
+}
 int emac_gpu_event_destroy(void *ev) { return ev ? ok(hipEventDestroy(static_cast<hipEvent_t>(ev))) : 0; }
 int emac_gpu_event_record(void *ev, void *stream) {
   return ok(hipEventRecord(static_cast<hipEvent_t>(ev), static_cast<hipStream_t>(stream)));

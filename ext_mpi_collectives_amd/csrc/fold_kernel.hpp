@@ -52,6 +52,11 @@ constexpr int kMaxLevels = 4;  // 16 leaves with radix >= 2
 // get away with a single fence each (ipc.hip).
 constexpr int kRemote = 256;
 constexpr int kSysCoherent = 17;  // sc0 | sc1
+// ISSUE bits 9 / 10: default-policy (allocating) stores / loads instead of nontemporal ones. A
+// launch whose bytes fit beside the 256 MiB Infinity Cache leaves its results there to drain to
+// HBM behind the next launch; nontemporal accesses win on the long streams (tools/pipebench.hip).
+constexpr int kPlainStore = 512;
+constexpr int kPlainLoad = 1024;
 typedef unsigned int U32x4 __attribute__((ext_vector_type(4)));
 
 template <typename V>
@@ -204,7 +209,7 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
   typedef typename Lane<T>::V V;
   typedef __attribute__((address_space(1))) V GV;
   constexpr bool SRC_MAJOR = ISSUE & 1;
-  constexpr int SLEEP = (ISSUE >> 1) & 127;
+  constexpr int SLEEP = (ISSUE >> 1) & 127;  // bits 1..7
   constexpr bool REMOTE = ISSUE & kRemote;
   // vectors of this tile still inside the bucket (wave-uniform); lane offsets are 32-bit so
   // every access is `global_*_dwordx4 v, v_off, s_base` with the tile base in SGPRs
@@ -219,6 +224,8 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
     const unsigned v = threadIdx.x + (unsigned)(u * EMAC_BLOCK);
     if constexpr (REMOTE) {
       if (FULL || (long)v < left) x[u][s] = sys_load16<V>((const void *)src[s], v * 16u);
+    } else if constexpr ((ISSUE & kPlainLoad) != 0) {
+      if (FULL || (long)v < left) x[u][s] = src[s][v];
     } else {
       if (FULL || (long)v < left) x[u][s] = __builtin_nontemporal_load(src[s] + v);
     }
@@ -239,6 +246,8 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
       const unsigned v = threadIdx.x + (unsigned)(u * EMAC_BLOCK);
       if constexpr (REMOTE) {
         if (FULL || (long)v < left) sys_store16<V>((void *)dst, v * 16u, r[u]);
+      } else if constexpr ((ISSUE & kPlainStore) != 0) {
+        if (FULL || (long)v < left) dst[v] = r[u];
       } else {
         if (FULL || (long)v < left) __builtin_nontemporal_store(r[u], dst + v);
       }

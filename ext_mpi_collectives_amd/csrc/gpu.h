@@ -61,6 +61,8 @@ int emac_gpu_stream_sync(void *stream);
 int emac_gpu_stream_query(void *stream); /* 1 idle, 0 busy, <0 error */
 int emac_gpu_device_sync(void);
 int emac_gpu_event_create(void **ev); /* timing disabled */
+int emac_gpu_event_create_timed(void **ev);
+int emac_gpu_event_elapsed_us(void *a, void *b, float *us); /* waits for b */
 int emac_gpu_event_destroy(void *ev);
 int emac_gpu_event_record(void *ev, void *stream);
 int emac_gpu_stream_wait(void *stream, void *ev); /* stream waits for ev */
@@ -165,6 +167,9 @@ void emac_split_alignment(emac_bucket *b, int nsrc, long len, int tsize);
 /* tree: 1 for a runtime-code tree (emac_tree_kind == 1), which has its own launch schedules */
 int emac_layout(emac_bucket *b, int nb, int op, int nsrc, int tree, int fan, emac_edge **edges, int *nedges,
                 long *ntiles, long *tiles_per_bucket, int *all_full, int *unroll);
+/* the same with the launch schedule given (forced = U | ISSUE << 4; 0: emac_gpu_pick_unroll) */
+int emac_layout_as(emac_bucket *b, int nb, int op, int nsrc, int tree, int fan, int forced, emac_edge **edges,
+                   int *nedges, long *ntiles, long *tiles_per_bucket, int *all_full, int *unroll);
 
 #ifdef __cplusplus
 }

@@ -61,11 +61,16 @@ int emac_tree_kind(const emac_codes *c, int op) {
 
 int emac_layout(emac_bucket *b, int nb, int op, int nsrc, int tree, int fan, emac_edge **edges_out, int *nedges,
                 long *ntiles_out, long *tpb_out, int *all_full_out, int *unroll_out) {
+  return emac_layout_as(b, nb, op, nsrc, tree, fan, 0, edges_out, nedges, ntiles_out, tpb_out, all_full_out, unroll_out);
+}
+
+int emac_layout_as(emac_bucket *b, int nb, int op, int nsrc, int tree, int fan, int forced, emac_edge **edges_out,
+                   int *nedges, long *ntiles_out, long *tpb_out, int *all_full_out, int *unroll_out) {
   long total = 0, tv, tiles = 0, uniform = -1;
   int i, ne = 0, unroll, all_full = 1;
   emac_edge *edges;
   for (i = 0; i < nb; i++) total += b[i].nvec;
-  unroll = emac_gpu_pick_unroll(op, nsrc, tree, fan, total); /* U | ISSUE << 4 */
+  unroll = forced > 0 ? forced : emac_gpu_pick_unroll(op, nsrc, tree, fan, total); /* U | ISSUE << 4 */
   tv = (long)EMAC_BLOCK * (unroll & 15);
   for (i = 0; i < nb; i++) {
     long t = (b[i].nvec + tv - 1) / tv;

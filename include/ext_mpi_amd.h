@@ -118,6 +118,10 @@ int ext_mpi_amd_wait(int handle);
  * device mirrors) are released locally. */
 int ext_mpi_amd_done(int handle);
 void *ext_mpi_amd_stream(int handle); /* hipStream_t the handle runs on */
+/* The fold's launch schedule (U 16-byte vectors per lane per leaf, load-issue schedule) and
+ * whether it was tuned on this handle's first Starts (1 kept, 0 still measuring, -1 not tuned:
+ * EXT_MPI_AMD_AUTOTUNE=0 or a shape with one schedule). Introspection for benchmarks. */
+int ext_mpi_amd_handle_schedule(int handle, int *unroll, int *issue, int *tuned);
 /* Run later Starts on a caller-owned hipStream_t (e.g. to serialise several handles). */
 int ext_mpi_amd_set_stream(int handle, void *hip_stream);
 /* Start a subset of the legs (benchmarking / profiling): the reference interleaves them in one

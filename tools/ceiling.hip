@@ -4,7 +4,8 @@
 //   ceiling_read_glds: a read-only stream through LDS-DMA (global_load_lds_dwordx4, nontemporal):
 //                      the best read rate measured on MI355X in round 1 (tools/ldsbench.hip,
 //                      ~6.99 TB/s at 4 GiB against ~6.07 TB/s with nt loads into VGPRs).
-//   ceiling_copy_nt:   a nontemporal copy, 1 byte written per byte read (the node-form fold's mix).
+//   ceiling_copy:      a 1:1 copy (1 byte written per byte read: the node-form fold's mix), K = 4
+//                      vectors per lane in flight, nontemporal or default-policy accesses.
 // Each call enqueues `iters` launches over `bytes` (a multiple of 16 KiB) on `stream`.
 #include <hip/hip_runtime.h>
 
@@ -35,9 +36,24 @@ __global__ __launch_bounds__(256) void read_glds(const f4 *__restrict__ a, long 
   if (acc.x == 12345.f) out[0] = acc.y + acc.z + acc.w;
 }
 
-__global__ __launch_bounds__(256) void copy_nt(const f4 *__restrict__ a, f4 *__restrict__ b, long n) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-    __builtin_nontemporal_store(__builtin_nontemporal_load((const G4 *)a + i), (G4 *)b + i);
+// 1:1 copies, K = 4 vectors per lane in flight, grid-stride: nontemporal (the long streams'
+// best) or default-policy (the best below ~64 MiB, where the writes drain through the Infinity
+// Cache behind the next launch): tools/schedbench.hip, profiles/r03_schedbench_*.txt
+template <bool NT>
+__global__ __launch_bounds__(256) void copy_k4(const f4 *__restrict__ a, f4 *__restrict__ b, long n) {
+  const long step = (long)gridDim.x * 256 * 4;
+  for (long i0 = (long)blockIdx.x * 256 * 4 + threadIdx.x; i0 < n; i0 += step) {
+    f4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = NT ? __builtin_nontemporal_load((const G4 *)a + i0 + k * 256) : ((const G4 *)a)[i0 + k * 256];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (NT)
+        __builtin_nontemporal_store(v[k], (G4 *)b + i0 + k * 256);
+      else
+        ((G4 *)b)[i0 + k * 256] = v[k];
+    }
+  }
 }
 
 }  // namespace
@@ -53,12 +69,18 @@ int ceiling_read_glds(const void *buf, long bytes, int iters, float *sink, void 
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-int ceiling_copy_nt(const void *src, void *dst, long bytes, int iters, void *stream) {
+/* variant 0: nontemporal, 1: default policy */
+int ceiling_copy(const void *src, void *dst, long bytes, int iters, int variant, void *stream) {
   const long n = bytes / 16;
-  if (n % 256 || iters < 1) return -3;
-  for (int i = 0; i < iters; i++)
-    hipLaunchKernelGGL(copy_nt, dim3(8192), dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<const f4 *>(src),
-                       static_cast<f4 *>(dst), n);
+  if (n % 1024 || iters < 1) return -3;
+  for (int i = 0; i < iters; i++) {
+    if (variant == 0)
+      hipLaunchKernelGGL(copy_k4<true>, dim3(4096), dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<const f4 *>(src),
+                         static_cast<f4 *>(dst), n);
+    else
+      hipLaunchKernelGGL(copy_k4<false>, dim3(4096), dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<const f4 *>(src),
+                         static_cast<f4 *>(dst), n);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
