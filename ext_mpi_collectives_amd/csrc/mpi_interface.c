@@ -65,6 +65,15 @@ static int cfg_ports_nodes = 0;      /* EXT_MPI_NUM_PORTS: its nodes (0 unset, -
 static int cfg_ports[16];             /* ... its 0-terminated port list (parse_ports) */
 static int cfg_blocking = 0;
 static int cfg_rccl = 0; /* EXT_MPI_AMD_TRANSPORT=rccl: legs over RCCL instead of hipIpc mappings */
+/* Accepted as the reference reads them (ext_mpi.c:58-66, 88-116), with nothing to switch here:
+   EXT_MPI_ALTERNATING -- the reference keeps two byte-code copies and swaps them per Start
+   (ext_mpi_native.c:215-230, 554-617) so a Start's flags cannot meet the previous one's; here
+   every Start is stream-ordered behind the previous and the barrier epochs count per slot;
+   EXT_MPI_FAST -- executes the schedule as generated C source (source_code.c) with the same
+   arithmetic; there is no interpreter to replace. EXT_MPI_NOT_RECURSIVE selects the
+   non-recursive inter-node generator (allreduce.c), out of scope: communicators of several nodes
+   are refused under it (the blocking front end hands them to PMPI), one node is unaffected. */
+static int cfg_alternating = -1, cfg_fast = 0, cfg_not_recursive = 0;
 static int initialised = 0;
 static int comm_keyval = MPI_KEYVAL_INVALID;
 static int blocking_keyval = MPI_KEYVAL_INVALID;
@@ -158,6 +167,14 @@ static void read_env(void) {
     env_int("EXT_MPI_NUM_TASKS_PER_SOCKET", &cfg_tasks_per_socket);
     cfg_ports_nodes = parse_ports(getenv("EXT_MPI_NUM_PORTS"), cfg_ports); /* ext_mpi.c:124-157 */
     cfg_rccl = getenv("EXT_MPI_AMD_TRANSPORT") && !strcmp(getenv("EXT_MPI_AMD_TRANSPORT"), "rccl");
+    if (env_int("EXT_MPI_NOT_RECURSIVE", &cfg_not_recursive))
+      printf("# EXT_MPI not recursive = %d\n", cfg_not_recursive); /* ext_mpi.c:58-63 prints it always */
+    if (env_int("EXT_MPI_FAST", &cfg_fast) && cfg_verbose) printf("# EXT_MPI fast %d\n", cfg_fast);
+    if (getenv("EXT_MPI_ALTERNATING")) {
+      const char a = getenv("EXT_MPI_ALTERNATING")[0];
+      if (a == '0' || a == '1') cfg_alternating = a - '0';
+      if (cfg_verbose && cfg_alternating >= 0) printf(cfg_alternating ? "# EXT_MPI alternating\n" : "# EXT_MPI not alternating\n");
+    }
     if (c) {
       strncpy(cfg_copyin, c, sizeof(cfg_copyin) - 1);
       len = (int)strlen(cfg_copyin) + 1;
@@ -171,6 +188,9 @@ static void read_env(void) {
   PMPI_Bcast(&cfg_ports_nodes, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(cfg_ports, 16, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_rccl, 1, MPI_INT, 0, MPI_COMM_WORLD);
+  PMPI_Bcast(&cfg_alternating, 1, MPI_INT, 0, MPI_COMM_WORLD);
+  PMPI_Bcast(&cfg_fast, 1, MPI_INT, 0, MPI_COMM_WORLD);
+  PMPI_Bcast(&cfg_not_recursive, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&len, 1, MPI_INT, 0, MPI_COMM_WORLD);
   if (len > 0) PMPI_Bcast(cfg_copyin, len, MPI_CHAR, 0, MPI_COMM_WORLD);
   cfg_has_copyin = len > 0;
@@ -337,7 +357,7 @@ static int node_comm(MPI_Comm comm, const void *devbuf, int check_env, int *ext_
   if (!nodes) return EXT_MPI_AMD_ERROR_UNSUPPORTED; /* other inter-node shapes: out of scope */
   if (check_env && nodes > 1) {
     const int *hp;
-    if (env_ports(nodes, &hp)) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
+    if (cfg_not_recursive || env_ports(nodes, &hp)) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
   }
   ndev = ext_mpi_amd_gpu_device_count();
   device = ext_mpi_amd_gpu_device_of(devbuf);
@@ -584,7 +604,7 @@ static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int
     int nrank;
     comm_topology(comm, &b->nodes, &b->nsize, &nrank); /* collective: every rank, first call */
   }
-  if (!b->nodes) return 1; /* an inter-node shape this path does not take */
+  if (!b->nodes || (b->nodes > 1 && cfg_not_recursive)) return 1; /* an inter-node shape this path does not take */
   if (!b->loaded) blocking_load_rows(b, comm);
   on_dev = ext_mpi_amd_gpu_is_device_pointer(recvbuf) && ext_mpi_amd_gpu_is_device_pointer(sendbuf);
   side = on_dev && b->nrow[1] ? 1 : 0;
@@ -769,6 +789,7 @@ int EXT_MPI_Allreduce_init(const void *sendbuf, void *recvbuf, int count, MPI_Da
   if (cfg_num_sockets > 1 && nsize % cfg_num_sockets) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
   if (nodes > 1) { /* this handle's inter-node schedule: EXT_MPI_NUM_PORTS or the default */
     const int *hp;
+    if (cfg_not_recursive) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
     if (env_ports(nodes, &hp)) return EXT_MPI_AMD_ERROR_UNSUPPORTED;
     if ((rc = ext_mpi_amd_comm_set_node_ports(ext_comm, nodes, hp))) return rc;
   }

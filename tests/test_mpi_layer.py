@@ -183,3 +183,27 @@ def test_mpi_layer_multi_rank_one_gpu(tmp_path, n, args, extra):
     env.update(extra)
     res, out = _run(exe, n, args, env=env, timeout=180)
     assert res and res[0].startswith("RESULT ok"), out
+
+
+@pytest.mark.parametrize("env,n,want,printed", [
+    ({"EXT_MPI_ALTERNATING": "1", "EXT_MPI_VERBOSE": "1"}, 2, "RESULT no-device", "# EXT_MPI alternating"),
+    ({"EXT_MPI_ALTERNATING": "0", "EXT_MPI_VERBOSE": "1"}, 2, "RESULT no-device", "# EXT_MPI not alternating"),
+    ({"EXT_MPI_FAST": "1", "EXT_MPI_VERBOSE": "1"}, 2, "RESULT no-device", "# EXT_MPI fast 1"),
+    # the non-recursive inter-node generator (allreduce.c) is out of scope: one node unaffected,
+    # logical nodes refused (the reference prints the setting whatever EXT_MPI_VERBOSE says)
+    ({"EXT_MPI_NOT_RECURSIVE": "1"}, 2, "RESULT no-device", "# EXT_MPI not recursive = 1"),
+    ({"EXT_MPI_NOT_RECURSIVE": "1", "EXT_MPI_NUM_TASKS_PER_SOCKET": "1"}, 2, "RESULT fail rc=-4",
+     "# EXT_MPI not recursive = 1"),
+])
+def test_mpi_env_keys_without_gpu(tmp_path, env, n, want, printed):
+    """read_env's other keys (ext_mpi.c:58-116) are read on rank 0 and broadcast like the
+    reference's: EXT_MPI_ALTERNATING and EXT_MPI_FAST are accepted with nothing to switch (every
+    Start is stream-ordered; there is no byte-code interpreter), EXT_MPI_NOT_RECURSIVE refuses
+    communicators of several nodes."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    exe = _build(tmp_path)
+    res, out = _run(exe, n, [1000, "i", "dev"], env=env)
+    assert res and res[0].startswith(want), out
+    assert printed in out, out
