@@ -257,6 +257,23 @@ def LEG_STEP(s):
     return (s + 1) << LEG_STEP_SHIFT
 
 
+def default_node_ports(nodes):
+    """The inter-node ports list without EXT_MPI_NUM_PORTS (plan.c emac_node_sched_build): one
+    port per step for a power of two, else one step of radix `nodes` up to 16 nodes, else one
+    step per prime factor, largest first (the allgather steps in reverse)."""
+    k = (nodes - 1).bit_length()
+    if 1 << k == nodes:
+        return [-1] * k + [1] * k
+    if nodes <= MAX_RANKS:
+        return [-(nodes - 1), nodes - 1]
+    f, m = [], nodes
+    for d in range(MAX_RANKS, 1, -1):
+        while m % d == 0 and all(d % q for q in range(2, int(d ** 0.5) + 1)):
+            f.append(d)
+            m //= d
+    return [1 - d for d in f] + [d - 1 for d in reversed(f)]
+
+
 def node_steps(nodes, ports=None):
     """(exchange steps, copying allgather steps) of the inter-node schedule (plan.h
     emac_node_sched): the reduce-scatter steps and the allgather steps that still reduce inside
@@ -265,8 +282,7 @@ def node_steps(nodes, ports=None):
     if nodes <= 1:
         return 0, 0
     if ports is None:
-        k = (nodes - 1).bit_length()
-        ports = [-1] * k + [1] * k if 1 << k == nodes else [-(nodes - 1), nodes - 1]
+        ports = default_node_ports(nodes)
     rs = [1 - p for p in ports if p < 0]
     ag = [p + 1 for p in ports if p > 0]
     gm = nodes

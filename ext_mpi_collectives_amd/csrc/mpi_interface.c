@@ -38,7 +38,7 @@
  * bootstrapped with PMPI_Allgather; "rccl" runs the legs as RCCL point-to-point rounds,
  * bootstrapped with PMPI_Bcast of the unique id. One engine communicator per MPI communicator,
  * cached as an MPI attribute and destroyed with it. The communicator lies within one node, or
- * spans up to 16 nodes of equal size in node-major rank order: then the legs run over RCCL with
+ * spans up to EXT_MPI_AMD_MAX_NODES (64) nodes of equal size in node-major rank order: then the legs run over RCCL with
  * the reference's inter-node schedule (EXT_MPI_NUM_PORTS; unset: one port per step for a power of
  * two, else one step; ext_mpi_amd_comm_set_node_ports); other inter-node shapes return
  * EXT_MPI_AMD_ERROR_UNSUPPORTED (the blocking front end hands them to PMPI).
@@ -62,7 +62,8 @@ static int cfg_debug = 1;
 static int cfg_num_sockets = -1;
 static int cfg_tasks_per_socket = -1; /* EXT_MPI_NUM_TASKS_PER_SOCKET: ranks of a (logical) socket */
 static int cfg_ports_nodes = 0;      /* EXT_MPI_NUM_PORTS: its nodes (0 unset, -1 not this path) */
-static int cfg_ports[16];             /* ... its 0-terminated port list (parse_ports) */
+#define EMAC_PORTS_MAX 17 /* a 0-terminated ports list: 64 nodes at one port per step take 12 */
+static int cfg_ports[EMAC_PORTS_MAX]; /* ... its 0-terminated port list (parse_ports) */
 static int cfg_blocking = 0;
 static int cfg_rccl = 0; /* EXT_MPI_AMD_TRANSPORT=rccl: legs over RCCL instead of hipIpc mappings */
 /* Accepted as the reference reads them (ext_mpi.c:58-66, 88-116), with nothing to switch here:
@@ -100,7 +101,6 @@ static int env_int(const char *name, int *out) {
    many nodes. Returns the group's nodes and the 0-terminated list in ports[] (EMAC_PORTS_MAX
    entries at most), 0 for an empty string, or -1 when the string names anything else: several
    groups, a list ending in a reduce-scatter port (reduce_scatter_core), radices that do not fit G. */
-#define EMAC_PORTS_MAX 9
 static int parse_ports(const char *s, int *ports) {
   int groups = 0, bare = 0, nodes = 0, n = 0, in_group = 0, ok = 1, i, prs = 1, pag = 1, seen_ag = 0;
   const char *p = s;
@@ -130,7 +130,7 @@ static int parse_ports(const char *s, int *ports) {
       continue;
     }
     if (!in_group) bare = 1;
-    if (n == EMAC_PORTS_MAX - 1 || v == 0 || v < -16 || v > 16) {
+    if (n == EMAC_PORTS_MAX - 1 || v == 0 || v < -(EXT_MPI_AMD_MAX_NODES - 1) || v > EXT_MPI_AMD_MAX_NODES - 1) {
       ok = 0;
       continue;
     }
@@ -186,7 +186,7 @@ static void read_env(void) {
   PMPI_Bcast(&cfg_num_sockets, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_tasks_per_socket, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_ports_nodes, 1, MPI_INT, 0, MPI_COMM_WORLD);
-  PMPI_Bcast(cfg_ports, 16, MPI_INT, 0, MPI_COMM_WORLD);
+  PMPI_Bcast(cfg_ports, EMAC_PORTS_MAX, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_rccl, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_alternating, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_fast, 1, MPI_INT, 0, MPI_COMM_WORLD);
@@ -293,7 +293,7 @@ static int comm_attr_delete(MPI_Comm comm, int keyval, void *attr, void *extra) 
   return MPI_SUCCESS;
 }
 
-/* The communicator's node layout (collective): *nodes = 1 (one node) or up to 16 nodes of equal
+/* The communicator's node layout (collective): *nodes = 1 (one node) or up to 64 nodes of equal
    size in node-major rank order (the reference's row layout, ext_mpi_native.c:879-960), 0 for
    any other shape; *nsize = ranks per node, *nrank = rank in the node. The reference's node
    is EXT_MPI_NUM_TASKS_PER_SOCKET x sockets consecutive ranks when that is set (ext_mpi.c:195-215,
@@ -316,7 +316,7 @@ static void comm_topology(MPI_Comm comm, int *nodes, int *nsize, int *nrank) {
   }
   *nodes = *nsize > 0 && size % *nsize == 0 ? size / *nsize : 0;
   v[0] = *nsize == size;
-  v[1] = *nodes >= 2 && *nodes <= 16 && *nrank == rank % *nsize;
+  v[1] = *nodes >= 2 && *nodes <= EXT_MPI_AMD_MAX_NODES && *nrank == rank % *nsize;
   PMPI_Allreduce(MPI_IN_PLACE, v, 2, MPI_INT, MPI_MIN, comm);
   *nodes = v[0] ? 1 : v[1] ? *nodes : 0;
 }

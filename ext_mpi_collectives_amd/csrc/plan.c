@@ -381,7 +381,7 @@ int emac_comm_program(const emac_plan *p, int me, long send_phase, emac_p2p **op
 }
 
 int emac_node_sched_build(emac_node_sched *s, int nodes, const int *ports) {
-  int def[2 * EMAC_MAX_NODE_STEPS + 1], ag[2 * EMAC_MAX_NODE_STEPS], nag = 0, i, j, g, prod_rs = 1, prod_ag = 1;
+  int def[2 * EMAC_MAX_NODE_STEPS + 1], ag[2 * EMAC_MAX_NODE_STEPS] = {0}, nag = 0, i, j, g, prod_rs = 1, prod_ag = 1;
   if (!s || nodes < 1 || nodes > EMAC_MAX_NODES) return EMAC_ERR_ARG;
   memset(s, 0, sizeof(*s));
   s->nodes = nodes;
@@ -396,10 +396,28 @@ int emac_node_sched_build(emac_node_sched *s, int nodes, const int *ports) {
         def[k + i] = 1;
       }
       def[2 * k] = 0;
-    } else { /* one step of radix `nodes` */
+    } else if (nodes <= EMAC_MAX_RANKS) { /* one step of radix `nodes` */
       def[0] = -(nodes - 1);
       def[1] = nodes - 1;
       def[2] = 0;
+    } else { /* more nodes than one fold takes leaves: a step per prime factor, largest first */
+      int f[2 * EMAC_MAX_NODE_STEPS], nf = 0, m = nodes, d;
+      for (d = EMAC_MAX_RANKS; d >= 2; d--)
+        while (m % d == 0 && d > 1) {
+          int q, prime = 1;
+          for (q = 2; q * q <= d; q++)
+            if (d % q == 0) prime = 0;
+          if (!prime) break;
+          if (nf == EMAC_MAX_NODE_STEPS) return EMAC_ERR_UNSUPPORTED;
+          f[nf++] = d;
+          m /= d;
+        }
+      if (m != 1) return EMAC_ERR_UNSUPPORTED; /* a prime factor above EMAC_MAX_RANKS */
+      for (i = 0; i < nf; i++) {
+        def[i] = -(f[i] - 1);
+        def[nf + i] = f[nf - 1 - i] - 1;
+      }
+      def[2 * nf] = 0;
     }
     ports = def;
   }
@@ -409,7 +427,8 @@ int emac_node_sched_build(emac_node_sched *s, int nodes, const int *ports) {
      the same lines; the allgather steps whose block is still smaller than gm reduce inside it
      (:348-403), the others copy (:404-437). */
   for (i = 0; ports[i] < 0; i++) {
-    if (s->nsteps == EMAC_MAX_NODE_STEPS) return EMAC_ERR_UNSUPPORTED;
+    /* a step folds radix partials in one launch of at most EMAC_MAX_RANKS leaves */
+    if (s->nsteps == EMAC_MAX_NODE_STEPS || 1 - ports[i] > EMAC_MAX_RANKS) return EMAC_ERR_UNSUPPORTED;
     s->radix[s->nsteps++] = 1 - ports[i];
     prod_rs *= 1 - ports[i];
   }
@@ -422,7 +441,7 @@ int emac_node_sched_build(emac_node_sched *s, int nodes, const int *ports) {
   if (prod_ag != nodes || nodes % prod_rs) return EMAC_ERR_ARG;
   s->gm = nodes / prod_rs;
   for (j = 0, g = 1; g < s->gm; g *= ag[j], j++) {
-    if (s->nred == EMAC_MAX_NODE_STEPS) return EMAC_ERR_UNSUPPORTED;
+    if (s->nred == EMAC_MAX_NODE_STEPS || ag[j] > EMAC_MAX_RANKS) return EMAC_ERR_UNSUPPORTED;
     s->red_radix[s->nred++] = ag[j];
   }
   if (g != s->gm) return EMAC_ERR_UNSUPPORTED; /* an allgather step across the group boundary */

@@ -117,8 +117,8 @@ enum {
   EMAC_LEG_NODES_FOLD = 64,
   EMAC_LEG_NODES_AG = 128
 };
-#define EMAC_MAX_NODES 16
-#define EMAC_MAX_NODE_STEPS 4 /* inter-node reduce-scatter steps */
+#define EMAC_MAX_NODES 64
+#define EMAC_MAX_NODE_STEPS 6 /* inter-node reduce-scatter steps (one port per step over 64 nodes) */
 #define EMAC_LEG_STEP_SHIFT 8 /* node legs and folds carry their step: leg | step << 8 */
 
 /* The inter-node schedule of several nodes (src/core/allreduce_recursive.c:222-453, the

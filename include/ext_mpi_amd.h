@@ -63,6 +63,7 @@ extern "C" {
 
 #define EXT_MPI_AMD_UNIQUE_ID_BYTES 128
 #define EXT_MPI_AMD_MAX_RANKS 16
+#define EXT_MPI_AMD_MAX_NODES 64 /* nodes of one communicator's inter-node schedule */
 
 /* ---- persistent Allreduce, every node rank's buffers in this process (one device) ---- */
 int ext_mpi_amd_node_allreduce_init(int nranks, const void *const *sendbufs, void *const *recvbufs, long count,
@@ -174,7 +175,7 @@ typedef struct {
 int ext_mpi_amd_comm_program(int nranks, int rank, long count, int dtype, const char *copyin, long send_phase,
                              ext_mpi_amd_p2p *ops, int max_ops, int *nops, ext_mpi_amd_fold *folds, int max_folds,
                              int *nfolds, long *staging_bytes);
-/* The same for `nodes` (1..16) nodes of ranks_per_node ranks under the inter-node ports `ports`
+/* The same for `nodes` (1..EXT_MPI_AMD_MAX_NODES) nodes of ranks_per_node ranks under the inter-node ports `ports`
    (as ext_mpi_amd_comm_set_node_ports); `rank` is global (node-major); node legs and folds carry
    their step in leg >> 8. _nodes: the one-port schedule of a power of two. */
 int ext_mpi_amd_comm_program_node_ports(int nodes, const int *ports, int ranks_per_node, int rank, long count,
@@ -190,7 +191,7 @@ int ext_mpi_amd_comm_program_nodes(int nodes, int ranks_per_node, int rank, long
  * reduce_copies_* emission as one node, into shared memory), the inter-node algorithm of
  * src/core/allreduce_recursive.c:222-453 over the node partials (EXT_MPI_NUM_PORTS), the node's
  * copy-out (src/mpi/ext_mpi_native.c:879-1000). On an RCCL (or loopback) communicator whose ranks
- * [n * size/nodes, (n + 1) * size/nodes) form node n, nodes <= 16, set before
+ * [n * size/nodes, (n + 1) * size/nodes) form node n, nodes <= EXT_MPI_AMD_MAX_NODES, set before
  * ext_mpi_amd_allreduce_init; copyin then describes ONE node (its ranks_per_node positions).
  * `ports` is the reference's num_ports list, 0-terminated: the reduce-scatter ports (negative,
  * radix |p| + 1 each), then the allgather ports (positive) whose radices multiply to `nodes` --

@@ -96,8 +96,8 @@ done:
 /* rank_perm_heuristic, rank_permutation.c:12-87 (qsort over equal values taken as stable, as
    glibc's merge-sort qsort leaves them) */
 static void ref_perm_heuristic(int num_nodes, const long *counts, int *rank_perm) {
-  long value[16], v2[16], aval[16];
-  int key[16], color[16], k2[16], c2[16], akey[16], num_colors = num_nodes, i, j, k;
+  long value[REF_MAX_NODES], v2[REF_MAX_NODES], aval[REF_MAX_NODES];
+  int key[REF_MAX_NODES], color[REF_MAX_NODES], k2[REF_MAX_NODES], c2[REF_MAX_NODES], akey[REF_MAX_NODES], num_colors = num_nodes, i, j, k;
   for (i = 0; i < num_nodes; i++) {
     value[i] = counts[i];
     key[i] = color[i] = i;
@@ -186,12 +186,12 @@ static void ref_perm_heuristic(int num_nodes, const long *counts, int *rank_perm
 int ref_emulate_node_ports(int nodes, const int *ports, int R, long count, int dtype, int red, const char *copyin,
                            int in_place, int num_sockets, void *const *sendbufs, void *const *recvbufs) {
   const int ts = ref_type_size(dtype);
-  int rad[8], ag[8] = {0}, nrs = 0, nag = 0, task_node[16], node_task[16], n, r, t, k, s, i, j, G, g, gm, rc = 0, prod_rs = 1,
+  int rad[8], ag[8] = {0}, nrs = 0, nag = 0, task_node[REF_MAX_NODES], node_task[REF_MAX_NODES], n, r, t, k, s, i, j, G, g, gm, rc = 0, prod_rs = 1,
       prod_ag = 1;
-  long lo[17];
+  long lo[REF_MAX_NODES + 1];
   char **cur = NULL, **nxt = NULL;
   const size_t bytes = (size_t)count * (size_t)ts;
-  if (nodes < 1 || nodes > 16 || R < 1 || ts <= 0) return -1;
+  if (nodes < 1 || nodes > REF_MAX_NODES || R < 1 || ts <= 0) return -1;
   for (n = 0; n < nodes; n++)
     if ((rc = ref_emulate_op_s(R, count, dtype, red, copyin, in_place, num_sockets, sendbufs + n * R, recvbufs + n * R)))
       return rc;
@@ -214,7 +214,7 @@ int ref_emulate_node_ports(int nodes, const int *ports, int R, long count, int d
   for (j = 0, g = 1; g < gm; g *= ag[j], j++);
   if (g != gm) return -1; /* an allgather step straddling gm: not restated */
   {
-    long sz[16];
+    long sz[REF_MAX_NODES];
     int equal = 1;
     for (t = 0; t < nodes; t++) {
       sz[t] = nrs ? count / nodes + (t < count % nodes) : (t ? 0 : count);
@@ -247,7 +247,7 @@ int ref_emulate_node_ports(int nodes, const int *ports, int R, long count, int d
   for (G = nodes, s = 0; s < nrs; G /= rad[s], s++) {
     const int p = rad[s] - 1, Gn = G / rad[s], last = s == nrs - 1;
     for (t = 0; t < nodes; t++) {
-      int peer[16];
+      int peer[REF_MAX_NODES];
       const long a = lo[t / Gn * Gn], b = lo[t / Gn * Gn + Gn];
       char *acc = nxt[t] + a * ts;
       const long len = b - a;
@@ -281,7 +281,7 @@ int ref_emulate_node_ports(int nodes, const int *ports, int R, long count, int d
   for (j = 0, g = 1; g < gm; g *= ag[j], j++) {
     const int q = ag[j] - 1, gnext = g * ag[j], first = nrs == 0 && j == 0;
     for (t = 0; t < nodes; t++) {
-      int peer[16];
+      int peer[REF_MAX_NODES];
       const long a = lo[t / gm * gm], b = lo[t / gm * gm + gm], len = b - a;
       char *acc = nxt[t] + a * ts;
       for (i = 0; i < q; i++) peer[i] = (t + g * (i + 1)) % gnext + t / gnext * gnext;
@@ -331,8 +331,8 @@ out:
 /* one port per step over 2^k nodes ("-1 ... -1 1 ... 1") */
 int ref_emulate_nodes(int nodes, int R, long count, int dtype, int red, const char *copyin, int in_place,
                       int num_sockets, void *const *sendbufs, void *const *recvbufs) {
-  int ports[17], k = 0, i;
-  if (nodes < 1 || nodes > 16 || (nodes & (nodes - 1))) return -1;
+  int ports[2 * 8 + 1], k = 0, i;
+  if (nodes < 1 || nodes > REF_MAX_NODES || (nodes & (nodes - 1))) return -1;
   while ((1 << k) < nodes) k++;
   for (i = 0; i < k; i++) {
     ports[i] = -1;

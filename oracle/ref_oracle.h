@@ -104,7 +104,8 @@ int ref_emulate_op(int R, long count, int dtype, int op, const char *copyin, int
 int ref_emulate_op_s(int R, long count, int dtype, int op, const char *copyin, int in_place, int num_sockets,
                      void *const *sendbufs, void *const *recvbufs);
 
-/* nodes (<= 16) nodes of R ranks under the inter-node ports list `ports` (0-terminated, the
+#define REF_MAX_NODES 64 /* nodes of the inter-node emulation (the product: EMAC_MAX_NODES) */
+/* nodes (<= REF_MAX_NODES) nodes of R ranks under the inter-node ports list `ports` (0-terminated, the
    reference's EXT_MPI_NUM_PORTS: reduce-scatter ports, negative, then allgather ports;
    src/mpi/ext_mpi_native.c:879-1000 with src/core/allreduce_recursive.c:222-453, raw_code.c and
    rank_permutation.c): each node's copy-in, allreduce_core over the node partials task by task,
