@@ -363,6 +363,44 @@ def test_fold_handle_and_copy_reduce(code, nsrc, ndst):
             assert np.array_equal(d.cpu().numpy().view(np.uint8), want.view(np.uint8)), (how, nsrc, ndst)
 
 
+def test_copy_reduce_headline_instance():
+    """The device C-ABI (ext_mpi_amd_gpu_copy_reduce, the reference's ext_mpi_gpu_copy_reduce,
+    include/gpu/gpu_core.h:11-22, src/gpu/cuda_core.cu:88-106) and the persistent fold handle on
+    the bench headline's kernel instance: float, 8 leaves folded and fanned out to 8 destinations,
+    4 MiB per leaf -- the static schedule (U 4, staggered issue: fold_kernel<float, SUM, 8, 4,
+    linear, 8, 5>) -- then the handle's tuned schedule on later Starts, every result bitwise
+    equal to a sequential numpy left fold."""
+    count, nsrc = 1 << 20, 8
+    srcs_np = xorshift_inputs(nsrc, count, emac.FLOAT, seed_base=4242)
+    want = srcs_np[0].copy()
+    for x in srcs_np[1:]:
+        want = want + x
+    srcs = [_dev(x) for x in srcs_np]
+    dsts = [torch.full((count,), -1.0, device="cuda") for _ in range(nsrc)]
+    L = emac.lib()
+    L.ext_mpi_amd_gpu_copy_reduce.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                              ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.c_long, ctypes.c_void_p]
+    sp = (ctypes.c_void_p * nsrc)(*[t.data_ptr() for t in srcs])
+    dp = (ctypes.c_void_p * nsrc)(*[t.data_ptr() for t in dsts])
+    assert L.ext_mpi_amd_gpu_copy_reduce(emac.FLOAT, emac.SUM, nsrc, sp, nsrc, dp, count, None) == 0
+    for d in dsts:
+        assert np.array_equal(d.cpu().numpy().view(np.uint8), want.view(np.uint8))
+    h = emac.fold_init([t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts], count, emac.FLOAT)
+    seen = set()
+    for k in range(7):
+        for d in dsts:
+            d.fill_(-1.0)
+        emac.start(h)
+        emac.wait(h)
+        sc = emac.handle_schedule(h)
+        seen.add((sc["unroll"], sc["issue"], sc["tuned"]))
+        for d in dsts:
+            assert np.array_equal(d.cpu().numpy().view(np.uint8), want.view(np.uint8)), (k, sc)
+    emac.done(h)
+    assert (4, 5, 0) in seen  # the headline instance ran (static pick, before tuning kept one)
+    assert any(t == 1 for _, _, t in seen)  # and the tuned schedule after it
+
+
 def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=None, op=emac.SUM, repeats=1, nodes=1,
                       ports=None):
     """COMM form (one rank per communicator) on the in-process loopback transport: the legs run
