@@ -936,6 +936,7 @@ typedef struct {
   int refused;   /* [0]: the runtime refused to export one of this rank's buffers */
   int caller;    /* [0]: the exported send buffer is caller memory (not a library mirror) */
   int seg;       /* >= 0: an arena block, in the exporter's segment `seg` at `offset` (nothing exported) */
+  long lack;     /* [0]: arena bytes this rank could not place: every rank grows the arena first */
   long len;      /* bytes the peers access (the sample spans them) */
   unsigned char sample[EMAC_SAMPLE_BYTES]; /* the exporter's own read of the buffer (ipc_exchange) */
   unsigned char uuid[16];                  /* communicator set-up: the exporter's device */
@@ -1319,15 +1320,6 @@ static int arena_grow(emac_comm *cm, int rc, long need) {
   return EMAC_ERR_TRANSPORT;
 }
 
-/* Collective: the blocks this rank still lacks (`lack` bytes in total), carved after the arena
-   has grown if any rank needed it. */
-static int arena_get(emac_comm *cm, int rc, void **p, long bytes) {
-  const int miss = !rc && bytes > 0 && arena_alloc(cm, bytes, p) != 0;
-  rc = arena_grow(cm, rc, miss ? bytes : 0);
-  if (!rc && miss) rc = arena_alloc(cm, bytes, p);
-  return rc;
-}
-
 /* Byte offset of every piece of position `pos`'s owner chunk inside that rank's outbox: pieces
    back to back, each at the 16-byte phase its elements have in the message (so the fold's leaves,
    the outbox and the receive buffer agree on vector alignment). Returns the outbox bytes. */
@@ -1350,8 +1342,8 @@ enum { IPC_SEND = 0, IPC_OUTBOX = 1, IPC_NBUF = 2 };
    publishes its send buffer (an exported caller allocation with a sample of it, or an arena block)
    and its outbox (an arena block). On return peer[t][r] holds rank r's buffer t as reachable here,
    all[] the exports, and *miss a bit per rank whose send buffer this rank could not map or validate. */
-static int ipc_exchange(emac_handle *h, emac_comm *cm, int rc, ipc_export *all, void *(*peer)[EMAC_MAX_RANKS],
-                        unsigned *miss) {
+static int ipc_exchange(emac_handle *h, emac_comm *cm, int rc, long lack, ipc_export *all,
+                        void *(*peer)[EMAC_MAX_RANKS], unsigned *miss, int *grow) {
   ipc_export mine[IPC_NBUF];
   const int R = cm->size;
   void *own[IPC_NBUF] = {h->dsend[0], h->outbox};
@@ -1359,7 +1351,9 @@ static int ipc_exchange(emac_handle *h, emac_comm *cm, int rc, ipc_export *all, 
   int r, t, k;
   memset(mine, 0, sizeof(mine));
   *miss = 0;
-  for (t = 0; t < IPC_NBUF && !rc; t++) {
+  *grow = 0;
+  mine[0].lack = lack;
+  for (t = 0; t < IPC_NBUF && !rc && !lack; t++) {
     mine[t].len = len[t];
     if (arena_owns(cm, own[t], &k)) {
       mine[t].seg = k;
@@ -1384,9 +1378,11 @@ static int ipc_exchange(emac_handle *h, emac_comm *cm, int rc, ipc_export *all, 
   mine[0].status = rc == 0;
   mine[0].caller = mine[0].seg < 0 && !ipc_pool_owns(cm, h->dsend[0]);
   if (cm->ag(cm->ag_ctx, mine, all, (long)sizeof(mine))) return EMAC_ERR_TRANSPORT;
-  for (r = 0; r < R; r++)
+  for (r = 0; r < R; r++) {
     if (!all[IPC_NBUF * r].status && !rc) rc = EMAC_ERR_TRANSPORT;
-  if (rc) return rc;
+    if (all[IPC_NBUF * r].lack > 0) *grow = 1;
+  }
+  if (rc || *grow) return rc; /* (every rank reaches the same verdict) */
   {
     const void *pk[EMAC_MAX_RANKS];
     long pl[EMAC_MAX_RANKS];
@@ -1479,22 +1475,31 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
       h->outbox_bytes = (size_t)outbox_layout(&h->plan, h->me_pos, NULL);
       if (h->outbox_bytes < 16) h->outbox_bytes = 16;
     }
-    /* the outbox, and a send mirror map_buffers left to the arena (host or non-exportable memory) */
-    rc = arena_get(cm, rc, &h->outbox, (long)h->outbox_bytes);
-    {
-      void *p = NULL;
-      const int want = !rc && !h->dsend[0];
-      rc = arena_get(cm, rc, &p, want ? (long)h->bytes : 0);
-      if (!rc && want) {
-        h->dsend[0] = p;
-        h->send_arena = 1;
-        if (h->recv_mirror[0] && !h->drecv[0]) h->drecv[0] = p; /* in place */
-      }
-    }
     for (attempt = 0;; attempt++) {
       unsigned miss, allmiss[EMAC_MAX_RANKS], stale = 0;
-      int again = 0;
-      rc = ipc_exchange(h, cm, rc, all, peer, &miss);
+      int again = 0, grow = 0;
+      /* the outbox, and a send mirror left to the arena (host or non-exportable memory, or a send
+         buffer re-placed below); a rank that lacks room says so in the exchange, every rank then
+         grows the arena (one collective round) and exchanges again */
+      long lack = 0;
+      if (!rc && !h->outbox && arena_alloc(cm, (long)h->outbox_bytes, &h->outbox))
+        lack += (long)(h->outbox_bytes + EMAC_ARENA_ALIGN - 1) / EMAC_ARENA_ALIGN * EMAC_ARENA_ALIGN;
+      if (!rc && !h->dsend[0]) {
+        void *p = NULL;
+        if (arena_alloc(cm, (long)h->bytes, &p)) {
+          lack += (long)(h->bytes + EMAC_ARENA_ALIGN - 1) / EMAC_ARENA_ALIGN * EMAC_ARENA_ALIGN;
+        } else {
+          h->dsend[0] = p;
+          h->send_arena = 1;
+          if (h->recv_mirror[0] && !h->drecv[0]) h->drecv[0] = p; /* in place */
+        }
+      }
+      rc = ipc_exchange(h, cm, rc, lack, all, peer, &miss, &grow);
+      if (!rc && grow) {
+        if (attempt == EMAC_IPC_ATTEMPTS - 1) return EMAC_ERR_MALLOC; /* the same on every rank */
+        rc = arena_grow(cm, 0, lack);
+        continue;
+      }
       if (!rc && force && attempt == 0 && !h->send_arena) miss |= 1u << cm->rank; /* re-place mine */
       if (rc) miss = ~0u; /* a failed rank: the verdict below stops every rank */
       if (cm->ag(cm->ag_ctx, &miss, allmiss, (long)sizeof(miss))) return EMAC_ERR_TRANSPORT;
@@ -1513,21 +1518,16 @@ static int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf
       }
       for (r = 0; r < h->nmapped; r++) ipc_unmap(h->mapped[r]);
       h->nmapped = 0;
-      {
-        /* this rank's send buffer into an arena mirror, staged in on the handle's stream (in place:
-           the one buffer, staged in and out) */
-        void *p = NULL;
-        rc = arena_get(cm, rc, &p, stale ? (long)h->bytes : 0);
-        if (!rc && stale) {
-          if (h->dsend[0] == h->drecv[0]) {
-            h->recv_mirror[0] = 1;
-            h->drecv[0] = p;
-          } else {
-            h->send_mirror[0] = 1;
-          }
-          h->dsend[0] = p;
-          h->send_arena = 1;
+      if (stale) {
+        /* this rank's send buffer into an arena mirror (placed at the top of the next round),
+           staged in on the handle's stream; in place, the one buffer, staged in and out */
+        if (h->dsend[0] == h->drecv[0]) {
+          h->recv_mirror[0] = 1;
+          h->drecv[0] = NULL;
+        } else {
+          h->send_mirror[0] = 1;
         }
+        h->dsend[0] = NULL;
       }
     }
   }

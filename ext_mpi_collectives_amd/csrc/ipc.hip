@@ -148,22 +148,29 @@ int emac_gpu_peek(const void *const *ptrs, unsigned char *vals, int n, void *str
 }
 
 int emac_gpu_sample(const void *const *ptrs, const long *lens, int n, unsigned char *out, void *stream) {
+  /* the samples land in pinned, device-mapped host memory kept per device: a set-up makes several
+     of these calls, and a hipMalloc / hipFree pair per call would synchronise the device each time */
+  static unsigned char *pinned[64];
   SampleSet a;
-  unsigned char *d = nullptr;
+  int dev = 0;
   if (n < 0 || n > EMAC_PROBE_MAX) return EMAC_ERR_ARG;
   if (!n) return 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return EMAC_ERR_DEVICE;
+  if (!pinned[dev] && hipHostMalloc((void **)&pinned[dev], (size_t)EMAC_SAMPLE_BYTES * EMAC_PROBE_MAX,
+                                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    pinned[dev] = nullptr;
+    return EMAC_ERR_MALLOC;
+  }
   memset(&a, 0, sizeof(a));
   for (int i = 0; i < n; ++i) {
     a.p[i] = static_cast<const unsigned char *>(ptrs[i]);
     a.len[i] = lens[i];
   }
-  if (hipMalloc(&d, (size_t)EMAC_SAMPLE_BYTES * EMAC_PROBE_MAX) != hipSuccess) return EMAC_ERR_MALLOC;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(sample_kernel, dim3((unsigned)n), dim3(EMAC_SAMPLE_BYTES), 0, s, a, d);
+  hipLaunchKernelGGL(sample_kernel, dim3((unsigned)n), dim3(EMAC_SAMPLE_BYTES), 0, s, a, pinned[dev]);
   int rc = ok(hipGetLastError());
-  if (!rc) rc = ok(hipMemcpyAsync(out, d, (size_t)n * EMAC_SAMPLE_BYTES, hipMemcpyDeviceToHost, s));
   if (!rc) rc = ok(hipStreamSynchronize(s));
-  (void)hipFree(d);
+  if (!rc) memcpy(out, pinned[dev], (size_t)n * EMAC_SAMPLE_BYTES);
   return rc;
 }
 

@@ -64,7 +64,7 @@ def _digest(outs, codes, keep=12):
     return "\n".join(head) + "\n" + "\n".join(parts)
 
 
-def _run_world(world, extra_env=None, budget=150):
+def _run_world(world, extra_env=None, budget=None):
     port = _port()
     procs, logs = [], []
     # each rank writes to its own file: pipes read one after the other would fill up and block a
@@ -78,7 +78,8 @@ def _run_world(world, extra_env=None, budget=150):
         logs.append(tempfile.TemporaryFile(mode="w+"))
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "ipc_worker.py")], env=env,
                                       stdout=logs[-1], stderr=subprocess.STDOUT, text=True))
-    deadline = time.monotonic() + budget
+    # 8 processes time-share the one GPU: every set-up round trip and barrier is slower there
+    deadline = time.monotonic() + (budget or (300 if world >= 8 else 150))
     codes = []
     for p in procs:
         try:
