@@ -390,6 +390,7 @@ def test_copy_reduce_headline_instance():
     for k in range(7):
         for d in dsts:
             d.fill_(-1.0)
+        torch.cuda.synchronize()  # the fill runs on torch's stream, the fold on the handle's
         emac.start(h)
         emac.wait(h)
         sc = emac.handle_schedule(h)

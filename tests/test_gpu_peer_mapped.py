@@ -113,5 +113,6 @@ def test_ipc_forced_mirror(world):
     """EXT_MPI_AMD_IPC_FORCE_MIRROR=1: every rank's exported send buffer is re-placed in
     the first set-up round of every handle (an arena mirror), so the mirror path -- staged send buffers, a second
     exchange, re-validated mappings -- runs on every case, bitwise against the oracle."""
-    report = _run_world(world, {"EXT_MPI_AMD_IPC_FORCE_MIRROR": "1", "IPC_FUZZ": "4"})
+    report = _run_world(world, {"EXT_MPI_AMD_IPC_FORCE_MIRROR": "1", "IPC_FUZZ": "4",
+                                "IPC_SECTIONS": "realloc,newdata,concurrent,recycle"})
     assert "re-placing send" in report  # the forced round was taken (EXT_MPI_AMD_DEBUG_IPC)
