@@ -84,4 +84,28 @@ int ceiling_copy(const void *src, void *dst, long bytes, int iters, int variant,
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+/* A stream gate for bench.py's timed regions: the stream waits (hipStreamWaitValue32 on a pinned
+   host word) until the host opens the gate, so the work enqueued behind it -- the timed region's
+   start event and its first launches -- begins only once the host is ahead of the GPU; the timing
+   events then hold the kernels and their gaps, not the host's submission latency. */
+void *ceiling_gate_arm(void *stream) {
+  unsigned *flag = nullptr;
+  if (hipHostMalloc((void **)&flag, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return nullptr;
+  *flag = 0;
+  if (hipStreamWaitValue32(static_cast<hipStream_t>(stream), flag, 1, hipStreamWaitValueGte, 0xFFFFFFFFu) != hipSuccess) {
+    (void)hipHostFree(flag);
+    return nullptr;
+  }
+  return flag;
+}
+
+void ceiling_gate_open(void *gate) {
+  if (!gate) return;
+  __atomic_store_n(static_cast<unsigned *>(gate), 1u, __ATOMIC_SEQ_CST);
+}
+
+void ceiling_gate_free(void *gate) {
+  if (gate) (void)hipHostFree(gate);
+}
+
 }  // extern "C"
