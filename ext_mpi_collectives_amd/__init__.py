@@ -83,6 +83,8 @@ def lib():
         P = ctypes.POINTER
         L.ext_mpi_amd_node_allreduce_init.argtypes = [c_int, P(c_void_p), P(c_void_p), c_long, c_int, c_int,
                                                       ctypes.c_char_p, P(c_int)]
+        L.ext_mpi_amd_node_comm_allreduce_init.argtypes = [c_int, P(c_void_p), P(c_void_p), c_long, c_int, c_int,
+                                                           c_int, ctypes.c_char_p, P(c_int)]
         L.ext_mpi_amd_fold_init.argtypes = [c_int, P(c_void_p), c_int, P(c_void_p), c_long, c_int, c_int, P(c_int)]
         L.ext_mpi_amd_get_unique_id.argtypes = [c_void_p]
         L.ext_mpi_amd_comm_init.argtypes = [c_int, c_int, c_void_p, c_int, P(c_int)]
@@ -151,6 +153,20 @@ def node_allreduce_init(sendptrs, recvptrs, count, dtype, copyin=None, op=SUM):
     h = ctypes.c_int(-1)
     _check("ext_mpi_amd_node_allreduce_init",
            lib().ext_mpi_amd_node_allreduce_init(n, s, r, count, dtype, op, _enc(copyin), ctypes.byref(h)))
+    return h.value
+
+
+def node_comm_allreduce_init(sendptrs, recvptrs, count, dtype, comm, copyin=None, op=SUM):
+    """Persistent Allreduce over several nodes with every rank of this node in this process
+    (len(sendptrs) node ranks, device buffers on this process's GPU) and `comm` having one member
+    per node (RCCL or loopback): the NODE form's copy-in, the inter-node legs of every node rank,
+    the node's copy-out. Bits equal allreduce_init over size * len(sendptrs) ranks."""
+    n = len(sendptrs)
+    s = (ctypes.c_void_p * n)(*sendptrs)
+    r = (ctypes.c_void_p * n)(*recvptrs)
+    h = ctypes.c_int(-1)
+    _check("ext_mpi_amd_node_comm_allreduce_init",
+           lib().ext_mpi_amd_node_comm_allreduce_init(n, s, r, count, dtype, op, comm, _enc(copyin), ctypes.byref(h)))
     return h.value
 
 

@@ -225,6 +225,11 @@ typedef struct {
   unsigned char graph_failed[EXT_MPI_AMD_LEG_ALL + 1];
   emac_pipe *pipe; /* pipelined host staging (NODE form), or NULL */
   emac_tune tune;  /* launch-schedule tuning of the fold */
+  /* NODE form over several nodes (ext_mpi_amd_node_comm_allreduce_init): every rank of this node
+     in this process, the communicator's members being the nodes */
+  int hier;
+  long stage_stride;    /* staging bytes of each node rank's node legs */
+  emac_launch fanout;   /* the copy-out: every owner chunk into the node's other receive buffers */
 } emac_handle;
 
 static emac_handle *handles[MAX_HANDLES];
@@ -281,6 +286,8 @@ static void release(emac_handle *h) {
     emac_gpu_free(h->xfold[r].d_buckets);
     emac_gpu_free(h->xfold[r].d_edges);
   }
+  emac_gpu_free(h->fanout.d_buckets);
+  emac_gpu_free(h->fanout.d_edges);
   emac_gpu_free(h->staging);
   for (r = 0; r < h->nbuf; r++) {
     const int same = h->dsend[r] == h->drecv[r];
@@ -1750,8 +1757,200 @@ static int node_radix(const emac_node_sched *ns, int st) {
   return st < ns->nsteps ? ns->radix[st] : ns->red_radix[st - ns->nsteps];
 }
 
-static char *leg_base(const emac_handle *h, int buf) {
-  return buf == EMAC_BUF_SEND ? (char *)h->dsend[0] : buf == EMAC_BUF_RECV ? (char *)h->drecv[0] : (char *)h->staging;
+/* base of buffer `buf` of node rank `l` in this process (0 but in the NODE form over several nodes) */
+static char *leg_base_of(const emac_handle *h, int buf, int l) {
+  return buf == EMAC_BUF_SEND ? (char *)h->dsend[l]
+       : buf == EMAC_BUF_RECV ? (char *)h->drecv[l]
+                              : (char *)h->staging + (long)l * h->stage_stride;
+}
+
+static char *leg_base(const emac_handle *h, int buf) { return leg_base_of(h, buf, 0); }
+
+/* ------------------------- NODE form over several nodes ------------------------- */
+
+/* Every rank of this node in this process (the NODE form: all their buffers on this GPU), the
+   nodes joined by `comm`, whose members are the nodes (RCCL, or loopback for testing), under the
+   communicator's inter-node schedule (ext_mpi_amd_comm_set_node_ports with nodes == its size;
+   otherwise emac_node_sched_build's default). A Start runs
+    1. the node's copy-in: every owner chunk folded over the node's send buffers, in the plan's
+       leaf order, into its owner's receive buffer -- the COMM form's reduce-scatter leg and fold
+       without moving a byte, the leaves read where they lie (one launch, fold_launch);
+    2. the node legs of every node rank me (emac_comm_program_nodes of global rank
+       node * R + me; its column peers are rank me of the other nodes, i.e. the other members),
+       one RCCL group per leg for all node ranks, ordered by node rank within each peer so that
+       the k-th send of a pair matches its k-th receive, and each exchange step's fold for all
+       node ranks in one launch;
+    3. the copy-out: every owner chunk stored into the node's other receive buffers (the node
+       allgather, emac_gpu_copy_fan).
+   The bits are the COMM form's over nodes * R ranks, one per process -- the reference's
+   multi-node composition (ext_mpi_native.c:879-1000: reduce_copyin over the node, the
+   EXT_MPI_NUM_PORTS schedule between nodes, reduce_copyout). */
+int ext_mpi_amd_node_comm_allreduce_init(int nranks, const void *const *sendbufs, void *const *recvbufs, long count,
+                                         int dtype, int op, int comm, const char *copyin, int *handle) {
+  emac_handle *h;
+  emac_comm *cm;
+  emac_copyin cfg;
+  emac_bucket *b = NULL, *xb = NULL;
+  emac_p2p *prog_ops[EMAC_MAX_RANKS] = {0};
+  emac_fold *prog_folds[EMAC_MAX_RANKS] = {0};
+  int prog_nops[EMAC_MAX_RANKS] = {0}, prog_nf[EMAC_MAX_RANKS] = {0};
+  int nxb[2 * EMAC_MAX_NODE_STEPS] = {0};
+  const int R = nranks;
+  int rc, r, me, i, t, pc, c, nb = 0, nsteps, nf_all = 0, no_all = 0;
+  long stage_max = 0;
+  if (!handle || !sendbufs || !recvbufs || R < 1 || R > EMAC_MAX_RANKS || count < 0 || comm < 0 ||
+      comm >= MAX_COMMS || !comms[comm].used)
+    return EMAC_ERR_ARG;
+  *handle = -1;
+  cm = &comms[comm];
+  if (cm->ipc) return EMAC_ERR_UNSUPPORTED;                      /* RCCL or loopback members */
+  if (cm->nodes > 1 && cm->nodes != cm->size) return EMAC_ERR_ARG; /* the members are the nodes */
+  if ((rc = parse_cfg(copyin, R, &cfg))) return rc;
+  if (emac_gpu_set_device(cm->device)) return EMAC_ERR_DEVICE;
+  h = (emac_handle *)calloc(1, sizeof(emac_handle));
+  if (!h) return EMAC_ERR_MALLOC;
+  h->kind = KIND_COMM;
+  h->hier = 1;
+  h->comm = comm;
+  h->device = cm->device;
+  if ((rc = emac_plan_build(&h->plan, R, count, dtype, op, &cfg))) goto fail;
+  h->me = cm->rank; /* this node */
+  h->bytes = (size_t)count * (size_t)h->plan.tsize;
+  h->nodes = cm->size;
+  if (h->nodes > 1 && cm->nodes == cm->size)
+    h->ns = cm->ns; /* ext_mpi_amd_comm_set_node_ports */
+  else if (h->nodes > 1 && (rc = emac_node_sched_build(&h->ns, h->nodes, NULL)))
+    goto fail;
+  h->nbuf = R;
+  h->nsrc = R;
+  h->fan = 0;
+  for (r = 0; r < R; r++)
+    if ((rc = map_buffers(h, r, sendbufs[r], recvbufs[r]))) goto fail;
+  /* 1. the copy-in: owner chunk (piece pc, position c) into its owner's receive buffer */
+  b = (emac_bucket *)calloc((size_t)h->plan.npieces * R + 1, sizeof(emac_bucket));
+  if (!b) {
+    rc = EMAC_ERR_MALLOC;
+    goto fail;
+  }
+  for (pc = 0; pc < h->plan.npieces; pc++)
+    for (c = 0; c < R; c++) {
+      const long off = h->plan.chunk_off[(size_t)pc * R + c], len = h->plan.chunk_len[(size_t)pc * R + c];
+      emac_bucket *bk = &b[nb];
+      if (len <= 0) continue;
+      memset(bk, 0, sizeof(*bk));
+      for (t = 0; t < R; t++) bk->src[t] = h->dsend[h->plan.leaf_rank[c][t]];
+      bk->dst[0] = h->drecv[h->plan.pos_rank[c]];
+      bk->ndst = 1;
+      place_bucket(bk, R, off, len, h->plan.tsize);
+      nb++;
+    }
+  if ((rc = upload_buckets(h, b, nb))) goto fail;
+  /* 3. the copy-out: owner chunk into the R - 1 other receive buffers */
+  if (R > 1) {
+    emac_edge *edges = NULL;
+    int nfb = 0;
+    for (pc = 0; pc < h->plan.npieces; pc++)
+      for (c = 0; c < R; c++) {
+        const long off = h->plan.chunk_off[(size_t)pc * R + c], len = h->plan.chunk_len[(size_t)pc * R + c];
+        const int owner = h->plan.pos_rank[c];
+        emac_bucket *bk = &b[nfb];
+        if (len <= 0) continue;
+        memset(bk, 0, sizeof(*bk));
+        bk->src[0] = h->drecv[owner];
+        for (r = 0; r < R; r++)
+          if (r != owner) bk->dst[bk->ndst++] = h->drecv[r];
+        place_bucket(bk, 1, off, len, h->plan.tsize);
+        nfb++;
+      }
+    emac_launch *F = &h->fanout;
+    if ((rc = emac_layout(b, nfb, EMAC_SUM, 1, 0, 0, &edges, &F->nedges, &F->ntiles, &F->tiles_per_bucket,
+                          &F->all_full, &F->unroll)))
+      goto fail;
+    F->nb = nfb;
+    if (nfb && (rc = emac_gpu_malloc((void **)&F->d_buckets, sizeof(emac_bucket) * (size_t)nfb)) == 0)
+      rc = emac_gpu_memcpy(F->d_buckets, b, sizeof(emac_bucket) * (size_t)nfb);
+    if (!rc && F->nedges && (rc = emac_gpu_malloc((void **)&F->d_edges, sizeof(emac_edge) * (size_t)F->nedges)) == 0)
+      rc = emac_gpu_memcpy(F->d_edges, edges, sizeof(emac_edge) * (size_t)F->nedges);
+    free(edges);
+    if (rc) goto fail;
+  }
+  /* 2. the node legs of every node rank: their programs, the peers turned into members */
+  nsteps = h->nodes > 1 ? h->ns.nsteps + h->ns.nred : 0;
+  for (me = 0; me < R && h->nodes > 1; me++) {
+    long st = 0;
+    if ((rc = emac_comm_program_nodes(&h->plan, &h->ns, h->me, me, (long)((unsigned long)h->dsend[me] & 15ul),
+                                      &prog_ops[me], &prog_nops[me], &prog_folds[me], &prog_nf[me], &st)))
+      goto fail;
+    if (st > stage_max) stage_max = st;
+    no_all += prog_nops[me];
+    nf_all += prog_nf[me];
+  }
+  h->stage_stride = (stage_max + 255) / 256 * 256;
+  if ((rc = emac_gpu_malloc(&h->staging, (size_t)(h->stage_stride > 0 ? h->stage_stride * R : 16)))) goto fail;
+  h->ops = (emac_p2p *)malloc(sizeof(emac_p2p) * (size_t)(no_all + 1));
+  xb = (emac_bucket *)calloc(2 * EMAC_MAX_NODE_STEPS * ((size_t)nf_all + 1), sizeof(emac_bucket));
+  if (!h->ops || !xb) {
+    rc = EMAC_ERR_MALLOC;
+    goto fail;
+  }
+  /* legs in program order, node ranks in ascending order inside each (the pairs' matching order) */
+  for (me = 0; me < R; me++)
+    for (i = 0; i < prog_nops[me]; i++) {
+      emac_p2p o = prog_ops[me][i];
+      const int base = o.leg & ((1 << EMAC_LEG_STEP_SHIFT) - 1);
+      if (base != EMAC_LEG_NODES_RS && base != EMAC_LEG_NODES_AG) continue; /* the node's own legs: steps 1, 3 */
+      if (o.peer % R != me) {
+        rc = EMAC_ERR_UNSUPPORTED; /* not a program of this shape */
+        goto fail;
+      }
+      o.peer /= R;
+      o.local = me;
+      h->ops[h->nops++] = o;
+    }
+  for (me = 0; me < R; me++)
+    for (i = 0; i < prog_nf[me]; i++) {
+      const emac_fold *f = &prog_folds[me][i];
+      int step;
+      emac_bucket *bk;
+      if ((f->leg & ((1 << EMAC_LEG_STEP_SHIFT) - 1)) != EMAC_LEG_NODES_FOLD) continue; /* step 1 folds the node */
+      step = f->leg >> EMAC_LEG_STEP_SHIFT;
+      if (step < 0 || step >= nsteps) {
+        rc = EMAC_ERR_UNSUPPORTED; /* not a program of this shape */
+        goto fail;
+      }
+      bk = &xb[(size_t)step * ((size_t)nf_all + 1) + (size_t)nxb[step]++];
+      for (t = 0; t < f->nleaf; t++) bk->src[t] = leg_base_of(h, f->buf[t], me) + f->loff[t] - f->offset;
+      bk->dst[0] = h->drecv[me];
+      bk->ndst = 1;
+      place_bucket(bk, f->nleaf, f->offset / h->plan.tsize, f->count, h->plan.tsize);
+    }
+  for (i = 0; i < nsteps; i++)
+    if (nxb[i] &&
+        (rc = upload_launch_as(h, &h->xfold[i], xb + (size_t)i * ((size_t)nf_all + 1), nxb[i], node_radix(&h->ns, i), 0)))
+      goto fail;
+  if ((rc = emac_gpu_stream_create(&h->stream))) goto fail;
+  if (cm->loop_group >= 0) {
+    loop_group *g = &loops[cm->loop_group];
+    if (g->nh[h->me] < 0 || g->nh[h->me] >= MAX_LOOP_HANDLES) {
+      rc = EMAC_ERR_MALLOC;
+      goto fail;
+    }
+    h->loop_index = g->nh[h->me];
+  }
+  if ((rc = finish_init(h, handle))) goto fail;
+  if (cm->loop_group >= 0) loops[cm->loop_group].handle[h->me][loops[cm->loop_group].nh[h->me]++] = *handle;
+  rc = 0;
+  goto out;
+fail:
+  release(h);
+out:
+  for (me = 0; me < R; me++) {
+    free(prog_ops[me]);
+    free(prog_folds[me]);
+  }
+  free(b);
+  free(xb);
+  return rc;
 }
 
 static emac_handle *get(int handle);
@@ -1760,22 +1959,23 @@ static emac_handle *get(int handle);
    k-th send of q to me in this leg matches my k-th receive from q). */
 static int run_leg_loopback(emac_handle *h, int leg) {
   loop_group *g = &loops[comms[h->comm].loop_group];
-  int seen[EMAC_MAX_RANKS] = {0}, i, j, rc;
+  int seen[EMAC_MAX_RANKS][EMAC_MAX_RANKS], i, j, rc;
+  memset(seen, 0, sizeof(seen));
   for (i = 0; i < h->nops; i++) {
     const emac_p2p *o = &h->ops[i];
     emac_handle *hq;
     int q = o->peer, k, found = 0;
     if (o->leg != leg || o->is_send) continue;
-    k = seen[q]++;
+    k = seen[q][o->local]++; /* per (peer, node rank): the NODE form over nodes orders them so */
     if (h->loop_index >= g->nh[q]) return EMAC_ERR_TRANSPORT; /* peer has no matching handle */
     hq = get(g->handle[q][h->loop_index]);
     if (!hq) return EMAC_ERR_TRANSPORT;
     for (j = 0; j < hq->nops; j++) {
       const emac_p2p *so = &hq->ops[j];
-      if (so->leg == leg && so->is_send && so->peer == h->me && k-- == 0) {
+      if (so->leg == leg && so->is_send && so->peer == h->me && so->local == o->local && k-- == 0) {
         if (so->bytes != o->bytes) return EMAC_ERR_TRANSPORT;
-        if ((rc = emac_gpu_memcpy_async(leg_base(h, o->buf) + o->offset, leg_base(hq, so->buf) + so->offset,
-                                        (size_t)o->bytes, h->stream)))
+        if ((rc = emac_gpu_memcpy_async(leg_base_of(h, o->buf, o->local) + o->offset,
+                                        leg_base_of(hq, so->buf, so->local) + so->offset, (size_t)o->bytes, h->stream)))
           return rc;
         found = 1;
         break;
@@ -1797,7 +1997,7 @@ static int run_leg(emac_handle *h, int leg) {
     const emac_p2p *o = &h->ops[i];
     char *base;
     if (o->leg != leg) continue;
-    base = leg_base(h, o->buf);
+    base = leg_base_of(h, o->buf, o->local);
     if (o->is_send)
       bad = ncclSend(base + o->offset, (size_t)o->bytes, ncclInt8, o->peer, cm->nccl, s) != ncclSuccess;
     else
@@ -1910,7 +2110,7 @@ static int pipe_start(emac_handle *h) {
 static int enqueue_legs(emac_handle *h, int legs) {
   int rc, multi;
   const int core = EXT_MPI_AMD_LEG_REDUCE_SCATTER | EXT_MPI_AMD_LEG_FOLD | EXT_MPI_AMD_LEG_ALLGATHER;
-  multi = h->kind == KIND_COMM && h->plan.nranks > 1;
+  multi = h->kind == KIND_COMM && h->plan.nranks > 1 && !h->hier; /* the node's own p2p legs */
   if ((legs & EXT_MPI_AMD_LEG_STAGE_IN) && (rc = stage_in(h))) return rc;
   if (h->kind == KIND_IPC && h->fused && (legs & core) == core) {
     emac_comm *cm = &comms[h->comm];
@@ -1968,6 +2168,11 @@ static int enqueue_legs(emac_handle *h, int legs) {
     }
   }
   if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && multi && (rc = run_leg(h, EMAC_LEG_AG))) return rc;
+  if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && h->hier && h->fanout.nb &&
+      (rc = emac_gpu_copy_fan(h->plan.tsize, h->plan.nranks - 1, h->fanout.unroll, h->fanout.d_buckets, h->fanout.nb,
+                              h->fanout.ntiles, h->fanout.tiles_per_bucket, h->fanout.all_full, h->fanout.d_edges,
+                              h->fanout.nedges, h->stream)))
+    return rc;
   if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && h->kind == KIND_IPC && h->plan.nranks > 1) {
     static const emac_codes copy = {{1}, {1}, 1, 1}; /* one leaf: a copy */
     if ((rc = ipc_barrier(h, 1))) return rc;

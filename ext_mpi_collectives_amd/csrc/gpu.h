@@ -151,6 +151,11 @@ int emac_gpu_fold_remote(int dtype, int op, int nsrc, int unroll, const emac_cod
                          int nb, long ntiles, long tiles_per_bucket, int all_full, const emac_edge *d_edges, int nedges,
                          const unsigned *go, void *stream);
 
+/* Copy fan-out (fold_copy.hip): every bucket's one leaf stored into its `width` destinations
+   (1 .. EMAC_MAX_RANKS - 1), bits moved unchanged; tsize = element bytes (4 or 8). */
+int emac_gpu_copy_fan(int tsize, int width, int unroll, const emac_bucket *d_buckets, int nb, long ntiles,
+                      long tiles_per_bucket, int all_full, const emac_edge *d_edges, int nedges, void *stream);
+
 /* Fold-tree kind of a plan's codes (fold_kernel.hpp template parameter CH): 0 linear (one
    radix), a packed compile-time radix chain (5 bits per level, level 0 lowest) when the kernels
    instantiate it -- EMAC_CHAINS: -2 -2, -2 -2 -2, -4 -2, -2 -4, -2 -2 -2 -2, -4 -4 -- else 1

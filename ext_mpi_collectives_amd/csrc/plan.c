@@ -683,11 +683,11 @@ static int program_nodes(const emac_plan *p, const emac_node_sched *ns, int node
         qoff = p->chunk_off[(size_t)pc * R + p->rank_pos[q]] * ts;
         qlen = p->chunk_len[(size_t)pc * R + p->rank_pos[q]] * ts;
         if (leg == 0) {
-          if (qlen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_RS, g0 + q, 1, EMAC_BUF_SEND, qoff, qlen};
-          if (mylen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_RS, g0 + q, 0, EMAC_BUF_STAGE, SLOT(pc, q), mylen};
+          if (qlen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_RS, g0 + q, 1, EMAC_BUF_SEND, qoff, qlen, 0};
+          if (mylen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_RS, g0 + q, 0, EMAC_BUF_STAGE, SLOT(pc, q), mylen, 0};
         } else {
-          if (mylen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_AG, g0 + q, 1, EMAC_BUF_RECV, myoff, mylen};
-          if (qlen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_AG, g0 + q, 0, EMAC_BUF_RECV, qoff, qlen};
+          if (mylen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_AG, g0 + q, 1, EMAC_BUF_RECV, myoff, mylen, 0};
+          if (qlen > 0) ops[nops++] = (emac_p2p){EMAC_LEG_AG, g0 + q, 0, EMAC_BUF_RECV, qoff, qlen, 0};
         }
       }
     }
@@ -742,14 +742,14 @@ static int program_nodes(const emac_plan *p, const emac_node_sched *ns, int node
       hoff[1] = lo + hlen[0];
       hlen[1] = n - hlen[0];
       if (hlen[1 - bit] > 0)
-        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, partner, 1, EMAC_BUF_RECV, hoff[1 - bit] * ts, hlen[1 - bit] * ts};
+        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, partner, 1, EMAC_BUF_RECV, hoff[1 - bit] * ts, hlen[1 - bit] * ts, 0};
       if (hlen[bit] > 0) {
         emac_fold *f = &folds[nf++];
         /* raw_code.c's accumulator: the partner's partial first at the first and the last step,
            the own one in between */
         const int own = st > 0 && st < K - 1 ? 0 : 1;
         ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, partner, 0, EMAC_BUF_STAGE, xslot[(size_t)pc * nx + st],
-                                 hlen[bit] * ts};
+                                 hlen[bit] * ts, 0};
         f->piece = pc;
         f->offset = hoff[bit] * ts;
         f->count = hlen[bit];
@@ -759,10 +759,10 @@ static int program_nodes(const emac_plan *p, const emac_node_sched *ns, int node
         f->loff[own] = hoff[bit] * ts;
         f->buf[1 - own] = EMAC_BUF_STAGE;
         f->loff[1 - own] = xslot[(size_t)pc * nx + st];
-        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | la, partner, 1, EMAC_BUF_RECV, hoff[bit] * ts, hlen[bit] * ts};
+        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | la, partner, 1, EMAC_BUF_RECV, hoff[bit] * ts, hlen[bit] * ts, 0};
       }
       if (hlen[1 - bit] > 0)
-        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | la, partner, 0, EMAC_BUF_RECV, hoff[1 - bit] * ts, hlen[1 - bit] * ts};
+        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | la, partner, 0, EMAC_BUF_RECV, hoff[1 - bit] * ts, hlen[1 - bit] * ts, 0};
     }
   /* One reduce-scatter step over every node (N(-(N-1) ...)): every element's value is ONE fold
      of the N node partials, in the order its line's task gives (r_{N-2}, own, r_0, ..., r_{N-3}
@@ -779,8 +779,8 @@ static int program_nodes(const emac_plan *p, const emac_node_sched *ns, int node
       const long uo = off + len * u / nodes, ul = off + len * (u + 1) / nodes - uo;
       const int gp = ns->task_node[u] * R + me;
       if (u == task) continue;
-      if (ul > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS, gp, 1, EMAC_BUF_RECV, uo * ts, ul * ts};
-      if (ml > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS, gp, 0, EMAC_BUF_STAGE, xslot[(size_t)pc * nx + x], ml * ts};
+      if (ul > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS, gp, 1, EMAC_BUF_RECV, uo * ts, ul * ts, 0};
+      if (ml > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS, gp, 0, EMAC_BUF_STAGE, xslot[(size_t)pc * nx + x], ml * ts, 0};
       x++;
     }
     for (t = 0; t < nodes && ml > 0; t++) { /* my share, line by line */
@@ -809,8 +809,8 @@ static int program_nodes(const emac_plan *p, const emac_node_sched *ns, int node
       const long uo = off + len * u / nodes, ul = off + len * (u + 1) / nodes - uo;
       const int gp = ns->task_node[u] * R + me;
       if (u == task) continue;
-      if (ml > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG, gp, 1, EMAC_BUF_RECV, mo * ts, ml * ts};
-      if (ul > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG, gp, 0, EMAC_BUF_RECV, uo * ts, ul * ts};
+      if (ml > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG, gp, 1, EMAC_BUF_RECV, mo * ts, ml * ts, 0};
+      if (ul > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG, gp, 0, EMAC_BUF_RECV, uo * ts, ul * ts, 0};
     }
   }
   /* otherwise the lines are followed as the reference lays them out */
@@ -831,9 +831,9 @@ static int program_nodes(const emac_plan *p, const emac_node_sched *ns, int node
         long po, pl;
         task_lines(ns, count, peer_task[i] / Gn * Gn, peer_task[i] / Gn * Gn + Gn, &a, &b);
         clip(a, b, off, off + len, &po, &pl);
-        if (pl > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, gp, 1, EMAC_BUF_RECV, po * ts, pl * ts};
+        if (pl > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, gp, 1, EMAC_BUF_RECV, po * ts, pl * ts, 0};
         if (kl > 0)
-          ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, gp, 0, EMAC_BUF_STAGE, xslot[(size_t)pc * nx + xs + i], kl * ts};
+          ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, gp, 0, EMAC_BUF_STAGE, xslot[(size_t)pc * nx + xs + i], kl * ts, 0};
       }
       if (kl > 0) {
         emac_fold *f = &folds[nf++];
@@ -882,8 +882,8 @@ static int program_nodes(const emac_plan *p, const emac_node_sched *ns, int node
       if (hl <= 0) continue;
       for (i = 0; i < rad - 1; i++) {
         const int gp = ns->task_node[peer_task[i]] * R + me;
-        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, gp, 1, EMAC_BUF_RECV, ho * ts, hl * ts};
-        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, gp, 0, EMAC_BUF_STAGE, xslot[(size_t)pc * nx + xs + i], hl * ts};
+        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, gp, 1, EMAC_BUF_RECV, ho * ts, hl * ts, 0};
+        ops[nops++] = (emac_p2p){EMAC_LEG_NODES_RS | lg, gp, 0, EMAC_BUF_STAGE, xslot[(size_t)pc * nx + xs + i], hl * ts, 0};
       }
       {
         emac_fold *f = &folds[nf++];
@@ -924,8 +924,8 @@ static int program_nodes(const emac_plan *p, const emac_node_sched *ns, int node
         long po, pl;
         task_lines(ns, count, pt / g * g, pt / g * g + g, &a, &b);
         clip(a, b, off, off + len, &po, &pl);
-        if (ml > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | lg, gp, 1, EMAC_BUF_RECV, mo * ts, ml * ts};
-        if (pl > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | lg, gp, 0, EMAC_BUF_RECV, po * ts, pl * ts};
+        if (ml > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | lg, gp, 1, EMAC_BUF_RECV, mo * ts, ml * ts, 0};
+        if (pl > 0) ops[nops++] = (emac_p2p){EMAC_LEG_NODES_AG | lg, gp, 0, EMAC_BUF_RECV, po * ts, pl * ts, 0};
       }
     }
   }

@@ -152,6 +152,7 @@ typedef struct {
   int buf;     /* EMAC_BUF_* */
   long offset; /* bytes */
   long bytes;
+  int local;   /* the NODE form over several nodes: the node rank whose buffers the op uses (else 0) */
 } emac_p2p;
 
 typedef struct {

@@ -204,6 +204,18 @@ int ext_mpi_amd_comm_program_nodes(int nodes, int ranks_per_node, int rank, long
 int ext_mpi_amd_comm_set_node_ports(int comm, int nodes, const int *ports);
 int ext_mpi_amd_comm_set_nodes(int comm, int nodes);
 
+/* The same multi-node Allreduce with every rank of THIS node in this process (the NODE form's
+ * buffers: nranks send / receive buffers on this process's device) and `comm` (RCCL or loopback)
+ * having one member per node: member n is node n. The inter-node schedule is the one
+ * ext_mpi_amd_comm_set_node_ports(comm, size, ports) set, else the default for `size` nodes.
+ * A Start folds the node's copy-in over the send buffers where they lie (no intra-node transfer),
+ * runs every node rank's node legs (rank me of each node is a column peer of rank me of the
+ * others) as one RCCL group per leg, and stores each owner chunk into the node's other receive
+ * buffers. Bits identical to ext_mpi_amd_allreduce_init on size * nranks ranks of one process each
+ * (ext_mpi_native.c:879-1000). Peer-mapped communicators: EXT_MPI_AMD_ERROR_UNSUPPORTED. */
+int ext_mpi_amd_node_comm_allreduce_init(int nranks, const void *const *sendbufs, void *const *recvbufs, long count,
+                                         int dtype, int op, int comm, const char *copyin, int *handle);
+
 /* EXT_MPI_NUM_SOCKETS_PER_NODE (src/mpi/ext_mpi.c:43-187, a process-wide parameter): sockets per
  * node for every handle / plan made afterwards. It moves the tree method's (7 / 10) last-step
  * roots (reduce_copyin.c:860-864) and nothing else in the arithmetic. Returns the previous value,
