@@ -59,7 +59,7 @@ def parse():
                     help="N > 1: peer-mapped hipIpc form (default) or RCCL point-to-point legs")
     ap.add_argument("--shape", default=None, choices=["local256", "node256", "node16", "copy256", "int4", "long4"],
                     help="profiling: run only this fold shape (40 launches) and exit (PMC passes, tools/gpu_pmc_r02.sh)")
-    ap.add_argument("--child-transport", default=None, choices=["ipc", "rccl"], help=argparse.SUPPRESS)
+    ap.add_argument("--child-transport", default=None, choices=["ipc", "rccl", "node"], help=argparse.SUPPRESS)
     ap.add_argument("--child-full", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--child-result", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--alloc", default="hip", choices=["hip", "torch"],
@@ -749,6 +749,116 @@ def _node_point(emac, rank, world, dev, count, tdtype, code, dname, dist, torch,
         return {"error": str(e)[:200]}
 
 
+def _node_form_run(emac, comm, R, count, tdtype, code, copyin, steps, warmup, rank, world, dist, torch):
+    """N > 1 headline: configs[1]'s node (R ranks x count elements resident in this GPU) on every
+    GPU, the GPUs joined as nodes (ext_mpi_amd_node_comm_allreduce_init over an RCCL communicator
+    of one member per GPU): the node's copy-in fold, the inter-node legs over xGMI, the copy-out.
+    Returns the max-over-ranks wall time of `steps` Starts, the check, and each part's time."""
+    tsize = torch.empty((), dtype=tdtype).element_size()
+    np_dtype = {torch.float32: np.float32, torch.float64: np.float64, torch.int32: np.int32,
+                torch.int64: np.int64}[tdtype]
+    set_bytes = 2 * R * count * tsize
+    nsets = max(2, math.ceil(640 * MIB / max(1, set_bytes)))  # rotated past the 256 MiB Infinity Cache
+    stream = torch.cuda.Stream()
+    sets, handles, mine = [], [], None
+    for s in range(nsets):
+        sends, recvs = [], []
+        for r in range(R):
+            b = DevBuf(count * tsize)
+            a = host_random(count, np_dtype, 0x5EED0000 + 4099 * s + rank * R + r)  # global rank rank * R + r
+            b.upload(a)
+            if s == 0:
+                mine = (mine or []) + [a]
+            sends.append(b)
+            recvs.append(DevBuf(count * tsize))
+        h = emac.node_comm_allreduce_init([b.data_ptr() for b in sends], [b.data_ptr() for b in recvs], count, code,
+                                          comm, copyin)
+        emac.set_stream(h, stream.cuda_stream)
+        sets.append((sends, recvs))
+        handles.append(h)
+    try:
+        for k in range(max(warmup, nsets * TUNE_STARTS)):  # every handle past its fold tuning
+            emac.start(handles[k % nsets])
+        emac.start(handles[0])
+        stream.synchronize()
+        sched = emac.handle_schedule(handles[0])
+        # check set 0 against a float64 sum over every rank of every node (sampled)
+        idx = np.arange(0, count, max(1, count // (1 << 18)))
+        got = []
+        for b in (sets[0][1][0], sets[0][1][R - 1]):
+            a = np.empty(count, np_dtype)
+            b.download(a)
+            got.append(a[idx])
+        allin = [None] * world
+        dist.all_gather_object(allin, [a[idx] for a in mine])
+        ref = np.sum(np.stack([x.astype(np.float64) for node in allin for x in node]), axis=0)
+        tol = 1e-5 * world * R if np.dtype(np_dtype).kind == "f" else 0.0
+        good = bool(np.allclose(got[0].astype(np.float64), ref, rtol=0, atol=tol)) and np.array_equal(
+            got[0].view(np.uint8), got[1].view(np.uint8))
+        if not good:
+            log(f"rank {rank}: node form over {world} GPUs: result check failed")
+        ok = torch.tensor([int(good)])
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            emac.start(handles[k % nsets])
+        stream.synchronize()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        dist.barrier()
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+
+        def part(legs, n):  # one part of the Start alone on every GPU at once; max over ranks
+            dist.barrier()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for k in range(n):
+                emac.start_legs(handles[k % nsets], legs)
+            e1.record(stream)
+            stream.synchronize()
+            t = torch.tensor([e0.elapsed_time(e1) * 1e-3 / n], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return t.item()
+
+        parts = {"copy_in_fold_s": part(emac.LEG_FOLD, steps),
+                 "node_legs_s": part(emac.LEG_NODES_RS | emac.LEG_NODES_FOLD | emac.LEG_NODES_AG, steps),
+                 "copy_out_s": part(emac.LEG_ALLGATHER, steps)}
+        return {"wall": el.item(), "checked": bool(ok.item()), "schedule": sched, "nsets": nsets, **parts}
+    finally:
+        for h in handles:
+            emac.done(h)
+        for sends, recvs in sets:
+            for b in sends + recvs:
+                b.free()
+
+
+def node_child(args, emac, rank, world, dev, dist, torch):
+    """--child-transport node: the N > 1 headline (see _node_form_run) on an RCCL communicator of
+    one member per GPU, nodes joined by one inter-node step of radix N (EXT_MPI_NUM_PORTS
+    '-(N-1) (N-1)': every GPU trades with all N - 1 others at once, one xGMI link each)."""
+    tdtype, code, dname, tsize = dtype_info(args.dtype)
+    R = args.ranks
+    count = int(args.size_mib * MIB) // tsize
+    copyin = f"6;1 -{R} {R}"  # the node's own split (configs[1]); --copyin is the one-rank-per-GPU runs'
+    ports = [-(world - 1), world - 1] if world > 1 else []
+    uid = [emac.get_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    comm = emac.comm_init(rank, world, uid[0], dev)
+    try:
+        if world > 1:
+            emac.comm_set_nodes(comm, world, ports)
+        res = _node_form_run(emac, comm, R, count, tdtype, code, copyin, args.steps, args.warmup, rank, world, dist,
+                             torch)
+        log(f"rank {rank}: node form over {world} GPUs: {args.steps} steps in {res['wall'] * 1e3:.3f} ms, "
+            f"checked {res['checked']}")
+        res.update(ranks_per_gpu=R, copyin=copyin, ports=ports, bytes_per_rank=count * tsize)
+        return res
+    finally:
+        emac.comm_free(comm)
+
+
 def transport_child(args):
     """One transport's N > 1 measurement in a process of its own (spawned by multi_gpu): its own
     gloo group, its own HIP context. Writes this rank's results as JSON to --child-result."""
@@ -770,6 +880,14 @@ def transport_child(args):
     transport, full = args.child_transport, args.child_full
     res = {}
     log(f"rank {rank}: {transport} child on GPU {dev}: communicator set-up")
+    if transport == "node":
+        res = node_child(args, emac, rank, world, dev, dist, torch)
+        with open(args.child_result, "w") as f:
+            json.dump(res, f)
+        dist.barrier()
+        dist.destroy_process_group()
+        signal.alarm(0)
+        return
     if transport == "ipc":
         comm = emac.comm_init_ipc(rank, world, emac.torch_allgather(), dev)
     else:
@@ -905,7 +1023,7 @@ def multi_gpu(args):
             os.remove(out)
         cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(args.gpus), "--steps", str(args.steps),
                "--warmup", str(args.warmup), "--size-mib", str(args.size_mib), "--dtype", args.dtype,
-               "--child-transport", transport, "--child-result", out] + (["--child-full"] if full else []) + \
+               "--ranks", str(args.ranks), "--child-transport", transport, "--child-result", out] + (["--child-full"] if full else []) + \
               (["--copyin", args.copyin] if args.copyin else [])
         env = dict(os.environ, MASTER_PORT=str(base_port + 101 + i))
         env.pop("TORCHELASTIC_USE_AGENT_STORE", None)  # the children's rank 0 hosts their own store
@@ -920,8 +1038,13 @@ def multi_gpu(args):
             return r, (None if r.get("checked") else "result check failed")
         return {}, f"{transport} child exited with {rc}"
 
-    # the requested transport first; if it fails on any rank (every rank agrees before moving
-    # on), the other one produces the headline
+    # the headline: configs[1]'s node (8 ranks x 16 MiB resident in one GPU) on every GPU, the GPUs
+    # joined as nodes over RCCL -- the N = 1 workload scaled weakly
+    rn, err = run_child(9, "node", False)
+    if not everyone(err is None):
+        rn = {"error": err or "failed on another rank"}
+    # BASELINE configs[3] / [4] (one rank per GPU): the requested transport first; if it fails on
+    # any rank (every rank agrees before moving on), the other one
     order = [args.transport, "rccl" if args.transport == "ipc" else "ipc"]
     results = {}
     for i, transport in enumerate(order):
@@ -943,11 +1066,12 @@ def multi_gpu(args):
         for key in ("two_node_schedule", "four_node_schedule", "four_node_three_ports"):
             if key in results[t]:
                 extras[key] = results[t][key]
+    legacy = None
     if rank == 0 and primary is None:
-        emit(({"metric": "device-resident GB/s reduced (float32 MPI_SUM) per GPU; % HBM3E roofline",
-                          "value": 0.0, "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dname,
-                          "error": "no transport completed", "extras": extras}))
+        legacy = {"metric": "device-resident GB/s reduced (float32 MPI_SUM) per GPU; % HBM3E roofline",
+                  "value": 0.0, "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                  "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dname,
+                  "error": "no transport completed", "extras": extras}
     if rank == 0 and primary is not None:
         r = results[primary]
         wall, checked, kf = r["wall"], r["checked"], r["fold_s"]
@@ -1006,9 +1130,65 @@ def multi_gpu(args):
                          "algorithmic_bytes_per_launch": int(algo), "avg_launch_us": round(kl * 1e6, 2)},
             "extras": extras,
         }
-        emit(out)
+        legacy = out
+    if rank == 0:
+        if "wall" in rn and rn.get("checked"):
+            emit(node_form_line(args, world, dname, rn, legacy))
+        else:
+            legacy.setdefault("extras", {})["node_form_per_gpu"] = rn
+            emit(legacy)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def node_form_line(args, world, dname, rn, one_rank_per_gpu):
+    """The N > 1 JSON line: configs[1]'s node on each of the N GPUs (weak scaling of the N = 1
+    workload), the nodes joined over RCCL/xGMI. value = bytes reduced by the whole job per second
+    (N GPUs x R ranks x S bytes per Start); roofline = the node's copy-in fold (R leaves -> the
+    owner chunks, this GPU's HBM) timed on every GPU at once inside the job."""
+    R, S, steps = rn["ranks_per_gpu"], rn["bytes_per_rank"], args.steps
+    wall = rn["wall"]
+    t_in, t_x, t_out = rn["copy_in_fold_s"], rn["node_legs_s"], rn["copy_out_s"]
+    algo_in = (R + 1) * S  # R leaf reads of every owner chunk + one write of each (SURVEY.md 8d B_in)
+    achieved = algo_in / t_in / 1e9
+    xb = 2 * (world - 1) / world * S  # the node partial crosses xGMI out and back (reduce-scatter + allgather)
+    xgmi_bound = xb / (min(world - 1, 7) * 153e9)
+    extras = {
+        "form": "NODE form over nodes (ext_mpi_amd_node_comm_allreduce_init): per GPU one node of R ranks; "
+                "copy-in fold of the node in place, the inter-node legs of every node rank as one RCCL group per "
+                "leg (EXT_MPI_NUM_PORTS one step of radix N), the copy-out fan-out",
+        "parts_us": {"copy_in_fold": round(t_in * 1e6, 2), "node_legs_xgmi": round(t_x * 1e6, 2),
+                     "copy_out": round(t_out * 1e6, 2), "sum": round((t_in + t_x + t_out) * 1e6, 2),
+                     "start_to_wait": round(wall * 1e6 / steps, 2)},
+        "copy_out_achieved_gbps": round(R * S / t_out / 1e9, 1),
+        "node_legs_xgmi_bound_us": round(xgmi_bound * 1e6, 1),
+        "node_legs_frac_of_xgmi_bound": round(xgmi_bound / t_x, 3) if t_x > 0 else None,
+        "value_per_gpu_gbps": round(R * S * steps / wall / 1e9, 2),
+        "fold_schedule": rn.get("schedule"), "buffer_sets": rn.get("nsets"),
+        "one_rank_per_gpu": one_rank_per_gpu,
+    }
+    return {
+        "metric": "device-resident GB/s reduced (float32 MPI_SUM) per GPU; % HBM3E roofline",
+        "value": round(world * R * S * steps / wall / 1e9, 2),
+        "unit": "GB/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
+        "ms_per_step": round(wall * 1e3 / steps, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": dname,
+        "data": "synthetic: uniform [-1,1) per rank (seeded), device-resident (hipMalloc), "
+                f"{rn.get('nsets')} rotated buffer sets per GPU",
+        "config": {"workload": f"persistent Allreduce {args.dtype} MPI_SUM over {world} x {R} ranks: BASELINE "
+                               f"configs[1]'s node ({R} ranks x {S // MIB} MiB resident in one MI355X, "
+                               f"EXT_MPI_COPYIN '{rn['copyin']}') on each of {world} GPUs, the GPUs joined as "
+                               f"nodes over RCCL/xGMI (EXT_MPI_NUM_PORTS {rn['ports']}); value = bytes reduced by "
+                               f"the whole job per second ({world} x {R} x {S // MIB} MiB per step)",
+                   "ranks": world * R, "ranks_per_gpu": R, "message_bytes_per_rank": S, "copyin": rn["copyin"],
+                   "node_ports": rn["ports"], "layout": "node-per-gpu", "transport": "rccl",
+                   "checked_vs_fp64_sum": rn["checked"]},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                     "kernel": "fold_kernel (the node's copy-in: R leaves -> owner chunk, this GPU's HBM)",
+                     "algorithmic_bytes_per_launch": int(algo_in), "avg_launch_us": round(t_in * 1e6, 2)},
+        "extras": extras,
+    }
 
 
 def shape_only(args):
