@@ -154,7 +154,7 @@ def host_random(count, np_dtype, seed):
     return rng.integers(-lim, lim, count).astype(np_dtype)
 
 
-TUNE_STARTS = 5  # a handle's first Start, one per tuned candidate (at most 3), and the one that keeps the best
+TUNE_STARTS = 11  # a handle's first Start, 3 rounds of at most 3 tuned candidates, and the one that keeps the best
 
 
 def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * MIB, host=False, alloc="torch"):
@@ -300,6 +300,8 @@ def _ceiling_lib():
         return None
     L = ctypes.CDLL(path)
     L.ceiling_read_glds.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    L.ceiling_read_vgpr.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                    ctypes.c_void_p]
     L.ceiling_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     L.ceiling_gate_arm.argtypes = [ctypes.c_void_p]
     L.ceiling_gate_arm.restype = ctypes.c_void_p
@@ -329,8 +331,8 @@ class StreamGate:
 
 def measured_ceilings(steps=10, launch_bytes=256 * MIB):
     """Best HBM rates measured on this GPU in this run (tools/ceiling.hip), GB/s of algorithmic bytes:
-    read_glds -- a read-only LDS-DMA stream (global_load_lds_dwordx4 nt) over 4 GiB, the best read
-    rate measured on MI355X; copy -- the best of a nontemporal and a default-policy 1:1 copy
+    read -- the best of three read-only streams over 4 GiB: LDS-DMA (global_load_lds_dwordx4 nt)
+    and nontemporal global_load_dwordx4 into VGPRs with 4 or 8 vectors per lane in flight; copy -- the best of a nontemporal and a default-policy 1:1 copy
     (K = 4 vectors per lane), each timed over 4 GiB and over `launch_bytes` (read + written, the
     headline launch's bytes, three buffer sets rotated past the 256 MiB Infinity Cache): the rate
     of the node-form fold's 1:1 read/write mix."""
@@ -345,12 +347,18 @@ def measured_ceilings(steps=10, launch_bytes=256 * MIB):
     stream = torch.cuda.current_stream()
     out = {}
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    L.ceiling_read_glds(a.data_ptr(), n, 2, sink.data_ptr(), stream.cuda_stream)
-    e0.record(stream)
-    assert L.ceiling_read_glds(a.data_ptr(), n, steps, sink.data_ptr(), stream.cuda_stream) == 0
-    e1.record(stream)
-    torch.cuda.synchronize()
-    out["read_glds_gbps"] = round(steps * n / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+    reads = {}
+    for vname, fn in (("glds", lambda it: L.ceiling_read_glds(a.data_ptr(), n, it, sink.data_ptr(), stream.cuda_stream)),
+                      ("vgpr_k4", lambda it: L.ceiling_read_vgpr(a.data_ptr(), n, it, 4, sink.data_ptr(), stream.cuda_stream)),
+                      ("vgpr_k8", lambda it: L.ceiling_read_vgpr(a.data_ptr(), n, it, 8, sink.data_ptr(), stream.cuda_stream))):
+        fn(2)
+        e0.record(stream)
+        assert fn(steps) == 0
+        e1.record(stream)
+        torch.cuda.synchronize()
+        reads[vname] = round(steps * n / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+    out["read_ceiling_gbps"] = max(reads.values())
+    out["read_variants_gbps"] = reads
     copies = {}
     for variant, vname in ((0, "nt"), (1, "plain")):
         half = n // 2
@@ -515,8 +523,8 @@ def single_gpu(args):
             ceil = measured_ceilings()
             extras.update(ceil)
             if ceil:
-                out["roofline"]["measured_read_ceiling"] = ceil["read_glds_gbps"]
-                out["roofline"]["frac_of_measured_read_ceiling"] = round(achieved / ceil["read_glds_gbps"], 4)
+                out["roofline"]["measured_read_ceiling"] = ceil["read_ceiling_gbps"]
+                out["roofline"]["frac_of_measured_read_ceiling"] = round(achieved / ceil["read_ceiling_gbps"], 4)
                 out["roofline"]["measured_copy_ceiling"] = ceil["copy_gbps"]
                 # the fold against the best measured 1:1 copy of the same mix; a fold faster than
                 # every copy kernel measured makes that copy no ceiling: then only the flag is kept
@@ -534,8 +542,8 @@ def single_gpu(args):
             "achieved_gbps": round(2 * R * big * tsize / k256 / 1e9, 1),
             "frac_of_peak": round(2 * R * big * tsize / k256 / 1e9 / HBM_PEAK_GBPS, 4),
             "frac_of_guide_measured_copy": round(2 * R * big * tsize / k256 / 1e9 / HBM_GUIDE_COPY_GBPS, 4),
-            "frac_of_measured_read_ceiling": round(2 * R * big * tsize / k256 / 1e9 / extras["read_glds_gbps"], 4)
-            if "read_glds_gbps" in extras else None,
+            "frac_of_measured_read_ceiling": round(2 * R * big * tsize / k256 / 1e9 / extras["read_ceiling_gbps"], 4)
+            if "read_ceiling_gbps" in extras else None,
             "read_gbps": round(R * big * tsize / k256 / 1e9, 1),
             "avg_launch_us": round(k256 * 1e6, 1), "checked": r256["checked"], "fold_schedule": r256["schedule"],
             "traffic": traffic_from_profiles(f"node_r{R}_256mib_{args.dtype}")}
@@ -575,8 +583,8 @@ def single_gpu(args):
         lf["frac_of_peak"] = round(lf["achieved_gbps"] / HBM_PEAK_GBPS, 4)
         lf["algorithmic_bytes_per_launch"] = (R + 1) * lf["chunk_bytes"]
         lf["traffic"] = traffic_from_profiles(f"local_r{R}_{lf['chunk_bytes'] // MIB}mib_{args.dtype}")
-        if "read_glds_gbps" in extras:
-            lf["frac_of_measured_read_ceiling"] = round(lf["achieved_gbps"] / extras["read_glds_gbps"], 4)
+        if "read_ceiling_gbps" in extras:
+            lf["frac_of_measured_read_ceiling"] = round(lf["achieved_gbps"] / extras["read_ceiling_gbps"], 4)
         extras["local_fold_256MiB"] = lf
         hst = node_run(R, count, tdtype, code, copyin, 10, 3, host=True)
         os.environ["EXT_MPI_AMD_HOST_DIRECT"] = "0"  # staged through device mirrors, for comparison

@@ -141,23 +141,26 @@ typedef struct {
 } emac_launch;
 
 /* Launch-schedule tuning of a handle's fold (NODE form, and the COMM form's local fold): the
-   first Start runs the static pick (emac_gpu_pick_unroll) and warms the buffers, the next Starts
-   run one candidate schedule each between timing events, and the Start after them keeps the
-   fastest for the handle's lifetime. Every schedule folds in the same order -- the bits do not
-   depend on the choice. Measured on MI355X leases (tools/schedbench.hip,
-   profiles/r03_schedbench_*.txt): the fastest schedule of a shape moves between leases by more
-   than the spread within one (16 MiB x 8 node fold: U 2 48.1 us, U 4 51.8, U 4 staggered 54.1 on
-   one lease, where round 2's A/B leases had ranked the staggered one first), so no fixed
-   threshold table picks it everywhere. EXT_MPI_AMD_AUTOTUNE=0 keeps the static pick. */
+   first Start runs the static pick (emac_gpu_pick_unroll) and warms the buffers, the next
+   EMAC_TUNE_ROUNDS x candidates Starts run the candidates round-robin, each between timing events,
+   and the Start after them keeps the candidate with the shortest of its samples for the handle's
+   lifetime. Every schedule folds in the same order -- the bits do not depend on the choice.
+   Measured on MI355X leases (tools/schedbench.hip, tools/nodevar.hip, profiles/r03_schedbench_*,
+   profiles/r03_nodevar/): the fastest schedule of a shape moves between leases by more than the
+   spread within one (16 MiB x 8 node fold: U 2 48.1 us, U 4 51.8, U 4 staggered 54.1 on one
+   lease; U 2 47.1, U 4 46.2 on another), so no fixed threshold table picks it everywhere; one
+   sample per candidate (round 3's first tuner) kept U 2 on a lease where U 4 was 2 % faster, hence
+   the rounds. EXT_MPI_AMD_AUTOTUNE=0 keeps the static pick. */
 #define EMAC_TUNE_MAX 3
+#define EMAC_TUNE_ROUNDS 3
 #define EMAC_TUNE_MIN_BYTES (16L << 20) /* algorithmic bytes per launch: smaller launches keep the static pick */
 typedef struct {
   int n;      /* candidates (0: no tuning) */
   int chosen; /* index of the kept candidate, -1 while measuring */
   int starts;
   emac_launch L[EMAC_TUNE_MAX];
-  void *ev[EMAC_TUNE_MAX][2];
-  float us[EMAC_TUNE_MAX];
+  void *ev[EMAC_TUNE_MAX * EMAC_TUNE_ROUNDS][2]; /* sample i: candidate i % n, round i / n */
+  float us[EMAC_TUNE_MAX];                       /* shortest sample per candidate */
 } emac_tune;
 
 /* NODE form with host buffers: the message is staged in EMAC_PIPE_PARTS element ranges so that
@@ -279,6 +282,8 @@ static void release(emac_handle *h) {
   for (r = 0; r < h->tune.n; r++) {
     if (h->tune.L[r].d_buckets != h->d_buckets) emac_gpu_free(h->tune.L[r].d_buckets);
     if (h->tune.L[r].d_edges != h->d_edges) emac_gpu_free(h->tune.L[r].d_edges);
+  }
+  for (r = 0; r < EMAC_TUNE_MAX * EMAC_TUNE_ROUNDS; r++) {
     emac_gpu_event_destroy(h->tune.ev[r][0]);
     emac_gpu_event_destroy(h->tune.ev[r][1]);
   }
@@ -481,8 +486,10 @@ static int upload_buckets(emac_handle *h, emac_bucket *b, int nb) {
           free(edges);
         }
       }
-      if (!rc) rc = emac_gpu_event_create_timed(&h->tune.ev[k][0]);
-      if (!rc) rc = emac_gpu_event_create_timed(&h->tune.ev[k][1]);
+    }
+    for (i = 0; i < nc * EMAC_TUNE_ROUNDS && !rc; i++) {
+      rc = emac_gpu_event_create_timed(&h->tune.ev[i][0]);
+      if (!rc) rc = emac_gpu_event_create_timed(&h->tune.ev[i][1]);
     }
     free(tb);
   }
@@ -494,21 +501,25 @@ static int fold_launch(emac_handle *h) {
   emac_tune *t = &h->tune;
   int rc, k;
   if (t->n && t->chosen < 0) {
-    const int s = t->starts++;
-    if (s >= 1 && s <= t->n) { /* candidate s - 1, timed */
-      const emac_launch *L = &t->L[s - 1];
+    const int s = t->starts++, nsamples = t->n * EMAC_TUNE_ROUNDS;
+    if (s >= 1 && s <= nsamples) { /* sample s - 1: candidate (s - 1) % n, timed */
+      const emac_launch *L = &t->L[(s - 1) % t->n];
       if ((rc = emac_gpu_event_record(t->ev[s - 1][0], h->stream))) return rc;
       if ((rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, h->fan, L->unroll, &h->plan.codes, L->d_buckets, L->nb,
                               L->ntiles, L->tiles_per_bucket, L->all_full, L->d_edges, L->nedges, h->stream)))
         return rc;
       return emac_gpu_event_record(t->ev[s - 1][1], h->stream);
     }
-    if (s == t->n + 1) { /* keep the fastest: it becomes the handle's launch */
-      int best = 0;
-      for (k = 0; k < t->n; k++) {
-        if ((rc = emac_gpu_event_elapsed_us(t->ev[k][0], t->ev[k][1], &t->us[k]))) return rc;
-        if (t->us[k] < t->us[best]) best = k;
+    if (s == nsamples + 1) { /* keep the fastest: it becomes the handle's launch */
+      int best = 0, i;
+      for (k = 0; k < t->n; k++) t->us[k] = 1e30f;
+      for (i = 0; i < nsamples; i++) {
+        float us;
+        if ((rc = emac_gpu_event_elapsed_us(t->ev[i][0], t->ev[i][1], &us))) return rc;
+        if (us < t->us[i % t->n]) t->us[i % t->n] = us;
       }
+      for (k = 1; k < t->n; k++)
+        if (t->us[k] < t->us[best]) best = k;
       void *old_b = h->d_buckets, *old_e = h->d_edges; /* the static pick's upload */
       if (t->L[best].d_buckets != h->d_buckets) {
         h->d_buckets = t->L[best].d_buckets;

@@ -387,7 +387,7 @@ def test_copy_reduce_headline_instance():
         assert np.array_equal(d.cpu().numpy().view(np.uint8), want.view(np.uint8))
     h = emac.fold_init([t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts], count, emac.FLOAT)
     seen = set()
-    for k in range(7):
+    for k in range(13):  # the static pick, 3 rounds of 3 timed candidates, then the kept one
         for d in dsts:
             d.fill_(-1.0)
         torch.cuda.synchronize()  # the fill runs on torch's stream, the fold on the handle's

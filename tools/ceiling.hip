@@ -4,6 +4,10 @@
 //   ceiling_read_glds: a read-only stream through LDS-DMA (global_load_lds_dwordx4, nontemporal):
 //                      the best read rate measured on MI355X in round 1 (tools/ldsbench.hip,
 //                      ~6.99 TB/s at 4 GiB against ~6.07 TB/s with nt loads into VGPRs).
+//   ceiling_read_vgpr: a read-only stream of nontemporal global_load_dwordx4 into VGPRs, K = 4 or 8
+//                      vectors per lane in flight (round 3, tools/nodevar.hip,
+//                      profiles/r03_nodevar/: 6.85-7.06 TB/s, at or above the LDS-DMA stream on the
+//                      same lease); bench.py's read ceiling is the best of the three.
 //   ceiling_copy:      a 1:1 copy (1 byte written per byte read: the node-form fold's mix), K = 4
 //                      vectors per lane in flight, nontemporal or default-policy accesses.
 // Each call enqueues `iters` launches over `bytes` (a multiple of 16 KiB) on `stream`.
@@ -32,6 +36,20 @@ __global__ __launch_bounds__(256) void read_glds(const f4 *__restrict__ a, long 
     __syncthreads();
     acc += lds[threadIdx.x];
     __syncthreads();
+  }
+  if (acc.x == 12345.f) out[0] = acc.y + acc.z + acc.w;
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void read_vgpr(const f4 *__restrict__ a, long n, float *out) {
+  f4 acc = {0, 0, 0, 0};
+  const long step = (long)gridDim.x * 256 * K;
+  for (long i0 = (long)blockIdx.x * 256 * K + threadIdx.x; i0 < n; i0 += step) {
+    f4 v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = __builtin_nontemporal_load((const G4 *)a + i0 + k * 256);
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc += v[k];
   }
   if (acc.x == 12345.f) out[0] = acc.y + acc.z + acc.w;
 }
@@ -66,6 +84,21 @@ int ceiling_read_glds(const void *buf, long bytes, int iters, float *sink, void 
   for (int i = 0; i < iters; i++)
     hipLaunchKernelGGL(read_glds, dim3(2048), dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<const f4 *>(buf), n,
                        sink);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+/* k = 4 or 8 vectors per lane in flight */
+int ceiling_read_vgpr(const void *buf, long bytes, int iters, int k, float *sink, void *stream) {
+  const long n = bytes / 16;
+  if (n % (256 * 8) || iters < 1 || (k != 4 && k != 8)) return -3;
+  for (int i = 0; i < iters; i++) {
+    if (k == 4)
+      hipLaunchKernelGGL(read_vgpr<4>, dim3(4096), dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<const f4 *>(buf), n,
+                         sink);
+    else
+      hipLaunchKernelGGL(read_vgpr<8>, dim3(2048), dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<const f4 *>(buf), n,
+                         sink);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
