@@ -151,7 +151,7 @@ typedef struct {
    lease; U 2 47.1, U 4 46.2 on another), so no fixed threshold table picks it everywhere; one
    sample per candidate (round 3's first tuner) kept U 2 on a lease where U 4 was 2 % faster, hence
    the rounds. EXT_MPI_AMD_AUTOTUNE=0 keeps the static pick. */
-#define EMAC_TUNE_MAX 3
+#define EMAC_TUNE_MAX 5
 #define EMAC_TUNE_ROUNDS 3
 #define EMAC_TUNE_MIN_BYTES (16L << 20) /* algorithmic bytes per launch: smaller launches keep the static pick */
 typedef struct {
@@ -428,15 +428,23 @@ static int upload_launch(const emac_handle *h, emac_launch *L, emac_bucket *b, i
 static int tune_candidates(const emac_handle *h, int *sched) {
   const char *e = getenv("EXT_MPI_AMD_AUTOTUNE");
   const char *g = getenv("EXT_MPI_AMD_GRAPH"); /* captured Starts replay one schedule */
+  int n = 0;
   if ((e && atoi(e) <= 0) || (h->kind == KIND_COMM && g && atoi(g) > 0) || h->plan.op != EMAC_SUM || h->nsrc < 2 ||
       h->nsrc > 8 || h->host_direct ||
       emac_tree_kind(&h->plan.codes, h->plan.op) == 1 || (h->fan != 0 && h->fan != 1))
     return 0;
-  sched[0] = 2 | 1 << 4; /* fold_kernel.hpp instantiation policy: (U 2, burst), (U 4, burst) */
-  sched[1] = 4 | 1 << 4;
-  if (!h->fan) return 2;
-  sched[2] = 4 | 5 << 4; /* node fan-out: (U 4, s_sleep 2 every 4 loads) too */
-  return 3;
+  /* fold_kernel.hpp instantiation policy: (U 2, burst), (U 4, burst), for the node fan-out (U 4,
+     s_sleep 2 every 4 loads); deferred stores (kDeferShift) when every bucket has the same tile
+     count: (U 2, 4 tiles) and (U 4, 4 tiles) for one destination, (U 2, 4 tiles) and (U 4, 2
+     tiles) for the fan-out */
+  sched[n++] = 2 | 1 << 4;
+  sched[n++] = 4 | 1 << 4;
+  if (h->fan) sched[n++] = 4 | 5 << 4;
+  if (h->tiles_per_bucket > 0) {
+    sched[n++] = 2 | (1 | 2 << 11) << 4;
+    sched[n++] = 4 | (1 | (h->fan ? 1 : 2) << 11) << 4;
+  }
+  return n;
 }
 
 static int upload_buckets(emac_handle *h, emac_bucket *b, int nb) {

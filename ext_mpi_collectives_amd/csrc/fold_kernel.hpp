@@ -203,9 +203,10 @@ __device__ __forceinline__ void fold_scalar_element(const emac_bucket *b, long e
 // ISSUE (load issue schedule, measured in tools/ldsbench.hip): bit 0 = source-major order
 // (every vector of leaf 0, then leaf 1, ...) instead of vector-major; bits 1.. = s_sleep after
 // every 4 loads (0 = back-to-back burst).
-template <typename T, int OP, int N, int U, int CH, int D, bool FULL, int ISSUE = 1>
-__device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_base, long nvec, const emac_codes &c,
-                                             bool store = true) {
+// Loads and folds one tile: r[u] = the fold of every leaf's vector u of the tile.
+template <typename T, int OP, int N, int U, int CH, bool FULL, int ISSUE>
+__device__ __forceinline__ void load_fold(const emac_bucket *b, long tile_base, long nvec, const emac_codes &c,
+                                          typename Lane<T>::V (&r)[U]) {
   typedef typename Lane<T>::V V;
   typedef __attribute__((address_space(1))) V GV;
   constexpr bool SRC_MAJOR = ISSUE & 1;
@@ -233,9 +234,30 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
       if ((k & 3) == 3 && k + 1 < N * U) __builtin_amdgcn_s_sleep(SLEEP);
     }
   }
-  V r[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) r[u] = fold_leaves<OP, T, N, CH>(x[u], c);
+}
+
+// One 16-byte vector stored under the launch's store policy.
+template <typename V, int ISSUE>
+__device__ __forceinline__ void store_vec(__attribute__((address_space(1))) V *dst, unsigned v, V r) {
+  if constexpr ((ISSUE & kRemote) != 0)
+    sys_store16<V>((void *)dst, v * 16u, r);
+  else if constexpr ((ISSUE & kPlainStore) != 0)
+    dst[v] = r;
+  else
+    __builtin_nontemporal_store(r, dst + v);
+}
+
+template <typename T, int OP, int N, int U, int CH, int D, bool FULL, int ISSUE = 1>
+__device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_base, long nvec, const emac_codes &c,
+                                             bool store = true) {
+  typedef typename Lane<T>::V V;
+  typedef __attribute__((address_space(1))) V GV;
+  constexpr bool REMOTE = ISSUE & kRemote;
+  const long left = nvec - tile_base;
+  V r[U];
+  load_fold<T, OP, N, U, CH, FULL, ISSUE>(b, tile_base, nvec, c, r);
   // destination pointers are only needed now: their descriptor read overlaps the loads
   if (!store) return;  // peer-mapped launch whose phase-0 barrier failed (wave-uniform)
 #pragma unroll
@@ -244,18 +266,65 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const unsigned v = threadIdx.x + (unsigned)(u * EMAC_BLOCK);
-      if constexpr (REMOTE) {
-        if (FULL || (long)v < left) sys_store16<V>((void *)dst, v * 16u, r[u]);
-      } else if constexpr ((ISSUE & kPlainStore) != 0) {
-        if (FULL || (long)v < left) dst[v] = r[u];
-      } else {
-        if (FULL || (long)v < left) __builtin_nontemporal_store(r[u], dst + v);
-      }
+      if (FULL || (long)v < left) store_vec<V, ISSUE>(dst, v, r[u]);
     }
   }
   // a peer-mapped launch's stores are acknowledged by the owners' memory before the wave ends,
   // so the barrier launch after it can signal without a release fence
   if constexpr (REMOTE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ISSUE bits 11-12 (kDeferShift): deferred stores. A workgroup takes KB = 2^k consecutive tiles
+// of one bucket, folds them one after the other into LDS, then stores all KB tiles to every
+// destination in one burst. The workgroups, started together, then alternate between phases of
+// loads and phases of stores instead of mixing both all the time: fewer read/write turnarounds
+// at the HBM (tools/nodevar.hip, profiles/r03_nodevar/: the local fold 8 x 32 MiB -> 1 at 0.79-0.80
+// of 8 TB/s against 0.76-0.77 for the per-tile loop, 2-4 % at every size measured; the node fan-out
+// 2 % faster at 16 MiB per rank on one lease, slower on others). Each lane reads back only the LDS
+// slots it wrote, so no barrier is needed. Offered to the per-handle tuner (engine.c emac_tune);
+// the fold order -- and so every bit -- is the per-tile loop's.
+constexpr int kDeferShift = 11;
+constexpr int defer_tiles(int issue) { return ((issue >> kDeferShift) & 3) ? 1 << ((issue >> kDeferShift) & 3) : 1; }
+constexpr int defer(int kb) { return (kb == 2 ? 1 : kb == 4 ? 2 : kb == 8 ? 3 : 0) << kDeferShift; }
+
+template <typename T, int OP, int N, int U, int CH, int D, int ISSUE>
+__device__ __forceinline__ void fold_deferred(const emac_bucket *bk, long tpb, long ngroups, const emac_codes &c) {
+  typedef typename Lane<T>::V V;
+  typedef __attribute__((address_space(1))) V GV;
+  constexpr int KB = defer_tiles(ISSUE);
+  constexpr long TILE = (long)EMAC_BLOCK * U;
+  __shared__ V res[KB * U * EMAC_BLOCK];
+  const long gpb = (tpb + KB - 1) / KB;  // groups per bucket (the last one may hold fewer tiles)
+  for (long g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int bi = (int)(g / gpb);
+    const long t0 = (g - (long)bi * gpb) * KB;
+    const emac_bucket *b = bk + bi;
+    const long nvec = b->nvec, gbase = t0 * TILE;
+    const int nt = tpb - t0 < KB ? (int)(tpb - t0) : KB;  // wave-uniform
+#pragma unroll
+    for (int j = 0; j < KB; ++j) {
+      if (j < nt) {
+        const long tb = gbase + j * TILE;
+        V r[U];
+        if (tb + TILE <= nvec)
+          load_fold<T, OP, N, U, CH, true, ISSUE>(b, tb, nvec, c, r);
+        else
+          load_fold<T, OP, N, U, CH, false, ISSUE>(b, tb, nvec, c, r);
+#pragma unroll
+        for (int u = 0; u < U; ++u) res[(j * U + u) * EMAC_BLOCK + threadIdx.x] = r[u];
+      }
+    }
+    const long left = nvec - gbase;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      GV *dst = (GV *)b->dst[d] + gbase;
+#pragma unroll
+      for (int q = 0; q < KB * U; ++q) {
+        const unsigned v = threadIdx.x + (unsigned)(q * EMAC_BLOCK);
+        if (q < nt * U && (long)v < left) store_vec<V, ISSUE>(dst, v, res[q * EMAC_BLOCK + threadIdx.x]);
+      }
+    }
+  }
 }
 
 // ---- runtime leaf count (N = 0 in the templates below): MIN / MAX ----
@@ -360,6 +429,13 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_kernel(const emac_bucket *__r
   // the leaf loads and only waited for before the first store
   bool store = true;
   if constexpr ((ISSUE & kRemote) != 0) store = __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+  if constexpr (defer_tiles(ISSUE) > 1) {
+    static_assert(N > 0 && (ISSUE & kRemote) == 0, "deferred stores: compile-time leaves, local memory");
+    if (tiles_per_bucket > 0) {  // equal buckets (the tuner offers the schedule only then)
+      fold_deferred<T, OP, N, U, CH, D, ISSUE>(bk, tiles_per_bucket, (long)nb * ((tiles_per_bucket + defer_tiles(ISSUE) - 1) / defer_tiles(ISSUE)), codes);
+      return;
+    }
+  }
   for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     // bucket of this tile: arithmetic when every bucket has the same tile count (equal chunks:
     // the common case), else the last bucket whose first tile is <= tile (wave-uniform search;
@@ -546,9 +622,9 @@ __global__ __launch_bounds__(EMAC_BLOCK) void ipc_fused_kernel(Work fold, Work p
 // A launch schedule is encoded as U | ISSUE << 4 (sched). SUM, per fold-tree kind CH:
 // linear or compile-time chain (gpu.h EMAC_CHAINS), fan-out N (node form):
 //        N <= 8 -> (U 2, burst), (U 4, burst), (U 4, s_sleep 2 every 4 loads), (U 1, burst: host
-//        buffers); N > 8 -> (U 1, burst)
-// linear or chain, fan-out 1 (comm form, one-chunk fold): N <= 8 -> U in {1, 2, 4}, burst;
-//        N > 8 -> U = 1
+//        buffers), deferred stores (U 2, 4 tiles), (U 4, 2 tiles); N > 8 -> (U 1, burst)
+// linear or chain, fan-out 1 (comm form, one-chunk fold): N <= 8 -> U in {1, 2, 4}, burst, and
+//        deferred stores (U 2, 4 tiles), (U 4, 4 tiles); N > 8 -> U = 1
 // runtime-code tree (composite N, any chain), either fan-out: U = 4 / 2 / 1 for N <= 4 / <= 8 /
 //        > 8, burst; U = 2 also with s_sleep 2 every 4 loads (node form)
 // peer-mapped (IPC, ISSUE | kRemote): (U 2, burst) up to 8 leaves, (U 1) above; runtime trees U
@@ -573,7 +649,9 @@ struct Launch {
 
 template <typename T, int OP, int N, int U, int CH, int D, int ISSUE = 1>
 int launch_one(const Launch &L) {
-  const long grid = L.ntiles < 8192 ? L.ntiles : 8192;
+  constexpr int KB = defer_tiles(ISSUE);
+  const long work = (KB > 1 && L.tpb > 0) ? (long)L.nb * ((L.tpb + KB - 1) / KB) : L.ntiles;  // deferred: one per group
+  const long grid = work < 8192 ? work : 8192;
   if (grid > 0)
     hipLaunchKernelGGL((fold_kernel<T, OP, N, U, CH, D, ISSUE>), dim3((unsigned)grid), dim3(EMAC_BLOCK), 0, L.s, L.b, L.nb,
                        L.ntiles, L.tpb, L.all_full, *L.c, L.go, L.nrt);
@@ -604,11 +682,15 @@ int launch_sum(int unroll, const Launch &L) {
     if (unroll == sched(4, 5)) return launch_one<T, OP, N, 4, CH, D, 5>(L);
     if (unroll == sched(4, 1)) return launch_one<T, OP, N, 4, CH, D, 1>(L);
     if (unroll == sched(2, 1)) return launch_one<T, OP, N, 2, CH, D, 1>(L);
+    if (unroll == sched(2, 1 | defer(4))) return launch_one<T, OP, N, 2, CH, D, 1 | defer(4)>(L);
+    if (unroll == sched(4, 1 | defer(2))) return launch_one<T, OP, N, 4, CH, D, 1 | defer(2)>(L);
     return EMAC_ERR_UNSUPPORTED;
   } else {
     if (unroll == sched(4, 1)) return launch_one<T, OP, N, 4, CH, D>(L);
     if (unroll == sched(2, 1)) return launch_one<T, OP, N, 2, CH, D>(L);
     if (unroll == sched(1, 1)) return launch_one<T, OP, N, 1, CH, D>(L);
+    if (unroll == sched(2, 1 | defer(4))) return launch_one<T, OP, N, 2, CH, D, 1 | defer(4)>(L);
+    if (unroll == sched(4, 1 | defer(4))) return launch_one<T, OP, N, 4, CH, D, 1 | defer(4)>(L);
     return EMAC_ERR_UNSUPPORTED;
   }
 }

@@ -387,7 +387,7 @@ def test_copy_reduce_headline_instance():
         assert np.array_equal(d.cpu().numpy().view(np.uint8), want.view(np.uint8))
     h = emac.fold_init([t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts], count, emac.FLOAT)
     seen = set()
-    for k in range(13):  # the static pick, 3 rounds of 3 timed candidates, then the kept one
+    for k in range(19):  # the static pick, 3 rounds of 5 timed candidates, then the kept one
         for d in dsts:
             d.fill_(-1.0)
         torch.cuda.synchronize()  # the fill runs on torch's stream, the fold on the handle's
@@ -400,6 +400,60 @@ def test_copy_reduce_headline_instance():
     emac.done(h)
     assert (4, 5, 0) in seen  # the headline instance ran (static pick, before tuning kept one)
     assert any(t == 1 for _, _, t in seen)  # and the tuned schedule after it
+
+
+DEFER_SHIFT = 11  # fold_kernel.hpp kDeferShift: deferred-store schedules (issue bits 11-12)
+
+
+@pytest.mark.parametrize("copyin", ["6;1 -8 8", "6;1 -2 -2 -2 2 2 2"])
+@pytest.mark.parametrize("code", [emac.FLOAT, emac.DOUBLE])
+def test_every_tuned_schedule_bitwise(oracle, code, copyin):
+    """The per-handle schedule tuner (engine.c emac_tune) runs every candidate on a handle's first
+    Starts -- burst loads at U 2 / U 4, the staggered issue, and the deferred-store schedules
+    (fold_kernel.hpp fold_deferred: 4 or 2 tiles folded into LDS, then stored in one burst) -- and
+    keeps one. Every Start must give the oracle's bits: here a node form whose buckets end in a
+    partial tile and whose last group of tiles is short (41000 elements per chunk), and a local
+    fold (8 leaves -> 1, fold_init) of 512040 elements, each over 19 Starts."""
+    R, chunk = 8, 41000 if code == emac.FLOAT else 20500
+    count = R * chunk
+    sends = xorshift_inputs(R, count, code, seed_base=0x7E57)
+    want = oracle.allreduce(sends, copyin)
+    dsend = [_dev(x) for x in sends]
+    drecv = [torch.full((count,), -1, dtype=TORCH[code], device="cuda") for _ in range(R)]
+    h = emac.node_allreduce_init([t.data_ptr() for t in dsend], [t.data_ptr() for t in drecv], count, code, copyin)
+    seen = set()
+    try:
+        for k in range(19):
+            for t in drecv:
+                t.fill_(-1)
+            torch.cuda.synchronize()
+            emac.start(h)
+            emac.wait(h)
+            sc = emac.handle_schedule(h)
+            seen.add((sc["unroll"], sc["issue"], sc["tuned"]))
+            assert_bitwise([t.cpu().numpy() for t in drecv], want, f"node {copyin} Start {k} {sc}")
+    finally:
+        emac.done(h)
+    assert any(t == 1 for _, _, t in seen), seen
+    # the local fold: one destination, one bucket
+    n = 8 * 64000 + 40 if code == emac.FLOAT else 4 * 64000 + 20
+    srcs_np = xorshift_inputs(R, n, code, seed_base=0x10CA1)
+    lwant = srcs_np[0].copy()
+    for x in srcs_np[1:]:
+        lwant = lwant + x
+    srcs = [_dev(x) for x in srcs_np]
+    dst = torch.full((n,), -1, dtype=TORCH[code], device="cuda")
+    h = emac.fold_init([t.data_ptr() for t in srcs], [dst.data_ptr()], n, code)
+    try:
+        for k in range(19):
+            dst.fill_(-1)
+            torch.cuda.synchronize()
+            emac.start(h)
+            emac.wait(h)
+            sc = emac.handle_schedule(h)
+            assert_bitwise([dst.cpu().numpy()], [lwant], f"local fold Start {k} {sc}")
+    finally:
+        emac.done(h)
 
 
 def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=None, op=emac.SUM, repeats=1, nodes=1,

@@ -3,7 +3,7 @@
 # 32 MiB per rank (the local fold 8 x 32 MiB -> 1 of bench.py) and 256 MiB per rank.
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-for kib in 2048 4096 32768; do
+for kib in ${KIBS:-2048 4096 32768}; do
   r=7; p=10; [ $kib -gt 4096 ] && { r=5; p=4; }
   timeout -k 10 300 tools/nodevar $kib $r $p > gpurun_out/nodevar_$kib.txt 2>&1 || exit $?
   cat gpurun_out/nodevar_$kib.txt

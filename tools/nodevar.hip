@@ -104,6 +104,70 @@ __global__ __launch_bounds__(256) void lfold(const Bk *__restrict__ b, long ntil
   }
 }
 
+// the local fold with its stores deferred: each workgroup folds KB consecutive tiles into LDS,
+// then writes them out in one burst (fewer read/write turnarounds per DRAM page)
+template <int U, int KB>
+__global__ __launch_bounds__(256) void lfold_burst(const Bk *__restrict__ b, long ntiles) {
+  constexpr long TILE = 256L * U;
+  __shared__ f4 res[KB * U * 256];
+  for (long g = blockIdx.x; g * KB < ntiles; g += gridDim.x) {
+    for (int j = 0; j < KB; ++j) {
+      const long t = g * KB + j;
+      f4 x[U][R];
+#pragma unroll
+      for (int k = 0; k < R * U; ++k) {
+        const int s = k / U, u = k % U;
+        x[u][s] = __builtin_nontemporal_load((const G4 *)b->src[s] + t * TILE + threadIdx.x + u * 256);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        f4 a = x[u][0];
+#pragma unroll
+        for (int s = 1; s < R; ++s) a = a + x[u][s];
+        res[(j * U + u) * 256 + threadIdx.x] = a;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < KB * U; ++q)
+      __builtin_nontemporal_store(res[q * 256 + threadIdx.x], (G4 *)b->dst[0] + g * KB * TILE + q * 256 + threadIdx.x);
+  }
+}
+
+// the node fold with its stores deferred: KB consecutive tiles of one bucket folded into LDS,
+// then written to all R destinations in one burst
+template <int U, int KB>
+__global__ __launch_bounds__(256) void nfold_burst(const Bk *__restrict__ bk, int nb, long tpb) {
+  constexpr long TILE = 256L * U;
+  __shared__ f4 res[KB * U * 256];
+  const long ngroups = tpb / KB * nb;
+  for (long g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int bi = (int)(g / (tpb / KB));
+    const long t0 = (g % (tpb / KB)) * KB;
+    const Bk *b = bk + bi;
+    for (int j = 0; j < KB; ++j) {
+      const long t = t0 + j;
+      f4 x[U][R];
+#pragma unroll
+      for (int k = 0; k < R * U; ++k) {
+        const int s = k / U, u = k % U;
+        x[u][s] = __builtin_nontemporal_load((const G4 *)b->src[s] + t * TILE + threadIdx.x + u * 256);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        f4 a = x[u][0];
+#pragma unroll
+        for (int s = 1; s < R; ++s) a = a + x[u][s];
+        res[(j * U + u) * 256 + threadIdx.x] = a;
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < R; ++d)
+#pragma unroll
+      for (int q = 0; q < KB * U; ++q)
+        __builtin_nontemporal_store(res[q * 256 + threadIdx.x], (G4 *)b->dst[d] + t0 * TILE + q * 256 + threadIdx.x);
+  }
+}
+
 // pure read streams: K vectors per lane in flight into VGPRs (nt), or LDS-DMA (global_load_lds nt)
 template <int K>
 __global__ __launch_bounds__(256) void read_vgpr(const f4 *__restrict__ a, long n, float *out) {
@@ -229,6 +293,12 @@ int main(int argc, char **argv) {
       {"local_u1", 40, 0, {}},         {"local_u2", 41, 0, {}},        {"local_u4", 42, 0, {}},
       {"local_u2_g256", 41, 256, {}},  {"local_u2_g512", 41, 512, {}}, {"local_u4_g256", 42, 256, {}},
       {"local_u4_g512", 42, 512, {}},  {"local_u1_g1024", 40, 1024, {}}, {"local_u1_g2048", 40, 2048, {}},
+      {"local_burst_u2_k4", 43, 0, {}}, {"local_burst_u2_k8", 44, 0, {}}, {"local_burst_u4_k4", 45, 0, {}},
+      {"local_burst_u2_k8_g256", 44, 256, {}}, {"local_burst_u2_k4_g512", 43, 512, {}},
+      {"local_burst_u2_k4_g256", 43, 256, {}}, {"local_burst_u2_k4_g768", 43, 768, {}},
+      {"local_burst_u2_k8_g512", 44, 512, {}}, {"local_burst_u4_k4_g512", 45, 512, {}},
+      {"node_burst_u2_k2", 46, 0, {}}, {"node_burst_u2_k4", 47, 0, {}}, {"node_burst_u2_k2_g512", 46, 512, {}},
+      {"node_burst_u2_k4_g512", 47, 512, {}}, {"node_burst_u4_k2", 48, 0, {}}, {"node_burst_u2_k4_g256", 47, 256, {}},
       {"read_vgpr_k4", 50, 0, {}},     {"read_vgpr_k8", 51, 0, {}},    {"read_glds", 52, 0, {}}};
   auto run = [&](const V &v, int i) {
     const int st = i % nsets;
@@ -259,6 +329,12 @@ int main(int argc, char **argv) {
     case 40: hipLaunchKernelGGL((lfold<1>), dim3(g(lt1)), dim3(256), 0, s, dloc[st], lt1); break;
     case 41: hipLaunchKernelGGL((lfold<2>), dim3(g(lt1 / 2)), dim3(256), 0, s, dloc[st], lt1 / 2); break;
     case 42: hipLaunchKernelGGL((lfold<4>), dim3(g(lt1 / 4)), dim3(256), 0, s, dloc[st], lt1 / 4); break;
+    case 43: hipLaunchKernelGGL((lfold_burst<2, 4>), dim3(g(lt1 / 8)), dim3(256), 0, s, dloc[st], lt1 / 2); break;
+    case 44: hipLaunchKernelGGL((lfold_burst<2, 8>), dim3(g(lt1 / 16)), dim3(256), 0, s, dloc[st], lt1 / 2); break;
+    case 45: hipLaunchKernelGGL((lfold_burst<4, 4>), dim3(g(lt1 / 16)), dim3(256), 0, s, dloc[st], lt1 / 4); break;
+    case 46: hipLaunchKernelGGL((nfold_burst<2, 2>), dim3(g(n2 / 2)), dim3(256), 0, s, dvar[st], R, t2); break;
+    case 47: hipLaunchKernelGGL((nfold_burst<2, 4>), dim3(g(n2 / 4)), dim3(256), 0, s, dvar[st], R, t2); break;
+    case 48: hipLaunchKernelGGL((nfold_burst<4, 2>), dim3(g(n4 / 2)), dim3(256), 0, s, dvar[st], R, t4); break;
     case 50: hipLaunchKernelGGL((read_vgpr<4>), dim3(4096), dim3(256), 0, s, ca0, 2 * copy_n, dummy); break;
     case 51: hipLaunchKernelGGL((read_vgpr<8>), dim3(2048), dim3(256), 0, s, ca0, 2 * copy_n, dummy); break;
     case 52: hipLaunchKernelGGL(read_glds, dim3(2048), dim3(256), 0, s, ca0, 2 * copy_n, dummy); break;
@@ -270,11 +346,11 @@ int main(int argc, char **argv) {
     CHECK(hipStreamSynchronize(s));
     CHECK(hipMemcpy(want.data(), recvs[R - 1], S * 16, hipMemcpyDeviceToHost));
     for (const V &v : vs) {
-      if (v.id == 20 || v.id >= 40) continue;
+      if (v.id == 20 || v.id >= 50) continue;
       for (int r = 0; r < R; r++) CHECK(hipMemset(recvs[r], 0, S * 16));
       run(v, 0);
       CHECK(hipStreamSynchronize(s));
-      for (int r = 0; r < R; r++) {
+      for (int r = 0; r < (v.id >= 40 && v.id < 46 ? 1 : R); r++) {  // the local folds write rank 0's buffer only
         CHECK(hipMemcpy(got.data(), recvs[r], S * 16, hipMemcpyDeviceToHost));
         if (memcmp(got.data(), want.data(), S * 16)) printf("MISMATCH %s rank %d\n", v.name.c_str(), r);
       }
@@ -302,7 +378,7 @@ int main(int argc, char **argv) {
   for (V &v : vs) {
     std::sort(v.us.begin(), v.us.end());
     const float med = v.us[v.us.size() / 2];
-    const double bytes = v.id >= 50 ? 2.0 * copy_n * 16 : v.id >= 40 ? (R + 1.0) * S * 16 : 2.0 * R * S * 16;
+    const double bytes = v.id >= 50 ? 2.0 * copy_n * 16 : (v.id >= 40 && v.id < 46) ? (R + 1.0) * S * 16 : 2.0 * R * S * 16;
     printf("%-18s %9.2f %9.2f %9.2f  %6.3f TB/s  %.3f of 8\n", v.name.c_str(), med, v.us.front(), v.us.back(),
            bytes / med / 1e6, bytes / med / 1e6 / 8.0);
   }
