@@ -151,7 +151,7 @@ typedef struct {
    lease; U 2 47.1, U 4 46.2 on another), so no fixed threshold table picks it everywhere; one
    sample per candidate (round 3's first tuner) kept U 2 on a lease where U 4 was 2 % faster, hence
    the rounds. EXT_MPI_AMD_AUTOTUNE=0 keeps the static pick. */
-#define EMAC_TUNE_MAX 5
+#define EMAC_TUNE_MAX 6
 #define EMAC_TUNE_ROUNDS 3
 #define EMAC_TUNE_MIN_BYTES (16L << 20) /* algorithmic bytes per launch: smaller launches keep the static pick */
 typedef struct {
@@ -436,13 +436,15 @@ static int tune_candidates(const emac_handle *h, int *sched) {
   /* fold_kernel.hpp instantiation policy: (U 2, burst), (U 4, burst), for the node fan-out (U 4,
      s_sleep 2 every 4 loads); deferred stores (kDeferShift) when every bucket has the same tile
      count: (U 2, 4 tiles) and (U 4, 4 tiles) for one destination, (U 2, 4 tiles) and (U 4, 2
-     tiles) for the fan-out */
+     tiles) for the fan-out, and (U 2, 8 tiles) for it too (the best at 16 MiB per rank on one lease,
+     profiles/r03_nodevar/nodevar_2048.txt, and 7 % behind at 32 MiB) */
   sched[n++] = 2 | 1 << 4;
   sched[n++] = 4 | 1 << 4;
   if (h->fan) sched[n++] = 4 | 5 << 4;
   if (h->tiles_per_bucket > 0) {
     sched[n++] = 2 | (1 | 2 << 11) << 4;
     sched[n++] = 4 | (1 | (h->fan ? 1 : 2) << 11) << 4;
+    if (h->fan) sched[n++] = 2 | (1 | 3 << 11) << 4;
   }
   return n;
 }

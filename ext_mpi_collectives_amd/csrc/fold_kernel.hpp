@@ -622,7 +622,7 @@ __global__ __launch_bounds__(EMAC_BLOCK) void ipc_fused_kernel(Work fold, Work p
 // A launch schedule is encoded as U | ISSUE << 4 (sched). SUM, per fold-tree kind CH:
 // linear or compile-time chain (gpu.h EMAC_CHAINS), fan-out N (node form):
 //        N <= 8 -> (U 2, burst), (U 4, burst), (U 4, s_sleep 2 every 4 loads), (U 1, burst: host
-//        buffers), deferred stores (U 2, 4 tiles), (U 4, 2 tiles); N > 8 -> (U 1, burst)
+//        buffers), deferred stores (U 2, 4 tiles), (U 4, 2 tiles), (U 2, 8 tiles); N > 8 -> (U 1, burst)
 // linear or chain, fan-out 1 (comm form, one-chunk fold): N <= 8 -> U in {1, 2, 4}, burst, and
 //        deferred stores (U 2, 4 tiles), (U 4, 4 tiles); N > 8 -> U = 1
 // runtime-code tree (composite N, any chain), either fan-out: U = 4 / 2 / 1 for N <= 4 / <= 8 /
@@ -684,6 +684,7 @@ int launch_sum(int unroll, const Launch &L) {
     if (unroll == sched(2, 1)) return launch_one<T, OP, N, 2, CH, D, 1>(L);
     if (unroll == sched(2, 1 | defer(4))) return launch_one<T, OP, N, 2, CH, D, 1 | defer(4)>(L);
     if (unroll == sched(4, 1 | defer(2))) return launch_one<T, OP, N, 4, CH, D, 1 | defer(2)>(L);
+    if (unroll == sched(2, 1 | defer(8))) return launch_one<T, OP, N, 2, CH, D, 1 | defer(8)>(L);
     return EMAC_ERR_UNSUPPORTED;
   } else {
     if (unroll == sched(4, 1)) return launch_one<T, OP, N, 4, CH, D>(L);

@@ -387,7 +387,7 @@ def test_copy_reduce_headline_instance():
         assert np.array_equal(d.cpu().numpy().view(np.uint8), want.view(np.uint8))
     h = emac.fold_init([t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts], count, emac.FLOAT)
     seen = set()
-    for k in range(19):  # the static pick, 3 rounds of 5 timed candidates, then the kept one
+    for k in range(22):  # the static pick, 3 rounds of 6 timed candidates, then the kept one
         for d in dsts:
             d.fill_(-1.0)
         torch.cuda.synchronize()  # the fill runs on torch's stream, the fold on the handle's
@@ -410,10 +410,10 @@ DEFER_SHIFT = 11  # fold_kernel.hpp kDeferShift: deferred-store schedules (issue
 def test_every_tuned_schedule_bitwise(oracle, code, copyin):
     """The per-handle schedule tuner (engine.c emac_tune) runs every candidate on a handle's first
     Starts -- burst loads at U 2 / U 4, the staggered issue, and the deferred-store schedules
-    (fold_kernel.hpp fold_deferred: 4 or 2 tiles folded into LDS, then stored in one burst) -- and
+    (fold_kernel.hpp fold_deferred: 2, 4 or 8 tiles folded into LDS, then stored in one burst) -- and
     keeps one. Every Start must give the oracle's bits: here a node form whose buckets end in a
     partial tile and whose last group of tiles is short (41000 elements per chunk), and a local
-    fold (8 leaves -> 1, fold_init) of 512040 elements, each over 19 Starts."""
+    fold (8 leaves -> 1, fold_init) of 512040 elements, each over all the Starts of its tuning."""
     R, chunk = 8, 41000 if code == emac.FLOAT else 20500
     count = R * chunk
     sends = xorshift_inputs(R, count, code, seed_base=0x7E57)
@@ -423,7 +423,7 @@ def test_every_tuned_schedule_bitwise(oracle, code, copyin):
     h = emac.node_allreduce_init([t.data_ptr() for t in dsend], [t.data_ptr() for t in drecv], count, code, copyin)
     seen = set()
     try:
-        for k in range(19):
+        for k in range(22):
             for t in drecv:
                 t.fill_(-1)
             torch.cuda.synchronize()

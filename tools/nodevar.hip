@@ -299,6 +299,8 @@ int main(int argc, char **argv) {
       {"local_burst_u2_k8_g512", 44, 512, {}}, {"local_burst_u4_k4_g512", 45, 512, {}},
       {"node_burst_u2_k2", 46, 0, {}}, {"node_burst_u2_k4", 47, 0, {}}, {"node_burst_u2_k2_g512", 46, 512, {}},
       {"node_burst_u2_k4_g512", 47, 512, {}}, {"node_burst_u4_k2", 48, 0, {}}, {"node_burst_u2_k4_g256", 47, 256, {}},
+      {"node_burst_u2_k8", 60, 0, {}}, {"node_burst_u4_k4", 61, 0, {}}, {"node_burst_u1_k8", 62, 0, {}},
+      {"local_burst_u2_k16", 63, 0, {}}, {"local_burst_u4_k8", 64, 0, {}},
       {"read_vgpr_k4", 50, 0, {}},     {"read_vgpr_k8", 51, 0, {}},    {"read_glds", 52, 0, {}}};
   auto run = [&](const V &v, int i) {
     const int st = i % nsets;
@@ -335,6 +337,11 @@ int main(int argc, char **argv) {
     case 46: hipLaunchKernelGGL((nfold_burst<2, 2>), dim3(g(n2 / 2)), dim3(256), 0, s, dvar[st], R, t2); break;
     case 47: hipLaunchKernelGGL((nfold_burst<2, 4>), dim3(g(n2 / 4)), dim3(256), 0, s, dvar[st], R, t2); break;
     case 48: hipLaunchKernelGGL((nfold_burst<4, 2>), dim3(g(n4 / 2)), dim3(256), 0, s, dvar[st], R, t4); break;
+    case 60: hipLaunchKernelGGL((nfold_burst<2, 8>), dim3(g(n2 / 8)), dim3(256), 0, s, dvar[st], R, t2); break;
+    case 61: hipLaunchKernelGGL((nfold_burst<4, 4>), dim3(g(n4 / 4)), dim3(256), 0, s, dvar[st], R, t4); break;
+    case 62: hipLaunchKernelGGL((nfold_burst<1, 8>), dim3(g(n2 * 2 / 8)), dim3(256), 0, s, dvar[st], R, t2 * 2); break;
+    case 63: hipLaunchKernelGGL((lfold_burst<2, 16>), dim3(g(lt1 / 32)), dim3(256), 0, s, dloc[st], lt1 / 2); break;
+    case 64: hipLaunchKernelGGL((lfold_burst<4, 8>), dim3(g(lt1 / 32)), dim3(256), 0, s, dloc[st], lt1 / 4); break;
     case 50: hipLaunchKernelGGL((read_vgpr<4>), dim3(4096), dim3(256), 0, s, ca0, 2 * copy_n, dummy); break;
     case 51: hipLaunchKernelGGL((read_vgpr<8>), dim3(2048), dim3(256), 0, s, ca0, 2 * copy_n, dummy); break;
     case 52: hipLaunchKernelGGL(read_glds, dim3(2048), dim3(256), 0, s, ca0, 2 * copy_n, dummy); break;
@@ -346,11 +353,11 @@ int main(int argc, char **argv) {
     CHECK(hipStreamSynchronize(s));
     CHECK(hipMemcpy(want.data(), recvs[R - 1], S * 16, hipMemcpyDeviceToHost));
     for (const V &v : vs) {
-      if (v.id == 20 || v.id >= 50) continue;
+      if (v.id == 20 || (v.id >= 50 && v.id < 60)) continue;
       for (int r = 0; r < R; r++) CHECK(hipMemset(recvs[r], 0, S * 16));
       run(v, 0);
       CHECK(hipStreamSynchronize(s));
-      for (int r = 0; r < (v.id >= 40 && v.id < 46 ? 1 : R); r++) {  // the local folds write rank 0's buffer only
+      for (int r = 0; r < ((v.id >= 40 && v.id < 46) || v.id >= 63 ? 1 : R); r++) {  // the local folds write rank 0's buffer only
         CHECK(hipMemcpy(got.data(), recvs[r], S * 16, hipMemcpyDeviceToHost));
         if (memcmp(got.data(), want.data(), S * 16)) printf("MISMATCH %s rank %d\n", v.name.c_str(), r);
       }
@@ -378,7 +385,8 @@ int main(int argc, char **argv) {
   for (V &v : vs) {
     std::sort(v.us.begin(), v.us.end());
     const float med = v.us[v.us.size() / 2];
-    const double bytes = v.id >= 50 ? 2.0 * copy_n * 16 : (v.id >= 40 && v.id < 46) ? (R + 1.0) * S * 16 : 2.0 * R * S * 16;
+    const bool local = (v.id >= 40 && v.id < 46) || v.id >= 63, rd = v.id >= 50 && v.id < 60;
+    const double bytes = rd ? 2.0 * copy_n * 16 : local ? (R + 1.0) * S * 16 : 2.0 * R * S * 16;
     printf("%-18s %9.2f %9.2f %9.2f  %6.3f TB/s  %.3f of 8\n", v.name.c_str(), med, v.us.front(), v.us.back(),
            bytes / med / 1e6, bytes / med / 1e6 / 8.0);
   }
