@@ -555,9 +555,15 @@ static int fold_launch(emac_handle *h) {
         t->L[k].d_edges = h->d_edges;
       }
       t->chosen = best;
-      if (getenv("EXT_MPI_AMD_DEBUG_TUNE"))
-        fprintf(stderr, "ext_mpi_amd: fold schedule kept: U %d issue %d (%.1f us; %d candidates)\n", h->unroll & 15,
-                h->unroll >> 4, t->us[best], t->n);
+      if (getenv("EXT_MPI_AMD_DEBUG_TUNE")) {
+        char line[256];
+        int at = 0;
+        for (k = 0; k < t->n && at < (int)sizeof(line) - 32; k++)
+          at += snprintf(line + at, sizeof(line) - (size_t)at, " U%d/%d %.1f", t->L[k].unroll & 15, t->L[k].unroll >> 4,
+                         t->us[k]);
+        fprintf(stderr, "ext_mpi_amd: fold schedule kept: U %d issue %d (%.1f us; %d candidates:%s)\n", h->unroll & 15,
+                h->unroll >> 4, t->us[best], t->n, line);
+      }
     }
   }
   return emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, h->fan, h->unroll, &h->plan.codes, h->d_buckets, h->nb, h->ntiles,
