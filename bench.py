@@ -843,28 +843,47 @@ def _node_form_run(emac, comm, R, count, tdtype, code, copyin, steps, warmup, ra
 
 
 def node_child(args, emac, rank, world, dev, dist, torch):
-    """--child-transport node: the N > 1 headline (see _node_form_run) on an RCCL communicator of
-    one member per GPU, nodes joined by one inter-node step of radix N (EXT_MPI_NUM_PORTS
-    '-(N-1) (N-1)': every GPU trades with all N - 1 others at once, one xGMI link each)."""
+    """--child-transport node: the N > 1 headline (see _node_form_run), the nodes joined by one
+    inter-node step of radix N (EXT_MPI_NUM_PORTS '-(N-1) (N-1)': every GPU trades with all N - 1
+    others at once, one xGMI link each), first over a peer-mapped communicator (engine.c
+    node_ipc_init: the nodes' partials read in place over xGMI), then over RCCL (the node legs as
+    point-to-point groups). Every rank agrees on each transport's outcome before the next; the
+    headline is the peer-mapped one when it ran and checked, the other is reported beside it."""
     tdtype, code, dname, tsize = dtype_info(args.dtype)
     R = args.ranks
     count = int(args.size_mib * MIB) // tsize
     copyin = f"6;1 -{R} {R}"  # the node's own split (configs[1]); --copyin is the one-rank-per-GPU runs'
     ports = [-(world - 1), world - 1] if world > 1 else []
-    uid = [emac.get_unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(uid, src=0)
-    comm = emac.comm_init(rank, world, uid[0], dev)
-    try:
-        if world > 1:
-            emac.comm_set_nodes(comm, world, ports)
-        res = _node_form_run(emac, comm, R, count, tdtype, code, copyin, args.steps, args.warmup, rank, world, dist,
-                             torch)
-        log(f"rank {rank}: node form over {world} GPUs: {args.steps} steps in {res['wall'] * 1e3:.3f} ms, "
-            f"checked {res['checked']}")
-        res.update(ranks_per_gpu=R, copyin=copyin, ports=ports, bytes_per_rank=count * tsize)
-        return res
-    finally:
-        emac.comm_free(comm)
+    out = {}
+    for transport in ("ipc", "rccl"):
+        comm, res = None, None
+        try:
+            if transport == "ipc":
+                comm = emac.comm_init_ipc(rank, world, emac.torch_allgather(), dev)
+            else:
+                uid = [emac.get_unique_id() if rank == 0 else None]
+                dist.broadcast_object_list(uid, src=0)
+                comm = emac.comm_init(rank, world, uid[0], dev)
+            if world > 1:
+                emac.comm_set_nodes(comm, world, ports)
+            res = _node_form_run(emac, comm, R, count, tdtype, code, copyin, args.steps, args.warmup, rank, world, dist,
+                                 torch)
+            log(f"rank {rank}: node form over {world} GPUs ({transport}): {args.steps} steps in "
+                f"{res['wall'] * 1e3:.3f} ms, checked {res['checked']}")
+            res.update(ranks_per_gpu=R, copyin=copyin, ports=ports, bytes_per_rank=count * tsize, transport=transport)
+        except Exception as e:  # noqa: BLE001 -- every rank reports and agrees below
+            log(f"rank {rank}: node form over {world} GPUs ({transport}) failed: {e}")
+            res = {"error": str(e)[:200]}
+        finally:
+            if comm is not None:
+                try:
+                    emac.comm_free(comm)
+                except Exception:  # noqa: BLE001
+                    pass
+        ok = torch.tensor([int("wall" in res)])
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        out[transport] = res if ok.item() else (res if "error" in res else {"error": "failed on another rank"})
+    return out
 
 
 def transport_child(args):
@@ -890,6 +909,14 @@ def transport_child(args):
     log(f"rank {rank}: {transport} child on GPU {dev}: communicator set-up")
     if transport == "node":
         res = node_child(args, emac, rank, world, dev, dist, torch)
+        head = next((res[t] for t in ("ipc", "rccl") if "wall" in res[t] and res[t].get("checked")), None)
+        res = dict(head or {"error": "; ".join(f"{t}: {r.get('error', 'unchecked')}" for t, r in res.items())},
+                   transports={t: ({"ms_per_step": round(r["wall"] * 1e3 / args.steps, 4), "checked": r["checked"],
+                                    "parts_us": {k: round(r[k] * 1e6, 2) for k in ("copy_in_fold_s", "node_legs_s",
+                                                                                  "copy_out_s")}}
+                                   if "wall" in r else r) for t, r in res.items()})
+        if head is None:
+            res["checked"] = False
         with open(args.child_result, "w") as f:
             json.dump(res, f)
         dist.barrier()
@@ -1151,7 +1178,7 @@ def multi_gpu(args):
 
 def node_form_line(args, world, dname, rn, one_rank_per_gpu):
     """The N > 1 JSON line: configs[1]'s node on each of the N GPUs (weak scaling of the N = 1
-    workload), the nodes joined over RCCL/xGMI. value = bytes reduced by the whole job per second
+    workload), the nodes joined over xGMI (peer-mapped, else RCCL). value = bytes reduced by the whole job per second
     (N GPUs x R ranks x S bytes per Start); roofline = the node's copy-in fold (R leaves -> the
     owner chunks, this GPU's HBM) timed on every GPU at once inside the job."""
     R, S, steps = rn["ranks_per_gpu"], rn["bytes_per_rank"], args.steps
@@ -1162,9 +1189,15 @@ def node_form_line(args, world, dname, rn, one_rank_per_gpu):
     xb = 2 * (world - 1) / world * S  # the node partial crosses xGMI out and back (reduce-scatter + allgather)
     xgmi_bound = xb / (min(world - 1, 7) * 153e9)
     extras = {
-        "form": "NODE form over nodes (ext_mpi_amd_node_comm_allreduce_init): per GPU one node of R ranks; "
-                "copy-in fold of the node in place, the inter-node legs of every node rank as one RCCL group per "
-                "leg (EXT_MPI_NUM_PORTS one step of radix N), the copy-out fan-out",
+        "form": ("NODE form over peer-mapped nodes (ext_mpi_amd_node_comm_allreduce_init on an IPC communicator): "
+                 "per GPU one node of R ranks; copy-in fold into the node's partial block, barrier, fold of this "
+                 "node's share of every chunk over the N partials read in place over xGMI (EXT_MPI_NUM_PORTS one "
+                 "step of radix N), barrier, pull of every share, the copy-out fan-out"
+                 if rn.get("transport") == "ipc" else
+                 "NODE form over nodes (ext_mpi_amd_node_comm_allreduce_init): per GPU one node of R ranks; "
+                 "copy-in fold of the node in place, the inter-node legs of every node rank as one RCCL group per "
+                 "leg (EXT_MPI_NUM_PORTS one step of radix N), the copy-out fan-out"),
+        "node_transports": rn.get("transports"),
         "parts_us": {"copy_in_fold": round(t_in * 1e6, 2), "node_legs_xgmi": round(t_x * 1e6, 2),
                      "copy_out": round(t_out * 1e6, 2), "sum": round((t_in + t_x + t_out) * 1e6, 2),
                      "start_to_wait": round(wall * 1e6 / steps, 2)},
@@ -1186,10 +1219,11 @@ def node_form_line(args, world, dname, rn, one_rank_per_gpu):
         "config": {"workload": f"persistent Allreduce {args.dtype} MPI_SUM over {world} x {R} ranks: BASELINE "
                                f"configs[1]'s node ({R} ranks x {S // MIB} MiB resident in one MI355X, "
                                f"EXT_MPI_COPYIN '{rn['copyin']}') on each of {world} GPUs, the GPUs joined as "
-                               f"nodes over RCCL/xGMI (EXT_MPI_NUM_PORTS {rn['ports']}); value = bytes reduced by "
+                               f"nodes over xGMI ({'peer-mapped' if rn.get('transport') == 'ipc' else 'RCCL'}, "
+                               f"EXT_MPI_NUM_PORTS {rn['ports']}); value = bytes reduced by "
                                f"the whole job per second ({world} x {R} x {S // MIB} MiB per step)",
                    "ranks": world * R, "ranks_per_gpu": R, "message_bytes_per_rank": S, "copyin": rn["copyin"],
-                   "node_ports": rn["ports"], "layout": "node-per-gpu", "transport": "rccl",
+                   "node_ports": rn["ports"], "layout": "node-per-gpu", "transport": rn.get("transport", "rccl"),
                    "checked_vs_fp64_sum": rn["checked"]},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,

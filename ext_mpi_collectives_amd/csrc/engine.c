@@ -233,6 +233,9 @@ typedef struct {
   int hier;
   long stage_stride;    /* staging bytes of each node rank's node legs */
   emac_launch fanout;   /* the copy-out: every owner chunk into the node's other receive buffers */
+  /* ... over peer-mapped nodes (node_ipc_init): this node's partials (arena, read by the peers) */
+  void *part;
+  size_t part_bytes;
 } emac_handle;
 
 static emac_handle *handles[MAX_HANDLES];
@@ -309,6 +312,7 @@ static void release(emac_handle *h) {
   }
   for (r = 0; r < h->nmapped; r++) ipc_unmap(h->mapped[r]);
   if (h->outbox) arena_release(&comms[h->comm], h->outbox, (long)h->outbox_bytes);
+  if (h->part) arena_release(&comms[h->comm], h->part, (long)h->part_bytes);
   emac_gpu_event_destroy(h->ev_release);
   for (r = 0; r <= EXT_MPI_AMD_LEG_ALL; r++) emac_gpu_graph_destroy(h->graph[r]);
   if (h->kind == KIND_IPC && h->slot_held) {
@@ -1795,6 +1799,224 @@ static char *leg_base(const emac_handle *h, int buf) { return leg_base_of(h, buf
 
 /* ------------------------- NODE form over several nodes ------------------------- */
 
+/* The node's copy-out (its allgather): every owner chunk, from its owner's receive buffer, stored
+   into the R - 1 other receive buffers (one emac_gpu_copy_fan launch). `b`: scratch of npieces * R
+   buckets. */
+static int build_node_fanout(emac_handle *h, emac_bucket *b) {
+  const int R = h->plan.nranks;
+  emac_edge *edges = NULL;
+  emac_launch *F = &h->fanout;
+  int nfb = 0, pc, c, r, rc;
+  if (R < 2) return 0;
+  for (pc = 0; pc < h->plan.npieces; pc++)
+    for (c = 0; c < R; c++) {
+      const long off = h->plan.chunk_off[(size_t)pc * R + c], len = h->plan.chunk_len[(size_t)pc * R + c];
+      const int owner = h->plan.pos_rank[c];
+      emac_bucket *bk = &b[nfb];
+      if (len <= 0) continue;
+      memset(bk, 0, sizeof(*bk));
+      bk->src[0] = h->drecv[owner];
+      for (r = 0; r < R; r++)
+        if (r != owner) bk->dst[bk->ndst++] = h->drecv[r];
+      place_bucket(bk, 1, off, len, h->plan.tsize);
+      nfb++;
+    }
+  if ((rc = emac_layout(b, nfb, EMAC_SUM, 1, 0, 0, &edges, &F->nedges, &F->ntiles, &F->tiles_per_bucket, &F->all_full,
+                        &F->unroll)))
+    return rc;
+  F->nb = nfb;
+  if (nfb && (rc = emac_gpu_malloc((void **)&F->d_buckets, sizeof(emac_bucket) * (size_t)nfb)) == 0)
+    rc = emac_gpu_memcpy(F->d_buckets, b, sizeof(emac_bucket) * (size_t)nfb);
+  if (!rc && F->nedges && (rc = emac_gpu_malloc((void **)&F->d_edges, sizeof(emac_edge) * (size_t)F->nedges)) == 0)
+    rc = emac_gpu_memcpy(F->d_edges, edges, sizeof(emac_edge) * (size_t)F->nedges);
+  free(edges);
+  return rc;
+}
+
+/* a launch of `nsrc`-leaf buckets under the schedule of fan-out form `fan` (2: peer-mapped) */
+static int upload_launch_fan(const emac_handle *h, emac_launch *L, emac_bucket *b, int nb, int nsrc, int fan) {
+  emac_edge *edges = NULL;
+  int rc;
+  if ((rc = emac_layout(b, nb, nsrc > 1 ? h->plan.op : EMAC_SUM, nsrc, 0, fan, &edges, &L->nedges, &L->ntiles,
+                        &L->tiles_per_bucket, &L->all_full, &L->unroll)))
+    return rc;
+  L->nb = nb;
+  if (nb && (rc = emac_gpu_malloc((void **)&L->d_buckets, sizeof(emac_bucket) * (size_t)nb)) == 0)
+    rc = emac_gpu_memcpy(L->d_buckets, b, sizeof(emac_bucket) * (size_t)nb);
+  if (!rc && L->nedges && (rc = emac_gpu_malloc((void **)&L->d_edges, sizeof(emac_edge) * (size_t)L->nedges)) == 0)
+    rc = emac_gpu_memcpy(L->d_edges, edges, sizeof(emac_edge) * (size_t)L->nedges);
+  free(edges);
+  return rc;
+}
+
+/* The NODE form over peer-mapped nodes: node_comm_allreduce_init on an ext_mpi_amd_comm_init_ipc
+   communicator -- one process per GPU, each member a node of R ranks whose buffers all live on
+   its GPU. The inter-node schedule must be one reduce-scatter step over every node (EXT_MPI_NUM_PORTS
+   'N(-(N-1) (N-1))', the default for a node count that is not a power of two), or two nodes at one
+   port for SUM (emac_node_single): every element's value is then ONE fold of the N node partials
+   in its line's order, whoever computes it (plan.c emac_node_shares), so the inter-node legs become
+   peer loads instead of point-to-point lines. A Start runs
+    1. the node's copy-in: every owner chunk folded over the node's send buffers, in the plan's leaf
+       order, into this node's partial block (arena memory the peers map; fold_launch, tuned);
+    2. barrier(in); the fold of this node's share of every node rank's chunk: the N nodes' partials
+       read in place (system-coherent loads over xGMI), in the line's order, into this node's outbox
+       (arena); barrier(out) -- the IPC form's protocol (ipc_sync.hpp, epochs, timeout recovery);
+    3. the pull: every node's share (this node's own too) from its outbox into the chunk owner's
+       receive buffer, owners after this node first;
+    4. the copy-out: every owner chunk into the node's other receive buffers (emac_gpu_copy_fan).
+   No caller memory is exported -- the peers read only the two arena blocks -- so the handle's Done
+   is local. Collective over the communicator (the exchanges run whatever failed locally). */
+static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
+  typedef struct {
+    long lack;
+    int status;
+    int seg[2];
+    long offset[2];
+    unsigned char free_slots[EMAC_SYNC_SLOTS / 8];
+  } nx_export;
+  nx_export mine, all[EMAC_MAX_RANKS];
+  void *peer_part[EMAC_MAX_RANKS], *peer_out[EMAC_MAX_RANKS];
+  emac_share *sh[EMAC_MAX_RANKS] = {0};
+  int nsh[EMAC_MAX_RANKS] = {0};
+  emac_bucket *b = NULL;
+  const int N = cm->size, R = h->plan.nranks;
+  const long ts = h->plan.tsize;
+  int attempt, r, k, me, i, slot, nb, pc;
+  h->part_bytes = h->outbox_bytes = h->bytes > 16 ? h->bytes : 16;
+  for (attempt = 0;; attempt++) {
+    long lack = 0;
+    int grow = 0;
+    if (!rc && !h->part && arena_alloc(cm, (long)h->part_bytes, &h->part))
+      lack += (long)(h->part_bytes + EMAC_ARENA_ALIGN - 1) / EMAC_ARENA_ALIGN * EMAC_ARENA_ALIGN;
+    if (!rc && !h->outbox && arena_alloc(cm, (long)h->outbox_bytes, &h->outbox))
+      lack += (long)(h->outbox_bytes + EMAC_ARENA_ALIGN - 1) / EMAC_ARENA_ALIGN * EMAC_ARENA_ALIGN;
+    memset(&mine, 0, sizeof(mine));
+    for (k = 0; !rc && !lack && k < 2; k++) {
+      void *p = k ? h->outbox : h->part;
+      int sg;
+      if (!arena_owns(cm, p, &sg)) {
+        rc = EMAC_ERR_ARG;
+      } else {
+        mine.seg[k] = sg;
+        mine.offset[k] = (long)((char *)p - (char *)cm->seg[sg].base);
+      }
+    }
+    mine.lack = rc ? 0 : lack;
+    mine.status = rc == 0;
+    for (r = 0; r < EMAC_SYNC_SLOTS; r++)
+      if (!cm->slot_used[r]) mine.free_slots[r >> 3] |= (unsigned char)(1u << (r & 7));
+    if (cm->ag(cm->ag_ctx, &mine, all, (long)sizeof(mine))) return EMAC_ERR_TRANSPORT;
+    for (r = 0; r < N; r++) {
+      if (!all[r].status && !rc) rc = EMAC_ERR_TRANSPORT;
+      if (all[r].lack > 0) grow = 1;
+    }
+    if (rc) return rc; /* the same verdict on every rank */
+    if (!grow) break;
+    if (attempt == EMAC_IPC_ATTEMPTS - 1) return EMAC_ERR_MALLOC;
+    if ((rc = arena_grow(cm, 0, lack))) return rc;
+  }
+  for (r = 0; r < N; r++) {
+    if (r == cm->rank) {
+      peer_part[r] = h->part;
+      peer_out[r] = h->outbox;
+      continue;
+    }
+    peer_part[r] = all[r].seg[0] < cm->peer_nseg[r] ? (char *)cm->peer_seg[r][all[r].seg[0]] + all[r].offset[0] : NULL;
+    peer_out[r] = all[r].seg[1] < cm->peer_nseg[r] ? (char *)cm->peer_seg[r][all[r].seg[1]] + all[r].offset[1] : NULL;
+    if (!peer_part[r] || !peer_out[r]) rc = EMAC_ERR_TRANSPORT;
+  }
+  if ((rc = ipc_agree(cm, rc == 0))) return rc;
+  for (slot = 0; slot < EMAC_SYNC_SLOTS; slot++) { /* the lowest slot free on every rank */
+    for (r = 0; r < N && (all[r].free_slots[slot >> 3] >> (slot & 7)) & 1; r++);
+    if (r == N) break;
+  }
+  if (slot == EMAC_SYNC_SLOTS) return EMAC_ERR_MALLOC; /* the same verdict on every rank */
+  h->slot = slot;
+  cm->slot_used[slot] = 1;
+  h->slot_held = 1;
+  cm->err[slot] = 0;
+  {
+    const char *e = getenv("EXT_MPI_AMD_IPC_RELEASE"); /* as ipc_allreduce_init */
+    const int rel = e ? atoi(e) > 0 : cm->cross_device;
+    if (N > 1 && rel && (rc = emac_gpu_event_create_release(&h->ev_release))) return rc;
+  }
+  h->epoch[0] = cm->slot_epoch[slot][0];
+  h->epoch[1] = cm->slot_epoch[slot][1];
+  /* the parts of every node rank's chunk (plan.c emac_node_shares; one node: the chunk itself) */
+  for (me = 0; me < R && !rc; me++) {
+    if (N > 1) {
+      rc = emac_node_shares(&h->plan, &h->ns, me, &sh[me], &nsh[me]);
+    } else if (!(sh[me] = (emac_share *)calloc((size_t)h->plan.npieces + 1, sizeof(emac_share)))) {
+      rc = EMAC_ERR_MALLOC;
+    } else {
+      for (pc = 0; pc < h->plan.npieces; pc++) {
+        emac_share *x = &sh[me][nsh[me]++];
+        x->off = h->plan.chunk_off[(size_t)pc * R + h->plan.rank_pos[me]];
+        x->len = h->plan.chunk_len[(size_t)pc * R + h->plan.rank_pos[me]];
+        x->node = 0;
+        x->nleaf = 1;
+      }
+    }
+  }
+  for (me = 0, k = 0; me < R; me++) k += nsh[me];
+  if (!rc && !(b = (emac_bucket *)calloc((size_t)(k + h->plan.npieces * R) + 1, sizeof(emac_bucket)))) rc = EMAC_ERR_MALLOC;
+  /* 1. the copy-in: every owner chunk into this node's partial block (at its message offset) */
+  for (nb = 0, pc = 0; !rc && pc < h->plan.npieces; pc++)
+    for (i = 0; i < R; i++) {
+      const long off = h->plan.chunk_off[(size_t)pc * R + i], len = h->plan.chunk_len[(size_t)pc * R + i];
+      emac_bucket *bk = &b[nb];
+      int t;
+      if (len <= 0) continue;
+      memset(bk, 0, sizeof(*bk));
+      for (t = 0; t < R; t++) bk->src[t] = h->dsend[h->plan.leaf_rank[i][t]];
+      bk->dst[0] = h->part;
+      bk->ndst = 1;
+      place_bucket(bk, R, off, len, ts);
+      nb++;
+    }
+  h->nsrc = R;
+  h->fan = 0;
+  if (!rc) rc = upload_buckets(h, b, nb);
+  /* 2. this node's shares: the N partials in place, in the line's order, into the outbox */
+  for (nb = 0, me = 0; !rc && me < R; me++)
+    for (i = 0; i < nsh[me]; i++) {
+      const emac_share *x = &sh[me][i];
+      emac_bucket *bk = &b[nb];
+      int l;
+      if (x->node != cm->rank || x->len <= 0) continue;
+      memset(bk, 0, sizeof(*bk));
+      for (l = 0; l < x->nleaf; l++) bk->src[l] = peer_part[x->leaf_node[l]];
+      bk->dst[0] = h->outbox;
+      bk->ndst = 1;
+      place_bucket(bk, x->nleaf, x->off, x->len, ts);
+      nb++;
+    }
+  if (!rc) rc = upload_launch_fan(h, &h->xfold[0], b, nb, N, 2);
+  /* 3. the pull: every share from its node's outbox into the chunk owner's receive buffer, the
+     nodes after this one first (their loads head for different GPUs' links), this node's last */
+  for (nb = 0, k = 1; !rc && k <= N; k++) {
+    const int q = (cm->rank + k) % N;
+    for (me = 0; me < R; me++)
+      for (i = 0; i < nsh[me]; i++) {
+        const emac_share *x = &sh[me][i];
+        emac_bucket *bk = &b[nb];
+        if (x->node != q || x->len <= 0) continue;
+        memset(bk, 0, sizeof(*bk));
+        bk->src[0] = peer_out[q];
+        bk->dst[0] = h->drecv[me];
+        bk->ndst = 1;
+        place_bucket(bk, 1, x->off, x->len, ts);
+        nb++;
+      }
+  }
+  if (!rc) rc = upload_launch_fan(h, &h->pull, b, nb, 1, 2);
+  /* 4. the copy-out */
+  if (!rc) rc = build_node_fanout(h, b);
+  for (me = 0; me < R; me++) free(sh[me]);
+  free(b);
+  return rc;
+}
+
 /* Every rank of this node in this process (the NODE form: all their buffers on this GPU), the
    nodes joined by `comm`, whose members are the nodes (RCCL, or loopback for testing), under the
    communicator's inter-node schedule (ext_mpi_amd_comm_set_node_ports with nodes == its size;
@@ -1830,7 +2052,6 @@ int ext_mpi_amd_node_comm_allreduce_init(int nranks, const void *const *sendbufs
     return EMAC_ERR_ARG;
   *handle = -1;
   cm = &comms[comm];
-  if (cm->ipc) return EMAC_ERR_UNSUPPORTED;                      /* RCCL or loopback members */
   if (cm->nodes > 1 && cm->nodes != cm->size) return EMAC_ERR_ARG; /* the members are the nodes */
   if ((rc = parse_cfg(copyin, R, &cfg))) return rc;
   if (emac_gpu_set_device(cm->device)) return EMAC_ERR_DEVICE;
@@ -1851,6 +2072,16 @@ int ext_mpi_amd_node_comm_allreduce_init(int nranks, const void *const *sendbufs
   h->nbuf = R;
   h->nsrc = R;
   h->fan = 0;
+  if (cm->ipc) { /* peer-mapped nodes: collective from here on, whatever fails locally */
+    const int single = h->nodes > 1 ? emac_node_single(&h->ns) : 1;
+    if (!single || (single == 2 && op != EMAC_SUM)) rc = EMAC_ERR_UNSUPPORTED; /* (the same on every rank) */
+    for (r = 0; r < R && !rc; r++) rc = map_buffers(h, r, sendbufs[r], recvbufs[r]); /* local: device mirrors */
+    h->kind = KIND_IPC;
+    if ((rc = node_ipc_init(h, cm, rc))) goto fail;
+    if ((rc = emac_gpu_stream_create(&h->stream))) goto fail;
+    if ((rc = finish_init(h, handle))) goto fail;
+    return 0;
+  }
   for (r = 0; r < R; r++)
     if ((rc = map_buffers(h, r, sendbufs[r], recvbufs[r]))) goto fail;
   /* 1. the copy-in: owner chunk (piece pc, position c) into its owner's receive buffer */
@@ -1873,34 +2104,7 @@ int ext_mpi_amd_node_comm_allreduce_init(int nranks, const void *const *sendbufs
     }
   if ((rc = upload_buckets(h, b, nb))) goto fail;
   /* 3. the copy-out: owner chunk into the R - 1 other receive buffers */
-  if (R > 1) {
-    emac_edge *edges = NULL;
-    int nfb = 0;
-    for (pc = 0; pc < h->plan.npieces; pc++)
-      for (c = 0; c < R; c++) {
-        const long off = h->plan.chunk_off[(size_t)pc * R + c], len = h->plan.chunk_len[(size_t)pc * R + c];
-        const int owner = h->plan.pos_rank[c];
-        emac_bucket *bk = &b[nfb];
-        if (len <= 0) continue;
-        memset(bk, 0, sizeof(*bk));
-        bk->src[0] = h->drecv[owner];
-        for (r = 0; r < R; r++)
-          if (r != owner) bk->dst[bk->ndst++] = h->drecv[r];
-        place_bucket(bk, 1, off, len, h->plan.tsize);
-        nfb++;
-      }
-    emac_launch *F = &h->fanout;
-    if ((rc = emac_layout(b, nfb, EMAC_SUM, 1, 0, 0, &edges, &F->nedges, &F->ntiles, &F->tiles_per_bucket,
-                          &F->all_full, &F->unroll)))
-      goto fail;
-    F->nb = nfb;
-    if (nfb && (rc = emac_gpu_malloc((void **)&F->d_buckets, sizeof(emac_bucket) * (size_t)nfb)) == 0)
-      rc = emac_gpu_memcpy(F->d_buckets, b, sizeof(emac_bucket) * (size_t)nfb);
-    if (!rc && F->nedges && (rc = emac_gpu_malloc((void **)&F->d_edges, sizeof(emac_edge) * (size_t)F->nedges)) == 0)
-      rc = emac_gpu_memcpy(F->d_edges, edges, sizeof(emac_edge) * (size_t)F->nedges);
-    free(edges);
-    if (rc) goto fail;
-  }
+  if ((rc = build_node_fanout(h, b))) goto fail;
   /* 2. the node legs of every node rank: their programs, the peers turned into members */
   nsteps = h->nodes > 1 ? h->ns.nsteps + h->ns.nred : 0;
   for (me = 0; me < R && h->nodes > 1; me++) {
@@ -2139,6 +2343,39 @@ static int enqueue_legs(emac_handle *h, int legs) {
   const int core = EXT_MPI_AMD_LEG_REDUCE_SCATTER | EXT_MPI_AMD_LEG_FOLD | EXT_MPI_AMD_LEG_ALLGATHER;
   multi = h->kind == KIND_COMM && h->plan.nranks > 1 && !h->hier; /* the node's own p2p legs */
   if ((legs & EXT_MPI_AMD_LEG_STAGE_IN) && (rc = stage_in(h))) return rc;
+  if (h->kind == KIND_IPC && h->hier) { /* the NODE form over peer-mapped nodes (node_ipc_init) */
+    const int nodes = comms[h->comm].size;
+    if ((legs & EXT_MPI_AMD_LEG_FOLD) && (rc = fold_launch(h))) return rc; /* the copy-in */
+    if (legs & (EXT_MPI_AMD_LEG_NODES_RS | EXT_MPI_AMD_LEG_NODES_FOLD | EXT_MPI_AMD_LEG_NODES_AG)) {
+      static const emac_codes copy = {{1}, {1}, 1, 1}; /* one leaf: a copy */
+      const emac_launch *X = &h->xfold[0];
+      emac_codes lin;
+      memset(&lin, 0, sizeof(lin));
+      lin.first[0] = 1; /* one level: a left fold of the nodes' partials in the line's order */
+      lin.close[nodes - 1] = 1;
+      lin.nlev = 1;
+      lin.nleaf = nodes;
+      if ((rc = ipc_barrier(h, 0))) return rc;
+      if ((X->nb || X->nedges) &&
+          (rc = emac_gpu_fold_remote(h->plan.dtype, nodes > 1 ? h->plan.op : EMAC_SUM, nodes, X->unroll, &lin,
+                                     X->d_buckets, X->nb, X->ntiles, X->tiles_per_bucket, X->all_full, X->d_edges,
+                                     X->nedges, ipc_go(h), h->stream)))
+        return rc;
+      if ((rc = ipc_barrier(h, 1))) return rc;
+      if ((h->pull.nb || h->pull.nedges) &&
+          (rc = emac_gpu_fold_remote(h->plan.dtype, EMAC_SUM, 1, h->pull.unroll, &copy, h->pull.d_buckets, h->pull.nb,
+                                     h->pull.ntiles, h->pull.tiles_per_bucket, h->pull.all_full, h->pull.d_edges,
+                                     h->pull.nedges, ipc_go(h), h->stream)))
+        return rc;
+    }
+    if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && h->fanout.nb &&
+        (rc = emac_gpu_copy_fan(h->plan.tsize, h->plan.nranks - 1, h->fanout.unroll, h->fanout.d_buckets, h->fanout.nb,
+                                h->fanout.ntiles, h->fanout.tiles_per_bucket, h->fanout.all_full, h->fanout.d_edges,
+                                h->fanout.nedges, h->stream)))
+      return rc;
+    if ((legs & EXT_MPI_AMD_LEG_STAGE_OUT) && (rc = stage_out(h))) return rc;
+    return 0;
+  }
   if (h->kind == KIND_IPC && h->fused && (legs & core) == core) {
     emac_comm *cm = &comms[h->comm];
     unsigned long e0, e1;
@@ -2356,7 +2593,8 @@ int ext_mpi_amd_comm_set_node_ports(int comm, int nodes, const int *ports) {
   int rc;
   if (comm < 0 || comm >= MAX_COMMS || !comms[comm].used) return EMAC_ERR_ARG;
   if (nodes < 1 || comms[comm].size % nodes) return EMAC_ERR_ARG;
-  if (nodes > EMAC_MAX_NODES || (nodes > 1 && comms[comm].ipc)) return EMAC_ERR_UNSUPPORTED;
+  /* a peer-mapped communicator's members are nodes only as a whole (node_comm_allreduce_init) */
+  if (nodes > EMAC_MAX_NODES || (nodes > 1 && comms[comm].ipc && nodes != comms[comm].size)) return EMAC_ERR_UNSUPPORTED;
   if ((rc = emac_node_sched_build(&ns, nodes, ports))) return rc;
   comms[comm].nodes = nodes;
   comms[comm].ns = ns;

@@ -587,6 +587,52 @@ int emac_comm_program_nodes(const emac_plan *p, const emac_node_sched *ns, int n
   return program_nodes(p, ns, node, me, send_phase, count, ops_out, nops_out, folds_out, nfolds_out, staging_bytes);
 }
 
+int emac_node_single(const emac_node_sched *ns) {
+  if (ns->nodes == 2 && ns->nsteps == 1 && ns->nred == 0 && ns->radix[0] == 2) return 2;
+  if (ns->nsteps == 1 && ns->nred == 0 && ns->radix[0] == ns->nodes) return 1;
+  return 0;
+}
+
+int emac_node_shares(const emac_plan *p, const emac_node_sched *ns0, int me, emac_share **out, int *nout) {
+  emac_node_sched ns = *ns0;
+  const int R = p->nranks, N = ns.nodes, pos = p->rank_pos[me];
+  long count = 0;
+  int pc, q, u, t, i, n = 0;
+  emac_share *sh;
+  *out = NULL;
+  *nout = 0;
+  if (!emac_node_single(&ns) || me < 0 || me >= R) return EMAC_ERR_UNSUPPORTED;
+  for (pc = 0; pc < p->npieces; pc++)
+    for (q = 0; q < R; q++) count += p->chunk_len[(size_t)pc * R + q];
+  node_task_order(&ns, count);
+  sh = (emac_share *)calloc((size_t)p->npieces * (size_t)N * (size_t)N + 1, sizeof(emac_share));
+  if (!sh) return EMAC_ERR_MALLOC;
+  for (pc = 0; pc < p->npieces; pc++) {
+    const long off = p->chunk_off[(size_t)pc * R + pos], len = p->chunk_len[(size_t)pc * R + pos];
+    for (u = 0; u < N; u++) { /* task u's share (program_nodes: mo, ml), line by line */
+      const long mo = off + len * u / N, ml = off + len * (u + 1) / N - mo;
+      for (t = 0; t < N && ml > 0; t++) {
+        long a, b, so, sl;
+        emac_share *s;
+        task_lines(&ns, count, t, t + 1, &a, &b);
+        clip(a, b, mo, mo + ml, &so, &sl);
+        if (sl <= 0) continue;
+        s = &sh[n++];
+        s->off = so;
+        s->len = sl;
+        s->node = ns.task_node[u];
+        s->nleaf = N;
+        s->leaf_node[0] = ns.task_node[(t + N - 1) % N];
+        s->leaf_node[1] = ns.task_node[t];
+        for (i = 0; i < N - 2; i++) s->leaf_node[2 + i] = ns.task_node[(t + i + 1) % N];
+      }
+    }
+  }
+  *out = sh;
+  *nout = n;
+  return 0;
+}
+
 static int program_nodes(const emac_plan *p, const emac_node_sched *ns, int node, int me, long send_phase, long count,
                          emac_p2p **ops_out, int *nops_out, emac_fold **folds_out, int *nfolds_out,
                          long *staging_bytes) {

@@ -184,6 +184,24 @@ int emac_comm_program(const emac_plan *p, int me, long send_phase, emac_p2p **op
 int emac_comm_program_nodes(const emac_plan *p, const emac_node_sched *ns, int node, int me, long send_phase,
                             emac_p2p **ops, int *nops, emac_fold **folds, int *nfolds, long *staging_bytes);
 
+/* The NODE form over peer-mapped nodes (engine.c node_ipc_init) runs the inter-node schedule as
+   shares instead of point-to-point lines: one reduce-scatter step over every node (program_nodes'
+   "single" flow: every element's value is ONE fold of the N node partials, in the order its line's
+   task gives, whoever computes it). emac_node_single: 1 for such a schedule, 2 for two nodes at one
+   port (the halving flow: the same sums, partner + own), else 0. */
+int emac_node_single(const emac_node_sched *ns);
+typedef struct {
+  long off, len;                  /* elements of the message */
+  int node;                       /* the node that folds this part (every node copies it back) */
+  int nleaf;                      /* nodes whose partials it folds, in fold order */
+  int leaf_node[EMAC_MAX_NODES];
+} emac_share;
+/* The parts of node rank `me`'s chunk (every piece): node task_node[u] folds the u-th N-th of the
+   piece's chunk, cut at the line boundaries, each part with its line's leaf order (task t's line:
+   t - 1, t, t + 1, ..., t + N - 2 mod N, the last-step rule of raw_code.c). *out is malloc'd.
+   0 or an EMAC_ERR_* code. */
+int emac_node_shares(const emac_plan *p, const emac_node_sched *ns, int me, emac_share **out, int *nout);
+
 /* Build the plan of an nranks-rank Allreduce of `count` elements. 0 or an EMAC_ERR_* code. */
 int emac_plan_build(emac_plan *p, int nranks, long count, int dtype, int op, const emac_copyin *cfg);
 void emac_plan_free(emac_plan *p);
