@@ -212,7 +212,15 @@ int ext_mpi_amd_comm_set_nodes(int comm, int nodes);
  * runs every node rank's node legs (rank me of each node is a column peer of rank me of the
  * others) as one RCCL group per leg, and stores each owner chunk into the node's other receive
  * buffers. Bits identical to ext_mpi_amd_allreduce_init on size * nranks ranks of one process each
- * (ext_mpi_native.c:879-1000). Peer-mapped communicators: EXT_MPI_AMD_ERROR_UNSUPPORTED. */
+ * (ext_mpi_native.c:879-1000).
+ * On a peer-mapped communicator (ext_mpi_amd_comm_init_ipc; collective over it) the node legs are
+ * peer loads instead: the copy-in goes into a partial block of the communicator's arena, then
+ * barrier, each node folds its share of every node rank's chunk over the N partials read in place
+ * (in the reference's line order), barrier, every share is pulled into the chunk owners' receive
+ * buffers, and the copy-out follows. Only one reduce-scatter step over every node
+ * (ext_mpi_amd_comm_set_node_ports(comm, size, {-(size-1), size-1, 0}), the default when size is
+ * not a power of two) and two nodes at one port (SUM) are taken there; other lists return
+ * EXT_MPI_AMD_ERROR_UNSUPPORTED on every member. No caller memory is exported: Done is local. */
 int ext_mpi_amd_node_comm_allreduce_init(int nranks, const void *const *sendbufs, void *const *recvbufs, long count,
                                          int dtype, int op, int comm, const char *copyin, int *handle);
 
