@@ -1861,9 +1861,9 @@ static int upload_launch_fan(const emac_handle *h, emac_launch *L, emac_bucket *
     2. barrier(in); the fold of this node's share of every node rank's chunk: the N nodes' partials
        read in place (system-coherent loads over xGMI), in the line's order, into this node's outbox
        (arena); barrier(out) -- the IPC form's protocol (ipc_sync.hpp, epochs, timeout recovery);
-    3. the pull: every node's share (this node's own too) from its outbox into the chunk owner's
-       receive buffer, owners after this node first;
-    4. the copy-out: every owner chunk into the node's other receive buffers (emac_gpu_copy_fan).
+    3. the pull fused with the copy-out: every node's share (this node's own too) read once from
+       its outbox and stored into all R receive buffers (emac_gpu_copy_fan_remote), the nodes
+       after this one first.
    No caller memory is exported -- the peers read only the two arena blocks -- so the handle's Done
    is local. Collective over the communicator (the exchanges run whatever failed locally). */
 static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
@@ -1992,26 +1992,26 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
       nb++;
     }
   if (!rc) rc = upload_launch_fan(h, &h->xfold[0], b, nb, N, 2);
-  /* 3. the pull: every share from its node's outbox into the chunk owner's receive buffer, the
-     nodes after this one first (their loads head for different GPUs' links), this node's last */
+  /* 3. the pull, fused with the copy-out: every share read once from its node's outbox and stored
+     into all R receive buffers, the nodes after this one first (their loads head for different
+     GPUs' links), this node's own last */
   for (nb = 0, k = 1; !rc && k <= N; k++) {
     const int q = (cm->rank + k) % N;
     for (me = 0; me < R; me++)
       for (i = 0; i < nsh[me]; i++) {
         const emac_share *x = &sh[me][i];
         emac_bucket *bk = &b[nb];
+        int d;
         if (x->node != q || x->len <= 0) continue;
         memset(bk, 0, sizeof(*bk));
         bk->src[0] = peer_out[q];
-        bk->dst[0] = h->drecv[me];
-        bk->ndst = 1;
+        for (d = 0; d < R; d++) bk->dst[d] = h->drecv[d];
+        bk->ndst = R;
         place_bucket(bk, 1, x->off, x->len, ts);
         nb++;
       }
   }
   if (!rc) rc = upload_launch_fan(h, &h->pull, b, nb, 1, 2);
-  /* 4. the copy-out */
-  if (!rc) rc = build_node_fanout(h, b);
   for (me = 0; me < R; me++) free(sh[me]);
   free(b);
   return rc;
@@ -2347,7 +2347,6 @@ static int enqueue_legs(emac_handle *h, int legs) {
     const int nodes = comms[h->comm].size;
     if ((legs & EXT_MPI_AMD_LEG_FOLD) && (rc = fold_launch(h))) return rc; /* the copy-in */
     if (legs & (EXT_MPI_AMD_LEG_NODES_RS | EXT_MPI_AMD_LEG_NODES_FOLD | EXT_MPI_AMD_LEG_NODES_AG)) {
-      static const emac_codes copy = {{1}, {1}, 1, 1}; /* one leaf: a copy */
       const emac_launch *X = &h->xfold[0];
       emac_codes lin;
       memset(&lin, 0, sizeof(lin));
@@ -2363,9 +2362,9 @@ static int enqueue_legs(emac_handle *h, int legs) {
         return rc;
       if ((rc = ipc_barrier(h, 1))) return rc;
       if ((h->pull.nb || h->pull.nedges) &&
-          (rc = emac_gpu_fold_remote(h->plan.dtype, EMAC_SUM, 1, h->pull.unroll, &copy, h->pull.d_buckets, h->pull.nb,
-                                     h->pull.ntiles, h->pull.tiles_per_bucket, h->pull.all_full, h->pull.d_edges,
-                                     h->pull.nedges, ipc_go(h), h->stream)))
+          (rc = emac_gpu_copy_fan_remote(h->plan.tsize, h->plan.nranks, h->pull.unroll, h->pull.d_buckets, h->pull.nb,
+                                         h->pull.ntiles, h->pull.tiles_per_bucket, h->pull.all_full, h->pull.d_edges,
+                                         h->pull.nedges, ipc_go(h), h->stream)))
         return rc;
     }
     if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && h->fanout.nb &&

@@ -138,6 +138,19 @@ int emac_gpu_copy_fan(int tsize, int width, int unroll, const emac_bucket *d_buc
   return emac_copy_fan_launch(tsize, width, unroll, &L);
 }
 
+int emac_copy_fan_remote_launch(int tsize, int width, int unroll, const emac::Launch *L);
+
+int emac_gpu_copy_fan_remote(int tsize, int width, int unroll, const emac_bucket *d_buckets, int nb, long ntiles,
+                             long tiles_per_bucket, int all_full, const emac_edge *d_edges, int nedges, const unsigned *go,
+                             void *stream) {
+  static const emac_codes copy = {{1}, {1}, 1, 1}; /* one leaf */
+  const emac::Launch L = {&copy, d_buckets, nb, ntiles, tiles_per_bucket, all_full, d_edges, nedges,
+                          static_cast<hipStream_t>(stream), go, 1};
+  if (width < 1 || width > EMAC_MAX_RANKS || !go) return EMAC_ERR_ARG;
+  if (nb <= 0 || (ntiles <= 0 && nedges <= 0)) return 0;
+  return emac_copy_fan_remote_launch(tsize, width, unroll, &L);
+}
+
 int emac_gpu_fold_remote(int dtype, int op, int nsrc, int unroll, const emac_codes *codes, const emac_bucket *d_buckets,
                          int nb, long ntiles, long tiles_per_bucket, int all_full, const emac_edge *d_edges, int nedges,
                          const unsigned *go, void *stream) {

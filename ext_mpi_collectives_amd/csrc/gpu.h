@@ -155,6 +155,11 @@ int emac_gpu_fold_remote(int dtype, int op, int nsrc, int unroll, const emac_cod
    (1 .. EMAC_MAX_RANKS - 1), bits moved unchanged; tsize = element bytes (4 or 8). */
 int emac_gpu_copy_fan(int tsize, int width, int unroll, const emac_bucket *d_buckets, int nb, long ntiles,
                       long tiles_per_bucket, int all_full, const emac_edge *d_edges, int nedges, void *stream);
+/* the peer-mapped pull with fan-out: one leaf in a peer's memory (system-coherent loads), `width`
+   destinations (<= EMAC_MAX_RANKS); `go`: the phase-0 verdict word */
+int emac_gpu_copy_fan_remote(int tsize, int width, int unroll, const emac_bucket *d_buckets, int nb, long ntiles,
+                             long tiles_per_bucket, int all_full, const emac_edge *d_edges, int nedges, const unsigned *go,
+                             void *stream);
 
 /* Fold-tree kind of a plan's codes (fold_kernel.hpp template parameter CH): 0 linear (one
    radix), a packed compile-time radix chain (5 bits per level, level 0 lowest) when the kernels
