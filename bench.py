@@ -1201,7 +1201,8 @@ def node_form_line(args, world, dname, rn, one_rank_per_gpu):
         "parts_us": {"copy_in_fold": round(t_in * 1e6, 2), "node_legs_xgmi": round(t_x * 1e6, 2),
                      "copy_out": round(t_out * 1e6, 2), "sum": round((t_in + t_x + t_out) * 1e6, 2),
                      "start_to_wait": round(wall * 1e6 / steps, 2)},
-        "copy_out_achieved_gbps": round(R * S / t_out / 1e9, 1),
+        # (peer-mapped members: the copy-out is fused into the node legs' pull, its part is empty)
+        "copy_out_achieved_gbps": round(R * S / t_out / 1e9, 1) if t_out > 1e-6 else None,
         "node_legs_xgmi_bound_us": round(xgmi_bound * 1e6, 1),
         "node_legs_frac_of_xgmi_bound": round(xgmi_bound / t_x, 3) if t_x > 0 else None,
         "value_per_gpu_gbps": round(R * S * steps / wall / 1e9, 2),
