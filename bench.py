@@ -303,6 +303,7 @@ def _ceiling_lib():
     L.ceiling_read_vgpr.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                     ctypes.c_void_p]
     L.ceiling_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    L.ceiling_write.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_void_p]
     L.ceiling_gate_arm.argtypes = [ctypes.c_void_p]
     L.ceiling_gate_arm.restype = ctypes.c_void_p
     L.ceiling_gate_open.argtypes = [ctypes.c_void_p]
@@ -332,8 +333,9 @@ class StreamGate:
 def measured_ceilings(steps=10, launch_bytes=256 * MIB):
     """Best HBM rates measured on this GPU in this run (tools/ceiling.hip), GB/s of algorithmic bytes:
     read -- the best of three read-only streams over 4 GiB: LDS-DMA (global_load_lds_dwordx4 nt)
-    and nontemporal global_load_dwordx4 into VGPRs with 4 or 8 vectors per lane in flight; copy -- the best of a nontemporal and a default-policy 1:1 copy
-    (K = 4 vectors per lane), each timed over 4 GiB and over `launch_bytes` (read + written, the
+    and nontemporal global_load_dwordx4 into VGPRs with 4 or 8 vectors per lane in flight; write --
+    a nontemporal store stream over 4 GiB and at the launch's written bytes; copy -- the best of a nontemporal and a default-policy 1:1 copy
+    (K = 4 vectors per lane) and a nontemporal copy in phases (tools/ceiling.hip copy_phased), each timed over 4 GiB and over `launch_bytes` (read + written, the
     headline launch's bytes, three buffer sets rotated past the 256 MiB Infinity Cache): the rate
     of the node-form fold's 1:1 read/write mix."""
     import torch
@@ -359,8 +361,25 @@ def measured_ceilings(steps=10, launch_bytes=256 * MIB):
         reads[vname] = round(steps * n / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
     out["read_ceiling_gbps"] = max(reads.values())
     out["read_variants_gbps"] = reads
+    # write-only: over 4 GiB and at the launch's written bytes (three buffers rotated)
+    writes = {}
+    L.ceiling_write(a.data_ptr(), n, 2, stream.cuda_stream)
+    e0.record(stream)
+    assert L.ceiling_write(a.data_ptr(), n, steps, stream.cuda_stream) == 0
+    e1.record(stream)
+    torch.cuda.synchronize()
+    writes["write_4GiB"] = round(steps * n / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+    half = launch_bytes // 2
+    e0.record(stream)
+    for i in range(3 * steps):
+        assert L.ceiling_write(a.data_ptr() + (i % 3) * launch_bytes, half, 1, stream.cuda_stream) == 0
+    e1.record(stream)
+    torch.cuda.synchronize()
+    writes["write_launch"] = round(3 * steps * half / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+    out["write_ceiling_gbps"] = max(writes.values())
+    out["write_variants_gbps"] = writes
     copies = {}
-    for variant, vname in ((0, "nt"), (1, "plain")):
+    for variant, vname in ((0, "nt"), (1, "plain"), (2, "phased")):
         half = n // 2
         L.ceiling_copy(a.data_ptr(), a.data_ptr() + half, half, 2, variant, stream.cuda_stream)
         e0.record(stream)
@@ -382,6 +401,13 @@ def measured_ceilings(steps=10, launch_bytes=256 * MIB):
     del a, sink
     torch.cuda.empty_cache()
     return out
+
+
+def read_write_floor_s(ceil, read_bytes, write_bytes):
+    """The shortest time HBM can read `read_bytes` and write `write_bytes` on this GPU: the two
+    streams' times at the measured read and write ceilings, added (HBM does not read and write at
+    once; tools/nodevar.hip: the node fold at 256 MiB per rank took 0.97 of that sum)."""
+    return read_bytes / (ceil["read_ceiling_gbps"] * 1e9) + write_bytes / (ceil["write_ceiling_gbps"] * 1e9)
 
 
 def stream_copy_peak():
@@ -532,6 +558,11 @@ def single_gpu(args):
                     out["roofline"]["frac_of_measured_copy_ceiling"] = round(achieved / ceil["copy_gbps"], 4)
                 else:
                     out["roofline"]["kernel_above_measured_copy"] = True
+                # HBM does not read and write at once: a launch that reads B_r and writes B_w bytes
+                # takes at least B_r / read ceiling + B_w / write ceiling (both measured here)
+                fl = read_write_floor_s(ceil, algo_bytes / 2, algo_bytes / 2)
+                out["roofline"]["read_write_floor_us"] = round(fl * 1e6, 2)
+                out["roofline"]["frac_of_read_write_floor"] = round(fl / kernel_s, 4)
         except (RuntimeError, AssertionError) as e:
             log("ceiling probes failed:", e)
         big = (256 * MIB) // tsize
@@ -547,6 +578,10 @@ def single_gpu(args):
             "read_gbps": round(R * big * tsize / k256 / 1e9, 1),
             "avg_launch_us": round(k256 * 1e6, 1), "checked": r256["checked"], "fold_schedule": r256["schedule"],
             "traffic": traffic_from_profiles(f"node_r{R}_256mib_{args.dtype}")}
+        if "write_ceiling_gbps" in extras:
+            fl = read_write_floor_s(extras, R * big * tsize, R * big * tsize)
+            extras["point_256MiB"].update(read_write_floor_us=round(fl * 1e6, 1),
+                                          frac_of_read_write_floor=round(fl / k256, 4))
         # latency -> bandwidth crossover of the node form (cf. BASELINE configs[4] on 8 GPUs);
         # small points reuse one buffer set (as the reference's latency runs do), large ones rotate
         sweep = []
@@ -583,6 +618,10 @@ def single_gpu(args):
         lf["frac_of_peak"] = round(lf["achieved_gbps"] / HBM_PEAK_GBPS, 4)
         lf["algorithmic_bytes_per_launch"] = (R + 1) * lf["chunk_bytes"]
         lf["traffic"] = traffic_from_profiles(f"local_r{R}_{lf['chunk_bytes'] // MIB}mib_{args.dtype}")
+        if "write_ceiling_gbps" in extras:
+            fl = read_write_floor_s(extras, R * lf["chunk_bytes"], lf["chunk_bytes"])
+            lf["read_write_floor_us"] = round(fl * 1e6, 2)
+            lf["frac_of_read_write_floor"] = round(fl / (lf["avg_launch_us"] * 1e-6), 4)
         if "read_ceiling_gbps" in extras:
             lf["frac_of_measured_read_ceiling"] = round(lf["achieved_gbps"] / extras["read_ceiling_gbps"], 4)
         extras["local_fold_256MiB"] = lf

@@ -8,6 +8,9 @@
 //                      vectors per lane in flight (round 3, tools/nodevar.hip,
 //                      profiles/r03_nodevar/: 6.85-7.06 TB/s, at or above the LDS-DMA stream on the
 //                      same lease); bench.py's read ceiling is the best of the three.
+//   ceiling_write:     a write-only stream of nontemporal global_store_dwordx4, K = 4 vectors per lane
+//                      (round 3): with the read ceiling it prices a launch that reads and writes as
+//                      the sum of its two streams' times (HBM does not read and write at once).
 //   ceiling_copy:      a 1:1 copy (1 byte written per byte read: the node-form fold's mix), K = 4
 //                      vectors per lane in flight, nontemporal or default-policy accesses.
 // Each call enqueues `iters` launches over `bytes` (a multiple of 16 KiB) on `stream`.
@@ -52,6 +55,28 @@ __global__ __launch_bounds__(256) void read_vgpr(const f4 *__restrict__ a, long 
     for (int k = 0; k < K; ++k) acc += v[k];
   }
   if (acc.x == 12345.f) out[0] = acc.y + acc.z + acc.w;
+}
+
+__global__ __launch_bounds__(256) void write_k4(f4 *__restrict__ b, long n, float v0) {
+  const long step = (long)gridDim.x * 256 * 4;
+  const f4 v = {v0, v0, v0, v0};
+  for (long i0 = (long)blockIdx.x * 256 * 4 + threadIdx.x; i0 < n; i0 += step) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(v, (G4 *)b + i0 + k * 256);
+  }
+}
+
+// a 1:1 copy in phases (the deferred-store order of fold_kernel.hpp fold_deferred): each
+// workgroup loads 8 x 256 vectors into LDS, then stores them (tools/nodevar.hip: 6.24 / 6.01 TB/s
+// at 128 MiB / 2 GiB against 6.16 / 5.47 for copy_k4 on the same lease)
+__global__ __launch_bounds__(256) void copy_phased(const f4 *__restrict__ a, f4 *__restrict__ b, long n) {
+  __shared__ f4 res[8 * 256];
+  for (long g0 = (long)blockIdx.x * 2048; g0 < n; g0 += (long)gridDim.x * 2048) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) res[q * 256 + threadIdx.x] = __builtin_nontemporal_load((const G4 *)a + g0 + q * 256 + threadIdx.x);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) __builtin_nontemporal_store(res[q * 256 + threadIdx.x], (G4 *)b + g0 + q * 256 + threadIdx.x);
+  }
 }
 
 // 1:1 copies, K = 4 vectors per lane in flight, grid-stride: nontemporal (the long streams'
@@ -102,12 +127,24 @@ int ceiling_read_vgpr(const void *buf, long bytes, int iters, int k, float *sink
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-/* variant 0: nontemporal, 1: default policy */
-int ceiling_copy(const void *src, void *dst, long bytes, int iters, int variant, void *stream) {
+int ceiling_write(void *buf, long bytes, int iters, void *stream) {
   const long n = bytes / 16;
   if (n % 1024 || iters < 1) return -3;
+  for (int i = 0; i < iters; i++)
+    hipLaunchKernelGGL(write_k4, dim3(4096), dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<f4 *>(buf), n, 1.0f);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+/* variant 0: nontemporal, 1: default policy, 2: nontemporal in phases (copy_phased) */
+int ceiling_copy(const void *src, void *dst, long bytes, int iters, int variant, void *stream) {
+  const long n = bytes / 16;
+  if (n % 2048 || iters < 1) return -3;
   for (int i = 0; i < iters; i++) {
-    if (variant == 0)
+    if (variant == 2) {
+      const long groups = n / 2048;
+      hipLaunchKernelGGL(copy_phased, dim3((unsigned)(groups < (1L << 20) ? groups : (1L << 20))), dim3(256), 0,
+                         static_cast<hipStream_t>(stream), static_cast<const f4 *>(src), static_cast<f4 *>(dst), n);
+    } else if (variant == 0)
       hipLaunchKernelGGL(copy_k4<true>, dim3(4096), dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<const f4 *>(src),
                          static_cast<f4 *>(dst), n);
     else

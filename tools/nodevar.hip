@@ -168,6 +168,30 @@ __global__ __launch_bounds__(256) void nfold_burst(const Bk *__restrict__ bk, in
   }
 }
 
+// pure write stream (nontemporal stores), K vectors per lane
+template <int K>
+__global__ __launch_bounds__(256) void write_k(f4 *__restrict__ b, long n, float v0) {
+  const long step = (long)gridDim.x * 256 * K;
+  const f4 v = {v0, v0, v0, v0};
+  for (long i0 = (long)blockIdx.x * 256 * K + threadIdx.x; i0 < n; i0 += step) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) __builtin_nontemporal_store(v, (G4 *)b + i0 + k * 256);
+  }
+}
+
+// a 1:1 copy in phases: each workgroup loads KB x 256 x U vectors into LDS, then stores them
+template <int U, int KB>
+__global__ __launch_bounds__(256) void copy_phased(const f4 *__restrict__ a, f4 *__restrict__ b, long n) {
+  __shared__ f4 res[KB * U * 256];
+  constexpr long G = 256L * U * KB;
+  for (long g0 = (long)blockIdx.x * G; g0 < n; g0 += (long)gridDim.x * G) {
+#pragma unroll
+    for (int q = 0; q < KB * U; ++q) res[q * 256 + threadIdx.x] = __builtin_nontemporal_load((const G4 *)a + g0 + q * 256 + threadIdx.x);
+#pragma unroll
+    for (int q = 0; q < KB * U; ++q) __builtin_nontemporal_store(res[q * 256 + threadIdx.x], (G4 *)b + g0 + q * 256 + threadIdx.x);
+  }
+}
+
 // pure read streams: K vectors per lane in flight into VGPRs (nt), or LDS-DMA (global_load_lds nt)
 template <int K>
 __global__ __launch_bounds__(256) void read_vgpr(const f4 *__restrict__ a, long n, float *out) {
@@ -301,6 +325,8 @@ int main(int argc, char **argv) {
       {"node_burst_u2_k4_g512", 47, 512, {}}, {"node_burst_u4_k2", 48, 0, {}}, {"node_burst_u2_k4_g256", 47, 256, {}},
       {"node_burst_u2_k8", 60, 0, {}}, {"node_burst_u4_k4", 61, 0, {}}, {"node_burst_u1_k8", 62, 0, {}},
       {"local_burst_u2_k16", 63, 0, {}}, {"local_burst_u4_k8", 64, 0, {}},
+      {"write_k4", 53, 0, {}}, {"copy_phased_u2_k4", 54, 0, {}}, {"copy_phased_u2_k8", 55, 0, {}},
+      {"copy_phased_u4_k4_g512", 56, 512, {}},
       {"read_vgpr_k4", 50, 0, {}},     {"read_vgpr_k8", 51, 0, {}},    {"read_glds", 52, 0, {}}};
   auto run = [&](const V &v, int i) {
     const int st = i % nsets;
@@ -342,6 +368,10 @@ int main(int argc, char **argv) {
     case 62: hipLaunchKernelGGL((nfold_burst<1, 8>), dim3(g(n2 * 2 / 8)), dim3(256), 0, s, dvar[st], R, t2 * 2); break;
     case 63: hipLaunchKernelGGL((lfold_burst<2, 16>), dim3(g(lt1 / 32)), dim3(256), 0, s, dloc[st], lt1 / 2); break;
     case 64: hipLaunchKernelGGL((lfold_burst<4, 8>), dim3(g(lt1 / 32)), dim3(256), 0, s, dloc[st], lt1 / 4); break;
+    case 53: hipLaunchKernelGGL((write_k<4>), dim3(4096), dim3(256), 0, s, ca0 + copy_n, copy_n, 1.0f); break;
+    case 54: hipLaunchKernelGGL((copy_phased<2, 4>), dim3((unsigned)std::min<long>(copy_n / 2048, 1L << 20)), dim3(256), 0, s, ca0, ca0 + copy_n, copy_n); break;
+    case 55: hipLaunchKernelGGL((copy_phased<2, 8>), dim3((unsigned)std::min<long>(copy_n / 4096, 1L << 20)), dim3(256), 0, s, ca0, ca0 + copy_n, copy_n); break;
+    case 56: hipLaunchKernelGGL((copy_phased<4, 4>), dim3(512), dim3(256), 0, s, ca0, ca0 + copy_n, copy_n); break;
     case 50: hipLaunchKernelGGL((read_vgpr<4>), dim3(4096), dim3(256), 0, s, ca0, 2 * copy_n, dummy); break;
     case 51: hipLaunchKernelGGL((read_vgpr<8>), dim3(2048), dim3(256), 0, s, ca0, 2 * copy_n, dummy); break;
     case 52: hipLaunchKernelGGL(read_glds, dim3(2048), dim3(256), 0, s, ca0, 2 * copy_n, dummy); break;
@@ -386,7 +416,7 @@ int main(int argc, char **argv) {
     std::sort(v.us.begin(), v.us.end());
     const float med = v.us[v.us.size() / 2];
     const bool local = (v.id >= 40 && v.id < 46) || v.id >= 63, rd = v.id >= 50 && v.id < 60;
-    const double bytes = rd ? 2.0 * copy_n * 16 : local ? (R + 1.0) * S * 16 : 2.0 * R * S * 16;
+    const double bytes = v.id == 53 ? 1.0 * copy_n * 16 : rd ? 2.0 * copy_n * 16 : local ? (R + 1.0) * S * 16 : 2.0 * R * S * 16;
     printf("%-18s %9.2f %9.2f %9.2f  %6.3f TB/s  %.3f of 8\n", v.name.c_str(), med, v.us.front(), v.us.back(),
            bytes / med / 1e6, bytes / med / 1e6 / 8.0);
   }
