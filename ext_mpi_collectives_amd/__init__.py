@@ -273,6 +273,20 @@ def LEG_STEP(s):
     return (s + 1) << LEG_STEP_SHIFT
 
 
+def node_shares(nodes, ports, ranks_per_node, count, dtype, copyin, me, max_shares=4096):
+    """The parts of node rank `me`'s chunk the peer-mapped node join folds: list of
+    (off, len, folding node, [leaf nodes in fold order]) (ext_mpi_amd_node_shares)."""
+    off = (ctypes.c_long * max_shares)()
+    ln = (ctypes.c_long * max_shares)()
+    nd = (ctypes.c_int * max_shares)()
+    lv = (ctypes.c_int * (max_shares * nodes))()
+    n = ctypes.c_int(0)
+    _check("ext_mpi_amd_node_shares", lib().ext_mpi_amd_node_shares(nodes, _ports(ports), ranks_per_node, count, dtype,
+                                                                       _enc(copyin), me, off, ln, nd, lv, max_shares,
+                                                                       ctypes.byref(n)))
+    return [(off[i], ln[i], nd[i], list(lv[i * nodes:(i + 1) * nodes])) for i in range(n.value)]
+
+
 def default_node_ports(nodes):
     """The inter-node ports list without EXT_MPI_NUM_PORTS (plan.c emac_node_sched_build): one
     port per step for a power of two, else one step of radix `nodes` up to 16 nodes, else one

@@ -2605,6 +2605,33 @@ int ext_mpi_amd_comm_set_nodes(int comm, int nodes) {
   return ext_mpi_amd_comm_set_node_ports(comm, nodes, NULL);
 }
 
+int ext_mpi_amd_node_shares(int nodes, const int *ports, int ranks_per_node, long count, int dtype, const char *copyin,
+                            int me, long *off, long *len, int *node, int *leaf_nodes, int max_shares, int *nshares) {
+  emac_node_sched ns;
+  emac_plan p;
+  emac_copyin cfg;
+  emac_share *sh = NULL;
+  int rc, i, l, n = 0;
+  if (!nshares || ranks_per_node < 1 || ranks_per_node > EMAC_MAX_RANKS || nodes < 2 || nodes > EMAC_MAX_NODES ||
+      me < 0 || me >= ranks_per_node || count < 0)
+    return EMAC_ERR_ARG;
+  if ((rc = emac_node_sched_build(&ns, nodes, ports))) return rc;
+  if ((rc = parse_cfg(copyin, ranks_per_node, &cfg))) return rc;
+  if ((rc = emac_plan_build(&p, ranks_per_node, count, dtype, EMAC_SUM, &cfg))) return rc;
+  rc = emac_node_shares(&p, &ns, me, &sh, &n);
+  for (i = 0; !rc && i < n && i < max_shares; i++) {
+    off[i] = sh[i].off;
+    len[i] = sh[i].len;
+    node[i] = sh[i].node;
+    for (l = 0; l < nodes; l++) leaf_nodes[(size_t)i * (size_t)nodes + l] = sh[i].leaf_node[l];
+  }
+  if (!rc) *nshares = n;
+  if (!rc && n > max_shares) rc = EMAC_ERR_ARG;
+  free(sh);
+  emac_plan_free(&p);
+  return rc;
+}
+
 int ext_mpi_amd_comm_program_nodes(int nodes, int ranks_per_node, int rank, long count, int dtype, const char *copyin,
                                    long send_phase, ext_mpi_amd_p2p *ops, int max_ops, int *nops,
                                    ext_mpi_amd_fold *folds, int max_folds, int *nfolds, long *staging_bytes) {

@@ -224,6 +224,15 @@ int ext_mpi_amd_comm_set_nodes(int comm, int nodes);
 int ext_mpi_amd_node_comm_allreduce_init(int nranks, const void *const *sendbufs, void *const *recvbufs, long count,
                                          int dtype, int op, int comm, const char *copyin, int *handle);
 
+/* The shares the peer-mapped node join folds (introspection for tests, no GPU): for node rank `me`
+ * of `ranks_per_node`, under the inter-node list `ports` (0-terminated, NULL: the default) over
+ * `nodes` nodes, each part of me's chunk as (off[i], len[i]) elements of the message, the node that
+ * folds it (node[i]) and the nodes whose partials it folds, in order (leaf_nodes[i * nodes ..]).
+ * Only one reduce-scatter step over every node, or two nodes at one port; else
+ * EXT_MPI_AMD_ERROR_UNSUPPORTED. *nshares receives the count (ERROR_ARG if above max_shares). */
+int ext_mpi_amd_node_shares(int nodes, const int *ports, int ranks_per_node, long count, int dtype, const char *copyin,
+                            int me, long *off, long *len, int *node, int *leaf_nodes, int max_shares, int *nshares);
+
 /* EXT_MPI_NUM_SOCKETS_PER_NODE (src/mpi/ext_mpi.c:43-187, a process-wide parameter): sockets per
  * node for every handle / plan made afterwards. It moves the tree method's (7 / 10) last-step
  * roots (reduce_copyin.c:860-864) and nothing else in the arithmetic. Returns the previous value,
