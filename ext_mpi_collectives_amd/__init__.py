@@ -274,17 +274,18 @@ def LEG_STEP(s):
 
 
 def node_shares(nodes, ports, ranks_per_node, count, dtype, copyin, me, max_shares=4096):
-    """The parts of node rank `me`'s chunk the peer-mapped node join folds: list of
-    (off, len, folding node, [leaf nodes in fold order]) (ext_mpi_amd_node_shares)."""
+    """The parts of node rank `me`'s chunk the peer-mapped node join folds: (levels, list of
+    (off, len, folding node, [leaf nodes in fold order])) -- levels 1: a left fold of the leaves,
+    k: k levels of pairs of consecutive leaves (ext_mpi_amd_node_shares)."""
     off = (ctypes.c_long * max_shares)()
     ln = (ctypes.c_long * max_shares)()
     nd = (ctypes.c_int * max_shares)()
     lv = (ctypes.c_int * (max_shares * nodes))()
-    n = ctypes.c_int(0)
+    n, levels = ctypes.c_int(0), ctypes.c_int(1)
     _check("ext_mpi_amd_node_shares", lib().ext_mpi_amd_node_shares(nodes, _ports(ports), ranks_per_node, count, dtype,
                                                                        _enc(copyin), me, off, ln, nd, lv, max_shares,
-                                                                       ctypes.byref(n)))
-    return [(off[i], ln[i], nd[i], list(lv[i * nodes:(i + 1) * nodes])) for i in range(n.value)]
+                                                                       ctypes.byref(n), ctypes.byref(levels)))
+    return levels.value, [(off[i], ln[i], nd[i], list(lv[i * nodes:(i + 1) * nodes])) for i in range(n.value)]
 
 
 def default_node_ports(nodes):

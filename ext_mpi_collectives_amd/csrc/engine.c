@@ -236,6 +236,7 @@ typedef struct {
   /* ... over peer-mapped nodes (node_ipc_init): this node's partials (arena, read by the peers) */
   void *part;
   size_t part_bytes;
+  emac_codes xcodes; /* ... and its share fold's tree (a left fold, or pairs for the halving flow) */
 } emac_handle;
 
 static emac_handle *handles[MAX_HANDLES];
@@ -1849,13 +1850,40 @@ static int upload_launch_fan(const emac_handle *h, emac_launch *L, emac_bucket *
   return rc;
 }
 
+/* The fold tree of a share of the peer-mapped node join over n partials: a left fold (levels 1),
+   or `levels` levels of pairs (the halving flow) -- the shape of a '6;1 -2 ... 2 ...' plan */
+static int node_fold_codes(int n, int levels, int dtype, emac_codes *c) {
+  emac_copyin cfg;
+  emac_plan p;
+  char cp[96];
+  int at, k, rc;
+  memset(c, 0, sizeof(*c));
+  if (levels <= 1) {
+    c->first[0] = 1;
+    c->close[n - 1] = 1;
+    c->nlev = 1;
+    c->nleaf = n;
+    return 0;
+  }
+  at = snprintf(cp, sizeof(cp), "6;1");
+  for (k = 0; k < levels; k++) at += snprintf(cp + at, sizeof(cp) - (size_t)at, " -2");
+  for (k = 0; k < levels; k++) at += snprintf(cp + at, sizeof(cp) - (size_t)at, " 2");
+  if ((rc = emac_parse_copyin(cp, &cfg))) return rc;
+  cfg.sockets = 1;
+  if ((rc = emac_plan_build(&p, n, (long)n * 16, dtype, EMAC_SUM, &cfg))) return rc;
+  *c = p.codes;
+  emac_plan_free(&p);
+  return 0;
+}
+
 /* The NODE form over peer-mapped nodes: node_comm_allreduce_init on an ext_mpi_amd_comm_init_ipc
    communicator -- one process per GPU, each member a node of R ranks whose buffers all live on
    its GPU. The inter-node schedule must be one reduce-scatter step over every node (EXT_MPI_NUM_PORTS
-   'N(-(N-1) (N-1))', the default for a node count that is not a power of two), or two nodes at one
-   port for SUM (emac_node_single): every element's value is then ONE fold of the N node partials
-   in its line's order, whoever computes it (plan.c emac_node_shares), so the inter-node legs become
-   peer loads instead of point-to-point lines. A Start runs
+   'N(-(N-1) (N-1))', the default for a node count that is not a power of two) -- every element's
+   value is then ONE fold of the N node partials in its line's order, whoever computes it -- or,
+   for SUM, one port per step over 2^k nodes (the default there) -- every value a balanced tree of
+   pairs over the task bits (plan.c emac_node_single, emac_node_shares): so the inter-node legs
+   become peer loads instead of point-to-point lines. A Start runs
     1. the node's copy-in: every owner chunk folded over the node's send buffers, in the plan's leaf
        order, into this node's partial block (arena memory the peers map; fold_launch, tuned);
     2. barrier(in); the fold of this node's share of every node rank's chunk: the N nodes' partials
@@ -1959,6 +1987,7 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
     }
   }
   for (me = 0, k = 0; me < R; me++) k += nsh[me];
+  if (!rc) rc = node_fold_codes(N, k && nsh[0] ? sh[0][0].nlev : 1, h->plan.dtype, &h->xcodes);
   if (!rc && !(b = (emac_bucket *)calloc((size_t)(k + h->plan.npieces * R) + 1, sizeof(emac_bucket)))) rc = EMAC_ERR_MALLOC;
   /* 1. the copy-in: every owner chunk into this node's partial block (at its message offset) */
   for (nb = 0, pc = 0; !rc && pc < h->plan.npieces; pc++)
@@ -1985,7 +2014,7 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
       int l;
       if (x->node != cm->rank || x->len <= 0) continue;
       memset(bk, 0, sizeof(*bk));
-      for (l = 0; l < x->nleaf; l++) bk->src[l] = peer_part[x->leaf_node[l]];
+      for (l = 0; l < x->nleaf; l++) bk->src[l] = peer_part[x->leaf_node[l]]; /* in h->xcodes' order */
       bk->dst[0] = h->outbox;
       bk->ndst = 1;
       place_bucket(bk, x->nleaf, x->off, x->len, ts);
@@ -2348,15 +2377,9 @@ static int enqueue_legs(emac_handle *h, int legs) {
     if ((legs & EXT_MPI_AMD_LEG_FOLD) && (rc = fold_launch(h))) return rc; /* the copy-in */
     if (legs & (EXT_MPI_AMD_LEG_NODES_RS | EXT_MPI_AMD_LEG_NODES_FOLD | EXT_MPI_AMD_LEG_NODES_AG)) {
       const emac_launch *X = &h->xfold[0];
-      emac_codes lin;
-      memset(&lin, 0, sizeof(lin));
-      lin.first[0] = 1; /* one level: a left fold of the nodes' partials in the line's order */
-      lin.close[nodes - 1] = 1;
-      lin.nlev = 1;
-      lin.nleaf = nodes;
       if ((rc = ipc_barrier(h, 0))) return rc;
       if ((X->nb || X->nedges) &&
-          (rc = emac_gpu_fold_remote(h->plan.dtype, nodes > 1 ? h->plan.op : EMAC_SUM, nodes, X->unroll, &lin,
+          (rc = emac_gpu_fold_remote(h->plan.dtype, nodes > 1 ? h->plan.op : EMAC_SUM, nodes, X->unroll, &h->xcodes,
                                      X->d_buckets, X->nb, X->ntiles, X->tiles_per_bucket, X->all_full, X->d_edges,
                                      X->nedges, ipc_go(h), h->stream)))
         return rc;
@@ -2606,7 +2629,8 @@ int ext_mpi_amd_comm_set_nodes(int comm, int nodes) {
 }
 
 int ext_mpi_amd_node_shares(int nodes, const int *ports, int ranks_per_node, long count, int dtype, const char *copyin,
-                            int me, long *off, long *len, int *node, int *leaf_nodes, int max_shares, int *nshares) {
+                            int me, long *off, long *len, int *node, int *leaf_nodes, int max_shares, int *nshares,
+                            int *levels) {
   emac_node_sched ns;
   emac_plan p;
   emac_copyin cfg;
@@ -2626,6 +2650,7 @@ int ext_mpi_amd_node_shares(int nodes, const int *ports, int ranks_per_node, lon
     for (l = 0; l < nodes; l++) leaf_nodes[(size_t)i * (size_t)nodes + l] = sh[i].leaf_node[l];
   }
   if (!rc) *nshares = n;
+  if (!rc && levels) *levels = emac_node_single(&ns) == 2 ? ns.nsteps : 1;
   if (!rc && n > max_shares) rc = EMAC_ERR_ARG;
   free(sh);
   emac_plan_free(&p);

@@ -588,7 +588,10 @@ int emac_comm_program_nodes(const emac_plan *p, const emac_node_sched *ns, int n
 }
 
 int emac_node_single(const emac_node_sched *ns) {
-  if (ns->nodes == 2 && ns->nsteps == 1 && ns->nred == 0 && ns->radix[0] == 2) return 2;
+  int st, halving = ns->nsteps > 0 && ns->nred == 0 && ns->nagp == ns->nsteps; /* program_nodes' condition */
+  for (st = 0; st < ns->nsteps; st++) halving &= ns->radix[st] == 2;
+  for (st = 0; st < ns->nagp; st++) halving &= ns->agp_radix[st] == 2;
+  if (halving) return 2;
   if (ns->nsteps == 1 && ns->nred == 0 && ns->radix[0] == ns->nodes) return 1;
   return 0;
 }
@@ -597,11 +600,12 @@ int emac_node_shares(const emac_plan *p, const emac_node_sched *ns0, int me, ema
   emac_node_sched ns = *ns0;
   const int R = p->nranks, N = ns.nodes, pos = p->rank_pos[me];
   long count = 0;
+  const int flow = emac_node_single(&ns), K = ns.nsteps;
   int pc, q, u, t, i, n = 0;
   emac_share *sh;
   *out = NULL;
   *nout = 0;
-  if (!emac_node_single(&ns) || me < 0 || me >= R) return EMAC_ERR_UNSUPPORTED;
+  if (!flow || me < 0 || me >= R) return EMAC_ERR_UNSUPPORTED;
   for (pc = 0; pc < p->npieces; pc++)
     for (q = 0; q < R; q++) count += p->chunk_len[(size_t)pc * R + q];
   node_task_order(&ns, count);
@@ -611,6 +615,20 @@ int emac_node_shares(const emac_plan *p, const emac_node_sched *ns0, int me, ema
     const long off = p->chunk_off[(size_t)pc * R + pos], len = p->chunk_len[(size_t)pc * R + pos];
     for (u = 0; u < N; u++) { /* task u's share (program_nodes: mo, ml), line by line */
       const long mo = off + len * u / N, ml = off + len * (u + 1) / N - mo;
+      if (flow == 2 && ml > 0) { /* halving: one tree for the whole share, leaves by bit-reversed task */
+        emac_share *s = &sh[n++];
+        s->off = mo;
+        s->len = ml;
+        s->node = ns.task_node[u];
+        s->nleaf = N;
+        s->nlev = K;
+        for (i = 0; i < N; i++) {
+          int b, r = 0;
+          for (b = 0; b < K; b++) r |= ((i >> b) & 1) << (K - 1 - b);
+          s->leaf_node[i] = ns.task_node[r];
+        }
+        continue;
+      }
       for (t = 0; t < N && ml > 0; t++) {
         long a, b, so, sl;
         emac_share *s;
@@ -622,6 +640,7 @@ int emac_node_shares(const emac_plan *p, const emac_node_sched *ns0, int me, ema
         s->len = sl;
         s->node = ns.task_node[u];
         s->nleaf = N;
+        s->nlev = 1;
         s->leaf_node[0] = ns.task_node[(t + N - 1) % N];
         s->leaf_node[1] = ns.task_node[t];
         for (i = 0; i < N - 2; i++) s->leaf_node[2 + i] = ns.task_node[(t + i + 1) % N];

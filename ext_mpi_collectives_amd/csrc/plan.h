@@ -187,19 +187,23 @@ int emac_comm_program_nodes(const emac_plan *p, const emac_node_sched *ns, int n
 /* The NODE form over peer-mapped nodes (engine.c node_ipc_init) runs the inter-node schedule as
    shares instead of point-to-point lines: one reduce-scatter step over every node (program_nodes'
    "single" flow: every element's value is ONE fold of the N node partials, in the order its line's
-   task gives, whoever computes it). emac_node_single: 1 for such a schedule, 2 for two nodes at one
-   port (the halving flow: the same sums, partner + own), else 0. */
+   task gives, whoever computes it); or one port per step over 2^k nodes (program_nodes' halving
+   flow: every value a balanced tree of pairwise sums over the task bits, high bit first -- the same
+   whoever computes each pair, for SUM, where a + b == b + a). emac_node_single: 1 for one step over
+   every node, 2 for the halving flow, else 0. */
 int emac_node_single(const emac_node_sched *ns);
 typedef struct {
   long off, len;                  /* elements of the message */
   int node;                       /* the node that folds this part (every node copies it back) */
   int nleaf;                      /* nodes whose partials it folds, in fold order */
+  int nlev;                       /* 1: a left fold of the leaves; k: k levels of pairs (halving) */
   int leaf_node[EMAC_MAX_NODES];
 } emac_share;
 /* The parts of node rank `me`'s chunk (every piece): node task_node[u] folds the u-th N-th of the
-   piece's chunk, cut at the line boundaries, each part with its line's leaf order (task t's line:
-   t - 1, t, t + 1, ..., t + N - 2 mod N, the last-step rule of raw_code.c). *out is malloc'd.
-   0 or an EMAC_ERR_* code. */
+   piece's chunk -- for one step over every node cut at the line boundaries, each part with its
+   line's leaf order (task t's line: t - 1, t, t + 1, ..., t + N - 2 mod N, the last-step rule of
+   raw_code.c); for the halving flow with the tasks in bit-reversed order, folded as k levels of
+   pairs. *out is malloc'd. 0 or an EMAC_ERR_* code. */
 int emac_node_shares(const emac_plan *p, const emac_node_sched *ns, int me, emac_share **out, int *nout);
 
 /* Build the plan of an nranks-rank Allreduce of `count` elements. 0 or an EMAC_ERR_* code. */

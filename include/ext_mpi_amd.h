@@ -219,8 +219,8 @@ int ext_mpi_amd_comm_set_nodes(int comm, int nodes);
  * (in the reference's line order), barrier, every share is pulled into the chunk owners' receive
  * buffers, and the copy-out follows. Only one reduce-scatter step over every node
  * (ext_mpi_amd_comm_set_node_ports(comm, size, {-(size-1), size-1, 0}), the default when size is
- * not a power of two) and two nodes at one port (SUM) are taken there; other lists return
- * EXT_MPI_AMD_ERROR_UNSUPPORTED on every member. No caller memory is exported: Done is local. */
+ * not a power of two) and, for SUM, one port per step over 2^k nodes (the default there) are
+ * taken there; other lists return EXT_MPI_AMD_ERROR_UNSUPPORTED on every member. No caller memory is exported: Done is local. */
 int ext_mpi_amd_node_comm_allreduce_init(int nranks, const void *const *sendbufs, void *const *recvbufs, long count,
                                          int dtype, int op, int comm, const char *copyin, int *handle);
 
@@ -228,10 +228,12 @@ int ext_mpi_amd_node_comm_allreduce_init(int nranks, const void *const *sendbufs
  * of `ranks_per_node`, under the inter-node list `ports` (0-terminated, NULL: the default) over
  * `nodes` nodes, each part of me's chunk as (off[i], len[i]) elements of the message, the node that
  * folds it (node[i]) and the nodes whose partials it folds, in order (leaf_nodes[i * nodes ..]).
- * Only one reduce-scatter step over every node, or two nodes at one port; else
+ * Only one reduce-scatter step over every node (every part a left fold: *levels = 1) or one port
+ * per step over 2^k nodes (every part k levels of pairs of consecutive leaves: *levels = k); else
  * EXT_MPI_AMD_ERROR_UNSUPPORTED. *nshares receives the count (ERROR_ARG if above max_shares). */
 int ext_mpi_amd_node_shares(int nodes, const int *ports, int ranks_per_node, long count, int dtype, const char *copyin,
-                            int me, long *off, long *len, int *node, int *leaf_nodes, int max_shares, int *nshares);
+                            int me, long *off, long *len, int *node, int *leaf_nodes, int max_shares, int *nshares,
+                            int *levels);
 
 /* EXT_MPI_NUM_SOCKETS_PER_NODE (src/mpi/ext_mpi.c:43-187, a process-wide parameter): sockets per
  * node for every handle / plan made afterwards. It moves the tree method's (7 / 10) last-step

@@ -51,17 +51,19 @@ def cases(N):
                 (emac.LONG, 77777, 2, "6;1 -2 2", single, emac.MAX, 1, False, False)]
     if N == 3:  # the default list for 3 nodes is the one step
         out += [(emac.FLOAT, 65539, 4, "6;1 -4 4", None, emac.SUM, 1, False, False)]
-    if N == 2:  # two nodes at one port (the default): the same sums
-        out += [(emac.DOUBLE, 65539, 4, "6;1 -4 4", None, emac.SUM, 1, False, False)]
+    if N & (N - 1) == 0:  # one port per step (the default for 2^k nodes): pairs over the task bits, SUM
+        out += [(emac.DOUBLE, 65539, 4, "6;1 -4 4", None, emac.SUM, 1, False, False),
+                (emac.FLOAT, 100003, 2, "6;1 -2 2", None, emac.SUM, 2, False, False),
+                (emac.FLOAT, 4 << 20, 8, "6;1 -8 8", None, emac.SUM, 1, False, False)]
     return out
 
 
 def unsupported(N):
-    """lists the peer-mapped join refuses (several steps, or MIN at one port): every node gets
-    ERROR_UNSUPPORTED from the same collective call and goes on"""
-    out = [(emac.FLOAT, 1000, 2, "6;1 -2 2", [-1, 1], emac.MIN)] if N == 2 else []
+    """lists the peer-mapped join refuses (MIN / MAX at one port per step, allgather steps that
+    reduce): every node gets ERROR_UNSUPPORTED from the same collective call and goes on"""
+    out = [(emac.FLOAT, 1000, 2, "6;1 -2 2", None, emac.MIN)] if N & (N - 1) == 0 else []
     if N == 4:
-        out += [(emac.FLOAT, 1000, 2, "6;1 -2 2", None, emac.SUM)]  # default: one port per step
+        out += [(emac.FLOAT, 1000, 2, "6;1 -2 2", [3], emac.SUM)]  # '4(3)': the allgather steps reduce
     return out
 
 

@@ -17,6 +17,8 @@ CASES = [
     (4, [-3, 3], 8, "6;1 -8 8"), (4, [-3, 3], 4, "6;1 -2 -2 2 2"), (5, [-4, 4], 3, "6;1 -3 3"),
     (6, [-5, 5], 2, "6;-64 -2 2"), (7, [-6, 6], 1, "6;1 -1 1"), (8, [-7, 7], 8, "6;1 -8 8"),
     (8, [-7, 7], 4, "7;1 -2 -2 2 2"), (3, [-2, 2], 4, "5;1 -4 4"), (4, [-3, 3], 4, "6;3 -4 4"),
+    # one port per step over 2^k nodes (the default list there): pairs over the task bits
+    (4, None, 4, "6;1 -4 4"), (8, None, 2, "6;1 -2 2"), (16, None, 2, "6;1 -2 2"), (4, [-1, -1, 1, 1], 3, "6;1 -3 3"),
 ]
 
 
@@ -27,13 +29,21 @@ def _node_join(sends, code, copyin, nodes, ports):
     out = np.empty_like(sends[0])
     cover = np.zeros(count, np.int32)
     for me in range(R):
-        for off, ln, who, leaves in emac.node_shares(nodes, ports, R, count, code, copyin, me):
+        levels, shares = emac.node_shares(nodes, ports, R, count, code, copyin, me)
+        for off, ln, who, leaves in shares:
             seg = slice(off, off + ln)
             assert 0 <= who < nodes and sorted(leaves) == list(range(nodes))
             with np.errstate(over="ignore"):
-                acc = part[leaves[0]][seg].copy()
-                for n in leaves[1:]:
-                    acc = acc + part[n][seg]
+                if levels == 1:  # a left fold in the listed order
+                    acc = part[leaves[0]][seg].copy()
+                    for n in leaves[1:]:
+                        acc = acc + part[n][seg]
+                else:  # levels of pairs of consecutive leaves
+                    vals = [part[n][seg] for n in leaves]
+                    for _ in range(levels):
+                        vals = [vals[2 * i] + vals[2 * i + 1] for i in range(len(vals) // 2)]
+                    assert len(vals) == 1
+                    acc = vals[0]
             out[seg] = acc
             cover[seg] += 1
     assert np.all(cover == 1), "the parts do not tile the message"
@@ -54,13 +64,16 @@ def test_node_shares_replay_equals_oracle(oracle, nodes, ports, R, copyin, code)
 
 
 def test_node_shares_balanced_and_refused():
-    """Every node folds an equal share (±1 element per piece); lists of several steps are refused."""
+    """Every node folds an equal share (±1 element per piece); lists of several steps that are not
+    one port each, or whose allgather steps reduce, are refused."""
     for nodes in (3, 4, 8):
         per = [0] * nodes
         for me in range(8):
-            for off, ln, who, _ in emac.node_shares(nodes, [-(nodes - 1), nodes - 1], 8, 1 << 20, emac.FLOAT, "6;1 -8 8", me):
+            for off, ln, who, _ in emac.node_shares(nodes, [-(nodes - 1), nodes - 1], 8, 1 << 20, emac.FLOAT, "6;1 -8 8",
+                                                    me)[1]:
                 per[who] += ln
         assert max(per) - min(per) <= 8, per
-    with pytest.raises(emac.ExtMpiError) as e:
-        emac.node_shares(4, [-1, -1, 1, 1], 2, 1000, emac.FLOAT, "6;1 -2 2", 0)
-    assert e.value.code == emac.ERROR_UNSUPPORTED
+    for ports in ([-1, -2, 2, 1], [-2, -1, 1, 2], [3]):  # several steps with larger radices, reducing allgathers
+        with pytest.raises(emac.ExtMpiError) as e:
+            emac.node_shares(6 if len(ports) > 1 else 4, ports, 2, 1000, emac.FLOAT, "6;1 -2 2", 0)
+        assert e.value.code == emac.ERROR_UNSUPPORTED
