@@ -1987,7 +1987,8 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
     }
   }
   for (me = 0, k = 0; me < R; me++) k += nsh[me];
-  if (!rc) rc = node_fold_codes(N, k && nsh[0] ? sh[0][0].nlev : 1, h->plan.dtype, &h->xcodes);
+  if (!rc) /* the halving flow folds log2 N levels of pairs, one step over every node a left fold */
+    rc = node_fold_codes(N, N > 1 && emac_node_single(&h->ns) == 2 ? h->ns.nsteps : 1, h->plan.dtype, &h->xcodes);
   if (!rc && !(b = (emac_bucket *)calloc((size_t)(k + h->plan.npieces * R) + 1, sizeof(emac_bucket)))) rc = EMAC_ERR_MALLOC;
   /* 1. the copy-in: every owner chunk into this node's partial block (at its message offset) */
   for (nb = 0, pc = 0; !rc && pc < h->plan.npieces; pc++)
