@@ -54,7 +54,8 @@ def cases(N):
     if N & (N - 1) == 0:  # one port per step (the default for 2^k nodes): pairs over the task bits, SUM
         out += [(emac.DOUBLE, 65539, 4, "6;1 -4 4", None, emac.SUM, 1, False, False),
                 (emac.FLOAT, 100003, 2, "6;1 -2 2", None, emac.SUM, 2, False, False),
-                (emac.FLOAT, 4 << 20, 8, "6;1 -8 8", None, emac.SUM, 1, False, False)]
+                (emac.FLOAT, 4 << 20, 8, "6;1 -8 8", None, emac.SUM, 1, False, False),
+                (emac.FLOAT, 100, 4, "6;-64 -4 4", None, emac.SUM, 1, False, False)]  # ranks with no elements
     return out
 
 
