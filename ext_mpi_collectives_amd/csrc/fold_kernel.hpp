@@ -287,10 +287,46 @@ constexpr int kDeferShift = 11;
 constexpr int defer_tiles(int issue) { return ((issue >> kDeferShift) & 3) ? 1 << ((issue >> kDeferShift) & 3) : 1; }
 constexpr int defer(int kb) { return (kb == 2 ? 1 : kb == 4 ? 2 : kb == 8 ? 3 : 0) << kDeferShift; }
 
-template <typename T, int OP, int N, int U, int CH, int D, int ISSUE>
-__device__ __forceinline__ void fold_deferred(const emac_bucket *bk, long tpb, long ngroups, const emac_codes &c) {
+// One group of fold_deferred: nt (<= KB) consecutive tiles of bucket b from vector gbase. ALL_FULL
+// (host-known: every tile of every bucket whole) skips the bucket's vector count -- a dependent
+// scalar load that would otherwise stand before the group's first leaf load.
+template <typename T, int OP, int N, int U, int CH, int D, int ISSUE, bool ALL_FULL>
+__device__ __forceinline__ void fold_group(const emac_bucket *b, long gbase, int nt, const emac_codes &c,
+                                           typename Lane<T>::V *res) {
   typedef typename Lane<T>::V V;
   typedef __attribute__((address_space(1))) V GV;
+  constexpr int KB = defer_tiles(ISSUE);
+  constexpr long TILE = (long)EMAC_BLOCK * U;
+  const long nvec = ALL_FULL ? 0 : b->nvec;
+#pragma unroll
+  for (int j = 0; j < KB; ++j) {
+    if (j < nt) {
+      const long tb = gbase + j * TILE;
+      V r[U];
+      if (ALL_FULL || tb + TILE <= nvec)
+        load_fold<T, OP, N, U, CH, true, ISSUE>(b, tb, nvec, c, r);
+      else
+        load_fold<T, OP, N, U, CH, false, ISSUE>(b, tb, nvec, c, r);
+#pragma unroll
+      for (int u = 0; u < U; ++u) res[(j * U + u) * EMAC_BLOCK + threadIdx.x] = r[u];
+    }
+  }
+  const long left = nvec - gbase;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    GV *dst = (GV *)b->dst[d] + gbase;
+#pragma unroll
+    for (int q = 0; q < KB * U; ++q) {
+      const unsigned v = threadIdx.x + (unsigned)(q * EMAC_BLOCK);
+      if (q < nt * U && (ALL_FULL || (long)v < left)) store_vec<V, ISSUE>(dst, v, res[q * EMAC_BLOCK + threadIdx.x]);
+    }
+  }
+}
+
+template <typename T, int OP, int N, int U, int CH, int D, int ISSUE>
+__device__ __forceinline__ void fold_deferred(const emac_bucket *bk, long tpb, long ngroups, int all_full,
+                                              const emac_codes &c) {
+  typedef typename Lane<T>::V V;
   constexpr int KB = defer_tiles(ISSUE);
   constexpr long TILE = (long)EMAC_BLOCK * U;
   __shared__ V res[KB * U * EMAC_BLOCK];
@@ -298,32 +334,11 @@ __device__ __forceinline__ void fold_deferred(const emac_bucket *bk, long tpb, l
   for (long g = blockIdx.x; g < ngroups; g += gridDim.x) {
     const int bi = (int)(g / gpb);
     const long t0 = (g - (long)bi * gpb) * KB;
-    const emac_bucket *b = bk + bi;
-    const long nvec = b->nvec, gbase = t0 * TILE;
     const int nt = tpb - t0 < KB ? (int)(tpb - t0) : KB;  // wave-uniform
-#pragma unroll
-    for (int j = 0; j < KB; ++j) {
-      if (j < nt) {
-        const long tb = gbase + j * TILE;
-        V r[U];
-        if (tb + TILE <= nvec)
-          load_fold<T, OP, N, U, CH, true, ISSUE>(b, tb, nvec, c, r);
-        else
-          load_fold<T, OP, N, U, CH, false, ISSUE>(b, tb, nvec, c, r);
-#pragma unroll
-        for (int u = 0; u < U; ++u) res[(j * U + u) * EMAC_BLOCK + threadIdx.x] = r[u];
-      }
-    }
-    const long left = nvec - gbase;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      GV *dst = (GV *)b->dst[d] + gbase;
-#pragma unroll
-      for (int q = 0; q < KB * U; ++q) {
-        const unsigned v = threadIdx.x + (unsigned)(q * EMAC_BLOCK);
-        if (q < nt * U && (long)v < left) store_vec<V, ISSUE>(dst, v, res[q * EMAC_BLOCK + threadIdx.x]);
-      }
-    }
+    if (all_full)
+      fold_group<T, OP, N, U, CH, D, ISSUE, true>(bk + bi, t0 * TILE, nt, c, res);
+    else
+      fold_group<T, OP, N, U, CH, D, ISSUE, false>(bk + bi, t0 * TILE, nt, c, res);
   }
 }
 
@@ -432,7 +447,9 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_kernel(const emac_bucket *__r
   if constexpr (defer_tiles(ISSUE) > 1) {
     static_assert(N > 0 && (ISSUE & kRemote) == 0, "deferred stores: compile-time leaves, local memory");
     if (tiles_per_bucket > 0) {  // equal buckets (the tuner offers the schedule only then)
-      fold_deferred<T, OP, N, U, CH, D, ISSUE>(bk, tiles_per_bucket, (long)nb * ((tiles_per_bucket + defer_tiles(ISSUE) - 1) / defer_tiles(ISSUE)), codes);
+      fold_deferred<T, OP, N, U, CH, D, ISSUE>(bk, tiles_per_bucket,
+                                               (long)nb * ((tiles_per_bucket + defer_tiles(ISSUE) - 1) / defer_tiles(ISSUE)),
+                                               all_full, codes);
       return;
     }
   }

@@ -257,7 +257,7 @@ int main(int argc, char **argv) {
   const long S = R * C;             // vectors per rank's message
   const long set_bytes = 2L * R * S * 16;
   const int nsets = (int)std::max<long>(2, (1024L << 20) / set_bytes + 1);
-  std::vector<emac_bucket *> dprod(nsets);
+  std::vector<emac_bucket *> dprod(nsets), dplocal(nsets);
   std::vector<Bk *> dvar(nsets), dloc(nsets);
   float *dummy;
   CHECK(hipMalloc(&dummy, 64));
@@ -280,6 +280,17 @@ int main(int argc, char **argv) {
     }
     CHECK(hipMalloc(&dprod[st], sizeof(emac_bucket) * R));
     CHECK(hipMemcpy(dprod[st], bk.data(), sizeof(emac_bucket) * R, hipMemcpyHostToDevice));
+    {  // the production kernel's local fold: one bucket, every rank's whole send buffer -> rank 0's receive buffer
+      emac_bucket pl;
+      memset(&pl, 0, sizeof(pl));
+      for (int t = 0; t < R; t++) pl.src[t] = sends[st * R + t];
+      pl.dst[0] = recvs[st * R];
+      pl.ndst = 1;
+      pl.count = S * 4;
+      pl.nvec = S;
+      CHECK(hipMalloc(&dplocal[st], sizeof(emac_bucket)));
+      CHECK(hipMemcpy(dplocal[st], &pl, sizeof(emac_bucket), hipMemcpyHostToDevice));
+    }
     Bk lb;  // the local fold: every rank's whole send buffer (8 leaves of S) -> rank 0's receive buffer
     for (int t = 0; t < R; t++) lb.src[t] = sends[st * R + t];
     for (int r = 0; r < R; r++) lb.dst[r] = recvs[st * R];
@@ -327,6 +338,8 @@ int main(int argc, char **argv) {
       {"local_burst_u2_k16", 63, 0, {}}, {"local_burst_u4_k8", 64, 0, {}},
       {"write_k4", 53, 0, {}}, {"copy_phased_u2_k4", 54, 0, {}}, {"copy_phased_u2_k8", 55, 0, {}},
       {"copy_phased_u4_k4_g512", 56, 512, {}},
+      {"plocal_u2", 70, 0, {}}, {"plocal_u4", 71, 0, {}}, {"plocal_u2_defer4", 72, 0, {}}, {"plocal_u4_defer4", 73, 0, {}},
+      {"pnode_u2_defer4", 74, 0, {}}, {"pnode_u4_defer2", 75, 0, {}},
       {"read_vgpr_k4", 50, 0, {}},     {"read_vgpr_k8", 51, 0, {}},    {"read_glds", 52, 0, {}}};
   auto run = [&](const V &v, int i) {
     const int st = i % nsets;
@@ -372,6 +385,31 @@ int main(int argc, char **argv) {
     case 54: hipLaunchKernelGGL((copy_phased<2, 4>), dim3((unsigned)std::min<long>(copy_n / 2048, 1L << 20)), dim3(256), 0, s, ca0, ca0 + copy_n, copy_n); break;
     case 55: hipLaunchKernelGGL((copy_phased<2, 8>), dim3((unsigned)std::min<long>(copy_n / 4096, 1L << 20)), dim3(256), 0, s, ca0, ca0 + copy_n, copy_n); break;
     case 56: hipLaunchKernelGGL((copy_phased<4, 4>), dim3(512), dim3(256), 0, s, ca0, ca0 + copy_n, copy_n); break;
+    case 70:
+    case 71:
+    case 72:
+    case 73: {
+      const int U = (v.id == 70 || v.id == 72) ? 2 : 4;
+      const long nt = S / (256L * U), groups = v.id >= 72 ? (nt + 3) / 4 : nt;
+      const unsigned grid = (unsigned)std::min<long>(groups, 8192);
+      if (v.id == 70)
+        hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 2, 0, 1, 1>), dim3(grid), dim3(256), 0, s, dplocal[st], 1, nt, nt, 1, codes, (const unsigned *)nullptr, R);
+      else if (v.id == 71)
+        hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 4, 0, 1, 1>), dim3(grid), dim3(256), 0, s, dplocal[st], 1, nt, nt, 1, codes, (const unsigned *)nullptr, R);
+      else if (v.id == 72)
+        hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 2, 0, 1, 1 | emac::defer(4)>), dim3(grid), dim3(256), 0, s, dplocal[st], 1, nt, nt, 1, codes, (const unsigned *)nullptr, R);
+      else
+        hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 4, 0, 1, 1 | emac::defer(4)>), dim3(grid), dim3(256), 0, s, dplocal[st], 1, nt, nt, 1, codes, (const unsigned *)nullptr, R);
+      break;
+    }
+    case 74:
+      hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 2, 0, R, 1 | emac::defer(4)>), dim3((unsigned)std::min<long>(n2 / 4, 8192)), dim3(256), 0, s, dprod[st], R,
+                         n2, t2, 1, codes, (const unsigned *)nullptr, R);
+      break;
+    case 75:
+      hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 4, 0, R, 1 | emac::defer(2)>), dim3((unsigned)std::min<long>(n4 / 2, 8192)), dim3(256), 0, s, dprod[st], R,
+                         n4, t4, 1, codes, (const unsigned *)nullptr, R);
+      break;
     case 50: hipLaunchKernelGGL((read_vgpr<4>), dim3(4096), dim3(256), 0, s, ca0, 2 * copy_n, dummy); break;
     case 51: hipLaunchKernelGGL((read_vgpr<8>), dim3(2048), dim3(256), 0, s, ca0, 2 * copy_n, dummy); break;
     case 52: hipLaunchKernelGGL(read_glds, dim3(2048), dim3(256), 0, s, ca0, 2 * copy_n, dummy); break;
@@ -387,7 +425,8 @@ int main(int argc, char **argv) {
       for (int r = 0; r < R; r++) CHECK(hipMemset(recvs[r], 0, S * 16));
       run(v, 0);
       CHECK(hipStreamSynchronize(s));
-      for (int r = 0; r < ((v.id >= 40 && v.id < 46) || v.id >= 63 ? 1 : R); r++) {  // the local folds write rank 0's buffer only
+      const bool loc = (v.id >= 40 && v.id < 46) || (v.id >= 63 && v.id < 74);
+      for (int r = 0; r < (loc ? 1 : R); r++) {  // the local folds write rank 0's buffer only
         CHECK(hipMemcpy(got.data(), recvs[r], S * 16, hipMemcpyDeviceToHost));
         if (memcmp(got.data(), want.data(), S * 16)) printf("MISMATCH %s rank %d\n", v.name.c_str(), r);
       }
@@ -415,7 +454,7 @@ int main(int argc, char **argv) {
   for (V &v : vs) {
     std::sort(v.us.begin(), v.us.end());
     const float med = v.us[v.us.size() / 2];
-    const bool local = (v.id >= 40 && v.id < 46) || v.id >= 63, rd = v.id >= 50 && v.id < 60;
+    const bool local = (v.id >= 40 && v.id < 46) || (v.id >= 63 && v.id < 74), rd = v.id >= 50 && v.id < 60;
     const double bytes = v.id == 53 ? 1.0 * copy_n * 16 : rd ? 2.0 * copy_n * 16 : local ? (R + 1.0) * S * 16 : 2.0 * R * S * 16;
     printf("%-18s %9.2f %9.2f %9.2f  %6.3f TB/s  %.3f of 8\n", v.name.c_str(), med, v.us.front(), v.us.back(),
            bytes / med / 1e6, bytes / med / 1e6 / 8.0);
