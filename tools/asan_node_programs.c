@@ -3,7 +3,9 @@
    gcc -fsanitize=address,undefined (no GPU, no preload):
      gcc -O1 -g -fsanitize=address,undefined -std=gnu11 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include \
        -Iinclude -Iext_mpi_collectives_amd/csrc ext_mpi_collectives_amd/csrc/plan.c tools/asan_node_programs.c
-   Round 2: 12376 programs, no report, no leak. */
+   Round 2: 12376 programs, no report, no leak. Round 3 adds the peer-mapped join's shares
+   (emac_node_shares) of every node rank under every list it takes, each checked to tile the
+   rank's chunk exactly once. */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -17,7 +19,7 @@ int main(void) {
   static const char *copyins[] = {"6;1 -1 1", "6;1 -2 2", "6;1 -4 4", "6;3 -2 2", "6;-5 -2 2", "7;1 -2 2"};
   static const int Rs[] = {1, 2, 4, 2, 2, 2};
   long counts[] = {0, 1, 5, 7, 1031, 4099, 65543};
-  int li, ci, k, node, me, n = 0;
+  int li, ci, k, node, me, n = 0, nsh_total = 0;
   for (li = 0; li < (int)(sizeof(nodes_of) / sizeof(int)); li++) {
     emac_node_sched ns;
     int rc = emac_node_sched_build(&ns, nodes_of[li], lists[li]);
@@ -37,9 +39,18 @@ int main(void) {
             if (emac_comm_program_nodes(&p, &ns, node, me, 4, &ops, &no, &folds, &nf, &st)) { printf("prog fail\n"); return 1; }
             free(ops); free(folds); n++;
           }
+        for (me = 0; me < Rs[ci] && emac_node_single(&ns); me++) {
+          emac_share *sh; int nsh, i, pc; long covered = 0, want = 0;
+          if (emac_node_shares(&p, &ns, me, &sh, &nsh)) { printf("shares fail\n"); return 1; }
+          for (pc = 0; pc < p.npieces; pc++) want += p.chunk_len[(size_t)pc * Rs[ci] + p.rank_pos[me]];
+          for (i = 0; i < nsh; i++) covered += sh[i].len;
+          if (covered != want) { printf("shares cover %ld of %ld (list %d)\n", covered, want, li); return 1; }
+          nsh_total += nsh;
+          free(sh);
+        }
         emac_plan_free(&p);
       }
   }
-  printf("programs %d\n", n);
+  printf("programs %d, shares %d\n", n, nsh_total);
   return 0;
 }
