@@ -470,7 +470,12 @@ def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=Non
             emac.comm_set_nodes(c, nodes, ports)
     phase = phase or [0] * R
     keep = []
-    if host:
+    if host == "pinned":  # page-locked host memory (staged through device mirrors like pageable memory)
+        sbufs = [torch.from_numpy(s.copy()).pin_memory() for s in sends]
+        rbufs = sbufs if in_place else [torch.full((count,), -1, dtype=TORCH[code]).pin_memory() for _ in sends]
+        keep += sbufs + rbufs
+        ptrs = [(s.data_ptr(), r.data_ptr()) for s, r in zip(sbufs, rbufs)]
+    elif host:
         sbufs = [s.copy() for s in sends]
         rbufs = sbufs if in_place else [np.full(count, -1, dtype=s.dtype) for s in sends]
         ptrs = [(s.ctypes.data, r.ctypes.data) for s, r in zip(sbufs, rbufs)]
@@ -503,6 +508,19 @@ def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=Non
         for c in comms:
             emac.comm_free(c)
     return [np.asarray(r) if host else r.cpu().numpy() for r in rbufs]
+
+
+@pytest.mark.parametrize("R,copyin,in_place", [(2, "6;1 -2 2", False), (4, "6;1 -2 -2 2 2", True),
+                                               (8, "6;1 -8 8", False), (3, "6;-64 -3 3", False)])
+@pytest.mark.parametrize("code", CODES)
+def test_comm_loopback_pinned_host_buffers(oracle, R, copyin, in_place, code):
+    """COMM form with page-locked host send / receive buffers (torch pin_memory), staged through
+    device mirrors on the handle's stream -- bitwise against the oracle, in place too."""
+    for count in (1, 1031, 65536 + 5):
+        sends = xorshift_inputs(R, count, code, seed_base=0x9140 + count)
+        want = oracle.allreduce(sends, copyin, in_place=in_place)
+        got = run_comm_loopback(sends, code, copyin, host="pinned", in_place=in_place)
+        assert_bitwise(got, want, f"pinned comm R={R} {copyin} code={code} n={count}")
 
 
 COMM_CONFIGS = [(2, "6;1 -2 2"), (3, "6;1 -3 3"), (4, "6;1 -2 -2 2 2"), (6, "6;1 -3 -2 2 3"), (8, "6;1 -8 8"),
