@@ -457,7 +457,7 @@ def test_every_tuned_schedule_bitwise(oracle, code, copyin):
 
 
 def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=None, op=emac.SUM, repeats=1, nodes=1,
-                      ports=None):
+                      ports=None, each=None):
     """COMM form (one rank per communicator) on the in-process loopback transport: the legs run
     on every rank in lock-step -- stage-in, reduce-scatter, fold, [the two-node legs,] all-gather,
     stage-out -- so the staging slots, fold buckets and leg programs of the multi-GPU path execute
@@ -502,12 +502,32 @@ def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=Non
                     emac.start_legs(h, leg)
                 for h in hs:
                     emac.wait(h)
+            if each is not None:  # every Start's results, with every rank's fold schedule
+                each(rep, [np.asarray(r) if host else r.cpu().numpy() for r in rbufs],
+                     [emac.handle_schedule(h) for h in hs])
     finally:
         for h in hs:
             emac.done(h)
         for c in comms:
             emac.comm_free(c)
     return [np.asarray(r) if host else r.cpu().numpy() for r in rbufs]
+
+
+def test_comm_form_tuned_fold_every_start(oracle):
+    """The COMM form's local fold (R staged slices of the owner chunk -> the receive buffer) is
+    tuned per handle like the NODE form's (engine.c emac_tune: per-tile and deferred-store
+    candidates, 3 rounds): 8 loopback ranks x 16 MiB float, every one of 20 Starts bitwise."""
+    R, count = 8, (16 << 20) // 4
+    sends = xorshift_inputs(R, count, emac.FLOAT, seed_base=0x7A11)
+    want = oracle.allreduce(sends, "6;1 -8 8")
+    seen = set()
+
+    def each(rep, got, scheds):
+        assert_bitwise(got, want, f"Start {rep}")
+        seen.update((sc["unroll"], sc["issue"], sc["tuned"]) for sc in scheds)
+
+    run_comm_loopback(sends, emac.FLOAT, "6;1 -8 8", repeats=20, each=each)
+    assert any(t == 1 for _, _, t in seen), seen  # the tuning finished and kept a schedule
 
 
 @pytest.mark.parametrize("R,copyin,in_place", [(2, "6;1 -2 2", False), (4, "6;1 -2 -2 2 2", True),
