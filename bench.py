@@ -597,6 +597,19 @@ def single_gpu(args):
                           "gbps_reduced": round(R * cnt * tsize * st / r["wall_s"] / 1e9, 2),
                           "checked": r["checked"]})
         extras["sweep_node_form"] = sweep
+        # BASELINE configs[4]'s EXT_MPI_COPYIN radix sweep on the node form (8 ranks in this GPU):
+        # the radix chains and the small-message -64 fractions from latency to bandwidth sizes
+        rsweep = []
+        for cp in ("6;1 -2 -2 -2 2 2 2", "6;1 -4 -2 2 4", "6;-64 -8 8"):
+            for nbytes in (8, 64 << 10, 1 << 20, 16 << 20):
+                cnt = max(1, nbytes // tsize)
+                st = 200 if nbytes <= (1 << 20) else 40
+                r = node_run(R, cnt, tdtype, code, cp, st, 5, min_set_bytes=0 if nbytes < (16 << 20) else 640 * MIB,
+                             alloc=args.alloc)
+                rsweep.append({"copyin": cp, "bytes_per_rank": cnt * tsize,
+                               "us_per_allreduce": round(r["wall_s"] * 1e6 / st, 2),
+                               "gpu_us_per_allreduce": round(r["event_ms"] * 1e3 / st, 2), "checked": r["checked"]})
+        extras["radix_sweep_node_form"] = rsweep
         # radix chains (compile-time fold trees) against the linear fold, measured alike and
         # alternated twice (median of each), so a drifting clock does not favour either
         chains, runs = {}, {}
