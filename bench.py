@@ -595,7 +595,7 @@ def single_gpu(args):
             sweep.append({"bytes_per_rank": cnt * tsize, "us_per_allreduce": round(r["wall_s"] * 1e6 / st, 2),
                           "gpu_us_per_allreduce": round(r["event_ms"] * 1e3 / st, 2),
                           "gbps_reduced": round(R * cnt * tsize * st / r["wall_s"] / 1e9, 2),
-                          "checked": r["checked"]})
+                          "checked": r["checked"], "fold_schedule": r.get("schedule")})
         extras["sweep_node_form"] = sweep
         # BASELINE configs[4]'s EXT_MPI_COPYIN radix sweep on the node form (8 ranks in this GPU):
         # the radix chains and the small-message -64 fractions from latency to bandwidth sizes
