@@ -287,9 +287,10 @@ constexpr int kDeferShift = 11;
 constexpr int defer_tiles(int issue) { return ((issue >> kDeferShift) & 3) ? 1 << ((issue >> kDeferShift) & 3) : 1; }
 constexpr int defer(int kb) { return (kb == 2 ? 1 : kb == 4 ? 2 : kb == 8 ? 3 : 0) << kDeferShift; }
 
-// One group of fold_deferred: nt (<= KB) consecutive tiles of bucket b from vector gbase. ALL_FULL
-// (host-known: every tile of every bucket whole) skips the bucket's vector count -- a dependent
-// scalar load that would otherwise stand before the group's first leaf load.
+// One group of fold_deferred_kernel: nt (<= KB) consecutive tiles of bucket b from vector gbase. ALL_FULL
+// (host-known: every tile of every bucket whole and every group KB tiles) skips the bucket's vector
+// count -- a dependent scalar load that would otherwise stand before the group's first leaf load --
+// and every guard on nt.
 template <typename T, int OP, int N, int U, int CH, int D, int ISSUE, bool ALL_FULL>
 __device__ __forceinline__ void fold_group(const emac_bucket *b, long gbase, int nt, const emac_codes &c,
                                            typename Lane<T>::V *res) {
@@ -300,7 +301,7 @@ __device__ __forceinline__ void fold_group(const emac_bucket *b, long gbase, int
   const long nvec = ALL_FULL ? 0 : b->nvec;
 #pragma unroll
   for (int j = 0; j < KB; ++j) {
-    if (j < nt) {
+    if (ALL_FULL || j < nt) {
       const long tb = gbase + j * TILE;
       V r[U];
       if (ALL_FULL || tb + TILE <= nvec)
@@ -318,27 +319,29 @@ __device__ __forceinline__ void fold_group(const emac_bucket *b, long gbase, int
 #pragma unroll
     for (int q = 0; q < KB * U; ++q) {
       const unsigned v = threadIdx.x + (unsigned)(q * EMAC_BLOCK);
-      if (q < nt * U && (ALL_FULL || (long)v < left)) store_vec<V, ISSUE>(dst, v, res[q * EMAC_BLOCK + threadIdx.x]);
+      if (ALL_FULL || (q < nt * U && (long)v < left)) store_vec<V, ISSUE>(dst, v, res[q * EMAC_BLOCK + threadIdx.x]);
     }
   }
 }
 
-template <typename T, int OP, int N, int U, int CH, int D, int ISSUE>
-__device__ __forceinline__ void fold_deferred(const emac_bucket *bk, long tpb, long ngroups, int all_full,
-                                              const emac_codes &c) {
+// The deferred-store schedule as a kernel of its own (equal buckets of tpb tiles: the tuner offers
+// the schedule only then), so its code holds nothing of the per-tile loop's.
+template <typename T, int OP, int N, int U, int CH, int D, int ISSUE, bool ALL_FULL>
+__global__ __launch_bounds__(EMAC_BLOCK) void fold_deferred_kernel(const emac_bucket *__restrict__ bk, long tpb,
+                                                                   long ngroups, emac_codes codes) {
   typedef typename Lane<T>::V V;
+  static_assert(N > 0 && (ISSUE & kRemote) == 0, "deferred stores: compile-time leaves, local memory");
   constexpr int KB = defer_tiles(ISSUE);
   constexpr long TILE = (long)EMAC_BLOCK * U;
   __shared__ V res[KB * U * EMAC_BLOCK];
-  const long gpb = (tpb + KB - 1) / KB;  // groups per bucket (the last one may hold fewer tiles)
+  // groups per bucket (the last one may hold fewer tiles); group counts fit 32 bits (< 2^31 groups
+  // of >= 8 KiB), and 32-bit division is a short sequence ahead of the group's first load
+  const unsigned gpb = (unsigned)((tpb + KB - 1) / KB);
   for (long g = blockIdx.x; g < ngroups; g += gridDim.x) {
-    const int bi = (int)(g / gpb);
+    const int bi = (int)((unsigned)g / gpb);
     const long t0 = (g - (long)bi * gpb) * KB;
     const int nt = tpb - t0 < KB ? (int)(tpb - t0) : KB;  // wave-uniform
-    if (all_full)
-      fold_group<T, OP, N, U, CH, D, ISSUE, true>(bk + bi, t0 * TILE, nt, c, res);
-    else
-      fold_group<T, OP, N, U, CH, D, ISSUE, false>(bk + bi, t0 * TILE, nt, c, res);
+    fold_group<T, OP, N, U, CH, D, ISSUE, ALL_FULL>(bk + bi, t0 * TILE, nt, codes, res);
   }
 }
 
@@ -444,15 +447,7 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_kernel(const emac_bucket *__r
   // the leaf loads and only waited for before the first store
   bool store = true;
   if constexpr ((ISSUE & kRemote) != 0) store = __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
-  if constexpr (defer_tiles(ISSUE) > 1) {
-    static_assert(N > 0 && (ISSUE & kRemote) == 0, "deferred stores: compile-time leaves, local memory");
-    if (tiles_per_bucket > 0) {  // equal buckets (the tuner offers the schedule only then)
-      fold_deferred<T, OP, N, U, CH, D, ISSUE>(bk, tiles_per_bucket,
-                                               (long)nb * ((tiles_per_bucket + defer_tiles(ISSUE) - 1) / defer_tiles(ISSUE)),
-                                               all_full, codes);
-      return;
-    }
-  }
+  static_assert(defer_tiles(ISSUE) == 1, "deferred stores: fold_deferred_kernel");
   for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     // bucket of this tile: arithmetic when every bucket has the same tile count (equal chunks:
     // the common case), else the last bucket whose first tile is <= tile (wave-uniform search;
@@ -667,11 +662,22 @@ struct Launch {
 template <typename T, int OP, int N, int U, int CH, int D, int ISSUE = 1>
 int launch_one(const Launch &L) {
   constexpr int KB = defer_tiles(ISSUE);
-  const long work = (KB > 1 && L.tpb > 0) ? (long)L.nb * ((L.tpb + KB - 1) / KB) : L.ntiles;  // deferred: one per group
-  const long grid = work < 8192 ? work : 8192;
-  if (grid > 0)
-    hipLaunchKernelGGL((fold_kernel<T, OP, N, U, CH, D, ISSUE>), dim3((unsigned)grid), dim3(EMAC_BLOCK), 0, L.s, L.b, L.nb,
-                       L.ntiles, L.tpb, L.all_full, *L.c, L.go, L.nrt);
+  if constexpr (KB > 1) {  // one workgroup per group of KB tiles
+    if (L.tpb <= 0) return launch_one<T, OP, N, U, CH, D, ISSUE & ~(3 << kDeferShift)>(L);  // unequal buckets
+    const long groups = (long)L.nb * ((L.tpb + KB - 1) / KB);
+    const unsigned grid = (unsigned)(groups < 8192 ? groups : 8192);
+    if (L.all_full && L.tpb % KB == 0)
+      hipLaunchKernelGGL((fold_deferred_kernel<T, OP, N, U, CH, D, ISSUE, true>), dim3(grid), dim3(EMAC_BLOCK), 0, L.s, L.b,
+                         L.tpb, groups, *L.c);
+    else
+      hipLaunchKernelGGL((fold_deferred_kernel<T, OP, N, U, CH, D, ISSUE, false>), dim3(grid), dim3(EMAC_BLOCK), 0, L.s, L.b,
+                         L.tpb, groups, *L.c);
+  } else {
+    const long grid = L.ntiles < 8192 ? L.ntiles : 8192;
+    if (grid > 0)
+      hipLaunchKernelGGL((fold_kernel<T, OP, N, U, CH, D, ISSUE>), dim3((unsigned)grid), dim3(EMAC_BLOCK), 0, L.s, L.b,
+                         L.nb, L.ntiles, L.tpb, L.all_full, *L.c, L.go, L.nrt);
+  }
   if (L.nedges > 0)
     hipLaunchKernelGGL((fold_edge_kernel<T, OP, N, CH, D, (ISSUE & kRemote) != 0>), dim3((unsigned)L.nedges),
                        dim3(EMAC_BLOCK), 0, L.s, L.b, L.edges, *L.c, L.go, L.nrt);

@@ -397,18 +397,18 @@ int main(int argc, char **argv) {
       else if (v.id == 71)
         hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 4, 0, 1, 1>), dim3(grid), dim3(256), 0, s, dplocal[st], 1, nt, nt, 1, codes, (const unsigned *)nullptr, R);
       else if (v.id == 72)
-        hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 2, 0, 1, 1 | emac::defer(4)>), dim3(grid), dim3(256), 0, s, dplocal[st], 1, nt, nt, 1, codes, (const unsigned *)nullptr, R);
+        hipLaunchKernelGGL((emac::fold_deferred_kernel<float, EMAC_SUM, R, 2, 0, 1, 1 | emac::defer(4), true>), dim3(grid), dim3(256), 0, s, dplocal[st], nt, groups, codes);
       else
-        hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 4, 0, 1, 1 | emac::defer(4)>), dim3(grid), dim3(256), 0, s, dplocal[st], 1, nt, nt, 1, codes, (const unsigned *)nullptr, R);
+        hipLaunchKernelGGL((emac::fold_deferred_kernel<float, EMAC_SUM, R, 4, 0, 1, 1 | emac::defer(4), true>), dim3(grid), dim3(256), 0, s, dplocal[st], nt, groups, codes);
       break;
     }
     case 74:
-      hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 2, 0, R, 1 | emac::defer(4)>), dim3((unsigned)std::min<long>(n2 / 4, 8192)), dim3(256), 0, s, dprod[st], R,
-                         n2, t2, 1, codes, (const unsigned *)nullptr, R);
+      hipLaunchKernelGGL((emac::fold_deferred_kernel<float, EMAC_SUM, R, 2, 0, R, 1 | emac::defer(4), true>), dim3((unsigned)std::min<long>(n2 / 4, 8192)), dim3(256), 0, s, dprod[st],
+                         t2, n2 / 4, codes);
       break;
     case 75:
-      hipLaunchKernelGGL((emac::fold_kernel<float, EMAC_SUM, R, 4, 0, R, 1 | emac::defer(2)>), dim3((unsigned)std::min<long>(n4 / 2, 8192)), dim3(256), 0, s, dprod[st], R,
-                         n4, t4, 1, codes, (const unsigned *)nullptr, R);
+      hipLaunchKernelGGL((emac::fold_deferred_kernel<float, EMAC_SUM, R, 4, 0, R, 1 | emac::defer(2), true>), dim3((unsigned)std::min<long>(n4 / 2, 8192)), dim3(256), 0, s, dprod[st],
+                         t4, n4 / 2, codes);
       break;
     case 50: hipLaunchKernelGGL((read_vgpr<4>), dim3(4096), dim3(256), 0, s, ca0, 2 * copy_n, dummy); break;
     case 51: hipLaunchKernelGGL((read_vgpr<8>), dim3(2048), dim3(256), 0, s, ca0, 2 * copy_n, dummy); break;
