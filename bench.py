@@ -85,6 +85,15 @@ def fill(t, seed):
         t.random_(-(1 << 20), (1 << 20), generator=g)
 
 
+DEFER_SHIFT = 11  # fold_kernel.hpp kDeferShift: issue bits 11-12 select the deferred-store kernel
+
+
+def fold_kernel_name(schedule):
+    """the kernel a fold schedule runs (fold_kernel.hpp launch_one): the per-tile loop, or
+    fold_deferred_kernel when the issue word carries deferred-store bits"""
+    return "fold_deferred_kernel" if schedule and (schedule.get("issue", 0) >> DEFER_SHIFT) & 3 else "fold_kernel"
+
+
 def traffic_from_profiles(tag):
     """HBM bytes per launch measured by rocprofv3 PMC (profiles/traffic_<tag>.json), or None."""
     path = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
@@ -537,7 +546,7 @@ def single_gpu(args):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": traffic_from_profiles(f"node_r{R}_{S // MIB}mib_{args.dtype}"),
-                     "kernel": "fold_kernel", "algorithmic_bytes_per_launch": algo_bytes,
+                     "kernel": fold_kernel_name(main["schedule"]), "algorithmic_bytes_per_launch": algo_bytes,
                      "avg_launch_us": round(kernel_s * 1e6, 2),
                      "guide_measured_copy": HBM_GUIDE_COPY_GBPS,
                      "frac_of_guide_measured_copy": round(achieved / HBM_GUIDE_COPY_GBPS, 4)},
@@ -1004,7 +1013,8 @@ def transport_child(args):
             # inside the N-GPU job, against the same kernel on rank 0's GPU while the others idle
             chunk = max(1, count // world)
             dist.barrier()
-            lf = torch.tensor([comm_shape_fold(world, chunk, tdtype, code, 100)["avg_launch_us"]], dtype=torch.float64)
+            lfr = comm_shape_fold(world, chunk, tdtype, code, 100)
+            lf = torch.tensor([lfr["avg_launch_us"]], dtype=torch.float64)
             dist.all_reduce(lf, op=dist.ReduceOp.MAX)
             dist.barrier()
             lf_alone = torch.zeros(1, dtype=torch.float64)
@@ -1014,7 +1024,7 @@ def transport_child(args):
             dist.broadcast(lf_alone, src=0)
             res["local_fold"] = {"leaves": world, "chunk_bytes": chunk * tsize, "us_all_gpus": lf.item(),
                                  "us_rank0_alone": lf_alone.item(),
-                                 "rate_retained": round(lf_alone.item() / lf.item(), 3)}
+                                 "rate_retained": round(lf_alone.item() / lf.item(), 3), "schedule": lfr["schedule"]}
         emac.done(h)
         send.free()
         recv.free()
@@ -1213,7 +1223,8 @@ def multi_gpu(args):
                        "transport": primary, "checked_vs_fp64_sum": checked},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                         "kernel": "fold_kernel (local fold: R leaves of the run's chunk -> 1, this GPU's HBM)",
+                         "kernel": f"{fold_kernel_name(lfd.get('schedule'))} (local fold: R leaves of the run's chunk -> 1, "
+                                   "this GPU's HBM)",
                          "algorithmic_bytes_per_launch": int(algo), "avg_launch_us": round(kl * 1e6, 2)},
             "extras": extras,
         }
@@ -1280,7 +1291,7 @@ def node_form_line(args, world, dname, rn, one_rank_per_gpu):
                    "checked_vs_fp64_sum": rn["checked"]},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                     "kernel": "fold_kernel (the node's copy-in: R leaves -> owner chunk, this GPU's HBM)",
+                     "kernel": f"{fold_kernel_name(rn.get('schedule'))} (the node's copy-in: R leaves -> owner chunk, this GPU's HBM)",
                      "algorithmic_bytes_per_launch": int(algo_in), "avg_launch_us": round(t_in * 1e6, 2)},
         "extras": extras,
     }

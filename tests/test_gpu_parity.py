@@ -410,7 +410,7 @@ DEFER_SHIFT = 11  # fold_kernel.hpp kDeferShift: deferred-store schedules (issue
 def test_every_tuned_schedule_bitwise(oracle, code, copyin):
     """The per-handle schedule tuner (engine.c emac_tune) runs every candidate on a handle's first
     Starts -- burst loads at U 2 / U 4, the staggered issue, and the deferred-store schedules
-    (fold_kernel.hpp fold_deferred: 2, 4 or 8 tiles folded into LDS, then stored in one burst) -- and
+    (fold_kernel.hpp fold_deferred_kernel: 2, 4 or 8 tiles folded into LDS, then stored in one burst) -- and
     keeps one. Every Start must give the oracle's bits: here a node form whose buckets end in a
     partial tile and whose last group of tiles is short (41000 elements per chunk), and a local
     fold (8 leaves -> 1, fold_init) of 512040 elements, each over all the Starts of its tuning."""

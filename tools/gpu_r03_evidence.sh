@@ -25,7 +25,7 @@ rm -rf gpurun_out/prof
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- \
   python3 $R/bench.py --no-cpu-baseline --no-extras > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err || exit $?
 cat gpurun_out/bench_prof.json
-f=$(find gpurun_out/prof -name "*kernel_stats.csv" | head -1); grep fold_kernel "$f"
-t=$(find gpurun_out/prof -name "*kernel_trace.csv" | head -1); python3 tools/prof_dispatches.py "$t" fold_kernel 5 > gpurun_out/bench_dispatches.txt
+f=$(find gpurun_out/prof -name "*kernel_stats.csv" | head -1); grep -E "fold_(deferred_)?kernel<" "$f"
+t=$(find gpurun_out/prof -name "*kernel_trace.csv" | head -1); python3 tools/prof_dispatches.py "$t" "fold_(deferred_)?kernel<" 5 > gpurun_out/bench_dispatches.txt
 cat gpurun_out/bench_dispatches.txt
 exit 0

@@ -6,14 +6,17 @@ Both counters are in KiB. Usage: pmc_traffic.py <fetch_dir> <write_dir> <out.jso
 import csv
 import glob
 import json
+import re
 import sys
+
+FOLD = re.compile(r"\bfold_(deferred_)?kernel<")  # the per-tile loop or the deferred-store kernel
 
 
 def per_dispatch(d, counter):
     vals = []
     for path in glob.glob(f"{d}/**/*counter_collection*.csv", recursive=True):
         for row in csv.DictReader(open(path)):
-            if "fold_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+            if FOLD.search(row.get("Kernel_Name", "")) and row.get("Counter_Name") == counter:
                 vals.append(float(row["Counter_Value"]))
     return vals
 
@@ -29,7 +32,7 @@ def main():
     w.sort()
     fetch = f[len(f) // 2] * 1024 * 2  # median dispatch, KiB -> B, x2 gfx950 correction
     write = w[len(w) // 2] * 1024
-    res = {"tag": tag, "kernel": "fold_kernel", "dispatches": [len(f), len(w)],
+    res = {"tag": tag, "kernel": "fold_kernel / fold_deferred_kernel", "dispatches": [len(f), len(w)],
            "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
            "hbm_bytes_per_launch": fetch + write,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; median dispatch; "

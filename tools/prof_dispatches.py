@@ -1,17 +1,18 @@
 """Per-dispatch durations of one kernel family from a rocprofv3 --kernel-trace CSV, grouped by
 (kernel name, grid size): which launch shape took how long, and the gaps between consecutive
 dispatches of the same group (launch-boundary cost). Usage:
-  prof_dispatches.py run_kernel_trace.csv [name-substring = fold_kernel] [min calls = 5]"""
+  prof_dispatches.py run_kernel_trace.csv [name regex = fold_(deferred_)?kernel<] [min calls = 5]"""
 import csv
+import re
 import statistics
 import sys
 
 
 def main():
     path = sys.argv[1]
-    sub = sys.argv[2] if len(sys.argv) > 2 else "fold_kernel"
+    sub = re.compile(sys.argv[2] if len(sys.argv) > 2 else r"\bfold_(deferred_)?kernel<")
     minc = int(sys.argv[3]) if len(sys.argv) > 3 else 5
-    rows = [r for r in csv.DictReader(open(path)) if sub in r["Kernel_Name"]]
+    rows = [r for r in csv.DictReader(open(path)) if sub.search(r["Kernel_Name"])]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     groups = {}
     for r in rows:
