@@ -101,6 +101,7 @@ def lib():
         L.ext_mpi_amd_stream.argtypes = [c_int]
         L.ext_mpi_amd_stream.restype = c_void_p
         L.ext_mpi_amd_handle_schedule.argtypes = [c_int, P(c_int), P(c_int), P(c_int)]
+        L.ext_mpi_amd_handle_candidates.argtypes = [c_int, P(c_int), P(c_int), c_int]
         L.ext_mpi_amd_plan_describe.argtypes = [c_int, c_long, c_int, ctypes.c_char_p, c_int, P(c_long),
                                                 P(c_long), c_int, P(c_int), P(c_int), P(ctypes.c_ubyte),
                                                 P(ctypes.c_ubyte), P(c_int)]
@@ -358,6 +359,13 @@ def handle_schedule(h):
     _check("ext_mpi_amd_handle_schedule", lib().ext_mpi_amd_handle_schedule(h, ctypes.byref(u), ctypes.byref(i),
                                                                            ctypes.byref(t)))
     return {"unroll": u.value, "issue": i.value, "tuned": t.value}
+
+
+def handle_candidates(h):
+    """The schedules the tuner measures on the handle's first Starts: [(unroll, issue)], [] untuned."""
+    n, sched = ctypes.c_int(), (ctypes.c_int * 16)()
+    _check("ext_mpi_amd_handle_candidates", lib().ext_mpi_amd_handle_candidates(h, ctypes.byref(n), sched, 16))
+    return [(sched[k] & 15, sched[k] >> 4) for k in range(min(n.value, 16))]
 
 
 def plan_describe(nranks, count, dtype, copyin, pos, max_pieces=4096):

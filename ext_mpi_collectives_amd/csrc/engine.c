@@ -429,8 +429,9 @@ static int upload_launch(const emac_handle *h, emac_launch *L, emac_bucket *b, i
   return upload_launch_as(h, L, b, nb, h->nsrc, emac_tree_kind(&h->plan.codes, h->plan.op) == 1);
 }
 
-/* the candidates of emac_tune for a fold of nsrc leaves, fan-out `fan` (0 / 1), or 0 */
-static int tune_candidates(const emac_handle *h, int *sched) {
+/* the candidates of emac_tune for a fold of nsrc leaves, fan-out `fan` (0 / 1), vec 16-byte vectors
+   per leaf over all buckets, or 0 */
+static int tune_candidates(const emac_handle *h, long vec, int *sched) {
   const char *e = getenv("EXT_MPI_AMD_AUTOTUNE");
   const char *g = getenv("EXT_MPI_AMD_GRAPH"); /* captured Starts replay one schedule */
   int n = 0;
@@ -442,14 +443,19 @@ static int tune_candidates(const emac_handle *h, int *sched) {
      s_sleep 2 every 4 loads); deferred stores (kDeferShift) when every bucket has the same tile
      count: (U 2, 4 tiles) and (U 4, 4 tiles) for one destination, (U 2, 4 tiles) and (U 4, 2
      tiles) for the fan-out, and (U 2, 8 tiles) for it too (the best at 16 MiB per rank on one lease,
-     profiles/r03_nodevar/nodevar_2048.txt, and 7 % behind at 32 MiB) */
+     profiles/r03_nodevar/nodevar_2048.txt, and 7 % behind at 32 MiB). A launch of fewer than 256
+     groups of (U 2, 4 tiles) -- under 8 MiB per leaf -- leaves CUs idle under the deferred
+     schedules; there (U 1, burst), twice the per-tile loop's workgroups, takes the place of (U 2,
+     8 tiles) */
+  const int small = vec < 256L * 4 * 2 * EMAC_BLOCK;
   sched[n++] = 2 | 1 << 4;
   sched[n++] = 4 | 1 << 4;
   if (h->fan) sched[n++] = 4 | 5 << 4;
+  if (small) sched[n++] = 1 | 1 << 4;
   if (h->tiles_per_bucket > 0) {
     sched[n++] = 2 | (1 | 2 << 11) << 4;
     sched[n++] = 4 | (1 | (h->fan ? 1 : 2) << 11) << 4;
-    if (h->fan) sched[n++] = 2 | (1 | 3 << 11) << 4;
+    if (h->fan && !small) sched[n++] = 2 | (1 | 3 << 11) << 4;
   }
   return n;
 }
@@ -470,7 +476,7 @@ static int upload_buckets(emac_handle *h, emac_bucket *b, int nb) {
     rc = emac_gpu_memcpy(h->d_edges, edges, sizeof(emac_edge) * (size_t)h->nedges);
   free(edges);
   for (i = 0; i < nb; i++) vec += b[i].nvec;
-  nc = rc ? 0 : tune_candidates(h, sched);
+  nc = rc ? 0 : tune_candidates(h, vec, sched);
   if (!nc || vec * 16 * (h->nsrc + (h->fan ? h->nsrc : 1)) < EMAC_TUNE_MIN_BYTES) return rc;
   {
     emac_bucket *tb = (emac_bucket *)malloc(sizeof(emac_bucket) * (size_t)nb);
@@ -581,6 +587,15 @@ int ext_mpi_amd_handle_schedule(int handle, int *unroll, int *issue, int *tuned)
   if (unroll) *unroll = h->unroll & 15;
   if (issue) *issue = h->unroll >> 4;
   if (tuned) *tuned = h->tune.n ? (h->tune.chosen >= 0 ? 1 : 0) : -1;
+  return 0;
+}
+
+int ext_mpi_amd_handle_candidates(int handle, int *n, int *sched, int max) {
+  const emac_handle *h = (handle >= 0 && handle < MAX_HANDLES) ? handles[handle] : NULL;
+  int k;
+  if (!h || !n || (max > 0 && !sched)) return EMAC_ERR_ARG;
+  *n = h->tune.n;
+  for (k = 0; k < h->tune.n && k < max; k++) sched[k] = h->tune.L[k].unroll;
   return 0;
 }
 

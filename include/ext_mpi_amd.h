@@ -123,6 +123,9 @@ void *ext_mpi_amd_stream(int handle); /* hipStream_t the handle runs on */
  * whether it was tuned on this handle's first Starts (1 kept, 0 still measuring, -1 not tuned:
  * EXT_MPI_AMD_AUTOTUNE=0 or a shape with one schedule). Introspection for benchmarks. */
 int ext_mpi_amd_handle_schedule(int handle, int *unroll, int *issue, int *tuned);
+/* The schedules the tuner measures on this handle's first Starts: *n of them (0: untuned), the
+ * first min(*n, max) written to sched as U | issue << 4. Introspection for tests. */
+int ext_mpi_amd_handle_candidates(int handle, int *n, int *sched, int max);
 /* Run later Starts on a caller-owned hipStream_t (e.g. to serialise several handles). */
 int ext_mpi_amd_set_stream(int handle, void *hip_stream);
 /* Start a subset of the legs (benchmarking / profiling): the reference interleaves them in one

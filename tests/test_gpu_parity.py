@@ -412,29 +412,34 @@ def test_every_tuned_schedule_bitwise(oracle, code, copyin):
     Starts -- burst loads at U 2 / U 4, the staggered issue, and the deferred-store schedules
     (fold_kernel.hpp fold_deferred_kernel: 2, 4 or 8 tiles folded into LDS, then stored in one burst) -- and
     keeps one. Every Start must give the oracle's bits: here a node form whose buckets end in a
-    partial tile and whose last group of tiles is short (41000 elements per chunk), and a local
+    partial tile and whose last group of tiles is short (41000 elements per chunk: under 8 MiB per
+    leaf, so (U 1, burst) among the candidates; 262147: above, so (U 2, 8 tiles)), and a local
     fold (8 leaves -> 1, fold_init) of 512040 elements, each over all the Starts of its tuning."""
-    R, chunk = 8, 41000 if code == emac.FLOAT else 20500
-    count = R * chunk
-    sends = xorshift_inputs(R, count, code, seed_base=0x7E57)
-    want = oracle.allreduce(sends, copyin)
-    dsend = [_dev(x) for x in sends]
-    drecv = [torch.full((count,), -1, dtype=TORCH[code], device="cuda") for _ in range(R)]
-    h = emac.node_allreduce_init([t.data_ptr() for t in dsend], [t.data_ptr() for t in drecv], count, code, copyin)
-    seen = set()
-    try:
-        for k in range(22):
-            for t in drecv:
-                t.fill_(-1)
-            torch.cuda.synchronize()
-            emac.start(h)
-            emac.wait(h)
-            sc = emac.handle_schedule(h)
-            seen.add((sc["unroll"], sc["issue"], sc["tuned"]))
-            assert_bitwise([t.cpu().numpy() for t in drecv], want, f"node {copyin} Start {k} {sc}")
-    finally:
-        emac.done(h)
-    assert any(t == 1 for _, _, t in seen), seen
+    R = 8
+    for chunk in ((41000, 262147) if code == emac.FLOAT else (20500, 131075)):
+        count = R * chunk
+        sends = xorshift_inputs(R, count, code, seed_base=0x7E57 + chunk)
+        want = oracle.allreduce(sends, copyin)
+        dsend = [_dev(x) for x in sends]
+        drecv = [torch.full((count,), -1, dtype=TORCH[code], device="cuda") for _ in range(R)]
+        h = emac.node_allreduce_init([t.data_ptr() for t in dsend], [t.data_ptr() for t in drecv], count, code, copyin)
+        cands = emac.handle_candidates(h)
+        seen = set()
+        try:
+            for k in range(22):
+                for t in drecv:
+                    t.fill_(-1)
+                torch.cuda.synchronize()
+                emac.start(h)
+                emac.wait(h)
+                sc = emac.handle_schedule(h)
+                seen.add((sc["unroll"], sc["issue"], sc["tuned"]))
+                assert_bitwise([t.cpu().numpy() for t in drecv], want, f"node {copyin} chunk {chunk} Start {k} {sc}")
+        finally:
+            emac.done(h)
+        assert any(t == 1 for _, _, t in seen), seen
+        small = chunk * R * sends[0].itemsize < 8 << 20
+        assert ((1, 1) in cands) == small and ((2, 1 | 3 << DEFER_SHIFT) in cands) != small, (chunk, cands)
     # the local fold: one destination, one bucket
     n = 8 * 64000 + 40 if code == emac.FLOAT else 4 * 64000 + 20
     srcs_np = xorshift_inputs(R, n, code, seed_base=0x10CA1)
