@@ -133,6 +133,36 @@ __global__ __launch_bounds__(256) void lfold_burst(const Bk *__restrict__ b, lon
   }
 }
 
+// leaf-major groups: a workgroup's KB consecutive tiles are read leaf after leaf (each leaf's
+// KB * U vectors back to back: KB * U KiB contiguous per wave) and accumulated in registers in the
+// leaves' order (the linear fold's bits), then stored to every destination in one burst
+template <int U, int KB, int D>
+__global__ __launch_bounds__(256) void fold_leafmajor(const Bk *__restrict__ bk, int nb, long tpb) {
+  constexpr long TILE = 256L * U;
+  const long ngroups = tpb / KB * nb;
+  for (long g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const int bi = (int)((unsigned)g / (unsigned)(tpb / KB));
+    const long base = ((long)g - (long)bi * (tpb / KB)) * KB * TILE;
+    const Bk *b = bk + bi;
+    f4 acc[KB * U];
+#pragma unroll
+    for (int q = 0; q < KB * U; ++q) acc[q] = __builtin_nontemporal_load((const G4 *)b->src[0] + base + q * 256 + threadIdx.x);
+#pragma unroll
+    for (int s = 1; s < R; ++s) {
+      f4 x[KB * U];
+#pragma unroll
+      for (int q = 0; q < KB * U; ++q) x[q] = __builtin_nontemporal_load((const G4 *)b->src[s] + base + q * 256 + threadIdx.x);
+#pragma unroll
+      for (int q = 0; q < KB * U; ++q) acc[q] = acc[q] + x[q];
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+      for (int q = 0; q < KB * U; ++q)
+        __builtin_nontemporal_store(acc[q], (G4 *)b->dst[d] + base + q * 256 + threadIdx.x);
+  }
+}
+
 // the node fold with its stores deferred: KB consecutive tiles of one bucket folded into LDS,
 // then written to all R destinations in one burst
 template <int U, int KB>
@@ -340,6 +370,10 @@ int main(int argc, char **argv) {
       {"copy_phased_u4_k4_g512", 56, 512, {}},
       {"plocal_u2", 70, 0, {}}, {"plocal_u4", 71, 0, {}}, {"plocal_u2_defer4", 72, 0, {}}, {"plocal_u4_defer4", 73, 0, {}},
       {"pnode_u2_defer4", 74, 0, {}}, {"pnode_u4_defer2", 75, 0, {}},
+      {"node_leaf_u2_k4", 80, 0, {}}, {"node_leaf_u2_k8", 81, 0, {}}, {"node_leaf_u4_k4", 82, 0, {}},
+      {"node_leaf_u1_k8", 86, 0, {}},
+      {"local_leaf_u2_k4", 83, 0, {}}, {"local_leaf_u2_k8", 84, 0, {}}, {"local_leaf_u4_k4", 85, 0, {}},
+      {"local_leaf_u1_k8", 87, 0, {}},
       {"read_vgpr_k4", 50, 0, {}},     {"read_vgpr_k8", 51, 0, {}},    {"read_glds", 52, 0, {}}};
   auto run = [&](const V &v, int i) {
     const int st = i % nsets;
@@ -410,6 +444,14 @@ int main(int argc, char **argv) {
       hipLaunchKernelGGL((emac::fold_deferred_kernel<float, EMAC_SUM, R, 4, 0, R, 1 | emac::defer(2), true>), dim3((unsigned)std::min<long>(n4 / 2, 8192)), dim3(256), 0, s, dprod[st],
                          t4, n4 / 2, codes);
       break;
+    case 80: hipLaunchKernelGGL((fold_leafmajor<2, 4, R>), dim3(g(n2 / 4)), dim3(256), 0, s, dvar[st], R, t2); break;
+    case 81: hipLaunchKernelGGL((fold_leafmajor<2, 8, R>), dim3(g(n2 / 8)), dim3(256), 0, s, dvar[st], R, t2); break;
+    case 82: hipLaunchKernelGGL((fold_leafmajor<4, 4, R>), dim3(g(n4 / 4)), dim3(256), 0, s, dvar[st], R, t4); break;
+    case 86: hipLaunchKernelGGL((fold_leafmajor<1, 8, R>), dim3(g(2 * n2 / 8)), dim3(256), 0, s, dvar[st], R, 2 * t2); break;
+    case 83: hipLaunchKernelGGL((fold_leafmajor<2, 4, 1>), dim3(g(lt1 / 8)), dim3(256), 0, s, dloc[st], 1, lt1 / 2); break;
+    case 84: hipLaunchKernelGGL((fold_leafmajor<2, 8, 1>), dim3(g(lt1 / 16)), dim3(256), 0, s, dloc[st], 1, lt1 / 2); break;
+    case 85: hipLaunchKernelGGL((fold_leafmajor<4, 4, 1>), dim3(g(lt1 / 16)), dim3(256), 0, s, dloc[st], 1, lt1 / 4); break;
+    case 87: hipLaunchKernelGGL((fold_leafmajor<1, 8, 1>), dim3(g(lt1 / 8)), dim3(256), 0, s, dloc[st], 1, lt1); break;
     case 50: hipLaunchKernelGGL((read_vgpr<4>), dim3(4096), dim3(256), 0, s, ca0, 2 * copy_n, dummy); break;
     case 51: hipLaunchKernelGGL((read_vgpr<8>), dim3(2048), dim3(256), 0, s, ca0, 2 * copy_n, dummy); break;
     case 52: hipLaunchKernelGGL(read_glds, dim3(2048), dim3(256), 0, s, ca0, 2 * copy_n, dummy); break;
@@ -425,7 +467,7 @@ int main(int argc, char **argv) {
       for (int r = 0; r < R; r++) CHECK(hipMemset(recvs[r], 0, S * 16));
       run(v, 0);
       CHECK(hipStreamSynchronize(s));
-      const bool loc = (v.id >= 40 && v.id < 46) || (v.id >= 63 && v.id < 74);
+      const bool loc = (v.id >= 40 && v.id < 46) || (v.id >= 63 && v.id < 74) || (v.id >= 83 && v.id <= 85) || v.id == 87;
       for (int r = 0; r < (loc ? 1 : R); r++) {  // the local folds write rank 0's buffer only
         CHECK(hipMemcpy(got.data(), recvs[r], S * 16, hipMemcpyDeviceToHost));
         if (memcmp(got.data(), want.data(), S * 16)) printf("MISMATCH %s rank %d\n", v.name.c_str(), r);
@@ -454,7 +496,7 @@ int main(int argc, char **argv) {
   for (V &v : vs) {
     std::sort(v.us.begin(), v.us.end());
     const float med = v.us[v.us.size() / 2];
-    const bool local = (v.id >= 40 && v.id < 46) || (v.id >= 63 && v.id < 74), rd = v.id >= 50 && v.id < 60;
+    const bool local = (v.id >= 40 && v.id < 46) || (v.id >= 63 && v.id < 74) || (v.id >= 83 && v.id <= 85) || v.id == 87, rd = v.id >= 50 && v.id < 60;
     const double bytes = v.id == 53 ? 1.0 * copy_n * 16 : rd ? 2.0 * copy_n * 16 : local ? (R + 1.0) * S * 16 : 2.0 * R * S * 16;
     printf("%-18s %9.2f %9.2f %9.2f  %6.3f TB/s  %.3f of 8\n", v.name.c_str(), med, v.us.front(), v.us.back(),
            bytes / med / 1e6, bytes / med / 1e6 / 8.0);
