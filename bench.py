@@ -163,7 +163,7 @@ def host_random(count, np_dtype, seed):
     return rng.integers(-lim, lim, count).astype(np_dtype)
 
 
-TUNE_STARTS = 20  # a handle's first Start, 3 rounds of at most 6 tuned candidates, and the one that keeps the best
+TUNE_STARTS = 56  # a handle's first Start, 3 rounds of at most 6 candidates on three Starts each, and the keeping one
 
 
 def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * MIB, host=False, alloc="torch"):

@@ -150,9 +150,19 @@ typedef struct {
    spread within one (16 MiB x 8 node fold: U 2 48.1 us, U 4 51.8, U 4 staggered 54.1 on one
    lease; U 2 47.1, U 4 46.2 on another), so no fixed threshold table picks it everywhere; one
    sample per candidate (round 3's first tuner) kept U 2 on a lease where U 4 was 2 % faster, hence
-   the rounds. EXT_MPI_AMD_AUTOTUNE=0 keeps the static pick. */
+   the rounds. A sample runs one candidate on EMAC_TUNE_SPAN Starts in a row: the first, right
+   after another schedule's launch, untimed, the others timed as one window with no event between
+   them, on events without the system-scope fence (hipEventDisableSystemFence): a single launch
+   between two fenced events ranked the schedules against their back-to-back rate (the leaf-major
+   deferred schedule 46-47 us alone, 43.9-44.4 us per Start in the bench's steady state, where the
+   tile-major one it lost to ran 45.5-46.4 us; profiles/r03_tune/force_ab.txt). Where the caller
+   interleaves several handles the window also holds their launches; every candidate sees the same
+   pattern. EXT_MPI_AMD_AUTOTUNE=0
+   keeps the static pick; EXT_MPI_AMD_FOLD_SCHEDULE=<U | issue << 4> makes one schedule the only
+   candidate (A/B runs). */
 #define EMAC_TUNE_MAX 6
 #define EMAC_TUNE_ROUNDS 3
+#define EMAC_TUNE_SPAN 3 /* Starts per sample: one untimed, then the timed window */
 #define EMAC_TUNE_MIN_BYTES (16L << 20) /* algorithmic bytes per launch: smaller launches keep the static pick */
 typedef struct {
   int n;      /* candidates (0: no tuning) */
@@ -441,21 +451,29 @@ static int tune_candidates(const emac_handle *h, long vec, int *sched) {
     return 0;
   /* fold_kernel.hpp instantiation policy: (U 2, burst), (U 4, burst), for the node fan-out (U 4,
      s_sleep 2 every 4 loads); deferred stores (kDeferShift) when every bucket has the same tile
-     count: (U 2, 4 tiles) and (U 4, 4 tiles) for one destination, (U 2, 4 tiles) and (U 4, 2
-     tiles) for the fan-out, and (U 2, 8 tiles) for it too (the best at 16 MiB per rank on one lease,
-     profiles/r03_nodevar/nodevar_2048.txt, and 7 % behind at 32 MiB). A launch of fewer than 256
-     groups of (U 2, 4 tiles) -- under 8 MiB per leaf -- leaves CUs idle under the deferred
-     schedules; there (U 1, burst), twice the per-tile loop's workgroups, takes the place of (U 2,
-     8 tiles) */
+     count: (U 2, 4 tiles) and (U 4, 4 tiles) for one destination, (U 2, 4 tiles) and, for the
+     fan-out, its leaf-major form (kLeafMajor) over the linear fold or (U 4, 2 tiles) over fold
+     trees. A launch of fewer than 256 groups of (U 2, 4 tiles) -- under 8 MiB per leaf -- leaves
+     CUs idle under the deferred schedules; there (U 1, burst), twice the per-tile loop's
+     workgroups, is offered too. (U 2, 8 tiles), compiled, is no longer offered: never kept. */
   const int small = vec < 256L * 4 * 2 * EMAC_BLOCK;
+  const char *f = getenv("EXT_MPI_AMD_FOLD_SCHEDULE"); /* A/B runs: one schedule word, U | issue << 4 */
+  if (f && atoi(f) > 0) {
+    sched[0] = atoi(f);
+    return 1;
+  }
   sched[n++] = 2 | 1 << 4;
   sched[n++] = 4 | 1 << 4;
   if (h->fan) sched[n++] = 4 | 5 << 4;
   if (small) sched[n++] = 1 | 1 << 4;
   if (h->tiles_per_bucket > 0) {
     sched[n++] = 2 | (1 | 2 << 11) << 4;
-    sched[n++] = 4 | (1 | (h->fan ? 1 : 2) << 11) << 4;
-    if (h->fan && !small) sched[n++] = 2 | (1 | 3 << 11) << 4;
+    if (!h->fan)
+      sched[n++] = 4 | (1 | 2 << 11) << 4;
+    else if (emac_tree_kind(&h->plan.codes, h->plan.op) == 0)
+      sched[n++] = 2 | (1 | 2 << 11 | 1 << 13) << 4; /* leaf-major groups: the linear fold's order only */
+    else
+      sched[n++] = 4 | (1 | 1 << 11) << 4;
   }
   return n;
 }
@@ -523,20 +541,24 @@ static int fold_launch(emac_handle *h) {
   int rc, k;
   if (t->n && t->chosen < 0) {
     const int s = t->starts++, nsamples = t->n * EMAC_TUNE_ROUNDS;
-    if (s >= 1 && s <= nsamples) { /* sample s - 1: candidate (s - 1) % n, timed */
-      const emac_launch *L = &t->L[(s - 1) % t->n];
-      if ((rc = emac_gpu_event_record(t->ev[s - 1][0], h->stream))) return rc;
+    if (s >= 1 && s <= EMAC_TUNE_SPAN * nsamples) {
+      /* sample p: candidate p % n on EMAC_TUNE_SPAN Starts in a row, the first untimed (it follows
+         another schedule's launch), the others timed as one window */
+      const int p = (s - 1) / EMAC_TUNE_SPAN, pos = (s - 1) % EMAC_TUNE_SPAN;
+      const emac_launch *L = &t->L[p % t->n];
+      if (pos == 1 && (rc = emac_gpu_event_record(t->ev[p][0], h->stream))) return rc;
       if ((rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, h->fan, L->unroll, &h->plan.codes, L->d_buckets, L->nb,
                               L->ntiles, L->tiles_per_bucket, L->all_full, L->d_edges, L->nedges, h->stream)))
         return rc;
-      return emac_gpu_event_record(t->ev[s - 1][1], h->stream);
+      return pos == EMAC_TUNE_SPAN - 1 ? emac_gpu_event_record(t->ev[p][1], h->stream) : 0;
     }
-    if (s == nsamples + 1) { /* keep the fastest: it becomes the handle's launch */
+    if (s == EMAC_TUNE_SPAN * nsamples + 1) { /* keep the fastest: it becomes the handle's launch */
       int best = 0, i;
       for (k = 0; k < t->n; k++) t->us[k] = 1e30f;
       for (i = 0; i < nsamples; i++) {
         float us;
         if ((rc = emac_gpu_event_elapsed_us(t->ev[i][0], t->ev[i][1], &us))) return rc;
+        us /= EMAC_TUNE_SPAN - 1;
         if (us < t->us[i % t->n]) t->us[i % t->n] = us;
       }
       for (k = 1; k < t->n; k++)

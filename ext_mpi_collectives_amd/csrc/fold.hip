@@ -299,7 +299,10 @@ int emac_gpu_event_create(void **ev) {
 }
 int emac_gpu_event_create_timed(void **ev) {
   hipEvent_t e;
-  if (hipEventCreate(&e) != hipSuccess) return EMAC_ERR_DEVICE;
+  /* timing only (the tuner's samples): no system-scope fence on record -- the default event's
+     cache writeback and invalidate would sit between the launches it brackets and change how
+     they run (the deferred-store schedules most) */
+  if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return EMAC_ERR_DEVICE;
   *ev = e;
   return 0;
 }

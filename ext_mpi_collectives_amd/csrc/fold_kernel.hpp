@@ -286,6 +286,13 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
 constexpr int kDeferShift = 11;
 constexpr int defer_tiles(int issue) { return ((issue >> kDeferShift) & 3) ? 1 << ((issue >> kDeferShift) & 3) : 1; }
 constexpr int defer(int kb) { return (kb == 2 ? 1 : kb == 4 ? 2 : kb == 8 ? 3 : 0) << kDeferShift; }
+// ISSUE bit 13 (with deferred stores, linear fold only): leaf-major groups. The group's KB * U
+// vectors per lane are read leaf after leaf -- each leaf's KB * U KiB per wave back to back -- and
+// accumulated in registers in the leaves' order, ((x0 + x1) + x2) + ..., the linear fold's bits;
+// no LDS, 80 VGPRs at KB * U = 8 (occupancy 6 against 4). The node fan-out only: 3.5-4.5 % faster
+// than the LDS groups per Start in the bench's steady state at 16 MiB per rank
+// (profiles/r03_tune/force_ab.txt).
+constexpr int kLeafMajor = 1 << 13;
 
 // One group of fold_deferred_kernel: nt (<= KB) consecutive tiles of bucket b from vector gbase. ALL_FULL
 // (host-known: every tile of every bucket whole and every group KB tiles) skips the bucket's vector
@@ -324,6 +331,44 @@ __device__ __forceinline__ void fold_group(const emac_bucket *b, long gbase, int
   }
 }
 
+// One leaf-major group (kLeafMajor): vector q of the group is lane vector q * EMAC_BLOCK + lane
+// from gbase (the KB tiles of U vectors are contiguous).
+template <typename T, int OP, int N, int U, int D, int ISSUE, bool ALL_FULL>
+__device__ __forceinline__ void fold_group_leaf(const emac_bucket *b, long gbase, int nt) {
+  typedef typename Lane<T>::V V;
+  typedef __attribute__((address_space(1))) V GV;
+  constexpr int Q = defer_tiles(ISSUE) * U;
+  const long left = ALL_FULL ? 0 : b->nvec - gbase;
+  auto in = [&](int q) {  // wave-uniform but for the bucket's last partial tile
+    return ALL_FULL || (q < nt * U && (long)(threadIdx.x + (unsigned)(q * EMAC_BLOCK)) < left);
+  };
+  V acc[Q];
+  {
+    const GV *src = (const GV *)b->src[0] + gbase;
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+      if (in(q)) acc[q] = __builtin_nontemporal_load(src + threadIdx.x + (unsigned)(q * EMAC_BLOCK));
+  }
+#pragma unroll
+  for (int s = 1; s < N; ++s) {
+    const GV *src = (const GV *)b->src[s] + gbase;
+    V x[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+      if (in(q)) x[q] = __builtin_nontemporal_load(src + threadIdx.x + (unsigned)(q * EMAC_BLOCK));
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+      if (in(q)) acc[q] = combine<OP, T>(acc[q], x[q]);
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    GV *dst = (GV *)b->dst[d] + gbase;
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+      if (in(q)) store_vec<V, ISSUE>(dst, threadIdx.x + (unsigned)(q * EMAC_BLOCK), acc[q]);
+  }
+}
+
 // The deferred-store schedule as a kernel of its own (equal buckets of tpb tiles: the tuner offers
 // the schedule only then), so its code holds nothing of the per-tile loop's.
 template <typename T, int OP, int N, int U, int CH, int D, int ISSUE, bool ALL_FULL>
@@ -331,9 +376,11 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_deferred_kernel(const emac_bu
                                                                    long ngroups, emac_codes codes) {
   typedef typename Lane<T>::V V;
   static_assert(N > 0 && (ISSUE & kRemote) == 0, "deferred stores: compile-time leaves, local memory");
+  static_assert((ISSUE & kLeafMajor) == 0 || CH == 0, "leaf-major groups: the linear fold's order");
   constexpr int KB = defer_tiles(ISSUE);
   constexpr long TILE = (long)EMAC_BLOCK * U;
-  __shared__ V res[KB * U * EMAC_BLOCK];
+  constexpr bool LEAF = (ISSUE & kLeafMajor) != 0;
+  __shared__ V res[LEAF ? 1 : KB * U * EMAC_BLOCK];
   // groups per bucket (the last one may hold fewer tiles); group counts fit 32 bits (< 2^31 groups
   // of >= 8 KiB), and 32-bit division is a short sequence ahead of the group's first load
   const unsigned gpb = (unsigned)((tpb + KB - 1) / KB);
@@ -341,7 +388,10 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_deferred_kernel(const emac_bu
     const int bi = (int)((unsigned)g / gpb);
     const long t0 = (g - (long)bi * gpb) * KB;
     const int nt = tpb - t0 < KB ? (int)(tpb - t0) : KB;  // wave-uniform
-    fold_group<T, OP, N, U, CH, D, ISSUE, ALL_FULL>(bk + bi, t0 * TILE, nt, codes, res);
+    if constexpr (LEAF)
+      fold_group_leaf<T, OP, N, U, D, ISSUE, ALL_FULL>(bk + bi, t0 * TILE, nt);
+    else
+      fold_group<T, OP, N, U, CH, D, ISSUE, ALL_FULL>(bk + bi, t0 * TILE, nt, codes, res);
   }
 }
 
@@ -663,7 +713,7 @@ template <typename T, int OP, int N, int U, int CH, int D, int ISSUE = 1>
 int launch_one(const Launch &L) {
   constexpr int KB = defer_tiles(ISSUE);
   if constexpr (KB > 1) {  // one workgroup per group of KB tiles
-    if (L.tpb <= 0) return launch_one<T, OP, N, U, CH, D, ISSUE & ~(3 << kDeferShift)>(L);  // unequal buckets
+    if (L.tpb <= 0) return launch_one<T, OP, N, U, CH, D, ISSUE & ~(3 << kDeferShift | kLeafMajor)>(L);  // unequal buckets
     const long groups = (long)L.nb * ((L.tpb + KB - 1) / KB);
     const unsigned grid = (unsigned)(groups < 8192 ? groups : 8192);
     if (L.all_full && L.tpb % KB == 0)
@@ -708,6 +758,9 @@ int launch_sum(int unroll, const Launch &L) {
     if (unroll == sched(2, 1 | defer(4))) return launch_one<T, OP, N, 2, CH, D, 1 | defer(4)>(L);
     if (unroll == sched(4, 1 | defer(2))) return launch_one<T, OP, N, 4, CH, D, 1 | defer(2)>(L);
     if (unroll == sched(2, 1 | defer(8))) return launch_one<T, OP, N, 2, CH, D, 1 | defer(8)>(L);
+    if constexpr (CH == 0) {
+      if (unroll == sched(2, 1 | defer(4) | kLeafMajor)) return launch_one<T, OP, N, 2, CH, D, 1 | defer(4) | kLeafMajor>(L);
+    }
     return EMAC_ERR_UNSUPPORTED;
   } else {
     if (unroll == sched(4, 1)) return launch_one<T, OP, N, 4, CH, D>(L);

@@ -387,7 +387,7 @@ def test_copy_reduce_headline_instance():
         assert np.array_equal(d.cpu().numpy().view(np.uint8), want.view(np.uint8))
     h = emac.fold_init([t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts], count, emac.FLOAT)
     seen = set()
-    for k in range(22):  # the static pick, 3 rounds of 6 timed candidates, then the kept one
+    for k in range(58):  # the static pick, 3 rounds of 6 candidates on three Starts each, then the kept one
         for d in dsts:
             d.fill_(-1.0)
         torch.cuda.synchronize()  # the fill runs on torch's stream, the fold on the handle's
@@ -403,6 +403,7 @@ def test_copy_reduce_headline_instance():
 
 
 DEFER_SHIFT = 11  # fold_kernel.hpp kDeferShift: deferred-store schedules (issue bits 11-12)
+LEAF_MAJOR = 1 << 13  # fold_kernel.hpp kLeafMajor: leaf-major deferred groups (the linear fold)
 
 
 @pytest.mark.parametrize("copyin", ["6;1 -8 8", "6;1 -2 -2 -2 2 2 2"])
@@ -410,10 +411,11 @@ DEFER_SHIFT = 11  # fold_kernel.hpp kDeferShift: deferred-store schedules (issue
 def test_every_tuned_schedule_bitwise(oracle, code, copyin):
     """The per-handle schedule tuner (engine.c emac_tune) runs every candidate on a handle's first
     Starts -- burst loads at U 2 / U 4, the staggered issue, and the deferred-store schedules
-    (fold_kernel.hpp fold_deferred_kernel: 2, 4 or 8 tiles folded into LDS, then stored in one burst) -- and
+    (fold_kernel.hpp fold_deferred_kernel: 2 or 4 tiles folded into LDS, or leaf after leaf in
+    registers, then stored in one burst) -- and
     keeps one. Every Start must give the oracle's bits: here a node form whose buckets end in a
     partial tile and whose last group of tiles is short (41000 elements per chunk: under 8 MiB per
-    leaf, so (U 1, burst) among the candidates; 262147: above, so (U 2, 8 tiles)), and a local
+    leaf, so (U 1, burst) among the candidates; 262147: above), and a local
     fold (8 leaves -> 1, fold_init) of 512040 elements, each over all the Starts of its tuning."""
     R = 8
     for chunk in ((41000, 262147) if code == emac.FLOAT else (20500, 131075)):
@@ -426,7 +428,7 @@ def test_every_tuned_schedule_bitwise(oracle, code, copyin):
         cands = emac.handle_candidates(h)
         seen = set()
         try:
-            for k in range(22):
+            for k in range(58):
                 for t in drecv:
                     t.fill_(-1)
                 torch.cuda.synchronize()
@@ -439,7 +441,9 @@ def test_every_tuned_schedule_bitwise(oracle, code, copyin):
             emac.done(h)
         assert any(t == 1 for _, _, t in seen), seen
         small = chunk * R * sends[0].itemsize < 8 << 20
-        assert ((1, 1) in cands) == small and ((2, 1 | 3 << DEFER_SHIFT) in cands) != small, (chunk, cands)
+        assert ((1, 1) in cands) == small, (chunk, cands)
+        leaf = (2, 1 | 2 << DEFER_SHIFT | LEAF_MAJOR)  # leaf-major groups: the linear fold only
+        assert (leaf in cands) == (copyin == "6;1 -8 8") and ((4, 1 | 1 << DEFER_SHIFT) in cands) != (leaf in cands), cands
     # the local fold: one destination, one bucket
     n = 8 * 64000 + 40 if code == emac.FLOAT else 4 * 64000 + 20
     srcs_np = xorshift_inputs(R, n, code, seed_base=0x10CA1)
@@ -450,7 +454,7 @@ def test_every_tuned_schedule_bitwise(oracle, code, copyin):
     dst = torch.full((n,), -1, dtype=TORCH[code], device="cuda")
     h = emac.fold_init([t.data_ptr() for t in srcs], [dst.data_ptr()], n, code)
     try:
-        for k in range(19):
+        for k in range(58):
             dst.fill_(-1)
             torch.cuda.synchronize()
             emac.start(h)
@@ -521,7 +525,7 @@ def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=Non
 def test_comm_form_tuned_fold_every_start(oracle):
     """The COMM form's local fold (R staged slices of the owner chunk -> the receive buffer) is
     tuned per handle like the NODE form's (engine.c emac_tune: per-tile and deferred-store
-    candidates, 3 rounds): 8 loopback ranks x 16 MiB float, every one of 20 Starts bitwise."""
+    candidates, 3 rounds of three Starts each): 8 loopback ranks x 16 MiB float, every one of 58 Starts bitwise."""
     R, count = 8, (16 << 20) // 4
     sends = xorshift_inputs(R, count, emac.FLOAT, seed_base=0x7A11)
     want = oracle.allreduce(sends, "6;1 -8 8")
@@ -531,7 +535,7 @@ def test_comm_form_tuned_fold_every_start(oracle):
         assert_bitwise(got, want, f"Start {rep}")
         seen.update((sc["unroll"], sc["issue"], sc["tuned"]) for sc in scheds)
 
-    run_comm_loopback(sends, emac.FLOAT, "6;1 -8 8", repeats=20, each=each)
+    run_comm_loopback(sends, emac.FLOAT, "6;1 -8 8", repeats=58, each=each)
     assert any(t == 1 for _, _, t in seen), seen  # the tuning finished and kept a schedule
 
 
