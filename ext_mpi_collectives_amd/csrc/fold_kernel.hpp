@@ -279,10 +279,11 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
 // destination in one burst. The workgroups, started together, then alternate between phases of
 // loads and phases of stores instead of mixing both all the time: fewer read/write turnarounds
 // at the HBM (tools/nodevar.hip, profiles/r03_nodevar/: the local fold 8 x 32 MiB -> 1 at 0.79-0.80
-// of 8 TB/s against 0.76-0.77 for the per-tile loop, 2-4 % at every size measured; the node fan-out
-// 2 % faster at 16 MiB per rank on one lease, slower on others). Each lane reads back only the LDS
-// slots it wrote, so no barrier is needed. Offered to the per-handle tuner (engine.c emac_tune);
-// the fold order -- and so every bit -- is the per-tile loop's.
+// of 8 TB/s against 0.76-0.77 for the per-tile loop, 2-4 % at every size measured back to back; the
+// node fan-out 2 % faster at 16 MiB per rank on one lease, slower on others, and behind the
+// staggered per-tile schedule in the bench's steady state, profiles/r03_tune/force_ab.txt). Each
+// lane reads back only the LDS slots it wrote, so no barrier is needed. Offered to the per-handle
+// tuner (engine.c emac_tune); the fold order -- and so every bit -- is the per-tile loop's.
 constexpr int kDeferShift = 11;
 constexpr int defer_tiles(int issue) { return ((issue >> kDeferShift) & 3) ? 1 << ((issue >> kDeferShift) & 3) : 1; }
 constexpr int defer(int kb) { return (kb == 2 ? 1 : kb == 4 ? 2 : kb == 8 ? 3 : 0) << kDeferShift; }
