@@ -501,5 +501,51 @@ int main(int argc, char **argv) {
     printf("%-18s %9.2f %9.2f %9.2f  %6.3f TB/s  %.3f of 8\n", v.name.c_str(), med, v.us.front(), v.us.back(),
            bytes / med / 1e6, bytes / med / 1e6 / 8.0);
   }
+  // the tuner's view (engine.c emac_tune): each launch alone between two timing events, the
+  // stream synchronised after it, against the back-to-back figure above
+  printf("isolated launches (events around each, synchronised): median min us\n");
+  for (V &v : vs) {
+    if (!(v.id == 0 || v.id == 1 || v.id == 74 || v.id == 75 || v.id == 80 || v.id == 86 || v.id == 72 || v.id == 83))
+      continue;
+    std::vector<float> iso;
+    for (int r = 0; r < rounds; r++)
+      for (int i = 0; i < per; i++) {
+        CHECK(hipEventRecord(e0, s));
+        run(v, i);
+        CHECK(hipEventRecord(e1, s));
+        CHECK(hipEventSynchronize(e1));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        iso.push_back(ms * 1000.f);
+      }
+    std::sort(iso.begin(), iso.end());
+    printf("iso %-18s %9.2f %9.2f\n", v.name.c_str(), iso[iso.size() / 2], iso.front());
+  }
+  // back to back but with a timing event between launches (the tuner's round-robin in a Start
+  // sequence enqueued without host waits)
+  printf("events between back-to-back launches: median min us\n");
+  for (V &v : vs) {
+    if (!(v.id == 0 || v.id == 1 || v.id == 74 || v.id == 75 || v.id == 80 || v.id == 86 || v.id == 72 || v.id == 83))
+      continue;
+    std::vector<hipEvent_t> ev(per + 1);
+    for (auto &e : ev) CHECK(hipEventCreate(&e));
+    std::vector<float> b2b;
+    for (int r = 0; r < rounds; r++) {
+      CHECK(hipEventRecord(ev[0], s));
+      for (int i = 0; i < per; i++) {
+        run(v, i);
+        CHECK(hipEventRecord(ev[i + 1], s));
+      }
+      CHECK(hipEventSynchronize(ev[per]));
+      for (int i = 1; i < per; i++) {  // the first launch follows an idle stream
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+        b2b.push_back(ms * 1000.f);
+      }
+    }
+    for (auto &e : ev) CHECK(hipEventDestroy(e));
+    std::sort(b2b.begin(), b2b.end());
+    printf("ev  %-18s %9.2f %9.2f\n", v.name.c_str(), b2b[b2b.size() / 2], b2b.front());
+  }
   return 0;
 }
