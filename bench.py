@@ -62,6 +62,7 @@ def parse():
     ap.add_argument("--child-transport", default=None, choices=["ipc", "rccl", "node"], help=argparse.SUPPRESS)
     ap.add_argument("--child-full", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--child-result", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--child-deadline", type=float, default=600.0, help=argparse.SUPPRESS)
     ap.add_argument("--alloc", default="hip", choices=["hip", "torch"],
                     help="device buffers from hipMalloc (library device ABI, like the reference's "
                          "tests/benchmark_gpu.c cudaMalloc) or torch's caching allocator")
@@ -163,7 +164,7 @@ def host_random(count, np_dtype, seed):
     return rng.integers(-lim, lim, count).astype(np_dtype)
 
 
-TUNE_STARTS = 56  # a handle's first Start, 3 rounds of at most 6 candidates on three Starts each, and the keeping one
+TUNE_STARTS = 1 + 3 * 3 * 8 + 1  # a handle's first Start, 3 rounds of at most 8 candidates on three Starts each, and the keeping one
 
 
 def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * MIB, host=False, alloc="torch"):
@@ -957,7 +958,7 @@ def transport_child(args):
     local = int(os.environ.get("LOCAL_RANK", rank))
     import signal
     signal.signal(signal.SIGALRM, lambda *_: (log(f"rank {rank}: watchdog expired"), os._exit(3)))
-    signal.alarm(600)  # a rank stuck in a collective must not hang the job
+    signal.alarm(max(1, int(args.child_deadline)))  # a rank stuck in a collective must not hang the job
     ndev = torch.cuda.device_count()
     dev = local % ndev  # one rank per GPU; ranks share a GPU only when there are fewer GPUs (rehearsal)
     torch.cuda.set_device(dev)
@@ -1094,11 +1095,63 @@ def transport_child(args):
     signal.alarm(0)
 
 
+MULTI_DEADLINE_S = 1200.0  # the whole N > 1 bench (every child of every rank), EXT_MPI_AMD_BENCH_DEADLINE overrides
+CHILD_MAX_S = 600.0  # one child at most (its own watchdog, --child-deadline, fires first)
+
+
+def run_child_process(cmd, env, timeout_s, tail_lines=12):
+    """Run one child (its stderr passed through line by line, its last lines kept) under a time
+    limit; returns (rc or "timeout", elapsed seconds, last stderr lines). A child that outlives its
+    limit is killed with its whole process group."""
+    import collections
+    import signal
+    import subprocess
+    import threading
+    tail = collections.deque(maxlen=tail_lines)
+    t0 = time.monotonic()
+    p = subprocess.Popen(cmd, env=env, stderr=subprocess.PIPE, start_new_session=True)
+
+    def pump():
+        for raw in iter(p.stderr.readline, b""):
+            line = raw.decode(errors="replace").rstrip()
+            tail.append(line[:300])
+            print(line, file=sys.stderr, flush=True)
+
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    try:
+        rc = p.wait(timeout=max(1.0, timeout_s))
+    except subprocess.TimeoutExpired:
+        rc = "timeout"
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except OSError:
+            pass
+        p.wait()
+    th.join(timeout=5)
+    return rc, round(time.monotonic() - t0, 1), list(tail)
+
+
+def child_outcome(transport, rc, elapsed, tail, result):
+    """(result or {}, None) for a child that completed and checked, else ({}, failure record): the
+    transport, the exit code ("timeout" when killed at its limit), its time and last stderr lines."""
+    if rc == 0 and result is not None:
+        if result.get("checked"):
+            return result, None
+        return result, {"transport": transport, "rc": 0, "error": "result check failed", "elapsed_s": elapsed,
+                        "stderr_tail": tail}
+    what = "timed out" if rc == "timeout" else f"exited with {rc}" if rc != 0 else "wrote no result"
+    return {}, {"transport": transport, "rc": rc, "error": f"{transport} child {what}", "elapsed_s": elapsed,
+                "stderr_tail": tail}
+
+
 def multi_gpu(args):
     """N > 1 driver rank. It never touches the GPU itself: each transport runs in a child process
     per rank (own gloo group, own HIP context), so a transport that fails -- even by a GPU fault
-    that ends its processes -- leaves these ranks alive to agree on it and try the other one."""
-    import subprocess
+    that ends its processes -- leaves these ranks alive to agree on it and try the other one. The
+    whole run is bounded (MULTI_DEADLINE_S): each child gets at most what is left of it, and a
+    child killed at its limit, or one that fails, is reported with its exit code and last stderr
+    lines in the line's extras -- a valid JSON line comes out either way."""
     import torch
     import torch.distributed as dist
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -1108,50 +1161,71 @@ def multi_gpu(args):
     S = count * tsize
     copyin = args.copyin or f"6;1 -{world} {world}"
     base_port = int(os.environ.get("MASTER_PORT", "29500"))
+    deadline = time.monotonic() + float(os.environ.get("EXT_MPI_AMD_BENCH_DEADLINE", MULTI_DEADLINE_S))
 
     def everyone(ok):
         t = torch.tensor([int(bool(ok))])
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return bool(t.item())
 
-    def run_child(i, transport, full):
+    def run_child(i, transport, full, share):
         out = os.path.join("/tmp", f"emac_bench_{base_port}_{i}_{rank}.json")
         if os.path.exists(out):
             os.remove(out)
+        # this child's share of what is left of the run (every rank computes the same budget)
+        budget = min(CHILD_MAX_S, max(30.0, (deadline - time.monotonic()) * share))
         cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(args.gpus), "--steps", str(args.steps),
                "--warmup", str(args.warmup), "--size-mib", str(args.size_mib), "--dtype", args.dtype,
-               "--ranks", str(args.ranks), "--child-transport", transport, "--child-result", out] + (["--child-full"] if full else []) + \
+               "--ranks", str(args.ranks), "--child-transport", transport, "--child-result", out,
+               "--child-deadline", str(int(budget))] + (["--child-full"] if full else []) + \
               (["--copyin", args.copyin] if args.copyin else [])
         env = dict(os.environ, MASTER_PORT=str(base_port + 101 + i))
         env.pop("TORCHELASTIC_USE_AGENT_STORE", None)  # the children's rank 0 hosts their own store
-        try:
-            rc = subprocess.run(cmd, env=env, timeout=700).returncode
-        except subprocess.TimeoutExpired:
-            rc = "timeout"
+        rc, elapsed, tail = run_child_process(cmd, env, budget + 20)  # the child's watchdog fires first
+        result = None
         if rc == 0 and os.path.exists(out):
             with open(out) as f:
-                r = json.load(f)
+                result = json.load(f)
             os.remove(out)
-            return r, (None if r.get("checked") else "result check failed")
-        return {}, f"{transport} child exited with {rc}"
+        return child_outcome(transport, rc, elapsed, tail, result)
 
+    failures = []
     # the headline: configs[1]'s node (8 ranks x 16 MiB resident in one GPU) on every GPU, the GPUs
-    # joined as nodes over RCCL -- the N = 1 workload scaled weakly
-    rn, err = run_child(9, "node", False)
-    if not everyone(err is None):
-        rn = {"error": err or "failed on another rank"}
+    # joined as nodes -- the N = 1 workload scaled weakly
+    rn, fail = run_child(9, "node", False, 0.4)
+    if fail:
+        failures.append(dict(fail, rank=rank))
+    if not everyone(fail is None):
+        rn = fail or {"error": "failed on another rank"}
     # BASELINE configs[3] / [4] (one rank per GPU): the requested transport first; if it fails on
     # any rank (every rank agrees before moving on), the other one
     order = [args.transport, "rccl" if args.transport == "ipc" else "ipc"]
     results = {}
     for i, transport in enumerate(order):
         full = not any("wall" in r for r in results.values())
-        r, err = run_child(i, transport, full)
-        if not everyone(err is None):
-            r = {"error": err or "failed on another rank"}
+        r, fail = run_child(i, transport, full, 0.6 if i == 0 else 0.9)
+        if fail:
+            failures.append(dict(fail, rank=rank))
+        if not everyone(fail is None):
+            r = fail or {"error": "failed on another rank"}
         results[transport] = r
+    allf = [None] * world
+    dist.all_gather_object(allf, failures)
+    if rank == 0:
+        emit(multi_gpu_line(args, world, dname, S, copyin, rn, results, order, torch.cuda.device_count(),
+                            [f for fs in allf for f in fs]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def multi_gpu_line(args, world, dname, S, copyin, rn, results, order, gpus_visible, failures):
+    """The N > 1 JSON line from the children's results (pure: tests/test_bench_cpu.py feeds it
+    fabricated ones): the node form's line when its child ran and checked, else the one-rank-per-GPU
+    line of the first transport that completed, else a zero line naming every failure."""
     primary = next((t for t in order if "wall" in results[t] and "fold_s" in results[t]), None)
-    extras = {"gpus_visible": torch.cuda.device_count(), "process_per_transport": True}
+    extras = {"gpus_visible": gpus_visible, "process_per_transport": True}
+    if failures:
+        extras["failures"] = failures  # per rank: transport, exit code or "timeout", last stderr lines
     for t in order:
         if t != primary:
             r = results[t]
@@ -1163,17 +1237,22 @@ def multi_gpu(args):
         for key in ("two_node_schedule", "four_node_schedule", "four_node_three_ports"):
             if key in results[t]:
                 extras[key] = results[t][key]
-    legacy = None
-    if rank == 0 and primary is None:
-        legacy = {"metric": "device-resident GB/s reduced (float32 MPI_SUM) per GPU; % HBM3E roofline",
-                  "value": 0.0, "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                  "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dname,
-                  "error": "no transport completed", "extras": extras}
-    if rank == 0 and primary is not None:
+    metric = "device-resident GB/s reduced (float32 MPI_SUM) per GPU; % HBM3E roofline"
+    if primary is None:
+        legacy = {"metric": metric, "value": 0.0, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+                  "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
+                  "vs_baseline": None, "dtype": dname, "data": "synthetic", "error": "no transport completed",
+                  "config": {"workload": f"persistent Allreduce {args.dtype} MPI_SUM, {S // MIB} MiB per rank, one rank "
+                                         f"per GPU, EXT_MPI_COPYIN '{copyin}' (no transport completed: "
+                                         + "; ".join(f"{t}: {results[t].get('error', 'unchecked')}" for t in order)
+                                         + ")",
+                             "ranks": world, "message_bytes_per_rank": S, "copyin": copyin, "layout": "rank-per-gpu"},
+                  "roofline": None, "extras": extras}
+    else:
         r = results[primary]
         wall, checked, kf = r["wall"], r["checked"], r["fold_s"]
         extras["transport"] = primary
-        extras["sweep"] = r["sweep"]
+        extras["sweep"] = r.get("sweep", [])
         extras["radix_sweep"] = r.get("radix_sweep", [])
         extras["local_fold_rate_retained"] = r.get("local_fold")
         extras["host_buffers_pcie_inclusive"] = r.get("host_buffers")
@@ -1202,15 +1281,15 @@ def multi_gpu(args):
         # that bound, and what N = 1 measures instead
         extras["end_to_end_frac_of_xgmi_bound"] = (
             round(extras["xgmi_bound_us"] / (wall * 1e6 / args.steps), 3)
-            if extras["gpus_visible"] >= world else None)  # ranks sharing a GPU cross no xGMI
+            if gpus_visible >= world else None)  # ranks sharing a GPU cross no xGMI
         extras["note_vs_n1"] = ("N = 1 is BASELINE configs[1]: 8 node ranks resident in one GPU's HBM, HBM-bound; "
                                 "N > 1 is one rank per GPU, every rank's chunk crossing xGMI (bound: xgmi_bound_us)")
         form = ("peer-mapped (hipIpc over xGMI): barrier kernel, fold of the owned chunk over the peers' send "
                 "buffers into the own receive buffer, barrier kernel, pull of the other owners' chunks"
                 if primary == "ipc" else
                 "reduce-scatter + allgather legs over RCCL/xGMI, fold on the owner GPU")
-        out = {
-            "metric": "device-resident GB/s reduced (float32 MPI_SUM) per GPU; % HBM3E roofline",
+        legacy = {
+            "metric": metric,
             "value": round(world * S * args.steps / wall / 1e9, 2),
             "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(wall * 1e3 / args.steps, 4), "higher_is_better": True, "scaling": "weak",
@@ -1228,15 +1307,13 @@ def multi_gpu(args):
                          "algorithmic_bytes_per_launch": int(algo), "avg_launch_us": round(kl * 1e6, 2)},
             "extras": extras,
         }
-        legacy = out
-    if rank == 0:
-        if "wall" in rn and rn.get("checked"):
-            emit(node_form_line(args, world, dname, rn, legacy))
-        else:
-            legacy.setdefault("extras", {})["node_form_per_gpu"] = rn
-            emit(legacy)
-    dist.barrier()
-    dist.destroy_process_group()
+    if "wall" in rn and rn.get("checked"):
+        line = node_form_line(args, world, dname, rn, legacy)
+        if failures:
+            line["extras"]["failures"] = failures
+        return line
+    legacy["extras"]["node_form_per_gpu"] = rn
+    return legacy
 
 
 def node_form_line(args, world, dname, rn, one_rank_per_gpu):

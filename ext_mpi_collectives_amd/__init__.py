@@ -21,6 +21,7 @@ DOUBLE, LONG, FLOAT, INT = 0, 1, 2, 3
 SUM, MIN, MAX = 0, 1, 2  # element operations (include/ext_mpi_amd.h EXT_MPI_AMD_SUM / _MIN / _MAX)
 UNIQUE_ID_BYTES = 128
 MAX_RANKS = 16
+TUNE_MAX = 8  # include/ext_mpi_amd.h EXT_MPI_AMD_TUNE_MAX
 ERRORS = {-1: "ERROR_MALLOC", -2: "ERROR_SHMEM", -3: "ERROR_ARG", -4: "ERROR_UNSUPPORTED",
           -5: "ERROR_DEVICE", -6: "ERROR_TRANSPORT"}
 ERROR_MALLOC, ERROR_SHMEM, ERROR_ARG, ERROR_UNSUPPORTED, ERROR_DEVICE, ERROR_TRANSPORT = -1, -2, -3, -4, -5, -6
@@ -102,6 +103,8 @@ def lib():
         L.ext_mpi_amd_stream.restype = c_void_p
         L.ext_mpi_amd_handle_schedule.argtypes = [c_int, P(c_int), P(c_int), P(c_int)]
         L.ext_mpi_amd_handle_candidates.argtypes = [c_int, P(c_int), P(c_int), c_int]
+        L.ext_mpi_amd_handle_tune_info.argtypes = [c_int, c_void_p]
+        L.ext_mpi_amd_tune_cache_clear.argtypes = []
         L.ext_mpi_amd_plan_describe.argtypes = [c_int, c_long, c_int, ctypes.c_char_p, c_int, P(c_long),
                                                 P(c_long), c_int, P(c_int), P(c_int), P(ctypes.c_ubyte),
                                                 P(ctypes.c_ubyte), P(c_int)]
@@ -303,6 +306,8 @@ def default_node_ports(nodes):
         while m % d == 0 and all(d % q for q in range(2, int(d ** 0.5) + 1)):
             f.append(d)
             m //= d
+    if m != 1:  # a prime factor above MAX_RANKS: plan.c emac_node_sched_build refuses it (UNSUPPORTED)
+        raise ValueError(f"{nodes} nodes: prime factor {m} > {MAX_RANKS} leaves per step")
     return [1 - d for d in f] + [d - 1 for d in reversed(f)]
 
 
@@ -366,6 +371,32 @@ def handle_candidates(h):
     n, sched = ctypes.c_int(), (ctypes.c_int * 16)()
     _check("ext_mpi_amd_handle_candidates", lib().ext_mpi_amd_handle_candidates(h, ctypes.byref(n), sched, 16))
     return [(sched[k] & 15, sched[k] >> 4) for k in range(min(n.value, 16))]
+
+
+class TuneInfo(ctypes.Structure):
+    """include/ext_mpi_amd.h ext_mpi_amd_tune_info"""
+    _fields_ = [("candidates", ctypes.c_int), ("chosen", ctypes.c_int), ("cached", ctypes.c_int),
+                ("isolated", ctypes.c_int), ("starts", ctypes.c_int), ("timed_starts_per_sample", ctypes.c_int),
+                ("samples", ctypes.c_int), ("schedule", ctypes.c_int * TUNE_MAX), ("us", ctypes.c_float * TUNE_MAX),
+                ("ops_in_sample", ctypes.c_int * (TUNE_MAX * 3))]
+
+
+def handle_tune_info(h):
+    """The tuner's state of a handle: dict(candidates, chosen, cached, isolated, starts,
+    timed_starts_per_sample, schedules=[(unroll, issue)], us=[per candidate], ops_in_sample=[...])."""
+    t = TuneInfo()
+    _check("ext_mpi_amd_handle_tune_info", lib().ext_mpi_amd_handle_tune_info(h, ctypes.byref(t)))
+    n = min(t.candidates, TUNE_MAX)
+    return {"candidates": t.candidates, "chosen": t.chosen, "cached": t.cached, "isolated": t.isolated,
+            "starts": t.starts, "timed_starts_per_sample": t.timed_starts_per_sample,
+            "schedules": [(t.schedule[k] & 15, t.schedule[k] >> 4) for k in range(n)],
+            "us": [round(t.us[k], 3) for k in range(n)],
+            "ops_in_sample": list(t.ops_in_sample[:min(t.samples, TUNE_MAX * 3)])}
+
+
+def tune_cache_clear():
+    """Forget every kept fold schedule of this process; returns the number of entries dropped."""
+    return lib().ext_mpi_amd_tune_cache_clear()
 
 
 def plan_describe(nranks, count, dtype, copyin, pos, max_pieces=4096):

@@ -29,6 +29,9 @@
 
 static void mirror_free(emac_handle *h, void *p);
 
+/* a launch or copy the handle enqueues (counted for the tuner's samples, emac_tune.ops) */
+#define OP(h, call) ((h)->tune.ops++, (call))
+
 emac_handle *g_handles[MAX_HANDLES];
 emac_comm g_comms[MAX_COMMS];
 
@@ -55,9 +58,9 @@ void handle_release(emac_handle *h) {
     if (h->tune.L[r].d_buckets != h->d_buckets) emac_gpu_free(h->tune.L[r].d_buckets);
     if (h->tune.L[r].d_edges != h->d_edges) emac_gpu_free(h->tune.L[r].d_edges);
   }
-  for (r = 0; r < EMAC_TUNE_MAX * EMAC_TUNE_ROUNDS; r++) {
-    emac_gpu_event_destroy(h->tune.ev[r][0]);
-    emac_gpu_event_destroy(h->tune.ev[r][1]);
+  for (r = 0; r < EMAC_TUNE_SAMPLES; r++) {
+    int e;
+    for (e = 0; e < 2 * (EMAC_TUNE_SPAN - 1); e++) emac_gpu_event_destroy(h->tune.ev[r][e]);
   }
   for (r = 0; r < 2 * EMAC_MAX_NODE_STEPS; r++) {
     emac_gpu_free(h->xfold[r].d_buckets);
@@ -247,7 +250,7 @@ int stage_in(emac_handle *h) {
   int r, rc;
   for (r = 0; r < h->nbuf; r++) {
     void *src = h->send_mirror[r] ? h->user_send[r] : (h->recv_mirror[r] && h->dsend[r] == h->drecv[r] ? h->user_recv[r] : NULL);
-    if (src && (rc = emac_gpu_memcpy_async(h->dsend[r], src, h->bytes, h->stream))) return rc;
+    if (src && (rc = OP(h, emac_gpu_memcpy_async(h->dsend[r], src, h->bytes, h->stream)))) return rc;
   }
   return 0;
 }
@@ -255,7 +258,7 @@ int stage_in(emac_handle *h) {
 int stage_out(emac_handle *h) {
   int r, rc;
   for (r = 0; r < h->nbuf; r++)
-    if (h->recv_mirror[r] && (rc = emac_gpu_memcpy_async(h->user_recv[r], h->drecv[r], h->bytes, h->stream)))
+    if (h->recv_mirror[r] && (rc = OP(h, emac_gpu_memcpy_async(h->user_recv[r], h->drecv[r], h->bytes, h->stream))))
       return rc;
   return 0;
 }
@@ -278,21 +281,21 @@ static int enqueue_legs(emac_handle *h, int legs) {
       const emac_launch *X = &h->xfold[0];
       if ((rc = ipc_barrier(h, 0))) return rc;
       if ((X->nb || X->nedges) &&
-          (rc = emac_gpu_fold_remote(h->plan.dtype, nodes > 1 ? h->plan.op : EMAC_SUM, nodes, X->unroll, &h->xcodes,
+          (rc = OP(h, emac_gpu_fold_remote(h->plan.dtype, nodes > 1 ? h->plan.op : EMAC_SUM, nodes, X->unroll, &h->xcodes,
                                      X->d_buckets, X->nb, X->ntiles, X->tiles_per_bucket, X->all_full, X->d_edges,
-                                     X->nedges, ipc_go(h), h->stream)))
+                                     X->nedges, ipc_go(h), h->stream))))
         return rc;
       if ((rc = ipc_barrier(h, 1))) return rc;
       if ((h->pull.nb || h->pull.nedges) &&
-          (rc = emac_gpu_copy_fan_remote(h->plan.tsize, h->plan.nranks, h->pull.unroll, h->pull.d_buckets, h->pull.nb,
+          (rc = OP(h, emac_gpu_copy_fan_remote(h->plan.tsize, h->plan.nranks, h->pull.unroll, h->pull.d_buckets, h->pull.nb,
                                          h->pull.ntiles, h->pull.tiles_per_bucket, h->pull.all_full, h->pull.d_edges,
-                                         h->pull.nedges, ipc_go(h), h->stream)))
+                                         h->pull.nedges, ipc_go(h), h->stream))))
         return rc;
     }
     if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && h->fanout.nb &&
-        (rc = emac_gpu_copy_fan(h->plan.tsize, h->plan.nranks - 1, h->fanout.unroll, h->fanout.d_buckets, h->fanout.nb,
+        (rc = OP(h, emac_gpu_copy_fan(h->plan.tsize, h->plan.nranks - 1, h->fanout.unroll, h->fanout.d_buckets, h->fanout.nb,
                                 h->fanout.ntiles, h->fanout.tiles_per_bucket, h->fanout.all_full, h->fanout.d_edges,
-                                h->fanout.nedges, h->stream)))
+                                h->fanout.nedges, h->stream))))
       return rc;
     if ((legs & EXT_MPI_AMD_LEG_STAGE_OUT) && (rc = stage_out(h))) return rc;
     return 0;
@@ -303,12 +306,12 @@ static int enqueue_legs(emac_handle *h, int legs) {
     if (h->ev_release && (rc = emac_gpu_event_record(h->ev_release, h->stream))) return rc; /* as ipc_barrier(h, 0) */
     e0 = ++h->epoch[0];
     e1 = ++h->epoch[1];
-    if ((rc = emac_gpu_fold_fused(h->plan.dtype, h->plan.op, h->nsrc, h->unroll, &h->plan.codes, h->d_buckets, h->nb, h->ntiles,
+    if ((rc = OP(h, emac_gpu_fold_fused(h->plan.dtype, h->plan.op, h->nsrc, h->unroll, &h->plan.codes, h->d_buckets, h->nb, h->ntiles,
                                   h->tiles_per_bucket, h->all_full, h->d_edges, h->nedges, h->pull.d_buckets, h->pull.nb,
                                   h->pull.ntiles, h->pull.tiles_per_bucket, h->pull.all_full, h->pull.d_edges,
                                   h->pull.nedges, cm->sync,
                                   (void *const *)cm->d_peer_sync, h->slot, cm->size, cm->rank, cm->err + h->slot,
-                                  cm->timeout_ticks, e0, e1, h->stream)))
+                                  cm->timeout_ticks, e0, e1, h->stream))))
       return rc;
     if ((legs & EXT_MPI_AMD_LEG_STAGE_OUT) && (rc = stage_out(h))) return rc;
     return 0;
@@ -318,8 +321,8 @@ static int enqueue_legs(emac_handle *h, int legs) {
     return rc;
   if ((legs & EXT_MPI_AMD_LEG_REDUCE_SCATTER) && multi && (rc = run_leg(h, EMAC_LEG_RS))) return rc;
   if ((legs & EXT_MPI_AMD_LEG_FOLD) && h->fan == 2 &&
-      (rc = emac_gpu_fold_remote(h->plan.dtype, h->plan.op, h->nsrc, h->unroll, &h->plan.codes, h->d_buckets, h->nb,
-                                 h->ntiles, h->tiles_per_bucket, h->all_full, h->d_edges, h->nedges, ipc_go(h), h->stream)))
+      (rc = OP(h, emac_gpu_fold_remote(h->plan.dtype, h->plan.op, h->nsrc, h->unroll, &h->plan.codes, h->d_buckets, h->nb,
+                                 h->ntiles, h->tiles_per_bucket, h->all_full, h->d_edges, h->nedges, ipc_go(h), h->stream))))
     return rc;
   if ((legs & EXT_MPI_AMD_LEG_FOLD) && h->fan != 2 && (rc = fold_launch(h))) return rc;
   if (h->kind == KIND_COMM && h->nodes > 1) {
@@ -342,8 +345,8 @@ static int enqueue_legs(emac_handle *h, int legs) {
       if ((legs & EXT_MPI_AMD_LEG_NODES_RS) && (rc = run_leg(h, EMAC_LEG_NODES_RS | st << EMAC_LEG_STEP_SHIFT)))
         return rc;
       if ((legs & EXT_MPI_AMD_LEG_NODES_FOLD) && X->nb &&
-          (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, rad, 0, X->unroll, &lin, X->d_buckets, X->nb,
-                              X->ntiles, X->tiles_per_bucket, X->all_full, X->d_edges, X->nedges, h->stream)))
+          (rc = OP(h, emac_gpu_fold(h->plan.dtype, h->plan.op, rad, 0, X->unroll, &lin, X->d_buckets, X->nb,
+                              X->ntiles, X->tiles_per_bucket, X->all_full, X->d_edges, X->nedges, h->stream))))
         return rc;
     }
     for (st = 0; st < h->ns.nagp; st++) { /* the copying allgather steps, block growing */
@@ -354,16 +357,16 @@ static int enqueue_legs(emac_handle *h, int legs) {
   }
   if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && multi && (rc = run_leg(h, EMAC_LEG_AG))) return rc;
   if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && h->hier && h->fanout.nb &&
-      (rc = emac_gpu_copy_fan(h->plan.tsize, h->plan.nranks - 1, h->fanout.unroll, h->fanout.d_buckets, h->fanout.nb,
+      (rc = OP(h, emac_gpu_copy_fan(h->plan.tsize, h->plan.nranks - 1, h->fanout.unroll, h->fanout.d_buckets, h->fanout.nb,
                               h->fanout.ntiles, h->fanout.tiles_per_bucket, h->fanout.all_full, h->fanout.d_edges,
-                              h->fanout.nedges, h->stream)))
+                              h->fanout.nedges, h->stream))))
     return rc;
   if ((legs & EXT_MPI_AMD_LEG_ALLGATHER) && h->kind == KIND_IPC && h->plan.nranks > 1) {
     static const emac_codes copy = {{1}, {1}, 1, 1}; /* one leaf: a copy */
     if ((rc = ipc_barrier(h, 1))) return rc;
-    if ((rc = emac_gpu_fold_remote(h->plan.dtype, EMAC_SUM, 1, h->pull.unroll, &copy, h->pull.d_buckets, h->pull.nb,
+    if ((rc = OP(h, emac_gpu_fold_remote(h->plan.dtype, EMAC_SUM, 1, h->pull.unroll, &copy, h->pull.d_buckets, h->pull.nb,
                                    h->pull.ntiles, h->pull.tiles_per_bucket, h->pull.all_full, h->pull.d_edges,
-                                   h->pull.nedges, ipc_go(h), h->stream)))
+                                   h->pull.nedges, ipc_go(h), h->stream))))
       return rc;
   }
   if ((legs & EXT_MPI_AMD_LEG_STAGE_OUT) && (rc = stage_out(h))) return rc;

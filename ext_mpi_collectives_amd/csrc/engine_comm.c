@@ -116,9 +116,7 @@ int ext_mpi_amd_allreduce_init(const void *sendbuf, void *recvbuf, long count, i
   h->nsrc = R;
   if (cm->ipc) {
     if (!rc) rc = emac_gpu_stream_create(&h->stream);
-    if ((rc = ipc_allreduce_init(h, cm, sendbuf, recvbuf, rc))) goto fail;
-    if ((rc = finish_init(h, handle))) goto fail;
-    return 0;
+    return ipc_init_settle(h, cm, ipc_allreduce_init(h, cm, sendbuf, recvbuf, rc), handle);
   }
   if (rc) goto fail;
   if ((rc = map_buffers(h, 0, sendbuf, recvbuf))) goto fail;
@@ -234,6 +232,7 @@ int run_leg(emac_handle *h, int leg) {
   emac_comm *cm = &g_comms[h->comm];
   hipStream_t s = (hipStream_t)h->stream;
   int i, bad = 0;
+  h->tune.ops++;
   if (cm->loop_group >= 0) return run_leg_loopback(h, leg);
   if (ncclGroupStart() != ncclSuccess) return EMAC_ERR_TRANSPORT;
   for (i = 0; i < h->nops && !bad; i++) {

@@ -133,9 +133,9 @@ typedef struct {
   int unroll;
 } emac_launch;
 
-/* Launch-schedule tuning of a handle's fold (NODE form, and the COMM form's local fold): the
-   first Start runs the static pick (emac_gpu_pick_unroll) and warms the buffers, the next
-   EMAC_TUNE_ROUNDS x candidates Starts run the candidates round-robin, each between timing events,
+/* Launch-schedule tuning of a handle's fold (NODE form, and the COMM / IPC / node-join forms'
+   local fold): the first Start runs the static pick (emac_gpu_pick_unroll) and warms the buffers,
+   the next EMAC_TUNE_SPAN x EMAC_TUNE_ROUNDS x candidates Starts sample the candidates round-robin,
    and the Start after them keeps the candidate with the shortest of its samples for the handle's
    lifetime. Every schedule folds in the same order -- the bits do not depend on the choice.
    Measured on MI355X leases (tools/schedbench.hip, tools/nodevar.hip, profiles/r03_schedbench_*,
@@ -144,26 +144,50 @@ typedef struct {
    lease; U 2 47.1, U 4 46.2 on another), so no fixed threshold table picks it everywhere; one
    sample per candidate (round 3's first tuner) kept U 2 on a lease where U 4 was 2 % faster, hence
    the rounds. A sample runs one candidate on EMAC_TUNE_SPAN Starts in a row: the first, right
-   after another schedule's launch, untimed, the others timed as one window with no event between
-   them, on events without the system-scope fence (hipEventDisableSystemFence): a single launch
-   between two fenced events ranked the schedules against their back-to-back rate (the leaf-major
-   deferred schedule 46-47 us alone, 43.9-44.4 us per Start in the bench's steady state, where the
-   tile-major one it lost to ran 45.5-46.4 us; profiles/r03_tune/force_ab.txt). Where the caller
-   interleaves several handles the window also holds their launches; every candidate sees the same
-   pattern. EXT_MPI_AMD_AUTOTUNE=0
-   keeps the static pick; EXT_MPI_AMD_FOLD_SCHEDULE=<U | issue << 4> makes one schedule the only
-   candidate (A/B runs). */
-#define EMAC_TUNE_MAX 6
+   after another schedule's launch, untimed; the others timed on events without the system-scope
+   fence (hipEventDisableSystemFence: a single launch between two fenced events ranked the
+   schedules against their back-to-back rate -- the leaf-major deferred schedule 46-47 us alone,
+   43.9-44.4 us per Start in the bench's steady state, where the tile-major one it lost to ran
+   45.5-46.4 us; profiles/r03_tune/force_ab.txt):
+   * NODE form on device buffers (nothing of the handle runs between the folds of two Starts): the
+     timed Starts as ONE window, no event between them -- the back-to-back rate. Where the caller
+     interleaves several handles the window also holds their launches; every candidate sees the
+     same pattern.
+   * every other form (`isolated`: the COMM form's RCCL legs, the peer-mapped barriers and pull,
+     the node join's legs, host staging copies sit between the folds): each timed fold launch
+     between its own pair of events, so a sample is the fold alone, never the network legs or a
+     late peer.
+   `ops` counts every operation the handle enqueues; a sample records how many of them fell inside
+   its timed span(s) (ext_mpi_amd_handle_tune_info): one fold per timed Start.
+   Kept schedules are shared per process (engine_tune.c): a handle whose shape (device, type, op,
+   leaves, fan-out, fold tree, buckets' vector counts) some earlier handle has tuned starts on that
+   schedule and spends no Start measuring (`cached`). EXT_MPI_AMD_AUTOTUNE=0 keeps the static pick;
+   EXT_MPI_AMD_TUNE_CACHE=0 tunes every handle afresh; EXT_MPI_AMD_FOLD_SCHEDULE=<U | issue << 4>
+   makes one schedule the only candidate (A/B runs; refused at init if the shape has no such
+   kernel). */
+#define EMAC_TUNE_MAX 8
 #define EMAC_TUNE_ROUNDS 3
-#define EMAC_TUNE_SPAN 3 /* Starts per sample: one untimed, then the timed window */
+#define EMAC_TUNE_SPAN 3 /* Starts per sample: one untimed, then the timed ones */
+#define EMAC_TUNE_SAMPLES (EMAC_TUNE_MAX * EMAC_TUNE_ROUNDS)
 #define EMAC_TUNE_MIN_BYTES (16L << 20) /* algorithmic bytes per launch: smaller launches keep the static pick */
+/* what a fold launch's schedule choice depends on (the tuning cache's key, engine_tune.c) */
 typedef struct {
-  int n;      /* candidates (0: no tuning) */
-  int chosen; /* index of the kept candidate, -1 while measuring */
+  int device, dtype, op, nsrc, fan, tree, nb, uniform;
+  long vec, vec0; /* 16-byte vectors per leaf over all buckets, in the first bucket */
+} emac_shape;
+typedef struct {
+  int n;        /* candidates (0: no tuning) */
+  int chosen;   /* index of the kept candidate, -1 while measuring */
   int starts;
+  int isolated; /* each timed fold between its own events (legs run between the folds of two Starts) */
+  int cached;   /* the kept schedule came from the per-process cache: no Start spent measuring */
+  emac_shape shape;
   emac_launch L[EMAC_TUNE_MAX];
-  void *ev[EMAC_TUNE_MAX * EMAC_TUNE_ROUNDS][2]; /* sample i: candidate i % n, round i / n */
-  float us[EMAC_TUNE_MAX];                       /* shortest sample per candidate */
+  void *ev[EMAC_TUNE_SAMPLES][2 * (EMAC_TUNE_SPAN - 1)]; /* sample i: candidate i % n, round i / n */
+  float us[EMAC_TUNE_MAX];          /* shortest sample per candidate, per timed Start */
+  unsigned long ops;                /* operations the handle has enqueued (folds, legs, copies, barriers) */
+  unsigned long op_mark;            /* ops at the open of the current timed span */
+  int span_ops[EMAC_TUNE_SAMPLES];  /* the handle's operations inside each sample's timed span(s) */
 } emac_tune;
 
 /* NODE form with host buffers: the message is staged in EMAC_PIPE_PARTS element ranges so that
@@ -286,6 +310,7 @@ int arena_owns(const emac_comm *cm, const void *p, int *seg);
 void arena_release(emac_comm *cm, void *p, long bytes);
 int arena_grow(emac_comm *cm, int rc, long need);
 int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf, void *recvbuf, int rc);
+int ipc_init_settle(emac_handle *h, emac_comm *cm, int rc, int *handle);
 unsigned *ipc_go(const emac_handle *h);
 int ipc_barrier(emac_handle *h, int phase);
 int ipc_status(const emac_handle *h);

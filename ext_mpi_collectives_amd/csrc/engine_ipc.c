@@ -413,6 +413,7 @@ typedef struct {
 } arena_export;
 
 static unsigned long long g_nonce_state;
+#define EMAC_ARENA_FAILED 0x80000000u /* arena_grow's verdict word: this rank failed locally */
 
 /* Collective: ranks that lack `need` bytes (0: none) add a segment of at least that size (and at
    least their arena's size so far, EMAC_ARENA_MIN at first); every rank maps every new segment
@@ -491,12 +492,25 @@ int arena_grow(emac_comm *cm, int rc, long need) {
         pl[n] = EMAC_SAMPLE_BYTES;
         who[n++] = r;
       }
-      if (n && (rc = emac_gpu_sample(pk, pl, n, seen, NULL))) return rc;
-      for (r = 0; r < n; r++)
+      /* a local failure still takes part in the verdict below (every peer is in that allgather) */
+      if (n && (rc = emac_gpu_sample(pk, pl, n, seen, NULL))) bad |= EMAC_ARENA_FAILED;
+      for (r = 0; !rc && r < n; r++)
         if (memcmp(seen + r * EMAC_SAMPLE_BYTES, all[who[r]].nonce, EMAC_SAMPLE_BYTES)) bad |= 1u << who[r];
     }
     if (cm->ag(cm->ag_ctx, &bad, allbad, (long)sizeof(unsigned))) return EMAC_ERR_TRANSPORT;
     for (r = 0; r < R; r++) badall |= allbad[r];
+    if (badall & EMAC_ARENA_FAILED) {
+      /* some rank could not validate this round: every rank drops the round's new segments (its own
+         kept aside, a peer may map it; freed with the communicator) and reports the failure */
+      for (r = 0; r < R; r++) {
+        if (!all[r].grow) continue;
+        if (r == cm->rank)
+          cm->bad_seg[cm->nbad++] = nb;
+        else if (mapped[r])
+          ipc_unmap(mapped[r]);
+      }
+      return rc ? rc : EMAC_ERR_TRANSPORT;
+    }
     for (r = 0; r < R; r++) {
       if (!all[r].grow) continue;
       if ((badall >> r) & 1) {
@@ -845,6 +859,30 @@ unsigned *ipc_go(const emac_handle *h) {
   return (unsigned *)((char *)g_comms[h->comm].sync + offsetof(emac_sync, go)) + h->slot;
 }
 
+/* The end of a peer-mapped handle's set-up (after ipc_allreduce_init / node_ipc_init, whose
+   exchanges every rank runs whatever failed locally): every rank learns whether every other one
+   succeeded. A local failure after the last exchange -- an upload, the release event, the handle
+   table -- would otherwise leave this rank's peers holding mappings of its send buffer and a
+   handle they would Start alone. On failure every rank releases its half-made handle (closing its
+   mappings) and, when some rank's exported send buffer is caller memory, the ranks agree once more
+   -- ext_mpi_amd_done's rule -- so that no peer maps a caller buffer when the init returns. Takes
+   ownership of h. */
+int ipc_init_settle(emac_handle *h, emac_comm *cm, int rc, int *handle) {
+  int agreed = 0, collective;
+  if (!rc) rc = finish_init(h, handle);
+  if (cm->size > 1) agreed = ipc_agree(cm, rc == 0);
+  if (!rc && !agreed) return 0;
+  if (!rc) { /* this rank succeeded, a peer did not */
+    g_handles[*handle] = NULL;
+    *handle = -1;
+    rc = agreed;
+  }
+  collective = h->done_collective && cm->size > 1;
+  handle_release(h);
+  if (collective) ipc_agree(cm, 1);
+  return rc;
+}
+
 /* IPC form: node barrier `phase` (0 before the fold: every rank's send buffer is ready and its
    receive buffer free; 1 after it: every fan-out store has landed) on the handle's stream. The
    Start is named by its phase-1 epoch (`tag`, ipc_sync.hpp). Phase 0 is preceded by a
@@ -854,6 +892,7 @@ int ipc_barrier(emac_handle *h, int phase) {
   emac_comm *cm = &g_comms[h->comm];
   int rc;
   unsigned long epoch, tag;
+  h->tune.ops++;
   if (phase == 0 && h->ev_release && (rc = emac_gpu_event_record(h->ev_release, h->stream))) return rc;
   epoch = ++h->epoch[phase];
   tag = phase ? epoch : h->epoch[1] + 1;

@@ -299,10 +299,10 @@ int ext_mpi_amd_node_comm_allreduce_init(int nranks, const void *const *sendbufs
     if (!single || (single == 2 && op != EMAC_SUM)) rc = EMAC_ERR_UNSUPPORTED; /* (the same on every rank) */
     for (r = 0; r < R && !rc; r++) rc = map_buffers(h, r, sendbufs[r], recvbufs[r]); /* local: device mirrors */
     h->kind = KIND_IPC;
-    if ((rc = node_ipc_init(h, cm, rc))) goto fail;
-    if ((rc = emac_gpu_stream_create(&h->stream))) goto fail;
-    if ((rc = finish_init(h, handle))) goto fail;
-    return 0;
+    rc = node_ipc_init(h, cm, rc);
+    if (!rc) rc = emac_gpu_stream_create(&h->stream);
+    rc = ipc_init_settle(h, cm, rc, handle);
+    goto out;
   }
   for (r = 0; r < R; r++)
     if ((rc = map_buffers(h, r, sendbufs[r], recvbufs[r]))) goto fail;

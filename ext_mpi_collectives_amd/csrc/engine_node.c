@@ -105,8 +105,8 @@ int ext_mpi_amd_node_allreduce_init(int nranks, const void *const *sendbufs, voi
     goto fail;
   }
   nb = node_buckets(h, 0, count, b);
+  if ((rc = node_pipe_init(h))) goto fail; /* first: a pipelined handle's main fold is never tuned */
   if ((rc = upload_buckets(h, b, nb))) goto fail;
-  if ((rc = node_pipe_init(h))) goto fail;
   free(b);
   b = NULL;
   if ((rc = emac_gpu_stream_create(&h->stream))) goto fail;

@@ -126,6 +126,14 @@ int emac_gpu_fold(int dtype, int op, int nsrc, int fan, int unroll, const emac_c
   return fold_dispatch(dtype, op, nsrc, fan, unroll, L, ch);
 }
 
+int emac_gpu_fold_supported(int dtype, int op, int nsrc, int fan, int tree, int unroll, int uniform) {
+  static const emac_codes none = {{0}, {0}, 1, 0};
+  emac::Launch L = {&none, nullptr, 1, 1, uniform ? 1 : 0, 1, nullptr, 0, nullptr, nullptr, nsrc};
+  L.dry = true;
+  if (op < EMAC_SUM || op > EMAC_MAX || (fan != 0 && fan != 1)) return 0;
+  return fold_dispatch(dtype, op, nsrc, fan, unroll, L, tree) == 0;
+}
+
 int emac_copy_fan_launch(int tsize, int width, int unroll, const emac::Launch *L);
 
 int emac_gpu_copy_fan(int tsize, int width, int unroll, const emac_bucket *d_buckets, int nb, long ntiles,

@@ -708,11 +708,13 @@ struct Launch {
   hipStream_t s;
   const unsigned *go;  // peer-mapped launches: the phase-0 verdict word (emac_sync.go[slot])
   int nrt;             // leaves (the runtime-leaf-count kernels)
+  bool dry = false;    // resolve the kernel only (emac_gpu_fold_supported): launch nothing
 };
 
 template <typename T, int OP, int N, int U, int CH, int D, int ISSUE = 1>
 int launch_one(const Launch &L) {
   constexpr int KB = defer_tiles(ISSUE);
+  if (L.dry) return 0;
   if constexpr (KB > 1) {  // one workgroup per group of KB tiles
     if (L.tpb <= 0) return launch_one<T, OP, N, U, CH, D, ISSUE & ~(3 << kDeferShift | kLeafMajor)>(L);  // unequal buckets
     const long groups = (long)L.nb * ((L.tpb + KB - 1) / KB);

@@ -145,6 +145,9 @@ int emac_gpu_pick_unroll(int op, int nsrc, int tree, int fan, long total_vectors
 int emac_gpu_fold(int dtype, int op, int nsrc, int fan, int unroll, const emac_codes *codes,
                   const emac_bucket *d_buckets, int nb, long ntiles, long tiles_per_bucket, int all_full,
                   const emac_edge *d_edges, int nedges, void *stream);
+/* 1 when emac_gpu_fold has a kernel for this shape and schedule (tree: emac_tree_kind; uniform:
+   every bucket the same tile count, which the deferred-store schedules need), else 0 */
+int emac_gpu_fold_supported(int dtype, int op, int nsrc, int fan, int tree, int unroll, int uniform);
 /* the same for a peer-mapped launch (fan 2): `go` is the device word the phase-0 barrier before
    it wrote (emac_sync.go[slot]); a workgroup that reads 0 stores nothing */
 int emac_gpu_fold_remote(int dtype, int op, int nsrc, int unroll, const emac_codes *codes, const emac_bucket *d_buckets,

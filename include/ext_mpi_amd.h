@@ -126,6 +126,30 @@ int ext_mpi_amd_handle_schedule(int handle, int *unroll, int *issue, int *tuned)
 /* The schedules the tuner measures on this handle's first Starts: *n of them (0: untuned), the
  * first min(*n, max) written to sched as U | issue << 4. Introspection for tests. */
 int ext_mpi_amd_handle_candidates(int handle, int *n, int *sched, int max);
+/* The tuner's state of a handle (introspection for tests and benchmarks). A sample is one
+ * candidate on three Starts in a row: the first untimed, the other timed_starts_per_sample timed --
+ * as one window in the NODE form on device buffers, each fold launch between its own events in
+ * every form that runs other operations between two folds (`isolated`: RCCL legs, barriers, pulls,
+ * staging copies). ops_in_sample[i] counts the operations the handle enqueued inside sample i's
+ * timed span(s): one fold per timed Start when the samples time the fold alone. `cached`: the
+ * schedule came from an earlier handle of the same shape (nothing measured on this one). */
+#define EXT_MPI_AMD_TUNE_MAX 8
+typedef struct {
+  int candidates;              /* 0: not tuned */
+  int chosen;                  /* kept candidate, -1 while measuring */
+  int cached;
+  int isolated;
+  int starts;                  /* Starts counted by the tuner */
+  int timed_starts_per_sample;
+  int samples;                 /* candidates x rounds (0 when cached) */
+  int schedule[EXT_MPI_AMD_TUNE_MAX]; /* U | issue << 4 per candidate */
+  float us[EXT_MPI_AMD_TUNE_MAX];     /* shortest sample per candidate, per timed Start (once kept) */
+  int ops_in_sample[EXT_MPI_AMD_TUNE_MAX * 3];
+} ext_mpi_amd_tune_info;
+int ext_mpi_amd_handle_tune_info(int handle, ext_mpi_amd_tune_info *info);
+/* Forget every kept schedule of this process (the next handle of each shape tunes afresh); returns
+ * the number of entries dropped. EXT_MPI_AMD_TUNE_CACHE=0 bypasses the cache altogether. */
+int ext_mpi_amd_tune_cache_clear(void);
 /* Run later Starts on a caller-owned hipStream_t (e.g. to serialise several handles). */
 int ext_mpi_amd_set_stream(int handle, void *hip_stream);
 /* Start a subset of the legs (benchmarking / profiling): the reference interleaves them in one

@@ -40,3 +40,107 @@ def test_bench_multi_rank_transport_isolation_without_gpu():
     ex = out["extras"]
     assert ex["process_per_transport"] is True
     assert "error" in ex["ipc_transport"] and "error" in ex["rccl_transport"]
+    # every failure is named with its transport, exit code and the child's last stderr lines
+    fails = ex["failures"]
+    assert {f["transport"] for f in fails} == {"node", "ipc", "rccl"}
+    assert all(f["rc"] != 0 and isinstance(f["stderr_tail"], list) and f["stderr_tail"] for f in fails), fails
+
+
+def _bench():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+class _Args:
+    steps, warmup, dtype, transport, copyin, size_mib, ranks = 20, 5, "float", "ipc", None, 16.0, 8
+
+
+MIB = 1 << 20
+
+
+def _node_ok(world):
+    S = 16 * MIB
+    return {"wall": 20 * 50e-6, "checked": True, "ranks_per_gpu": 8, "bytes_per_rank": S, "copyin": "6;1 -8 8",
+            "ports": [-(world - 1), world - 1], "transport": "ipc", "copy_in_fold_s": 25e-6, "node_legs_s": 20e-6,
+            "copy_out_s": 0.0, "schedule": {"unroll": 4, "issue": 5, "tuned": 1}, "nsets": 3,
+            "transports": {"ipc": {"ms_per_step": 0.05, "checked": True}}}
+
+
+def _one_rank_ok(world):
+    sweep = [{"dtype": "float", "bytes_per_rank": n, "us_per_allreduce": 10.0, "algbw_gbps": 1.0, "checked": True}
+             for n in (8, 64 << 10, 1 << 20, 16 << 20, 64 << 20, 256 << 20, 512 << 20)]
+    sweep.append({"dtype": "double", "bytes_per_rank": 256 << 20, "us_per_allreduce": 900.0, "algbw_gbps": 298.0,
+                  "checked": True})  # BASELINE configs[3]
+    return {"wall": 20 * 60e-6, "checked": True, "fold_s": 8e-6, "alone_s": 7.5e-6, "sweep": sweep,
+            "radix_sweep": [], "local_fold": {"leaves": world, "chunk_bytes": 2 * MIB, "us_all_gpus": 4.0,
+                                              "us_rank0_alone": 3.9, "rate_retained": 0.975, "schedule": None},
+            "host_buffers": {"checked": True}}
+
+
+REQUIRED = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "config", "roofline", "extras")
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_multi_gpu_line_from_fabricated_children(world):
+    """multi_gpu's assembly (bench.py multi_gpu_line / node_form_line) from fabricated child
+    results: every child ok; the node child failed (exit code, stderr tail); the node child timed
+    out and one transport failed; everything timed out. Each case yields one valid line with the
+    contract's keys that names what failed."""
+    b = _bench()
+    S = 16 * MIB
+    order = ["ipc", "rccl"]
+    ok_line = b.multi_gpu_line(_Args, world, "f32", S, f"6;1 -{world} {world}", _node_ok(world),
+                               {"ipc": _one_rank_ok(world), "rccl": {"wall": 1e-3, "checked": True}}, order, world, [])
+    json.dumps(ok_line)
+    assert all(k in ok_line for k in REQUIRED)
+    assert "configs[1]'s node" in ok_line["config"]["workload"] and ok_line["config"]["layout"] == "node-per-gpu"
+    assert ok_line["value"] == pytest.approx(world * 8 * S * 20 / (20 * 50e-6) / 1e9, rel=1e-3)
+    one = ok_line["extras"]["one_rank_per_gpu"]
+    assert any(p["dtype"] == "double" and p["bytes_per_rank"] == 256 << 20 for p in one["extras"]["sweep"])  # configs[3]
+    assert "failures" not in ok_line["extras"]
+
+    # the node child failed on one rank: the one-rank-per-GPU line, the node failure named
+    rc_fail, fail = b.child_outcome("node", 1, 12.5, ["Traceback ...", "RuntimeError: boom"], None)
+    assert rc_fail == {} and fail["rc"] == 1 and fail["stderr_tail"][-1] == "RuntimeError: boom"
+    line = b.multi_gpu_line(_Args, world, "f32", S, f"6;1 -{world} {world}", fail,
+                            {"ipc": _one_rank_ok(world), "rccl": {"wall": 1e-3, "checked": True}}, order, world,
+                            [dict(fail, rank=1)])
+    json.dumps(line)
+    assert all(k in line for k in REQUIRED) and line["config"]["layout"] == "rank-per-gpu" and line["value"] > 0
+    assert line["extras"]["node_form_per_gpu"]["transport"] == "node"
+    assert line["extras"]["failures"][0]["stderr_tail"][-1] == "RuntimeError: boom"
+
+    # the node child timed out, ipc failed its check, rccl ran: rccl's line
+    _, tmo = b.child_outcome("node", "timeout", 480.0, ["rank 0: node form ..."], None)
+    _, bad = b.child_outcome("ipc", 0, 30.0, [], {"wall": 1.0, "checked": False})
+    assert tmo["rc"] == "timeout" and "timed out" in tmo["error"] and bad["error"] == "result check failed"
+    line = b.multi_gpu_line(_Args, world, "f32", S, f"6;1 -{world} {world}", tmo, {"ipc": bad, "rccl": _one_rank_ok(world)},
+                            order, world, [tmo, bad])
+    assert line["config"]["transport"] == "rccl" and line["extras"]["ipc_transport"]["error"] == "result check failed"
+    assert line["extras"]["node_form_per_gpu"]["rc"] == "timeout"
+
+    # everything timed out: a zero line naming every failure
+    fails = [b.child_outcome(t, "timeout", 100.0, ["..."], None)[1] for t in ("node", "ipc", "rccl")]
+    line = b.multi_gpu_line(_Args, world, "f32", S, f"6;1 -{world} {world}", fails[0],
+                            {"ipc": fails[1], "rccl": fails[2]}, order, world, fails)
+    json.dumps(line)
+    assert all(k in line for k in REQUIRED)
+    assert line["value"] == 0.0 and line["error"] == "no transport completed"
+    assert "ipc: ipc child timed out" in line["config"]["workload"]
+    assert [f["transport"] for f in line["extras"]["failures"]] == ["node", "ipc", "rccl"]
+
+
+def test_child_process_limit_kills_and_reports():
+    """run_child_process: a child that outlives its limit is killed (its process group) and
+    reported as "timeout" with its last stderr lines; one that fails reports its exit code."""
+    b = _bench()
+    code = "import sys, time\nfor i in range(3): print('line', i, file=sys.stderr, flush=True)\ntime.sleep(60)"
+    rc, el, tail = b.run_child_process([sys.executable, "-c", code], dict(os.environ), 3.0)
+    assert rc == "timeout" and el < 30 and tail[-1] == "line 2"
+    rc, el, tail = b.run_child_process([sys.executable, "-c", "import sys; print('bad', file=sys.stderr); sys.exit(7)"],
+                                       dict(os.environ), 30.0)
+    assert rc == 7 and tail == ["bad"]

@@ -1,0 +1,266 @@
+"""The fold's launch-schedule tuner (engine_tune.c, engine_int.h emac_tune) on MI355X:
+
+* what a sample times -- in every form whose Starts enqueue other operations between two folds
+  (the COMM form's RCCL / loopback legs, the node join's legs, staging copies) each timed fold
+  launch between its own events, so a sample is the fold alone; in the NODE
+  form on device buffers the timed Starts back to back as one window. The introspection hook
+  (ext_mpi_amd_handle_tune_info) counts the operations the handle enqueued inside each sample's
+  timed span(s): one fold per timed Start;
+* the per-process cache of kept schedules: a handle of a shape some earlier
+  handle tuned starts on its kept schedule and spends no Start measuring;
+* a forced schedule (EXT_MPI_AMD_FOLD_SCHEDULE) the shape has no kernel for is refused at init.
+Every Start of every handle is checked bitwise against the oracle: the schedule never changes the
+bits (every candidate folds in the plan's order).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import ext_mpi_collectives_amd as emac
+from helpers import xorshift_inputs
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+TORCH = {emac.FLOAT: torch.float32, emac.DOUBLE: torch.float64, emac.INT: torch.int32, emac.LONG: torch.int64}
+MAX_TUNE_STARTS = 1 + 3 * 3 * emac.TUNE_MAX + 1  # the static pick, 3 rounds of <= 8 candidates x 3 Starts, the keeping one
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    emac.lib()
+
+
+@pytest.fixture
+def fresh_tuner(monkeypatch):
+    """every handle of the test tunes afresh unless the test enables the cache itself"""
+    monkeypatch.delenv("EXT_MPI_AMD_AUTOTUNE", raising=False)
+    monkeypatch.delenv("EXT_MPI_AMD_FOLD_SCHEDULE", raising=False)
+    monkeypatch.delenv("EXT_MPI_AMD_TUNE_CACHE", raising=False)
+    emac.tune_cache_clear()
+    yield
+    emac.tune_cache_clear()
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def assert_bitwise(got, want, what=""):
+    for r, (g, w) in enumerate(zip(got, want)):
+        if not np.array_equal(g.view(np.uint8), w.view(np.uint8)):
+            bad = np.nonzero(g.view(np.uint8) != w.view(np.uint8))[0]
+            raise AssertionError(f"{what}: rank {r}: {bad.size} differing bytes, first at byte {bad[0]}")
+
+
+def test_tune_cache_same_shape_handles(oracle, fresh_tuner):
+    """20 handles of one shape created and destroyed one after the other (the blocking front end's
+    LRU misses, an application re-creating its persistent request): the first tunes, every later
+    one starts on the kept schedule -- tuned == 1 from its first Start, nothing measured -- and
+    every Start of every handle is bitwise."""
+    R, count, copyin = 8, (2 << 20) // 4, "6;1 -8 8"  # 8 x 2 MiB float: 32 MiB per launch, tuned
+    sends = xorshift_inputs(R, count, emac.FLOAT, seed_base=0xCAC4E)
+    want = oracle.allreduce(sends, copyin)
+    dsend = [_dev(s) for s in sends]
+    drecv = [torch.full((count,), -1.0, device="cuda") for _ in range(R)]
+    kept = None
+    for i in range(21):
+        h = emac.node_allreduce_init([t.data_ptr() for t in dsend], [t.data_ptr() for t in drecv], count, emac.FLOAT,
+                                     copyin)
+        try:
+            info = emac.handle_tune_info(h)
+            if i == 0:
+                assert info["candidates"] > 1 and info["chosen"] == -1 and not info["cached"], info
+            else:
+                assert info["cached"] == 1 and info["candidates"] == 1 and info["samples"] == 0, (i, info)
+                assert emac.handle_schedule(h)["tuned"] == 1, i
+            starts = MAX_TUNE_STARTS if i == 0 else 3
+            for k in range(starts):
+                for t in drecv:
+                    t.fill_(-1.0)
+                torch.cuda.synchronize()
+                emac.start(h)
+                emac.wait(h)
+                assert_bitwise([t.cpu().numpy() for t in drecv], want, f"handle {i} Start {k}")
+                sc = emac.handle_schedule(h)
+                if i > 0:
+                    assert sc["tuned"] == 1 and (sc["unroll"], sc["issue"]) == kept, (i, k, sc, kept)
+            sc = emac.handle_schedule(h)
+            assert sc["tuned"] == 1, (i, sc)
+            if i == 0:
+                kept = (sc["unroll"], sc["issue"])
+                info = emac.handle_tune_info(h)
+                # NODE form on device buffers: the timed Starts as one window, one fold each
+                assert info["isolated"] == 0 and info["timed_starts_per_sample"] == 2, info
+                assert info["ops_in_sample"] == [2] * (3 * info["candidates"]), info
+        finally:
+            emac.done(h)
+    # EXT_MPI_AMD_TUNE_CACHE=0: the same shape tunes again
+    os.environ["EXT_MPI_AMD_TUNE_CACHE"] = "0"
+    try:
+        h = emac.node_allreduce_init([t.data_ptr() for t in dsend], [t.data_ptr() for t in drecv], count, emac.FLOAT,
+                                     copyin)
+        info = emac.handle_tune_info(h)
+        emac.done(h)
+        assert info["cached"] == 0 and info["candidates"] > 1, info
+    finally:
+        del os.environ["EXT_MPI_AMD_TUNE_CACHE"]
+
+
+def _tune_local_fold(R, chunk, code, seed):
+    """fold_init over R leaves of `chunk` elements -> one destination, run until its schedule is
+    kept; returns (kept (U, issue), tune info)"""
+    srcs_np = xorshift_inputs(R, chunk, code, seed_base=seed)
+    want = srcs_np[0].copy()
+    for x in srcs_np[1:]:
+        want = want + x
+    srcs = [_dev(x) for x in srcs_np]
+    dst = torch.full((chunk,), -1, dtype=TORCH[code], device="cuda")
+    h = emac.fold_init([t.data_ptr() for t in srcs], [dst.data_ptr()], chunk, code)
+    try:
+        for k in range(MAX_TUNE_STARTS):
+            emac.start(h)
+            emac.wait(h)
+        assert_bitwise([dst.cpu().numpy()], [want], "local fold")
+        sc = emac.handle_schedule(h)
+        assert sc["tuned"] == 1, sc
+        return (sc["unroll"], sc["issue"]), emac.handle_tune_info(h)
+    finally:
+        emac.done(h)
+
+
+def test_comm_loopback_samples_time_the_fold_alone(oracle, fresh_tuner):
+    """The COMM form, 8 loopback ranks x 16 MiB float ('6;1 -8 8'): between two folds of a rank
+    its allgather leg, the next Start's reduce-scatter leg (and staging) run. Each timed fold is
+    bracketed alone (`isolated`), one operation per timed span; the folds are driven one rank at a
+    time so that each runs alone on the GPU, as fold_init's does. The kept schedule is the one the
+    same shape's fold_init handle keeps (8 leaves of 2 MiB -> 1), or one that ties it within
+    noise in this handle's own samples; and its sample time is the fold's, not fold + legs."""
+    os.environ["EXT_MPI_AMD_TUNE_CACHE"] = "0"
+    try:
+        R, count, copyin = 8, (16 << 20) // 4, "6;1 -8 8"
+        ref_kept, ref = _tune_local_fold(R, count // R, emac.FLOAT, 0x10C0)
+        sends = xorshift_inputs(R, count, emac.FLOAT, seed_base=0x7A12)
+        want = oracle.allreduce(sends, copyin)
+        comms = emac.comm_init_loopback(R)
+        sbufs = [_dev(s) for s in sends]
+        rbufs = [torch.full((count,), -1.0, device="cuda") for _ in range(R)]
+        hs = []
+        try:
+            for r in range(R):
+                hs.append(emac.allreduce_init(sbufs[r].data_ptr(), rbufs[r].data_ptr(), count, emac.FLOAT, comms[r],
+                                              copyin))
+            for rep in range(MAX_TUNE_STARTS):
+                for t in rbufs:
+                    t.fill_(-1.0)
+                torch.cuda.synchronize()
+                for leg in emac.lockstep_legs():
+                    if leg == emac.LEG_FOLD:  # one rank's fold at a time: alone on the GPU
+                        for h in hs:
+                            emac.start_legs(h, leg)
+                            emac.wait(h)
+                        continue
+                    for h in hs:
+                        emac.start_legs(h, leg)
+                    for h in hs:
+                        emac.wait(h)
+                assert_bitwise([t.cpu().numpy() for t in rbufs], want, f"Start {rep}")
+            infos = [emac.handle_tune_info(h) for h in hs]
+            scheds = [emac.handle_schedule(h) for h in hs]
+        finally:
+            for h in hs:
+                emac.done(h)
+            for c in comms:
+                emac.comm_free(c)
+    finally:
+        del os.environ["EXT_MPI_AMD_TUNE_CACHE"]
+    for r, (info, sc) in enumerate(zip(infos, scheds)):
+        assert sc["tuned"] == 1 and info["isolated"] == 1, (r, info)
+        assert info["schedules"] == ref["schedules"], (r, info["schedules"], ref["schedules"])
+        # one fold per timed Start in every sample: nothing else of the handle inside a timed span
+        assert info["ops_in_sample"] == [info["timed_starts_per_sample"]] * (3 * info["candidates"]), (r, info)
+        kept = (sc["unroll"], sc["issue"])
+        us = dict(zip(info["schedules"], info["us"]))
+        assert kept == ref_kept or us[ref_kept] <= 1.03 * us[kept], (r, kept, ref_kept, info["us"], ref["us"])
+        # the fold alone: the local fold's time for the same shape, not fold + allgather + reduce-scatter
+        assert us[kept] <= 1.25 * min(ref["us"]), (r, us, ref["us"])
+
+
+def test_node_join_samples_time_the_fold_alone(oracle, fresh_tuner):
+    """The NODE form over two nodes (ext_mpi_amd_node_comm_allreduce_init, loopback members):
+    between two copy-in folds of a node run its inter-node legs, their folds and the copy-out.
+    Each timed copy-in fold is bracketed alone: one operation per timed span, every Start bitwise."""
+    nodes, R, count, copyin = 2, 8, (4 << 20) // 4, "6;1 -8 8"
+    W = nodes * R
+    sends = xorshift_inputs(W, count, emac.FLOAT, seed_base=0x401D)
+    want = oracle.allreduce_nodes(sends, copyin, nodes)
+    comms = emac.comm_init_loopback(nodes)
+    sbufs = [_dev(s) for s in sends]
+    rbufs = [torch.full((count,), -1.0, device="cuda") for _ in range(W)]
+    hs = []
+    try:
+        for n in range(nodes):
+            hs.append(emac.node_comm_allreduce_init([t.data_ptr() for t in sbufs[n * R:(n + 1) * R]],
+                                                    [t.data_ptr() for t in rbufs[n * R:(n + 1) * R]], count,
+                                                    emac.FLOAT, comms[n], copyin))
+        for rep in range(MAX_TUNE_STARTS):
+            for t in rbufs:
+                t.fill_(-1.0)
+            torch.cuda.synchronize()
+            for leg in emac.lockstep_legs(nodes):
+                for h in hs:
+                    emac.start_legs(h, leg)
+                for h in hs:
+                    emac.wait(h)
+            assert_bitwise([t.cpu().numpy() for t in rbufs], want, f"Start {rep}")
+        infos = [emac.handle_tune_info(h) for h in hs]
+        scheds = [emac.handle_schedule(h) for h in hs]
+    finally:
+        for h in hs:
+            emac.done(h)
+        for c in comms:
+            emac.comm_free(c)
+    for n, (info, sc) in enumerate(zip(infos, scheds)):
+        assert sc["tuned"] == 1 and info["isolated"] == 1 and info["candidates"] > 1, (n, info)
+        assert info["ops_in_sample"] == [info["timed_starts_per_sample"]] * (3 * info["candidates"]), (n, info)
+
+
+def test_forced_schedule_refused_at_init(fresh_tuner, monkeypatch):
+    """EXT_MPI_AMD_FOLD_SCHEDULE names the only candidate (A/B runs): a word the shape has no
+    kernel for is refused by the init (ERROR_UNSUPPORTED), not by a later Start; a valid one runs."""
+    R, count = 8, (2 << 20) // 4
+    dsend = [torch.ones(count, device="cuda") for _ in range(R)]
+    drecv = [torch.zeros(count, device="cuda") for _ in range(R)]
+    monkeypatch.setenv("EXT_MPI_AMD_FOLD_SCHEDULE", str(3 | 1 << 4))  # U 3: never instantiated
+    with pytest.raises(RuntimeError, match="UNSUPPORTED"):
+        emac.node_allreduce_init([t.data_ptr() for t in dsend], [t.data_ptr() for t in drecv], count, emac.FLOAT)
+    monkeypatch.setenv("EXT_MPI_AMD_FOLD_SCHEDULE", str(4 | 5 << 4))  # U 4 staggered: instantiated
+    h = emac.node_allreduce_init([t.data_ptr() for t in dsend], [t.data_ptr() for t in drecv], count, emac.FLOAT)
+    try:
+        for _ in range(3):
+            emac.start(h)
+            emac.wait(h)
+        assert emac.handle_candidates(h) == [(4, 5)]
+        assert all(torch.equal(t, torch.full_like(t, float(R))) for t in drecv)
+    finally:
+        emac.done(h)
+
+
+def test_pipelined_host_handle_not_tuned(fresh_tuner, monkeypatch):
+    """A pipelined host-staged NODE handle (EXT_MPI_AMD_PIPELINE=1) never launches its main fold
+    (pipe_start folds parts): it gets no tuner uploads or events."""
+    monkeypatch.setenv("EXT_MPI_AMD_PIPELINE", "1")
+    R, count = 8, (8 << 20) // 4
+    sends = [np.full(count, r + 1, dtype=np.float32) for r in range(R)]
+    recvs = [np.zeros(count, dtype=np.float32) for _ in range(R)]
+    h = emac.node_allreduce_init([s.ctypes.data for s in sends], [r.ctypes.data for r in recvs], count, emac.FLOAT)
+    try:
+        assert emac.handle_tune_info(h)["candidates"] == 0
+        emac.start(h)
+        emac.wait(h)
+        assert all(np.all(r == R * (R + 1) / 2) for r in recvs)
+    finally:
+        emac.done(h)
