@@ -57,8 +57,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=30.0, help="bound of the CPU baseline sample")
     ap.add_argument("--transport", default="ipc", choices=["ipc", "rccl"],
                     help="N > 1: peer-mapped hipIpc form (default) or RCCL point-to-point legs")
-    ap.add_argument("--shape", default=None, choices=["local256", "node256", "node16", "copy256", "int4", "long4"],
+    ap.add_argument("--shape", default=None, choices=["local256", "node16", "node64", "node256", "node512", "copy256",
+                                                      "int4", "long4"],
                     help="profiling: run only this fold shape (40 launches) and exit (PMC passes, tools/gpu_pmc_r02.sh)")
+    ap.add_argument("--schedules", default=None,
+                    help="--shape node*: comma-separated fold schedule words (U | issue << 4) to run in turn")
     ap.add_argument("--child-transport", default=None, choices=["ipc", "rccl", "node"], help=argparse.SUPPRESS)
     ap.add_argument("--child-full", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--child-result", default=None, help=argparse.SUPPRESS)
@@ -1380,7 +1383,7 @@ def shape_only(args):
     import torch
     import ext_mpi_collectives_amd as emac
     emac.lib()
-    MB = (256 if args.shape not in ("node16", "int4", "long4") else 16 if args.shape == "node16" else 4) * MIB
+    MB = {"node16": 16, "node64": 64, "node512": 512, "int4": 4, "long4": 4}.get(args.shape, 256) * MIB
     if args.shape == "local256":
         r = comm_shape_fold(8, MB // 8 // 4, torch.float32, emac.FLOAT, 40)
     elif args.shape == "copy256":  # the node256 launch's bytes as a 1:1 copy (tools/ceiling.hip), same lease
@@ -1390,7 +1393,7 @@ def shape_only(args):
         a.uniform_(-1, 1)
         stream = torch.cuda.current_stream()
         best = {}
-        for variant in (0, 1):
+        for variant in (0, 1, 2):  # nontemporal, default policy, phased (tools/ceiling.hip)
             for i in range(3):
                 L.ceiling_copy(a.data_ptr() + i * 2 * n, a.data_ptr() + i * 2 * n + n, n, 1, variant, stream.cuda_stream)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -1400,13 +1403,23 @@ def shape_only(args):
                 assert L.ceiling_copy(b, b + n, n, 1, variant, stream.cuda_stream) == 0
             e1.record(stream)
             torch.cuda.synchronize()
-            best["nt" if variant == 0 else "plain"] = round(e0.elapsed_time(e1) * 1e3 / 20, 2)
+            best[("nt", "plain", "phased")[variant]] = round(e0.elapsed_time(e1) * 1e3 / 20, 2)
         r = {"avg_launch_us": best, "bytes_per_launch": 2 * n}
     elif args.shape in ("int4", "long4"):  # BASELINE configs[2]'s launch (4 MiB per rank x 8)
         td, cd = (torch.int32, emac.INT) if args.shape == "int4" else (torch.int64, emac.LONG)
         ts = 4 if args.shape == "int4" else 8
         r = node_run(8, MB // ts, td, cd, "6;1 -8 8", 50, 5, alloc="hip")
         r = {"avg_launch_us": round(r["event_ms"] * 1e3 / 50, 2), "checked": r["checked"], "schedule": r["schedule"]}
+    elif args.schedules:  # every listed fold schedule in turn (EXT_MPI_AMD_FOLD_SCHEDULE), one handle set each
+        r = {}
+        for w in args.schedules.split(","):
+            os.environ["EXT_MPI_AMD_FOLD_SCHEDULE"] = w
+            x = node_run(8, MB // 4, torch.float32, emac.FLOAT, "6;1 -8 8", 40, 4, alloc="hip")
+            r[w] = {"avg_launch_us": round(x["event_ms"] * 1e3 / 40, 2), "checked": x["checked"],
+                    "schedule": x["schedule"]}
+            log(f"{args.shape} schedule {w}: {r[w]}")
+        del os.environ["EXT_MPI_AMD_FOLD_SCHEDULE"]
+        r = {"by_schedule": r}
     else:
         r = node_run(8, MB // 4, torch.float32, emac.FLOAT, "6;1 -8 8", 40, 4, alloc="hip")
         r = {"avg_launch_us": round(r["event_ms"] * 1e3 / 40, 2), "checked": r["checked"], "schedule": r["schedule"]}

@@ -14,7 +14,8 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libext_mpi_amd.so")
+# EXT_MPI_AMD_LIB: another build of the same library (A/B runs of build options, tools/ab/)
+LIB_PATH = os.environ.get("EXT_MPI_AMD_LIB") or os.path.join(HERE, "libext_mpi_amd.so")
 MPI_LIB_PATH = os.path.join(HERE, "libext_mpi_collectives.so")
 
 DOUBLE, LONG, FLOAT, INT = 0, 1, 2, 3
@@ -388,7 +389,7 @@ def handle_tune_info(h):
     _check("ext_mpi_amd_handle_tune_info", lib().ext_mpi_amd_handle_tune_info(h, ctypes.byref(t)))
     n = min(t.candidates, TUNE_MAX)
     return {"candidates": t.candidates, "chosen": t.chosen, "cached": t.cached, "isolated": t.isolated,
-            "starts": t.starts, "timed_starts_per_sample": t.timed_starts_per_sample,
+            "starts": t.starts, "timed_starts_per_sample": t.timed_starts_per_sample, "samples": t.samples,
             "schedules": [(t.schedule[k] & 15, t.schedule[k] >> 4) for k in range(n)],
             "us": [round(t.us[k], 3) for k in range(n)],
             "ops_in_sample": list(t.ops_in_sample[:min(t.samples, TUNE_MAX * 3)])}

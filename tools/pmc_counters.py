@@ -8,21 +8,31 @@ import re
 import sys
 
 
-def medians(d, kernel):
+def medians(d, kernel, by_kernel=False):
     vals = {}
     for path in glob.glob(f"{d}/**/*counter_collection*.csv", recursive=True):
         for row in csv.DictReader(open(path)):
-            if re.search(kernel, row.get("Kernel_Name", "")):
-                vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
-    return {k: sorted(v)[len(v) // 2] for k, v in vals.items()}
+            name = row.get("Kernel_Name", "")
+            if re.search(kernel, name):
+                key = (re.sub(r"\(.*", "", name), row["Counter_Name"]) if by_kernel else row["Counter_Name"]
+                vals.setdefault(key, []).append(float(row["Counter_Value"]))
+    if not by_kernel:
+        return {k: sorted(v)[len(v) // 2] for k, v in vals.items()}
+    out = {}
+    for (kname, c), v in vals.items():  # per kernel instance (template arguments = the schedule)
+        out.setdefault(kname, {})[c] = sorted(v)[len(v) // 2]
+        out[kname]["dispatches"] = len(v)
+    return out
 
 
 if __name__ == "__main__":
     kernel = r"\bfold_(deferred_)?kernel<"
-    dirs = []
+    dirs, by_kernel = [], False
     for a in sys.argv[1:]:
         if a.startswith("--kernel="):
             kernel = a.split("=", 1)[1]
+        elif a == "--by-kernel":
+            by_kernel = True
         else:
             dirs.append(a)
-    print(json.dumps({d: medians(d, kernel) for d in dirs}, indent=1))
+    print(json.dumps({d: medians(d, kernel, by_kernel) for d in dirs}, indent=1))
