@@ -167,11 +167,27 @@ def host_random(count, np_dtype, seed):
     return rng.integers(-lim, lim, count).astype(np_dtype)
 
 
+def free_sets(sets):
+    for sends, recvs in sets:
+        for b in list(sends) + list(recvs):
+            if isinstance(b, DevBuf):
+                b.free()
+
+
+def free_pool(pool):
+    for sets in pool.values():
+        free_sets(sets)
+    pool.clear()
+
+
 TUNE_STARTS = 1 + 3 * 3 * 8 + 1  # a handle's first Start, 3 rounds of at most 8 candidates on three Starts each, and the keeping one
 
 
-def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * MIB, host=False, alloc="torch"):
-    """Time `steps` node-form Allreduces (R ranks in this GPU). Returns dict of timings."""
+def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * MIB, host=False, alloc="torch",
+             pool=None):
+    """Time `steps` node-form Allreduces (R ranks in this GPU). Returns dict of timings. `pool`: a
+    dict that keeps the device buffer sets for the next call of the same shape (freed by the caller,
+    free_pool) instead of making and filling them again."""
     import torch
     import ext_mpi_collectives_amd as emac
     tsize = torch.empty((), dtype=tdtype).element_size()
@@ -182,8 +198,14 @@ def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * 
         nsets = max(2, math.ceil(min_set_bytes / max(1, set_bytes)))
     stream = torch.cuda.Stream()
     sets, handles = [], []
+    key = (R, count, str(tdtype), nsets, host, alloc)
+    pooled = pool is not None and key in pool
+    if pooled:
+        sets = pool[key]
     for s in range(nsets):
-        if host:
+        if pooled:
+            sends, recvs = sets[s]
+        elif host:
             sends = [torch.empty(count, dtype=tdtype).pin_memory() for _ in range(R)]
             recvs = [torch.empty(count, dtype=tdtype).pin_memory() for _ in range(R)]
             for r, t in enumerate(sends):
@@ -204,8 +226,11 @@ def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * 
                 fill(t, 0x5EED0000 + 97 * s + r)
         h = emac.node_allreduce_init([t.data_ptr() for t in sends], [t.data_ptr() for t in recvs], count, code, copyin)
         emac.set_stream(h, stream.cuda_stream)
-        sets.append((sends, recvs))
+        if not pooled:
+            sets.append((sends, recvs))
         handles.append(h)
+    if pool is not None:
+        pool[key] = sets
     torch.cuda.synchronize()
     # W untimed Starts -- and at least enough for every handle to finish its launch-schedule
     # tuning (its first TUNE_STARTS Starts, engine.c emac_tune): the timed Starts run the kept schedule
@@ -254,10 +279,8 @@ def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * 
     gate.free()
     for h in handles:
         emac.done(h)
-    for sends, recvs in sets:
-        for b in list(sends) + list(recvs):
-            if isinstance(b, DevBuf):
-                b.free()
+    if pool is None:
+        free_sets(sets)
     del sets
     return {"wall_s": t1 - t0, "event_ms": e0.elapsed_time(e1), "nsets": nsets, "checked": checked,
             "set_bytes": set_bytes, "schedule": sched}
@@ -1411,14 +1434,15 @@ def shape_only(args):
         r = node_run(8, MB // ts, td, cd, "6;1 -8 8", 50, 5, alloc="hip")
         r = {"avg_launch_us": round(r["event_ms"] * 1e3 / 50, 2), "checked": r["checked"], "schedule": r["schedule"]}
     elif args.schedules:  # every listed fold schedule in turn (EXT_MPI_AMD_FOLD_SCHEDULE), one handle set each
-        r = {}
+        r, pool = {}, {}
         for w in args.schedules.split(","):
             os.environ["EXT_MPI_AMD_FOLD_SCHEDULE"] = w
-            x = node_run(8, MB // 4, torch.float32, emac.FLOAT, "6;1 -8 8", 40, 4, alloc="hip")
+            x = node_run(8, MB // 4, torch.float32, emac.FLOAT, "6;1 -8 8", 40, 4, alloc="hip", pool=pool)
             r[w] = {"avg_launch_us": round(x["event_ms"] * 1e3 / 40, 2), "checked": x["checked"],
                     "schedule": x["schedule"]}
             log(f"{args.shape} schedule {w}: {r[w]}")
         del os.environ["EXT_MPI_AMD_FOLD_SCHEDULE"]
+        free_pool(pool)
         r = {"by_schedule": r}
     else:
         r = node_run(8, MB // 4, torch.float32, emac.FLOAT, "6;1 -8 8", 40, 4, alloc="hip")

@@ -365,6 +365,17 @@ int ext_mpi_amd_gpu_memcpy_hd(void *dst, const void *src, size_t bytes) {
 int ext_mpi_amd_gpu_memcpy_dh(void *dst, const void *src, size_t bytes) {
   return bytes ? ok(hipMemcpy(dst, src, bytes, hipMemcpyDefault)) : 0;
 }
+int ext_mpi_amd_gpu_memcpy_async(void *dst, const void *src, size_t bytes, void *hip_stream) {
+  return emac_gpu_memcpy_async(dst, src, bytes, hip_stream);
+}
+int ext_mpi_amd_gpu_after_default_stream(void *hip_stream) {
+  hipEvent_t e;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return EMAC_ERR_DEVICE;
+  int rc = ok(hipEventRecord(e, nullptr));
+  if (!rc) rc = ok(hipStreamWaitEvent(static_cast<hipStream_t>(hip_stream), e, 0));
+  (void)hipEventDestroy(e);  // released once the wait has been satisfied
+  return rc;
+}
 int ext_mpi_amd_gpu_is_device_pointer(const void *p) { return emac_gpu_is_device_pointer(p); }
 int ext_mpi_amd_gpu_synchronize(void) { return emac_gpu_device_sync(); }
 int ext_mpi_amd_gpu_device_count(void) { return emac_gpu_device_count(); }

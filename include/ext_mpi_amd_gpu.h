@@ -33,6 +33,13 @@ int ext_mpi_amd_gpu_device_count(void);
 int ext_mpi_amd_gpu_device_of(const void *p); /* device ordinal owning p, -1 for host memory */
 int ext_mpi_amd_gpu_copy_reduce(int dtype, int op, int nsrc, const void *const *srcs, int ndst, void *const *dsts,
                                 long count, void *hip_stream);
+/* Stream-ordered helpers of the MPI layer's staging (no reference counterpart: its copies are
+ * synchronous): a copy enqueued on hip_stream, and hip_stream made to wait (an event, no host
+ * synchronisation) for the work enqueued so far on the legacy default stream -- which itself
+ * waits for every blocking stream, where an application that does not synchronise before an MPI
+ * call leaves the work producing its send buffer. */
+int ext_mpi_amd_gpu_memcpy_async(void *dst, const void *src, size_t bytes, void *hip_stream);
+int ext_mpi_amd_gpu_after_default_stream(void *hip_stream);
 
 #ifdef __cplusplus
 }
