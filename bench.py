@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--child-full", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--child-result", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--child-deadline", type=float, default=600.0, help=argparse.SUPPRESS)
-    ap.add_argument("--alloc", default="hip", choices=["hip", "torch"],
+    ap.add_argument("--alloc", default="hip", choices=["hip", "torch", "contig"],
                     help="device buffers from hipMalloc (library device ABI, like the reference's "
                          "tests/benchmark_gpu.c cudaMalloc) or torch's caching allocator")
     return ap.parse_args()
@@ -110,12 +110,21 @@ def traffic_from_profiles(tag):
 
 
 class DevBuf:
-    """A device buffer from the library's device ABI (hipMalloc), filled from host data."""
+    """A device buffer from the library's device ABI (hipMalloc), filled from host data.
+    CONTIG (bench.py --alloc contig): physically contiguous memory instead (hipExtMallocWithFlags
+    hipDeviceMallocContiguous through tools/libceiling.so), an A/B of address translation."""
+    CONTIG = False
 
     def __init__(self, nbytes):
         import ext_mpi_collectives_amd as emac
         self.ptr = ctypes.c_void_p()
         self.nbytes = nbytes
+        self.contig = DevBuf.CONTIG
+        if self.contig:
+            C = _ceiling_lib()
+            if C is None or C.ceiling_malloc(ctypes.byref(self.ptr), ctypes.c_size_t(nbytes), 0x4) != 0:
+                raise MemoryError("contiguous device allocation failed")
+            return
         L = emac.lib()
         if L.ext_mpi_amd_gpu_malloc(ctypes.byref(self.ptr), ctypes.c_size_t(nbytes)) != 0:
             raise MemoryError("ext_mpi_amd_gpu_malloc failed")
@@ -134,7 +143,10 @@ class DevBuf:
     def free(self):
         import ext_mpi_collectives_amd as emac
         if self.ptr.value:
-            emac.lib().ext_mpi_amd_gpu_free(self.ptr)
+            if self.contig:
+                _ceiling_lib().ceiling_free(self.ptr)
+            else:
+                emac.lib().ext_mpi_amd_gpu_free(self.ptr)
             self.ptr = ctypes.c_void_p()
 
 
@@ -344,6 +356,8 @@ def _ceiling_lib():
     L.ceiling_gate_arm.restype = ctypes.c_void_p
     L.ceiling_gate_open.argtypes = [ctypes.c_void_p]
     L.ceiling_gate_free.argtypes = [ctypes.c_void_p]
+    L.ceiling_malloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+    L.ceiling_free.argtypes = [ctypes.c_void_p]
     return L
 
 
@@ -1406,14 +1420,18 @@ def shape_only(args):
     import torch
     import ext_mpi_collectives_amd as emac
     emac.lib()
+    DevBuf.CONTIG = args.alloc == "contig"
     MB = {"node16": 16, "node64": 64, "node512": 512, "int4": 4, "long4": 4}.get(args.shape, 256) * MIB
     if args.shape == "local256":
         r = comm_shape_fold(8, MB // 8 // 4, torch.float32, emac.FLOAT, 40)
     elif args.shape == "copy256":  # the node256 launch's bytes as a 1:1 copy (tools/ceiling.hip), same lease
         L = _ceiling_lib()
         n = 8 * MB  # 2 GiB read + 2 GiB written per launch, 3 buffer pairs rotated
-        a = torch.empty(3 * 2 * n // 4, dtype=torch.float32, device="cuda")
-        a.uniform_(-1, 1)
+        if DevBuf.CONTIG:
+            a = DevBuf(3 * 2 * n)  # contents do not matter to a copy
+        else:
+            a = torch.empty(3 * 2 * n // 4, dtype=torch.float32, device="cuda")
+            a.uniform_(-1, 1)
         stream = torch.cuda.current_stream()
         best = {}
         for variant in (0, 1, 2):  # nontemporal, default policy, phased (tools/ceiling.hip)

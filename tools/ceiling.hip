@@ -154,6 +154,13 @@ int ceiling_copy(const void *src, void *dst, long bytes, int iters, int variant,
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+/* Device memory with hipExtMallocWithFlags flags (bench.py --alloc contig: hipDeviceMallocContiguous,
+   physically contiguous, A/B of the translation cost against plain hipMalloc) */
+int ceiling_malloc(void **p, size_t bytes, unsigned flags) {
+  return hipExtMallocWithFlags(p, bytes, flags) == hipSuccess ? 0 : -1;
+}
+int ceiling_free(void *p) { return hipFree(p) == hipSuccess ? 0 : -5; }
+
 /* A stream gate for bench.py's timed regions: the stream waits (hipStreamWaitValue32 on a pinned
    host word) until the host opens the gate, so the work enqueued behind it -- the timed region's
    start event and its first launches -- begins only once the host is ahead of the GPU; the timing

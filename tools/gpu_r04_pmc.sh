@@ -18,10 +18,16 @@ for sz in 16 64 256 512; do
 done
 timeout -k 10 300 python3 bench.py --shape copy256 > $O/time_copy256.json 2> $O/time_copy256.err || exit $?
 cat $O/time_copy256.json
+# address translation A/B: the same launches on physically contiguous memory (hipDeviceMallocContiguous)
+timeout -k 10 300 python3 bench.py --shape node256 --alloc contig --schedules $TWO > $O/time_node256_contig.json 2> $O/time_node256_contig.err
+echo "time node256 contig rc=$? $(cat $O/time_node256_contig.json)"
+timeout -k 10 300 python3 bench.py --shape copy256 --alloc contig > $O/time_copy256_contig.json 2> $O/time_copy256_contig.err
+echo "time copy256 contig rc=$? $(cat $O/time_copy256_contig.json)"
 pass() {  # shape group counters...
   local shape=$1 group=$2; shift 2
   local extra=""
   [ "${shape#node}" != "$shape" ] && extra="--schedules $TWO"
+  [ "$group" = tlbcontig ] && extra="$extra --alloc contig"
   rm -rf $O/${shape}_$group
   timeout -s KILL 240 rocprofv3 --pmc "$@" -d $R/$O/${shape}_$group -o run --output-format csv -- \
     python3 $R/bench.py --shape $shape $extra > $O/${shape}_$group.json 2> $O/${shape}_$group.err
@@ -38,6 +44,7 @@ for shape in node16 node64 node256 node512 copy256; do
   pass $shape tlb TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum TCP_UTCL1_LFIFO_FULL_sum GRBM_GUI_ACTIVE
   pass $shape utcl2 GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE
 done
+pass node256 tlbcontig TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum TCP_UTCL1_LFIFO_FULL_sum GRBM_GUI_ACTIVE
 python3 tools/pmc_counters.py --by-kernel $O/node16_* $O/node64_* $O/node256_* $O/node512_* > $O/pmc_fold.json
 python3 tools/pmc_counters.py --by-kernel --kernel='copy_k4|copy_phased' $O/copy256_* > $O/pmc_copy.json
 find $O -name "*counter_collection*.csv" -size +2M -delete  # keep what merges back small
