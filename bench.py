@@ -62,7 +62,8 @@ def parse():
                     help="profiling: run only this fold shape (40 launches) and exit (PMC passes, tools/gpu_pmc_r02.sh)")
     ap.add_argument("--schedules", default=None,
                     help="--shape node*: comma-separated fold schedule words (U | issue << 4) to run in turn")
-    ap.add_argument("--child-transport", default=None, choices=["ipc", "rccl", "node"], help=argparse.SUPPRESS)
+    ap.add_argument("--child-transport", default=None, choices=["ipc", "rccl", "node-ipc", "node-rccl"],
+                    help=argparse.SUPPRESS)
     ap.add_argument("--child-full", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--child-result", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--child-deadline", type=float, default=600.0, help=argparse.SUPPRESS)
@@ -944,20 +945,21 @@ def _node_form_run(emac, comm, R, count, tdtype, code, copyin, steps, warmup, ra
                 b.free()
 
 
-def node_child(args, emac, rank, world, dev, dist, torch):
-    """--child-transport node: the N > 1 headline (see _node_form_run), the nodes joined by one
-    inter-node step of radix N (EXT_MPI_NUM_PORTS '-(N-1) (N-1)': every GPU trades with all N - 1
-    others at once, one xGMI link each), first over a peer-mapped communicator (engine.c
-    node_ipc_init: the nodes' partials read in place over xGMI), then over RCCL (the node legs as
-    point-to-point groups). Every rank agrees on each transport's outcome before the next; the
-    headline is the peer-mapped one when it ran and checked, the other is reported beside it."""
+def node_child(args, emac, rank, world, dev, dist, torch, transport):
+    """--child-transport node-ipc / node-rccl: the N > 1 headline (see _node_form_run), the nodes
+    joined by one inter-node step of radix N (EXT_MPI_NUM_PORTS '-(N-1) (N-1)': every GPU trades
+    with all N - 1 others at once, one xGMI link each) over a peer-mapped communicator (engine_join.c
+    node_ipc_init: the nodes' partials read in place over xGMI) or over RCCL (the node legs as
+    point-to-point groups). Each transport runs in a child of its own (multi_gpu), so one that hangs
+    or faults cannot take the other down; every rank agrees on the outcome. Returns the result (with
+    "checked") or {"error": ...}."""
     tdtype, code, dname, tsize = dtype_info(args.dtype)
     R = args.ranks
     count = int(args.size_mib * MIB) // tsize
     copyin = f"6;1 -{R} {R}"  # the node's own split (configs[1]); --copyin is the one-rank-per-GPU runs'
     ports = [-(world - 1), world - 1] if world > 1 else []
     out = {}
-    for transport in ("ipc", "rccl"):
+    for transport in (transport,):
         comm, res = None, None
         try:
             if transport == "ipc":
@@ -985,7 +987,10 @@ def node_child(args, emac, rank, world, dev, dist, torch):
         ok = torch.tensor([int("wall" in res)])
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         out[transport] = res if ok.item() else (res if "error" in res else {"error": "failed on another rank"})
-    return out
+    res = out[transport]
+    if "wall" not in res:
+        res["checked"] = False
+    return res
 
 
 def transport_child(args):
@@ -1009,16 +1014,8 @@ def transport_child(args):
     transport, full = args.child_transport, args.child_full
     res = {}
     log(f"rank {rank}: {transport} child on GPU {dev}: communicator set-up")
-    if transport == "node":
-        res = node_child(args, emac, rank, world, dev, dist, torch)
-        head = next((res[t] for t in ("ipc", "rccl") if "wall" in res[t] and res[t].get("checked")), None)
-        res = dict(head or {"error": "; ".join(f"{t}: {r.get('error', 'unchecked')}" for t, r in res.items())},
-                   transports={t: ({"ms_per_step": round(r["wall"] * 1e3 / args.steps, 4), "checked": r["checked"],
-                                    "parts_us": {k: round(r[k] * 1e6, 2) for k in ("copy_in_fold_s", "node_legs_s",
-                                                                                  "copy_out_s")}}
-                                   if "wall" in r else r) for t, r in res.items()})
-        if head is None:
-            res["checked"] = False
+    if transport.startswith("node-"):  # the N > 1 headline over one transport (node_child)
+        res = node_child(args, emac, rank, world, dev, dist, torch, transport[5:])
         with open(args.child_result, "w") as f:
             json.dump(res, f)
         dist.barrier()
@@ -1231,12 +1228,17 @@ def multi_gpu(args):
 
     failures = []
     # the headline: configs[1]'s node (8 ranks x 16 MiB resident in one GPU) on every GPU, the GPUs
-    # joined as nodes -- the N = 1 workload scaled weakly
-    rn, fail = run_child(9, "node", False, 0.4)
-    if fail:
-        failures.append(dict(fail, rank=rank))
-    if not everyone(fail is None):
-        rn = fail or {"error": "failed on another rank"}
+    # joined as nodes -- the N = 1 workload scaled weakly -- peer-mapped first, then over RCCL,
+    # each in its own children
+    node = {}
+    for i, (t, share) in enumerate((("ipc", 0.3), ("rccl", 0.35))):
+        r, fail = run_child(9 + i, f"node-{t}", False, share)
+        if fail:
+            failures.append(dict(fail, rank=rank))
+        if not everyone(fail is None):
+            r = fail or {"error": "failed on another rank"}
+        node[t] = r
+    rn = node_result(node, args.steps)
     # BASELINE configs[3] / [4] (one rank per GPU): the requested transport first; if it fails on
     # any rank (every rank agrees before moving on), the other one
     order = [args.transport, "rccl" if args.transport == "ipc" else "ipc"]
@@ -1256,6 +1258,19 @@ def multi_gpu(args):
                             [f for fs in allf for f in fs]))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def node_result(node, steps):
+    """The headline's node-form result from the per-transport ones: the peer-mapped one when it ran
+    and checked, else RCCL's, else an error naming both; `transports` keeps each one's summary."""
+    head = next((node[t] for t in ("ipc", "rccl") if t in node and "wall" in node[t] and node[t].get("checked")), None)
+    res = dict(head or {"error": "; ".join(f"{t}: {r.get('error', 'unchecked')}" for t, r in node.items()),
+                        "checked": False})
+    res["transports"] = {t: ({"ms_per_step": round(r["wall"] * 1e3 / steps, 4), "checked": r["checked"],
+                              "parts_us": {k: round(r[k] * 1e6, 2) for k in ("copy_in_fold_s", "node_legs_s",
+                                                                            "copy_out_s")}}
+                             if "wall" in r else r) for t, r in node.items()}
+    return res
 
 
 def multi_gpu_line(args, world, dname, S, copyin, rn, results, order, gpus_visible, failures):

@@ -219,21 +219,28 @@ def main():
             p = ctypes.c_void_p()
             assert L.ext_mpi_amd_gpu_malloc(ctypes.byref(p), 4 * n) == 0
             bufs.append(p)
-        fill = np.full(n, float((rank + 1) * (it + 1)), np.float32)
+        # the same contents in every re-allocation (a stale mapping of the previous
+        # allocation would pass the set-up's read-only sample), then new data before a second
+        # Start: a peer still reading the old memory would fold the old values
+        fill = np.full(n, float(rank + 1), np.float32)
         assert L.ext_mpi_amd_gpu_memcpy_hd(bufs[0], fill.ctypes.data, 4 * n) == 0
         h = emac.allreduce_init(bufs[0].value, bufs[1].value, n, emac.FLOAT, comm)
-        emac.start(h)
-        emac.wait(h)
         got = np.empty(n, np.float32)
-        assert L.ext_mpi_amd_gpu_memcpy_dh(got.ctypes.data, bufs[1], 4 * n) == 0
-        ok &= bool(np.all(got == (it + 1) * world * (world + 1) / 2))
+        for second in (False, True):
+            if second:
+                fill = np.full(n, float((rank + 1) * (it + 2)), np.float32)
+                assert L.ext_mpi_amd_gpu_memcpy_hd(bufs[0], fill.ctypes.data, 4 * n) == 0
+            emac.start(h)
+            emac.wait(h)
+            assert L.ext_mpi_amd_gpu_memcpy_dh(got.ctypes.data, bufs[1], 4 * n) == 0
+            ok &= bool(np.all(got == (it + 2 if second else 1) * world * (world + 1) / 2))
         if os.environ.get("EXT_MPI_AMD_DEBUG_IPC"):
             q = [got[j * n // world: (j + 1) * n // world] for j in range(world)]
             print(f"rank {rank} re-allocation {it}: {ok}; per chunk first/last/n_bad: "
                   f"{[(float(c[0]), float(c[-1]), int(np.sum(c != (it + 1) * world * (world + 1) / 2))) for c in q]}",
                   file=sys.stderr, flush=True)
         if rank == 0:
-            time.sleep(0.3)  # the others free, re-allocate and export first
+            time.sleep(0.3)  # the others reach Done first: it is collective, none frees before rank 0 closes
         emac.done(h)
         for p in bufs:
             L.ext_mpi_amd_gpu_free(p)

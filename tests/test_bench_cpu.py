@@ -42,7 +42,7 @@ def test_bench_multi_rank_transport_isolation_without_gpu():
     assert "error" in ex["ipc_transport"] and "error" in ex["rccl_transport"]
     # every failure is named with its transport, exit code and the child's last stderr lines
     fails = ex["failures"]
-    assert {f["transport"] for f in fails} == {"node", "ipc", "rccl"}
+    assert {f["transport"] for f in fails} == {"node-ipc", "node-rccl", "ipc", "rccl"}
     assert all(f["rc"] != 0 and isinstance(f["stderr_tail"], list) and f["stderr_tail"] for f in fails), fails
 
 
@@ -103,35 +103,46 @@ def test_multi_gpu_line_from_fabricated_children(world):
     assert any(p["dtype"] == "double" and p["bytes_per_rank"] == 256 << 20 for p in one["extras"]["sweep"])  # configs[3]
     assert "failures" not in ok_line["extras"]
 
-    # the node child failed on one rank: the one-rank-per-GPU line, the node failure named
-    rc_fail, fail = b.child_outcome("node", 1, 12.5, ["Traceback ...", "RuntimeError: boom"], None)
+    # the peer-mapped node children failed, RCCL's ran: its line, the failure beside it
+    rc_fail, fail = b.child_outcome("node-ipc", 1, 12.5, ["Traceback ...", "RuntimeError: boom"], None)
     assert rc_fail == {} and fail["rc"] == 1 and fail["stderr_tail"][-1] == "RuntimeError: boom"
-    line = b.multi_gpu_line(_Args, world, "f32", S, f"6;1 -{world} {world}", fail,
+    rn = b.node_result({"ipc": fail, "rccl": dict(_node_ok(world), transport="rccl")}, _Args.steps)
+    assert rn["transport"] == "rccl" and rn["transports"]["ipc"]["rc"] == 1
+    line = b.multi_gpu_line(_Args, world, "f32", S, f"6;1 -{world} {world}", rn,
+                            {"ipc": _one_rank_ok(world), "rccl": {"wall": 1e-3, "checked": True}}, order, world,
+                            [dict(fail, rank=1)])
+    assert line["config"]["layout"] == "node-per-gpu" and line["config"]["transport"] == "rccl"
+    assert line["extras"]["failures"][0]["transport"] == "node-ipc"
+    # both node children failed on one rank: the one-rank-per-GPU line, the node failures named
+    rn = b.node_result({"ipc": fail, "rccl": {"error": "failed on another rank"}}, _Args.steps)
+    assert rn["checked"] is False and "ipc: node-ipc child exited with 1" in rn["error"]
+    line = b.multi_gpu_line(_Args, world, "f32", S, f"6;1 -{world} {world}", rn,
                             {"ipc": _one_rank_ok(world), "rccl": {"wall": 1e-3, "checked": True}}, order, world,
                             [dict(fail, rank=1)])
     json.dumps(line)
     assert all(k in line for k in REQUIRED) and line["config"]["layout"] == "rank-per-gpu" and line["value"] > 0
-    assert line["extras"]["node_form_per_gpu"]["transport"] == "node"
+    assert line["extras"]["node_form_per_gpu"]["transports"]["ipc"]["transport"] == "node-ipc"
     assert line["extras"]["failures"][0]["stderr_tail"][-1] == "RuntimeError: boom"
 
     # the node child timed out, ipc failed its check, rccl ran: rccl's line
-    _, tmo = b.child_outcome("node", "timeout", 480.0, ["rank 0: node form ..."], None)
+    _, tmo = b.child_outcome("node-ipc", "timeout", 480.0, ["rank 0: node form ..."], None)
     _, bad = b.child_outcome("ipc", 0, 30.0, [], {"wall": 1.0, "checked": False})
     assert tmo["rc"] == "timeout" and "timed out" in tmo["error"] and bad["error"] == "result check failed"
-    line = b.multi_gpu_line(_Args, world, "f32", S, f"6;1 -{world} {world}", tmo, {"ipc": bad, "rccl": _one_rank_ok(world)},
-                            order, world, [tmo, bad])
+    line = b.multi_gpu_line(_Args, world, "f32", S, f"6;1 -{world} {world}", b.node_result({"ipc": tmo}, 20),
+                            {"ipc": bad, "rccl": _one_rank_ok(world)}, order, world, [tmo, bad])
     assert line["config"]["transport"] == "rccl" and line["extras"]["ipc_transport"]["error"] == "result check failed"
-    assert line["extras"]["node_form_per_gpu"]["rc"] == "timeout"
+    assert line["extras"]["node_form_per_gpu"]["transports"]["ipc"]["rc"] == "timeout"
 
     # everything timed out: a zero line naming every failure
-    fails = [b.child_outcome(t, "timeout", 100.0, ["..."], None)[1] for t in ("node", "ipc", "rccl")]
-    line = b.multi_gpu_line(_Args, world, "f32", S, f"6;1 -{world} {world}", fails[0],
-                            {"ipc": fails[1], "rccl": fails[2]}, order, world, fails)
+    fails = [b.child_outcome(t, "timeout", 100.0, ["..."], None)[1] for t in ("node-ipc", "node-rccl", "ipc", "rccl")]
+    line = b.multi_gpu_line(_Args, world, "f32", S, f"6;1 -{world} {world}",
+                            b.node_result({"ipc": fails[0], "rccl": fails[1]}, 20),
+                            {"ipc": fails[2], "rccl": fails[3]}, order, world, fails)
     json.dumps(line)
     assert all(k in line for k in REQUIRED)
     assert line["value"] == 0.0 and line["error"] == "no transport completed"
     assert "ipc: ipc child timed out" in line["config"]["workload"]
-    assert [f["transport"] for f in line["extras"]["failures"]] == ["node", "ipc", "rccl"]
+    assert [f["transport"] for f in line["extras"]["failures"]] == ["node-ipc", "node-rccl", "ipc", "rccl"]
 
 
 def test_child_process_limit_kills_and_reports():
