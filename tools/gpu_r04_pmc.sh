@@ -47,6 +47,7 @@ done
 pass node256 tlbcontig TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum TCP_UTCL1_LFIFO_FULL_sum GRBM_GUI_ACTIVE
 python3 tools/pmc_counters.py --by-kernel $O/node16_* $O/node64_* $O/node256_* $O/node512_* > $O/pmc_fold.json
 python3 tools/pmc_counters.py --by-kernel --kernel='copy_k4|copy_phased' $O/copy256_* > $O/pmc_copy.json
+python3 tools/pmc_r04_summary.py $O > $O/summary.json
 find $O -name "*counter_collection*.csv" -size +2M -delete  # keep what merges back small
 ls -la $O | head -60
 exit 0
