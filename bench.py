@@ -1461,25 +1461,25 @@ def shape_only(args):
             torch.cuda.synchronize()
             best[("nt", "plain", "phased")[variant]] = round(e0.elapsed_time(e1) * 1e3 / 20, 2)
         r = {"avg_launch_us": best, "bytes_per_launch": 2 * n}
-    elif args.shape in ("int4", "long4"):  # BASELINE configs[2]'s launch (4 MiB per rank x 8)
-        td, cd = (torch.int32, emac.INT) if args.shape == "int4" else (torch.int64, emac.LONG)
-        ts = 4 if args.shape == "int4" else 8
-        r = node_run(8, MB // ts, td, cd, "6;1 -8 8", 50, 5, alloc="hip")
-        r = {"avg_launch_us": round(r["event_ms"] * 1e3 / 50, 2), "checked": r["checked"], "schedule": r["schedule"]}
-    elif args.schedules:  # every listed fold schedule in turn (EXT_MPI_AMD_FOLD_SCHEDULE), one handle set each
-        r, pool = {}, {}
-        for w in args.schedules.split(","):
-            os.environ["EXT_MPI_AMD_FOLD_SCHEDULE"] = w
-            x = node_run(8, MB // 4, torch.float32, emac.FLOAT, "6;1 -8 8", 40, 4, alloc="hip", pool=pool)
-            r[w] = {"avg_launch_us": round(x["event_ms"] * 1e3 / 40, 2), "checked": x["checked"],
-                    "schedule": x["schedule"]}
-            log(f"{args.shape} schedule {w}: {r[w]}")
-        del os.environ["EXT_MPI_AMD_FOLD_SCHEDULE"]
-        free_pool(pool)
-        r = {"by_schedule": r}
-    else:
-        r = node_run(8, MB // 4, torch.float32, emac.FLOAT, "6;1 -8 8", 40, 4, alloc="hip")
-        r = {"avg_launch_us": round(r["event_ms"] * 1e3 / 40, 2), "checked": r["checked"], "schedule": r["schedule"]}
+    else:  # the node form: float at 16 - 512 MiB per rank, or BASELINE configs[2]'s int / long launch
+        if args.shape in ("int4", "long4"):  # (4 MiB per rank x 8)
+            td, cd, ts, steps = (torch.int32, emac.INT, 4, 50) if args.shape == "int4" else (torch.int64, emac.LONG, 8, 50)
+        else:
+            td, cd, ts, steps = torch.float32, emac.FLOAT, 4, 40
+        if args.schedules:  # every listed fold schedule in turn (EXT_MPI_AMD_FOLD_SCHEDULE), one handle set each
+            r, pool = {}, {}
+            for w in args.schedules.split(","):
+                os.environ["EXT_MPI_AMD_FOLD_SCHEDULE"] = w
+                x = node_run(8, MB // ts, td, cd, "6;1 -8 8", steps, 4, alloc="hip", pool=pool)
+                r[w] = {"avg_launch_us": round(x["event_ms"] * 1e3 / steps, 2), "checked": x["checked"],
+                        "schedule": x["schedule"]}
+                log(f"{args.shape} schedule {w}: {r[w]}")
+            del os.environ["EXT_MPI_AMD_FOLD_SCHEDULE"]
+            free_pool(pool)
+            r = {"by_schedule": r}
+        else:
+            x = node_run(8, MB // ts, td, cd, "6;1 -8 8", steps, 5, alloc="hip")
+            r = {"avg_launch_us": round(x["event_ms"] * 1e3 / steps, 2), "checked": x["checked"], "schedule": x["schedule"]}
     emit({"shape": args.shape, **r})
 
 

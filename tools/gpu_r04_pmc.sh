@@ -16,6 +16,9 @@ for sz in 16 64 256 512; do
   rc=$?; echo "time node$sz rc=$rc"; [ $rc -ne 0 ] && { tail -5 $O/time_node$sz.err; exit $rc; }
   cat $O/time_node$sz.json
 done
+# configs[2]'s int launch: U4 burst, U4 staggered, U2 burst, U2 / U1 half grid (two tiles per workgroup), U1 burst
+timeout -k 10 300 python3 bench.py --shape int4 --schedules 20,84,18,262162,262161,17 > $O/time_int4.json 2> $O/time_int4.err
+echo "time int4 rc=$? $(cat $O/time_int4.json)"
 timeout -k 10 300 python3 bench.py --shape copy256 > $O/time_copy256.json 2> $O/time_copy256.err || exit $?
 cat $O/time_copy256.json
 # address translation A/B: the same launches on physically contiguous memory (hipDeviceMallocContiguous)
