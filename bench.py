@@ -1175,8 +1175,8 @@ def child_outcome(transport, rc, elapsed, tail, result):
     if rc == 0 and result is not None:
         if result.get("checked"):
             return result, None
-        return result, {"transport": transport, "rc": 0, "error": "result check failed", "elapsed_s": elapsed,
-                        "stderr_tail": tail}
+        return result, {"transport": transport, "rc": 0, "error": result.get("error") or "result check failed",
+                        "elapsed_s": elapsed, "stderr_tail": tail}
     what = "timed out" if rc == "timeout" else f"exited with {rc}" if rc != 0 else "wrote no result"
     return {}, {"transport": transport, "rc": rc, "error": f"{transport} child {what}", "elapsed_s": elapsed,
                 "stderr_tail": tail}

@@ -13,7 +13,7 @@ gcc -O2 tools/mpi_blocking_time.c -o $O/mpi_blocking_time -Iinclude -I$M/include
 for np in 2 4; do
   for n in 256 262144 4194304; do
     for sync in 1 0; do
-      EXT_MPI_BLOCKING=1 EXT_MPI_AMD_SYNC_STAGE=$sync timeout -k 10 120 $M/bin/mpiexec -n $np $O/mpi_blocking_time $n 100 > $O/np${np}_n${n}_sync$sync.txt 2>&1
+      EXT_MPI_BLOCKING=1 EXT_MPI_AMD_ASYNC_STAGE=$((1-sync)) timeout -k 10 120 $M/bin/mpiexec -n $np $O/mpi_blocking_time $n 100 > $O/np${np}_n${n}_sync$sync.txt 2>&1
       rc=$?; echo "np=$np count=$n sync=$sync rc=$rc $(grep TIME $O/np${np}_n${n}_sync$sync.txt)"
       [ $rc -ne 0 ] && { tail -5 $O/np${np}_n${n}_sync$sync.txt; exit $rc; }
     done
