@@ -99,10 +99,10 @@ static int tune_candidates(const emac_handle *h, long vec, int *sched) {
      0.71-0.86 for the per-tile schedules) and is offered again for the linear fold (round 3 had
      replaced it by the leaf-major groups there). A launch of fewer than 256 groups of (U 2, 4
      tiles) -- under 8 MiB per leaf -- leaves CUs idle under the deferred schedules; there (U 1,
-     burst), twice the per-tile loop's workgroups, is offered too, and for the fan-out (U 2, half
-     grid): two tiles per workgroup one after the other, so that a launch of one wave of
-     workgroups overlaps one tile's stores with the next one's loads (fold_kernel.hpp kHalfGrid).
-     (U 2, 8 tiles), compiled, is no longer offered: never kept. */
+     burst), twice the per-tile loop's workgroups, is offered too. (U 2, 8 tiles), compiled, is no
+     longer offered: never kept. Two tiles per workgroup at U 2 or U 1 ("half grid", round 4) were
+     measured 13.7 us on configs[2]'s launch against 11.3 for U 4 (profiles/r04/pmc256/time_int4.json)
+     and are not built. */
   const int small = vec < 256L * 4 * 2 * EMAC_BLOCK;
   const char *f = getenv("EXT_MPI_AMD_FOLD_SCHEDULE"); /* A/B runs: one schedule word, U | issue << 4 */
   if (f && atoi(f) > 0) {
@@ -116,7 +116,6 @@ static int tune_candidates(const emac_handle *h, long vec, int *sched) {
   sched[n++] = 4 | 1 << 4;
   if (h->fan) sched[n++] = 4 | 5 << 4;
   if (small) sched[n++] = 1 | 1 << 4;
-  if (small && h->fan) sched[n++] = 2 | (1 | 1 << 14) << 4; /* half grid: two U 2 tiles per workgroup */
   if (h->tiles_per_bucket > 0) {
     sched[n++] = 2 | (1 | 2 << 11) << 4;
     if (!h->fan) {

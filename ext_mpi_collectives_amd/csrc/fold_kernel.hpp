@@ -294,12 +294,6 @@ constexpr int defer(int kb) { return (kb == 2 ? 1 : kb == 4 ? 2 : kb == 8 ? 3 : 
 // than the LDS groups per Start in the bench's steady state at 16 MiB per rank
 // (profiles/r03_tune/force_ab.txt).
 constexpr int kLeafMajor = 1 << 13;
-// ISSUE bit 14 (per-tile loop, node fan-out): half the grid -- every workgroup folds two tiles
-// one after the other, so a launch that is one wave of workgroups (configs[2]: 4 MiB per rank,
-// 256 tiles of U 4) becomes two tiles per workgroup at U 2 or U 1: the stores of a workgroup's
-// first tile drain while the loads of its second are in flight, instead of the whole chip reading
-// and then the whole chip writing. Offered to the tuner below 8 MiB per leaf.
-constexpr int kHalfGrid = 1 << 14;
 
 // One group of fold_deferred_kernel: nt (<= KB) consecutive tiles of bucket b from vector gbase. ALL_FULL
 // (host-known: every tile of every bucket whole and every group KB tiles) skips the bucket's vector
@@ -732,8 +726,7 @@ int launch_one(const Launch &L) {
       hipLaunchKernelGGL((fold_deferred_kernel<T, OP, N, U, CH, D, ISSUE, false>), dim3(grid), dim3(EMAC_BLOCK), 0, L.s, L.b,
                          L.tpb, groups, *L.c);
   } else {
-    const long want = (ISSUE & kHalfGrid) ? (L.ntiles + 1) / 2 : L.ntiles;
-    const long grid = want < 8192 ? want : 8192;
+    const long grid = L.ntiles < 8192 ? L.ntiles : 8192;
     if (grid > 0)
       hipLaunchKernelGGL((fold_kernel<T, OP, N, U, CH, D, ISSUE>), dim3((unsigned)grid), dim3(EMAC_BLOCK), 0, L.s, L.b,
                          L.nb, L.ntiles, L.tpb, L.all_full, *L.c, L.go, L.nrt);
@@ -771,8 +764,6 @@ int launch_sum(int unroll, const Launch &L) {
     if constexpr (CH == 0) {
       if (unroll == sched(2, 1 | defer(4) | kLeafMajor)) return launch_one<T, OP, N, 2, CH, D, 1 | defer(4) | kLeafMajor>(L);
     }
-    if (unroll == sched(2, 1 | kHalfGrid)) return launch_one<T, OP, N, 2, CH, D, 1 | kHalfGrid>(L);
-    if (unroll == sched(1, 1 | kHalfGrid)) return launch_one<T, OP, N, 1, CH, D, 1 | kHalfGrid>(L);
     return EMAC_ERR_UNSUPPORTED;
   } else {
     if (unroll == sched(4, 1)) return launch_one<T, OP, N, 4, CH, D>(L);

@@ -406,7 +406,6 @@ def test_copy_reduce_headline_instance():
 
 DEFER_SHIFT = 11  # fold_kernel.hpp kDeferShift: deferred-store schedules (issue bits 11-12)
 LEAF_MAJOR = 1 << 13  # fold_kernel.hpp kLeafMajor: leaf-major deferred groups (the linear fold)
-HALF_GRID = 1 << 14  # fold_kernel.hpp kHalfGrid: two tiles per workgroup (node fan-out below 8 MiB per leaf)
 
 
 @pytest.mark.parametrize("copyin", ["6;1 -8 8", "6;1 -2 -2 -2 2 2 2"])
@@ -446,7 +445,6 @@ def test_every_tuned_schedule_bitwise(oracle, code, copyin):
         assert any(t == 1 for _, _, t in seen), seen
         small = chunk * R * sends[0].itemsize < 8 << 20
         assert ((1, 1) in cands) == small, (chunk, cands)
-        assert ((2, 1 | HALF_GRID) in cands) == small, (chunk, cands)  # two tiles per workgroup
         leaf = (2, 1 | 2 << DEFER_SHIFT | LEAF_MAJOR)  # leaf-major groups: the linear fold only
         assert (leaf in cands) == (copyin == "6;1 -8 8") and (4, 1 | 1 << DEFER_SHIFT) in cands, cands
     # the local fold: one destination, one bucket
