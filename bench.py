@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--transport", default="ipc", choices=["ipc", "rccl"],
                     help="N > 1: peer-mapped hipIpc form (default) or RCCL point-to-point legs")
     ap.add_argument("--shape", default=None, choices=["local256", "node16", "node64", "node256", "node512", "copy256",
-                                                      "int4", "long4"],
+                                                      "int4", "long4", "small"],
                     help="profiling: run only this fold shape (40 launches) and exit (PMC passes, tools/gpu_pmc_r02.sh)")
     ap.add_argument("--schedules", default=None,
                     help="--shape node*: comma-separated fold schedule words (U | issue << 4) to run in turn")
@@ -1429,6 +1429,55 @@ def node_form_line(args, world, dname, rn, one_rank_per_gpu):
     }
 
 
+def _fit_line(xs, ys):
+    """least-squares y = a + b x: (a, b)"""
+    n = len(xs)
+    mx, my = sum(xs) / n, sum(ys) / n
+    b = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / sum((x - mx) ** 2 for x in xs)
+    return my - b * mx, b
+
+
+def small_sweep(emac, torch):
+    """BASELINE configs[2]'s launch size class: the int node form (8 ranks, MPI_SUM, tuned schedule)
+    at 0.5 - 16 MiB per rank against a 1:1 copy of the same bytes (tools/ceiling.hip, the best of
+    its three variants) on the same lease, both rotated past the 256 MiB Infinity Cache. A straight
+    line through launch time against bytes separates the fixed cost of a launch (its intercept:
+    dispatch, first-load latency, store drain) from the streaming rate (its slope)."""
+    L = _ceiling_lib()
+    stream = torch.cuda.current_stream()
+    pts = []
+    for mb in (0.5, 1, 2, 4, 8, 16):
+        per_rank = int(mb * MIB)
+        x = node_run(8, per_rank // 4, torch.int32, emac.INT, "6;1 -8 8", 50, 5, alloc="hip")
+        fold_us = x["event_ms"] * 1e3 / 50
+        n = 8 * per_rank  # the fold reads 8 x per_rank and writes 8 x per_rank: a copy of n bytes
+        pairs = max(3, math.ceil(640 * MIB / (2 * n)))
+        a = DevBuf(pairs * 2 * n)
+        best = None
+        for variant in (0, 1, 2):
+            for i in range(pairs):
+                L.ceiling_copy(a.data_ptr() + i * 2 * n, a.data_ptr() + i * 2 * n + n, n, 1, variant, stream.cuda_stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for i in range(50):
+                b = a.data_ptr() + (i % pairs) * 2 * n
+                assert L.ceiling_copy(b, b + n, n, 1, variant, stream.cuda_stream) == 0
+            e1.record(stream)
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / 50
+            best = us if best is None else min(best, us)
+        a.free()
+        pts.append({"mib_per_rank": mb, "bytes_per_launch": 2 * n, "fold_us": round(fold_us, 2),
+                    "copy_us": round(best, 2), "fold_frac_8tbs": round(2 * n / fold_us / 1e3 / HBM_PEAK_GBPS, 4),
+                    "fold_over_copy": round(best / fold_us, 3), "schedule": x["schedule"], "checked": x["checked"]})
+        log(f"small sweep {mb} MiB/rank: {pts[-1]}")
+    out = {"points": pts}
+    for k in ("fold", "copy"):
+        a0, b0 = _fit_line([p["bytes_per_launch"] for p in pts], [p[f"{k}_us"] for p in pts])
+        out[f"{k}_fit"] = {"fixed_us": round(a0, 2), "streaming_gbps": round(1e-3 / b0, 1)}
+    return out
+
+
 def shape_only(args):
     """One fold shape alone (for rocprofv3 PMC passes): the local fold (8 x 32 MiB -> 1) or the
     node-form Allreduce at 256 / 16 MiB per rank, 40 launches after warm-up."""
@@ -1439,6 +1488,8 @@ def shape_only(args):
     MB = {"node16": 16, "node64": 64, "node512": 512, "int4": 4, "long4": 4}.get(args.shape, 256) * MIB
     if args.shape == "local256":
         r = comm_shape_fold(8, MB // 8 // 4, torch.float32, emac.FLOAT, 40)
+    elif args.shape == "small":
+        r = small_sweep(emac, torch)
     elif args.shape == "copy256":  # the node256 launch's bytes as a 1:1 copy (tools/ceiling.hip), same lease
         L = _ceiling_lib()
         n = 8 * MB  # 2 GiB read + 2 GiB written per launch, 3 buffer pairs rotated
