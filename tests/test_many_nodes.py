@@ -120,3 +120,26 @@ def test_many_node_lists_refused(nodes, ports):
     with pytest.raises(emac.ExtMpiError) as e:
         emac.comm_program_nodes(nodes, 1, 0, 1000, emac.FLOAT, "6;1 -1 1", ports=ports)
     assert e.value.code in (emac.ERROR_UNSUPPORTED, emac.ERROR_ARG)
+
+
+@pytest.mark.parametrize("nodes", range(2, 65))
+def test_default_node_ports_matches_c(nodes):
+    """ext_mpi_collectives_amd.default_node_ports restates plan.c emac_node_sched_build's default
+    list: the program the C library builds with no list (NULL) equals the one it builds from the
+    Python list, rank by rank; where C refuses the default (a prime factor above 16 leaves per
+    step), Python raises."""
+    R, count = 1, 4 * nodes + 3
+    try:
+        ports = emac.default_node_ports(nodes)
+    except ValueError:
+        with pytest.raises(emac.ExtMpiError):
+            emac.comm_program_nodes(nodes, R, 0, count, emac.FLOAT)
+        return
+    prod = 1
+    for p in ports:
+        if p < 0:
+            prod *= 1 - p
+    assert prod == nodes
+    for r in sorted({0, nodes // 2, nodes - 1}):
+        assert emac.comm_program_nodes(nodes, R, r, count, emac.FLOAT) == \
+            emac.comm_program_nodes(nodes, R, r, count, emac.FLOAT, ports=ports)
