@@ -492,8 +492,13 @@ int arena_grow(emac_comm *cm, int rc, long need) {
         pl[n] = EMAC_SAMPLE_BYTES;
         who[n++] = r;
       }
-      /* a local failure still takes part in the verdict below (every peer is in that allgather) */
-      if (n && (rc = emac_gpu_sample(pk, pl, n, seen, NULL))) bad |= EMAC_ARENA_FAILED;
+      /* a local failure still takes part in the verdict below (every peer is in that allgather);
+         EXT_MPI_AMD_TEST_FAIL_ARENA_SAMPLE=1 fails the sample here (tests/ipc_worker.py "arenafault") */
+      if (n) {
+        const char *f = getenv("EXT_MPI_AMD_TEST_FAIL_ARENA_SAMPLE");
+        rc = f && atoi(f) > 0 ? EMAC_ERR_DEVICE : emac_gpu_sample(pk, pl, n, seen, NULL);
+        if (rc) bad |= EMAC_ARENA_FAILED;
+      }
       for (r = 0; !rc && r < n; r++)
         if (memcmp(seen + r * EMAC_SAMPLE_BYTES, all[who[r]].nonce, EMAC_SAMPLE_BYTES)) bad |= 1u << who[r];
     }

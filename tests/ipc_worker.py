@@ -88,6 +88,40 @@ def _report_mismatch(rank, world, k, got, want):
           f"want {want[bad[:6]].tolist()}; owner chunks {chunks[:8]}", file=sys.stderr, flush=True)
 
 
+def arena_fault(rank, world, dev):
+    """A rank that cannot validate its peers' new arena segments (engine_ipc.c
+    arena_grow) fails the set-up on EVERY rank -- none left waiting in an exchange the failed rank
+    skipped -- and the communicator stays usable: on a fresh communicator, whose first handle
+    grows every rank's arena, the last rank's validation sample is failed on purpose
+    (EXT_MPI_AMD_TEST_FAIL_ARENA_SAMPLE); every rank must see its allreduce_init refused, then the
+    same init again, with the fault cleared, must give the bit-exact sum."""
+    comm = emac.comm_init_ipc(rank, world, emac.torch_allgather(), dev)
+    n = 4099
+    x = torch.full((n,), float(rank + 1), device="cuda")
+    y = torch.full_like(x, -1.0)
+    if rank == world - 1:
+        os.environ["EXT_MPI_AMD_TEST_FAIL_ARENA_SAMPLE"] = "1"
+    try:
+        h = emac.allreduce_init(x.data_ptr(), y.data_ptr(), n, emac.FLOAT, comm)
+        emac.done(h)
+        refused = False
+    except emac.ExtMpiError as e:
+        refused = True
+        code = e.code
+    os.environ.pop("EXT_MPI_AMD_TEST_FAIL_ARENA_SAMPLE", None)
+    h = emac.allreduce_init(x.data_ptr(), y.data_ptr(), n, emac.FLOAT, comm)
+    emac.start(h)
+    emac.wait(h)
+    good = bool(torch.all(y == world * (world + 1) / 2).item())
+    emac.done(h)
+    emac.comm_free(comm)
+    if not (refused and good):
+        print(f"rank {rank}: arena fault: refused {refused}{f' ({code})' if refused else ''}, retry good {good}",
+              file=sys.stderr, flush=True)
+    print(f"IPC rank {rank}/{world} arena validation failure: {'ok' if refused and good else 'MISMATCH'}", flush=True)
+    return refused and good
+
+
 def timeout_recovery(rank, world):
     """A late rank costs one Start, not the communicator (ipc_sync.hpp): on a communicator with a
     0.3 s barrier timeout, rank 1 starts its second Allreduce 1 s late. Every rank must report
@@ -201,7 +235,7 @@ def main():
         failures += not ok
         print(f"IPC rank {rank}/{world} case {k} code {code} op {op} count {count} '{copyin}' in_place={in_place} "
               f"host={host} x{repeats}: {'ok' if ok else 'MISMATCH'}", flush=True)
-    sections = os.environ.get("IPC_SECTIONS", "realloc,newdata,concurrent,recycle,recovery").split(",")
+    sections = os.environ.get("IPC_SECTIONS", "realloc,newdata,concurrent,recycle,arenafault,recovery").split(",")
     if os.environ.get("IPC_CASES_ONLY"):
         emac.comm_free(comm)
         dist.barrier()
@@ -308,6 +342,8 @@ def main():
     failures += not ok
     print(f"IPC rank {rank}/{world} slot recycling ({1200 if world <= 4 else 200} handles): {'ok' if ok else 'MISMATCH'}",
           flush=True)
+    if "arenafault" in sections:
+        failures += not arena_fault(rank, world, dev)
     if "recovery" in sections:
         failures += not timeout_recovery(rank, world)
     emac.comm_free(comm)
