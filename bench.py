@@ -195,6 +195,22 @@ def free_pool(pool):
 
 TUNE_STARTS = 1 + 3 * 3 * 8 + 1  # a handle's first Start, 3 rounds of at most 8 candidates on three Starts each, and the keeping one
 
+# Rotated buffer sets: between two uses of one set, at least this many bytes of OTHER sets' inputs
+# are read (2.5x the 256 MiB Infinity Cache). Round 4 measured that a rotation sized by the whole
+# working set (>= 640 MiB, e.g. 3 sets of 8 x 16 MiB send + receive) still let the Infinity Cache
+# serve part of the reads: the time followed the send sets alone -- 3 send sets 45.3 us, 6 or 8
+# sets 49.7-50.3 us, whatever the receive rotation (tools/setsweep.hip, profiles/r04/rotation/).
+READ_REUSE_BYTES = 640 * MIB
+
+
+def rotation_sets(read_bytes_per_set, set_bytes=None):
+    """Buffer sets to rotate so every read comes from HBM: 1 + READ_REUSE_BYTES / the bytes one set's
+    launch reads. EXT_MPI_AMD_BENCH_ROTATION=legacy: rounds 1-3's rule (>= 640 MiB of whole sets,
+    `set_bytes`), for A/B runs only."""
+    if os.environ.get("EXT_MPI_AMD_BENCH_ROTATION") == "legacy" and set_bytes:
+        return max(2, math.ceil(640 * MIB / max(1, set_bytes)))
+    return 1 + math.ceil(READ_REUSE_BYTES / max(1, read_bytes_per_set))
+
 
 def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * MIB, host=False, alloc="torch",
              pool=None):
@@ -207,8 +223,8 @@ def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * 
     set_bytes = 2 * R * count * tsize
     if host or min_set_bytes <= 0:
         nsets = 1
-    else:
-        nsets = max(2, math.ceil(min_set_bytes / max(1, set_bytes)))
+    else:  # every read from HBM: R send buffers read per launch (READ_REUSE_BYTES)
+        nsets = rotation_sets(R * count * tsize, set_bytes)
     stream = torch.cuda.Stream()
     sets, handles = [], []
     key = (R, count, str(tdtype), nsets, host, alloc)
@@ -308,7 +324,7 @@ def comm_shape_fold(R, chunk, tdtype, code, steps):
     import ext_mpi_collectives_amd as emac
     tsize = torch.empty((), dtype=tdtype).element_size()
     nbytes = chunk * tsize
-    nsets = max(2, math.ceil(640 * MIB / ((R + 1) * nbytes)))
+    nsets = rotation_sets(R * nbytes, (R + 1) * nbytes)  # R leaves read per launch
     np_dtype = {torch.float32: np.float32, torch.float64: np.float64, torch.int32: np.int32,
                 torch.int64: np.int64}[tdtype]
     bufs, handles = [], []
@@ -387,7 +403,7 @@ def measured_ceilings(steps=10, launch_bytes=256 * MIB):
     and nontemporal global_load_dwordx4 into VGPRs with 4 or 8 vectors per lane in flight; write --
     a nontemporal store stream over 4 GiB and at the launch's written bytes; copy -- the best of a nontemporal and a default-policy 1:1 copy
     (K = 4 vectors per lane) and a nontemporal copy in phases (tools/ceiling.hip copy_phased), each timed over 4 GiB and over `launch_bytes` (read + written, the
-    headline launch's bytes, three buffer sets rotated past the 256 MiB Infinity Cache): the rate
+    headline launch's bytes, buffer sets rotated as the launches' are, rotation_sets): the rate
     of the node-form fold's 1:1 read/write mix."""
     import torch
     L = _ceiling_lib()
@@ -421,12 +437,13 @@ def measured_ceilings(steps=10, launch_bytes=256 * MIB):
     torch.cuda.synchronize()
     writes["write_4GiB"] = round(steps * n / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
     half = launch_bytes // 2
+    k = rotation_sets(half, launch_bytes)  # buffers rotated (as the launches' sets)
     e0.record(stream)
-    for i in range(3 * steps):
-        assert L.ceiling_write(a.data_ptr() + (i % 3) * launch_bytes, half, 1, stream.cuda_stream) == 0
+    for i in range(k * steps):
+        assert L.ceiling_write(a.data_ptr() + (i % k) * launch_bytes, half, 1, stream.cuda_stream) == 0
     e1.record(stream)
     torch.cuda.synchronize()
-    writes["write_launch"] = round(3 * steps * half / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+    writes["write_launch"] = round(k * steps * half / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
     out["write_ceiling_gbps"] = max(writes.values())
     out["write_variants_gbps"] = writes
     copies = {}
@@ -438,15 +455,16 @@ def measured_ceilings(steps=10, launch_bytes=256 * MIB):
         e1.record(stream)
         torch.cuda.synchronize()
         copies[f"copy_{vname}_4GiB"] = round(steps * 2 * half / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
-        half = launch_bytes // 2  # three sets of (src, dst) rotated: 3 x launch_bytes > 256 MiB
+        half = launch_bytes // 2  # k sets of (src, dst) rotated, every source read from HBM
+        k = rotation_sets(half, launch_bytes)
         L.ceiling_copy(a.data_ptr(), a.data_ptr() + half, half, 1, variant, stream.cuda_stream)
         e0.record(stream)
-        for i in range(3 * steps):
-            base = a.data_ptr() + (i % 3) * launch_bytes
+        for i in range(k * steps):
+            base = a.data_ptr() + (i % k) * launch_bytes
             assert L.ceiling_copy(base, base + half, half, 1, variant, stream.cuda_stream) == 0
         e1.record(stream)
         torch.cuda.synchronize()
-        copies[f"copy_{vname}_launch"] = round(3 * steps * 2 * half / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+        copies[f"copy_{vname}_launch"] = round(k * steps * 2 * half / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
     out["copy_gbps"] = max(copies.values())
     out["copy_variants_gbps"] = copies
     del a, sink
@@ -576,7 +594,8 @@ def single_gpu(args):
         "vs_baseline": None,
         "dtype": dname,
         "data": f"synthetic: uniform [-1,1) per rank (seeded), device-resident, {main['nsets']} rotated buffer sets "
-                f"({main['nsets'] * main['set_bytes'] // MIB} MiB > 256 MiB Infinity Cache)",
+                f"({main['nsets'] * main['set_bytes'] // MIB} MiB; {(main['nsets'] - 1) * main['set_bytes'] // 2 // MIB} "
+                f"MiB of other sets' inputs read between two uses of one set, 2.5x the 256 MiB Infinity Cache)",
         "config": {"workload": f"persistent Allreduce {args.dtype} MPI_SUM, {S // MIB} MiB per rank, {R} node ranks "
                                f"resident in one MI355X (BASELINE configs[1]), EXT_MPI_COPYIN '{copyin}', fused "
                                f"reduce_copyin + reduce_copyout fold",
@@ -869,7 +888,7 @@ def _node_form_run(emac, comm, R, count, tdtype, code, copyin, steps, warmup, ra
     np_dtype = {torch.float32: np.float32, torch.float64: np.float64, torch.int32: np.int32,
                 torch.int64: np.int64}[tdtype]
     set_bytes = 2 * R * count * tsize
-    nsets = max(2, math.ceil(640 * MIB / max(1, set_bytes)))  # rotated past the 256 MiB Infinity Cache
+    nsets = rotation_sets(R * count * tsize, set_bytes)  # every read from HBM (READ_REUSE_BYTES)
     stream = torch.cuda.Stream()
     sets, handles, mine = [], [], None
     for s in range(nsets):
@@ -1451,7 +1470,7 @@ def small_sweep(emac, torch):
         x = node_run(8, per_rank // 4, torch.int32, emac.INT, "6;1 -8 8", 50, 5, alloc="hip")
         fold_us = x["event_ms"] * 1e3 / 50
         n = 8 * per_rank  # the fold reads 8 x per_rank and writes 8 x per_rank: a copy of n bytes
-        pairs = max(3, math.ceil(640 * MIB / (2 * n)))
+        pairs = rotation_sets(n, 2 * n)
         a = DevBuf(pairs * 2 * n)
         best = None
         for variant in (0, 1, 2):

@@ -56,9 +56,13 @@ def main(db, sweep):
         if r["gap_med_us"] >= 0.5:  # host-bound runs: the duration is not the per-launch cost
             continue
         k = r["kernel"]
-        if k.startswith("emac::fold_kernel"):  # tiles of 256 lanes x U x 16 B; 8 leaves read, 8 written
-            u = int(k.split("<")[1].split(",")[3])
-            groups.setdefault("fold (tuned schedule)", {})[r["workgroups"] * 256 * u * 16 * 16] = r
+        if k.startswith("emac::fold_kernel") or k.startswith("emac::fold_deferred_kernel"):
+            # tiles of 256 lanes x U x 16 B (deferred groups: KB tiles each); 8 leaves read, 8 written
+            a = k.split("<")[1].split(",")
+            u, kb = int(a[3]), 1
+            if "deferred" in k:
+                kb = {0: 1, 1: 2, 2: 4, 3: 8}[(int(a[6]) >> 11) & 3]
+            groups.setdefault("fold (tuned schedule)", {})[r["workgroups"] * kb * 256 * u * 16 * 16] = r
         elif k.startswith("copy_phased"):  # a group per 2048 vectors of 16 B, read and written
             groups.setdefault(k, {})[r["workgroups"] * 2048 * 16 * 2] = r
         elif k.startswith("copy_k4"):  # a fixed grid: its back-to-back runs come in size order
