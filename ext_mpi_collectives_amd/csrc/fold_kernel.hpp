@@ -57,6 +57,15 @@ constexpr int kSysCoherent = 17;  // sc0 | sc1
 // HBM behind the next launch; nontemporal accesses win on the long streams (tools/pipebench.hip).
 constexpr int kPlainStore = 512;
 constexpr int kPlainLoad = 1024;
+// ISSUE bit 14: stores as 16-byte buffer stores at device scope, nontemporal (cache policy sc1 nt):
+// each store is written through the XCD's L2 instead of waiting there as a dirty line for the
+// launch's closing write-back. The best of eight store policies in tools/storepol.hip on two
+// leases (1-5 % over the default-scope nontemporal store at 16-256 MiB per rank); in the library's
+// own launch (U 4 burst, bench.py --schedules) 0.7-1 % faster at 64 and 256 MiB per rank, no gain
+// at 16 MiB and below (profiles/r04/storepol/). Offered to the tuner for large node fan-outs
+// (engine_tune.c).
+constexpr int kDevStore = 1 << 14;
+constexpr int kDevStreaming = 18;  // sc1 | nt
 typedef unsigned int U32x4 __attribute__((ext_vector_type(4)));
 
 template <typename V>
@@ -68,6 +77,11 @@ template <typename V>
 __device__ __forceinline__ void sys_store16(void *tile_base, unsigned byte_off, V v) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(tile_base, 0, 0x7FFFFFF0, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U32x4, v), r, byte_off, 0, kSysCoherent);
+}
+template <typename V>
+__device__ __forceinline__ void dev_store16(void *tile_base, unsigned byte_off, V v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(tile_base, 0, 0x7FFFFFF0, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U32x4, v), r, byte_off, 0, kDevStreaming);
 }
 
 // The element operation. SUM: a + b (integers in unsigned arithmetic). MIN / MAX as the
@@ -243,6 +257,8 @@ template <typename V, int ISSUE>
 __device__ __forceinline__ void store_vec(__attribute__((address_space(1))) V *dst, unsigned v, V r) {
   if constexpr ((ISSUE & kRemote) != 0)
     sys_store16<V>((void *)dst, v * 16u, r);
+  else if constexpr ((ISSUE & kDevStore) != 0)
+    dev_store16<V>((void *)dst, v * 16u, r);
   else if constexpr ((ISSUE & kPlainStore) != 0)
     dst[v] = r;
   else
@@ -763,6 +779,9 @@ int launch_sum(int unroll, const Launch &L) {
     if (unroll == sched(2, 1 | defer(8))) return launch_one<T, OP, N, 2, CH, D, 1 | defer(8)>(L);
     if constexpr (CH == 0) {
       if (unroll == sched(2, 1 | defer(4) | kLeafMajor)) return launch_one<T, OP, N, 2, CH, D, 1 | defer(4) | kLeafMajor>(L);
+    }
+    if constexpr (N == 4 || N == 8) {  // device-scope streaming stores: the node fan-outs of 4 and 8 ranks
+      if (unroll == sched(4, 1 | kDevStore)) return launch_one<T, OP, N, 4, CH, D, 1 | kDevStore>(L);
     }
     return EMAC_ERR_UNSUPPORTED;
   } else {
