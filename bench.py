@@ -61,7 +61,7 @@ def parse():
                                                       "int4", "long4", "small"],
                     help="profiling: run only this fold shape (40 launches) and exit (PMC passes, tools/gpu_pmc_r02.sh)")
     ap.add_argument("--schedules", default=None,
-                    help="--shape node*: comma-separated fold schedule words (U | issue << 4) to run in turn")
+                    help="--shape node* / local256: comma-separated fold schedule words (U | issue << 4) to run in turn")
     ap.add_argument("--child-transport", default=None, choices=["ipc", "rccl", "node-ipc", "node-rccl"],
                     help=argparse.SUPPRESS)
     ap.add_argument("--child-full", action="store_true", help=argparse.SUPPRESS)
@@ -1505,7 +1505,16 @@ def shape_only(args):
     emac.lib()
     DevBuf.CONTIG = args.alloc == "contig"
     MB = {"node16": 16, "node64": 64, "node512": 512, "int4": 4, "long4": 4}.get(args.shape, 256) * MIB
-    if args.shape == "local256":
+    if args.shape == "local256" and args.schedules:  # every listed schedule in turn (EXT_MPI_AMD_FOLD_SCHEDULE)
+        r = {}
+        for w in args.schedules.split(","):
+            os.environ["EXT_MPI_AMD_FOLD_SCHEDULE"] = w
+            x = comm_shape_fold(8, MB // 8 // 4, torch.float32, emac.FLOAT, 40)
+            r[w] = {"avg_launch_us": x["avg_launch_us"], "schedule": x["schedule"]}
+            log(f"{args.shape} schedule {w}: {r[w]}")
+        del os.environ["EXT_MPI_AMD_FOLD_SCHEDULE"]
+        r = {"by_schedule": r}
+    elif args.shape == "local256":
         r = comm_shape_fold(8, MB // 8 // 4, torch.float32, emac.FLOAT, 40)
     elif args.shape == "small":
         r = small_sweep(emac, torch)

@@ -114,11 +114,16 @@ static int tune_candidates(const emac_handle *h, long vec, int *sched) {
   }
   sched[n++] = 2 | 1 << 4;
   sched[n++] = 4 | 1 << 4;
-  if (h->fan) sched[n++] = 4 | 5 << 4;
+  /* the node fan-outs of 4 and 8 ranks: (U 4, staggered) with buffer loads (fold_kernel.hpp
+     kBufLoad), and from 32 MiB per leaf (U 4, burst) with buffer loads and device-scope streaming
+     stores (kDevStore; below 32 MiB no gain was measured); other widths (U 4, staggered) as is */
+  if (h->fan && (h->nsrc == 4 || h->nsrc == 8)) {
+    sched[n++] = 4 | (5 | 1 << 15) << 4;
+    if (vec * 16 >= (32L << 20)) sched[n++] = 4 | (1 | 1 << 14 | 1 << 15) << 4;
+  } else if (h->fan) {
+    sched[n++] = 4 | 5 << 4;
+  }
   if (small) sched[n++] = 1 | 1 << 4;
-  /* (U 4, burst) with device-scope streaming stores (fold_kernel.hpp kDevStore): node fan-outs of 4
-     and 8 ranks from 32 MiB per leaf (below it no gain was measured) */
-  if (h->fan && (h->nsrc == 4 || h->nsrc == 8) && vec * 16 >= (32L << 20)) sched[n++] = 4 | (1 | 1 << 14) << 4;
   if (h->tiles_per_bucket > 0) {
     sched[n++] = 2 | (1 | 2 << 11) << 4;
     if (!h->fan) {

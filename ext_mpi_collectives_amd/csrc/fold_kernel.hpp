@@ -62,10 +62,20 @@ constexpr int kPlainLoad = 1024;
 // launch's closing write-back. The best of eight store policies in tools/storepol.hip on two
 // leases (1-5 % over the default-scope nontemporal store at 16-256 MiB per rank); in the library's
 // own launch (U 4 burst, bench.py --schedules) 0.7-1 % faster at 64 and 256 MiB per rank, no gain
-// at 16 MiB and below (profiles/r04/storepol/). Offered to the tuner for large node fan-outs
-// (engine_tune.c).
+// at 16 MiB and below (profiles/r04/storepol/). Offered to the tuner for large node fan-outs,
+// with buffer loads (kBufLoad below; engine_tune.c).
 constexpr int kDevStore = 1 << 14;
 constexpr int kDevStreaming = 18;  // sc1 | nt
+// ISSUE bit 15: leaf loads as 16-byte buffer loads (nontemporal, a buffer resource per leaf tile)
+// instead of global loads with an SGPR base: the same bytes and cache policy, another address
+// path. tools/loadpol.hip: 1-4 % faster under every nontemporal policy on the node fan-out and the
+// local fold; in the library's own launch (bench.py --schedules, two passes,
+// profiles/r04/bufload/) (U 4, staggered) 0.7-1.2 % faster at 16 / 256 MiB per rank and 4.5 % at
+// configs[2]'s 4 MiB, with device-scope stores 0.6 % at 256 MiB, no gain for the other schedules
+// or the local fold. The tuner's (U 4, staggered) and device-scope candidates of the node fan-outs
+// of 4 and 8 ranks use them (engine_tune.c).
+constexpr int kBufLoad = 1 << 15;
+constexpr int kStreaming = 2;  // nt
 typedef unsigned int U32x4 __attribute__((ext_vector_type(4)));
 
 template <typename V>
@@ -77,6 +87,11 @@ template <typename V>
 __device__ __forceinline__ void sys_store16(void *tile_base, unsigned byte_off, V v) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(tile_base, 0, 0x7FFFFFF0, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U32x4, v), r, byte_off, 0, kSysCoherent);
+}
+template <typename V>
+__device__ __forceinline__ V nt_load16(const void *tile_base, unsigned byte_off) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(tile_base), 0, 0x7FFFFFF0, 0x00020000);
+  return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kStreaming));
 }
 template <typename V>
 __device__ __forceinline__ void dev_store16(void *tile_base, unsigned byte_off, V v) {
@@ -241,6 +256,8 @@ __device__ __forceinline__ void load_fold(const emac_bucket *b, long tile_base, 
       if (FULL || (long)v < left) x[u][s] = sys_load16<V>((const void *)src[s], v * 16u);
     } else if constexpr ((ISSUE & kPlainLoad) != 0) {
       if (FULL || (long)v < left) x[u][s] = src[s][v];
+    } else if constexpr ((ISSUE & kBufLoad) != 0) {
+      if (FULL || (long)v < left) x[u][s] = nt_load16<V>((const void *)src[s], v * 16u);
     } else {
       if (FULL || (long)v < left) x[u][s] = __builtin_nontemporal_load(src[s] + v);
     }
@@ -364,7 +381,13 @@ __device__ __forceinline__ void fold_group_leaf(const emac_bucket *b, long gbase
     const GV *src = (const GV *)b->src[0] + gbase;
 #pragma unroll
     for (int q = 0; q < Q; ++q)
-      if (in(q)) acc[q] = __builtin_nontemporal_load(src + threadIdx.x + (unsigned)(q * EMAC_BLOCK));
+      if (in(q)) {
+        const unsigned v = threadIdx.x + (unsigned)(q * EMAC_BLOCK);
+        if constexpr ((ISSUE & kBufLoad) != 0)
+          acc[q] = nt_load16<V>((const void *)src, v * 16u);
+        else
+          acc[q] = __builtin_nontemporal_load(src + v);
+      }
   }
 #pragma unroll
   for (int s = 1; s < N; ++s) {
@@ -372,7 +395,13 @@ __device__ __forceinline__ void fold_group_leaf(const emac_bucket *b, long gbase
     V x[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q)
-      if (in(q)) x[q] = __builtin_nontemporal_load(src + threadIdx.x + (unsigned)(q * EMAC_BLOCK));
+      if (in(q)) {
+        const unsigned v = threadIdx.x + (unsigned)(q * EMAC_BLOCK);
+        if constexpr ((ISSUE & kBufLoad) != 0)
+          x[q] = nt_load16<V>((const void *)src, v * 16u);
+        else
+          x[q] = __builtin_nontemporal_load(src + v);
+      }
 #pragma unroll
     for (int q = 0; q < Q; ++q)
       if (in(q)) acc[q] = combine<OP, T>(acc[q], x[q]);
@@ -780,8 +809,9 @@ int launch_sum(int unroll, const Launch &L) {
     if constexpr (CH == 0) {
       if (unroll == sched(2, 1 | defer(4) | kLeafMajor)) return launch_one<T, OP, N, 2, CH, D, 1 | defer(4) | kLeafMajor>(L);
     }
-    if constexpr (N == 4 || N == 8) {  // device-scope streaming stores: the node fan-outs of 4 and 8 ranks
-      if (unroll == sched(4, 1 | kDevStore)) return launch_one<T, OP, N, 4, CH, D, 1 | kDevStore>(L);
+    if constexpr (N == 4 || N == 8) {  // the node fan-outs of 4 and 8 ranks: buffer loads, device-scope stores
+      if (unroll == sched(4, 5 | kBufLoad)) return launch_one<T, OP, N, 4, CH, D, 5 | kBufLoad>(L);
+      if (unroll == sched(4, 1 | kDevStore | kBufLoad)) return launch_one<T, OP, N, 4, CH, D, 1 | kDevStore | kBufLoad>(L);
     }
     return EMAC_ERR_UNSUPPORTED;
   } else {

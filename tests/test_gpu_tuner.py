@@ -277,14 +277,16 @@ def test_pipelined_host_handle_not_tuned(fresh_tuner, monkeypatch):
 
 
 DEV_STORE = 1 << 14  # fold_kernel.hpp kDevStore: device-scope streaming stores (cache policy sc1 nt)
+BUF_LOAD = 1 << 15  # fold_kernel.hpp kBufLoad: leaf loads as buffer loads
 
 
 @pytest.mark.parametrize("code", [emac.FLOAT, emac.INT])
 def test_device_scope_store_candidate_bitwise(oracle, fresh_tuner, monkeypatch, code):
-    """(U 4, burst) with device-scope streaming stores: offered to the tuner for node fan-outs of
-    8 ranks from 32 MiB per leaf (engine_tune.c). Forced alone it gives the oracle's bits; tuned
-    with the others, every Start gives the first Start's bits (compared on the device: 8 x 32 MiB
-    per Start), and the candidate list holds it at 32 MiB per leaf but not below."""
+    """(U 4, burst) with buffer loads and device-scope streaming stores: offered to the tuner for
+    node fan-outs of 8 ranks from 32 MiB per leaf (engine_tune.c), beside (U 4, staggered) with
+    buffer loads at every size. Forced alone it gives the oracle's bits; tuned with the others,
+    every Start gives the first Start's bits (compared on the device: 8 x 32 MiB per Start), and
+    the candidate list holds it at 32 MiB per leaf but not below."""
     R, copyin = 8, "6;1 -8 8"
     count = (32 << 20) // 4 + 4099  # just past 32 MiB per leaf; the owner chunks end in partial tiles
     sends = xorshift_inputs(R, count, code, seed_base=0xDE57 + code)
@@ -292,10 +294,10 @@ def test_device_scope_store_candidate_bitwise(oracle, fresh_tuner, monkeypatch, 
     dsend = [_dev(s) for s in sends]
     drecv = [torch.full((count,), -1, dtype=TORCH[code], device="cuda") for _ in range(R)]
     ptrs = ([t.data_ptr() for t in dsend], [t.data_ptr() for t in drecv])
-    monkeypatch.setenv("EXT_MPI_AMD_FOLD_SCHEDULE", str(4 | (1 | DEV_STORE) << 4))
+    monkeypatch.setenv("EXT_MPI_AMD_FOLD_SCHEDULE", str(4 | (1 | DEV_STORE | BUF_LOAD) << 4))
     h = emac.node_allreduce_init(*ptrs, count, code, copyin)
     try:
-        assert emac.handle_candidates(h) == [(4, 1 | DEV_STORE)]
+        assert emac.handle_candidates(h) == [(4, 1 | DEV_STORE | BUF_LOAD)]
         emac.start(h)
         emac.wait(h)
         assert_bitwise([t.cpu().numpy() for t in drecv], want, "forced device-scope stores")
@@ -305,7 +307,7 @@ def test_device_scope_store_candidate_bitwise(oracle, fresh_tuner, monkeypatch, 
     ref = [t.clone() for t in drecv]
     h = emac.node_allreduce_init(*ptrs, count, code, copyin)
     try:
-        assert (4, 1 | DEV_STORE) in emac.handle_candidates(h)
+        assert (4, 1 | DEV_STORE | BUF_LOAD) in emac.handle_candidates(h)
         for k in range(MAX_TUNE_STARTS):
             for t in drecv:
                 t.fill_(-1)
@@ -317,11 +319,12 @@ def test_device_scope_store_candidate_bitwise(oracle, fresh_tuner, monkeypatch, 
     finally:
         emac.done(h)
     # the tuning is over and every candidate was timed, the device-scope one among them
-    k = info["schedules"].index((4, 1 | DEV_STORE))
+    k = info["schedules"].index((4, 1 | DEV_STORE | BUF_LOAD))
     assert info["chosen"] >= 0 and info["us"][k] > 0, info
     small = (16 << 20) // 4  # 16 MiB per leaf: not offered
     h = emac.node_allreduce_init([t.data_ptr() for t in dsend], [t.data_ptr() for t in drecv], small, code, copyin)
     try:
-        assert (4, 1 | DEV_STORE) not in emac.handle_candidates(h)
+        cands = emac.handle_candidates(h)
+        assert (4, 1 | DEV_STORE | BUF_LOAD) not in cands and (4, 5 | BUF_LOAD) in cands, cands
     finally:
         emac.done(h)
