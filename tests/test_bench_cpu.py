@@ -155,3 +155,21 @@ def test_child_process_limit_kills_and_reports():
     rc, el, tail = b.run_child_process([sys.executable, "-c", "import sys; print('bad', file=sys.stderr); sys.exit(7)"],
                                        dict(os.environ), 30.0)
     assert rc == 7 and tail == ["bad"]
+
+
+@pytest.mark.parametrize("read_mib", [4 * 8, 16 * 8, 64 * 8, 256 * 8, 512 * 8])
+def test_rotation_keeps_every_read_in_hbm(monkeypatch, read_mib):
+    """bench.rotation_sets: between two uses of one buffer set, at least READ_REUSE_BYTES (2.5x the
+    256 MiB Infinity Cache) of other sets' inputs are read, with no more sets than that needs;
+    EXT_MPI_AMD_BENCH_ROTATION=legacy gives rounds 1-3's whole-working-set rule."""
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.delenv("EXT_MPI_AMD_BENCH_ROTATION", raising=False)
+    rd = read_mib * bench.MIB
+    n = bench.rotation_sets(rd, 2 * rd)
+    assert (n - 1) * rd >= bench.READ_REUSE_BYTES and (n - 2) * rd < bench.READ_REUSE_BYTES and n >= 2
+    monkeypatch.setenv("EXT_MPI_AMD_BENCH_ROTATION", "legacy")
+    legacy = bench.rotation_sets(rd, 2 * rd)
+    assert legacy == max(2, -(-640 * bench.MIB // (2 * rd)))
+    if read_mib == 16 * 8:  # the headline: 6 sets now, 3 before
+        assert (n, legacy) == (6, 3)
