@@ -122,6 +122,8 @@ static int tune_candidates(const emac_handle *h, long vec, int *sched) {
     if (vec * 16 >= (32L << 20)) sched[n++] = 4 | (1 | 1 << 14 | 1 << 15) << 4;
   } else if (h->fan) {
     sched[n++] = 4 | 5 << 4;
+  } else if (h->nsrc == 4 || h->nsrc == 8) {  /* one destination: (U 4, staggered) with buffer loads */
+    sched[n++] = 4 | (5 | 1 << 15) << 4;
   }
   if (small) sched[n++] = 1 | 1 << 4;
   if (h->tiles_per_bucket > 0) {

@@ -73,7 +73,9 @@ constexpr int kDevStreaming = 18;  // sc1 | nt
 // profiles/r04/bufload/) (U 4, staggered) 0.7-1.2 % faster at 16 / 256 MiB per rank and 4.5 % at
 // configs[2]'s 4 MiB, with device-scope stores 0.6 % at 256 MiB, no gain for the other schedules
 // or the local fold. The tuner's (U 4, staggered) and device-scope candidates of the node fan-outs
-// of 4 and 8 ranks use them (engine_tune.c).
+// of 4 and 8 ranks use them, and a (U 4, staggered) buffer-load candidate of the local fold of 4
+// or 8 leaves (47.1-47.8 against 47.9 us for its kept LDS groups at 8 x 32 MiB, three passes,
+// profiles/r04/bufload/local_*.json) (engine_tune.c).
 constexpr int kBufLoad = 1 << 15;
 constexpr int kStreaming = 2;  // nt
 typedef unsigned int U32x4 __attribute__((ext_vector_type(4)));
@@ -820,6 +822,9 @@ int launch_sum(int unroll, const Launch &L) {
     if (unroll == sched(1, 1)) return launch_one<T, OP, N, 1, CH, D>(L);
     if (unroll == sched(2, 1 | defer(4))) return launch_one<T, OP, N, 2, CH, D, 1 | defer(4)>(L);
     if (unroll == sched(4, 1 | defer(4))) return launch_one<T, OP, N, 4, CH, D, 1 | defer(4)>(L);
+    if constexpr (N == 4 || N == 8) {  // one destination of 4 or 8 leaves: (U 4, staggered) with buffer loads
+      if (unroll == sched(4, 5 | kBufLoad)) return launch_one<T, OP, N, 4, CH, D, 5 | kBufLoad>(L);
+    }
     return EMAC_ERR_UNSUPPORTED;
   }
 }
