@@ -26,6 +26,7 @@ import ctypes
 import json
 import math
 import os
+import statistics
 import sys
 import time
 
@@ -180,6 +181,16 @@ def host_random(count, np_dtype, seed):
     return rng.integers(-lim, lim, count).astype(np_dtype)
 
 
+def poison(buf, nbytes):
+    """every byte of a receive buffer (DevBuf, HostBuf or tensor) set to 0xFF"""
+    if isinstance(buf, DevBuf):
+        buf.upload(np.full(nbytes, 0xFF, np.uint8))
+    elif isinstance(buf, HostBuf):
+        ctypes.memset(buf.data_ptr(), 0xFF, nbytes)
+    else:
+        buf.view(-1).view(__import__("torch").uint8)[:nbytes].fill_(0xFF)
+
+
 def free_sets(sets):
     for sends, recvs in sets:
         for b in list(sends) + list(recvs):
@@ -213,10 +224,11 @@ def rotation_sets(read_bytes_per_set, set_bytes=None):
 
 
 def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * MIB, host=False, alloc="torch",
-             pool=None):
+             pool=None, launch_times=False):
     """Time `steps` node-form Allreduces (R ranks in this GPU). Returns dict of timings. `pool`: a
     dict that keeps the device buffer sets for the next call of the same shape (freed by the caller,
-    free_pool) instead of making and filling them again."""
+    free_pool) instead of making and filling them again. `launch_times`: also each Start's own time,
+    between fence-free events recorded before and after every launch ("launch_us")."""
     import torch
     import ext_mpi_collectives_amd as emac
     tsize = torch.empty((), dtype=tdtype).element_size()
@@ -267,7 +279,14 @@ def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * 
         emac.start(handles[k % nsets])
     stream.synchronize()
     sched = emac.handle_schedule(handles[0])
-    # sanity: set 0 against a float64 sum (parity proper is tests/test_gpu_parity.py)
+    scheds = [emac.handle_schedule(h) for h in handles]
+    # sanity: set 0 against a float64 sum (parity proper is tests/test_gpu_parity.py). Its receive
+    # buffers are poisoned first (all bytes 0xFF: NaN / -1), so a schedule that writes nothing or
+    # only part of the result cannot pass on an earlier Start's output
+    stream.synchronize()
+    for b in sets[0][1]:
+        poison(b, count * tsize)
+    torch.cuda.synchronize()
     emac.start(handles[0])
     stream.synchronize()
     sends, recvs = sets[0]
@@ -291,31 +310,62 @@ def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * 
     torch.cuda.synchronize()
     # the timed region: the stream is held while the start event and the first two Starts are
     # enqueued, then runs; the wall clock starts when it is let go
+    C = _ceiling_lib() if launch_times else None
+    evs = [C.ceiling_event_create() for _ in range(steps + 1)] if C is not None else []
+    if evs and not all(evs):
+        for ev in evs:
+            C.ceiling_event_destroy(ev)
+        evs = []
+
+    def one(k):
+        if evs and k == 0:
+            C.ceiling_event_record(evs[0], stream.cuda_stream)
+        emac.start(handles[k % nsets])
+        if evs:
+            C.ceiling_event_record(evs[k + 1], stream.cuda_stream)
+
     gate = StreamGate(stream.cuda_stream)
     try:
         e0.record(stream)
         pre = min(2, steps)
         for k in range(pre):
-            emac.start(handles[k % nsets])
+            one(k)
     finally:  # a held stream must never outlive an error
         t0 = time.perf_counter()
         gate.open()
     for k in range(pre, steps):
-        emac.start(handles[k % nsets])
+        one(k)
     e1.record(stream)
     stream.synchronize()
     t1 = time.perf_counter()
     gate.free()
+    launch_us = []
+    if evs:
+        ms = ctypes.c_float()
+        for k in range(steps):
+            if C.ceiling_event_ms(evs[k], evs[k + 1], ctypes.byref(ms)) == 0:
+                launch_us.append(ms.value * 1e3)
+        for ev in evs:
+            C.ceiling_event_destroy(ev)
     for h in handles:
         emac.done(h)
     if pool is None:
         free_sets(sets)
     del sets
     return {"wall_s": t1 - t0, "event_ms": e0.elapsed_time(e1), "nsets": nsets, "checked": checked,
-            "set_bytes": set_bytes, "schedule": sched}
+            "set_bytes": set_bytes, "schedule": sched, "schedules": scheds, "launch_us": launch_us}
 
 
-def comm_shape_fold(R, chunk, tdtype, code, steps):
+def launch_stats(us):
+    """median / min / max / count of per-launch times (microseconds), or {} without them"""
+    if not us:
+        return {}
+    v = sorted(us)
+    return {"launches_timed": len(v), "median_launch_us": round(statistics.median(v), 1),
+            "min_launch_us": round(v[0], 1), "max_launch_us": round(v[-1], 1)}
+
+
+def comm_shape_fold(R, chunk, tdtype, code, steps, launch_times=False):
     """The COMM form's per-GPU fold (R leaves of one chunk -> 1 destination) on this one GPU, at
     the chunk size an R-GPU run of the same message uses: the 1-GPU reference for the
     'per-GPU rate retained at N GPUs' comparison. Buffer sets rotate past the
@@ -343,19 +393,47 @@ def comm_shape_fold(R, chunk, tdtype, code, steps):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     stream.synchronize()
     sched = emac.handle_schedule(handles[0])
+    C = _ceiling_lib() if launch_times else None
+    evs = [C.ceiling_event_create() for _ in range(steps + 1)] if C is not None else []
+    if evs and not all(evs):
+        for ev in evs:
+            C.ceiling_event_destroy(ev)
+        evs = []
     e0.record(stream)
+    if evs:
+        C.ceiling_event_record(evs[0], stream.cuda_stream)
     for k in range(steps):
         emac.start(handles[k % nsets])
+        if evs:
+            C.ceiling_event_record(evs[k + 1], stream.cuda_stream)
     e1.record(stream)
     stream.synchronize()
     t = e0.elapsed_time(e1) * 1e-3 / steps
+    launch_us = []
+    if evs:
+        ms = ctypes.c_float()
+        for k in range(steps):
+            if C.ceiling_event_ms(evs[k], evs[k + 1], ctypes.byref(ms)) == 0:
+                launch_us.append(ms.value * 1e3)
+        for ev in evs:
+            C.ceiling_event_destroy(ev)
+    scheds = [emac.handle_schedule(h) for h in handles]
     for h in handles:
         emac.done(h)
     for b in bufs:
         b.free()
     return {"chunk_bytes": nbytes, "leaves": R, "avg_launch_us": round(t * 1e6, 2),
             "gbps_reduced": round(R * nbytes / t / 1e9, 1), "achieved_gbps": round((R + 1) * nbytes / t / 1e9, 1),
-            "schedule": sched}
+            "schedule": sched, "schedules_per_set": schedule_counts(scheds), **launch_stats(launch_us)}
+
+
+def schedule_counts(scheds):
+    """{"U<u>/<issue>": number of handles that kept it}: every rotated set tunes on its own"""
+    out = {}
+    for sc in scheds:
+        k = f"U{sc['unroll']}/{sc['issue']}"
+        out[k] = out.get(k, 0) + 1
+    return out
 
 
 def _ceiling_lib():
@@ -369,6 +447,10 @@ def _ceiling_lib():
                                     ctypes.c_void_p]
     L.ceiling_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     L.ceiling_write.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_void_p]
+    L.ceiling_event_create.restype = ctypes.c_void_p
+    L.ceiling_event_record.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    L.ceiling_event_ms.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]
+    L.ceiling_event_destroy.argtypes = [ctypes.c_void_p]
     L.ceiling_gate_arm.argtypes = [ctypes.c_void_p]
     L.ceiling_gate_arm.restype = ctypes.c_void_p
     L.ceiling_gate_open.argtypes = [ctypes.c_void_p]
@@ -603,7 +685,8 @@ def single_gpu(args):
                    "buffers": "hipMalloc" if args.alloc == "hip" else "torch caching allocator",
                    "checked_vs_fp64_sum": main["checked"],
                    "warmup_starts": max(args.warmup, main["nsets"] * TUNE_STARTS),
-                   "fold_schedule": main["schedule"]},
+                   "fold_schedule": main["schedule"],
+                   "fold_schedules_per_set": schedule_counts(main["schedules"])},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": traffic_from_profiles(f"node_r{R}_{S // MIB}mib_{args.dtype}"),
@@ -636,8 +719,12 @@ def single_gpu(args):
         except (RuntimeError, AssertionError) as e:
             log("ceiling probes failed:", e)
         big = (256 * MIB) // tsize
-        r256 = node_run(R, big, tdtype, code, copyin, max(4, args.steps // 5), 2, alloc=args.alloc)
-        k256 = r256["event_ms"] * 1e-3 / max(4, args.steps // 5)
+        # at least 20 timed launches, each also between its own fence-free events (4
+        # launches could not tell a slow lease from noise); the median is the point's figure
+        n256 = max(20, args.steps // 5)
+        r256 = node_run(R, big, tdtype, code, copyin, n256, 2, alloc=args.alloc, launch_times=True)
+        k256 = r256["event_ms"] * 1e-3 / n256
+        st256 = launch_stats(r256["launch_us"])
         extras["point_256MiB"] = {
             "gbps_reduced": round(R * big * tsize / k256 / 1e9, 1),
             "achieved_gbps": round(2 * R * big * tsize / k256 / 1e9, 1),
@@ -646,7 +733,11 @@ def single_gpu(args):
             "frac_of_measured_read_ceiling": round(2 * R * big * tsize / k256 / 1e9 / extras["read_ceiling_gbps"], 4)
             if "read_ceiling_gbps" in extras else None,
             "read_gbps": round(R * big * tsize / k256 / 1e9, 1),
-            "avg_launch_us": round(k256 * 1e6, 1), "checked": r256["checked"], "fold_schedule": r256["schedule"],
+            "avg_launch_us": round(k256 * 1e6, 1), **st256,
+            "frac_of_peak_at_median": round(2 * R * big * tsize / (st256["median_launch_us"] * 1e-6) / 1e9 /
+                                            HBM_PEAK_GBPS, 4) if st256 else None,
+            "checked": r256["checked"], "fold_schedule": r256["schedule"],
+            "schedules_per_set": schedule_counts(r256["schedules"]),
             "traffic": traffic_from_profiles(f"node_r{R}_256mib_{args.dtype}")}
         if "write_ceiling_gbps" in extras:
             fl = read_write_floor_s(extras, R * big * tsize, R * big * tsize)
@@ -697,8 +788,11 @@ def single_gpu(args):
         # SURVEY.md 8(d)'s local fold at the north-star size: the owner's fold of the COMM / IPC
         # forms (R leaves of C = 256 MiB / R -> one destination, read-dominated), where the
         # ">= 80 % of HBM read bandwidth" target is defined
-        lf = comm_shape_fold(R, big // R, tdtype, code, 40)
+        lf = comm_shape_fold(R, big // R, tdtype, code, 40, launch_times=True)
         lf["frac_of_peak"] = round(lf["achieved_gbps"] / HBM_PEAK_GBPS, 4)
+        if "median_launch_us" in lf:
+            lf["frac_of_peak_at_median"] = round((R + 1) * lf["chunk_bytes"] / (lf["median_launch_us"] * 1e-6) / 1e9 /
+                                                 HBM_PEAK_GBPS, 4)
         lf["algorithmic_bytes_per_launch"] = (R + 1) * lf["chunk_bytes"]
         lf["traffic"] = traffic_from_profiles(f"local_r{R}_{lf['chunk_bytes'] // MIB}mib_{args.dtype}")
         if "write_ceiling_gbps" in extras:
@@ -1549,7 +1643,7 @@ def shape_only(args):
             r, pool = {}, {}
             for w in args.schedules.split(","):
                 os.environ["EXT_MPI_AMD_FOLD_SCHEDULE"] = w
-                x = node_run(8, MB // ts, td, cd, "6;1 -8 8", steps, 4, alloc="hip", pool=pool)
+                x = node_run(8, MB // ts, td, cd, args.copyin or "6;1 -8 8", steps, 4, alloc="hip", pool=pool)
                 r[w] = {"avg_launch_us": round(x["event_ms"] * 1e3 / steps, 2), "checked": x["checked"],
                         "schedule": x["schedule"]}
                 log(f"{args.shape} schedule {w}: {r[w]}")
@@ -1557,7 +1651,7 @@ def shape_only(args):
             free_pool(pool)
             r = {"by_schedule": r}
         else:
-            x = node_run(8, MB // ts, td, cd, "6;1 -8 8", steps, 5, alloc="hip")
+            x = node_run(8, MB // ts, td, cd, args.copyin or "6;1 -8 8", steps, 5, alloc="hip")
             r = {"avg_launch_us": round(x["event_ms"] * 1e3 / steps, 2), "checked": x["checked"], "schedule": x["schedule"]}
     emit({"shape": args.shape, **r})
 

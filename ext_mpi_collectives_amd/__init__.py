@@ -121,6 +121,7 @@ def lib():
         L.ext_mpi_amd_set_num_sockets.argtypes = [c_int]
         L.ext_mpi_amd_set_num_sockets.restype = c_int
         L.ext_mpi_amd_version.restype = ctypes.c_char_p
+        L.ext_mpi_amd_build_info.restype = ctypes.c_char_p
         L.ext_mpi_amd_gpu_malloc.argtypes = [P(c_void_p), ctypes.c_size_t]
         L.ext_mpi_amd_gpu_free.argtypes = [c_void_p]
         L.ext_mpi_amd_gpu_memcpy_hd.argtypes = [c_void_p, c_void_p, ctypes.c_size_t]
@@ -483,3 +484,22 @@ class num_sockets:
 
 def version():
     return lib().ext_mpi_amd_version().decode()
+
+
+def build_info():
+    """The loaded library's build stamp: {"sha": commit[+dirty], "src": source hash} (_stamp.py)."""
+    from . import _stamp
+    return _stamp.parse(lib().ext_mpi_amd_build_info().decode())
+
+
+def check_build():
+    """The loaded library's stamp against the sources beside it. Returns the stamp dict with "tree"
+    (this tree's source hash) and "match"; raises if the binary was built from other sources."""
+    from . import _stamp
+    info = build_info()
+    info["tree"] = _stamp.source_hash()
+    info["match"] = info.get("src") == info["tree"]
+    if not info["match"]:
+        raise RuntimeError(f"{LIB_PATH} was built from sources {info.get('src')}, this tree's are {info['tree']}: "
+                           "rebuild it (make -C ext_mpi_collectives_amd/csrc)")
+    return info

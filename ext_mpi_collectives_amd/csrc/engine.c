@@ -506,3 +506,8 @@ int ext_mpi_amd_plan_describe(int nranks, long count, int dtype, const char *cop
 }
 
 const char *ext_mpi_amd_version(void) { return "ext_mpi_collectives_amd 0.1 (gfx950)"; }
+
+/* "sha <HEAD>[+dirty] src <hash>": the commit and the product sources this binary was built from
+   (build/stamp.c, written by _stamp.py on every make) */
+extern const char emac_build_stamp[];
+const char *ext_mpi_amd_build_info(void) { return emac_build_stamp; }

@@ -173,6 +173,9 @@ typedef struct {
 /* what a fold launch's schedule choice depends on (the tuning cache's key, engine_tune.c) */
 typedef struct {
   int device, dtype, op, nsrc, fan, tree, nb, uniform;
+  int kind, hier, isolated; /* the handle's form and how its samples are timed: a schedule kept by one
+                               form (a fold_init local fold, say) is not reused unmeasured by another
+                               (a COMM rank's fold over freshly staged leaves) of the same launch shape */
   long vec, vec0; /* 16-byte vectors per leaf over all buckets, in the first bucket */
 } emac_shape;
 typedef struct {

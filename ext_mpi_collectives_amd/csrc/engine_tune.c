@@ -9,9 +9,13 @@
    fan-out form, fold tree, and the buckets' vector counts (their number, the total, the first
    bucket's and whether all are equal -- the tile layout follows from these). Handles of one shape
    run the same kernels over the same tiles, so the first handle's kept schedule serves every later
-   one: the blocking front end's cached handles (one per buffer set, mpi_interface.c), the bench's
-   rotated buffer sets, an application's re-created persistent requests. Entries are replaced
-   oldest first. */
+   one of the same form: the blocking front end's cached handles (one per buffer set,
+   mpi_interface.c), an application's re-created persistent requests. (The bench creates all its
+   rotated buffer sets before their first Start, so each of those tunes on its own; bench.py reports
+   every set's kept schedule.) The key also holds the handle's form (kind, hier) and whether its
+   samples were isolated: the same launch shape measured 4-20 % apart between a fold_init handle and
+   a COMM rank's fold of freshly staged leaves, so neither reuses the other's schedule. Entries are
+   replaced oldest first. */
 _Static_assert(EXT_MPI_AMD_TUNE_MAX == EMAC_TUNE_MAX && EXT_MPI_AMD_TUNE_MAX * 3 == EMAC_TUNE_SAMPLES,
                "ext_mpi_amd_tune_info mirrors emac_tune");
 #define EMAC_TUNE_CACHE 64
@@ -38,6 +42,9 @@ static void shape_key(const emac_handle *h, const emac_bucket *b, int nb, emac_s
   k->nsrc = h->nsrc;
   k->fan = h->fan;
   k->tree = emac_tree_kind(&h->plan.codes, h->plan.op);
+  k->kind = h->kind;
+  k->hier = h->hier;
+  k->isolated = h->tune.isolated;
   k->nb = nb;
   k->vec0 = nb ? b[0].nvec : 0;
   k->uniform = 1;
@@ -49,7 +56,8 @@ static void shape_key(const emac_handle *h, const emac_bucket *b, int nb, emac_s
 
 static int same_shape(const emac_shape *a, const emac_shape *k) {
   return a->device == k->device && a->dtype == k->dtype && a->op == k->op && a->nsrc == k->nsrc && a->fan == k->fan &&
-         a->tree == k->tree && a->nb == k->nb && a->uniform == k->uniform && a->vec == k->vec && a->vec0 == k->vec0;
+         a->tree == k->tree && a->kind == k->kind && a->hier == k->hier &&
+         a->isolated == k->isolated && a->nb == k->nb && a->uniform == k->uniform && a->vec == k->vec && a->vec0 == k->vec0;
 }
 
 static tune_entry *cache_find(const emac_shape *k) {
@@ -93,7 +101,8 @@ static int tune_candidates(const emac_handle *h, long vec, int *sched) {
   /* fold_kernel.hpp instantiation policy: (U 2, burst), (U 4, burst), for the node fan-out (U 4,
      s_sleep 2 every 4 loads); deferred stores (kDeferShift) when every bucket has the same tile
      count: (U 2, 4 tiles) and (U 4, 4 tiles) for one destination; for the fan-out (U 2, 4 tiles),
-     (U 4, 2 tiles) and, over the linear fold, the leaf-major form (kLeafMajor) of (U 2, 4 tiles).
+     (U 4, 2 tiles) and the leaf-major form (kLeafMajor) of (U 2, 4 tiles), over a compile-time chain
+     also of (U 2, 2 tiles).
      (U 4, 2 tiles) had the fewest DRAM credit stalls and the shortest busy time at 256 MiB per rank
      (profiles/r03_pmc_defer/stalls_per_request.txt: write-credit stalls 0.17 per request against
      0.71-0.86 for the per-tile schedules) and is offered again for the linear fold (round 3 had
@@ -106,11 +115,21 @@ static int tune_candidates(const emac_handle *h, long vec, int *sched) {
   const int small = vec < 256L * 4 * 2 * EMAC_BLOCK;
   const char *f = getenv("EXT_MPI_AMD_FOLD_SCHEDULE"); /* A/B runs: one schedule word, U | issue << 4 */
   if (f && atoi(f) > 0) {
+    int ns, fn, known = 0;
     sched[0] = atoi(f);
-    if (!emac_gpu_fold_supported(h->plan.dtype, h->plan.op, h->nsrc, h->fan, tree, sched[0],
-                                 h->tiles_per_bucket > 0))
-      return EMAC_ERR_UNSUPPORTED;
-    return 1;
+    if (emac_gpu_fold_supported(h->plan.dtype, h->plan.op, h->nsrc, h->fan, tree, sched[0], h->tiles_per_bucket > 0))
+      return 1;
+    /* a word some other tuned shape has a kernel for (a fan-out-only schedule met by a local fold, a
+       width-specific one by another leaf count): this handle keeps its static pick; a word no shape
+       has a kernel for is a mistake, refused at init */
+    for (ns = 2; ns <= 8 && !known; ns++)
+      for (fn = 0; fn <= 1 && !known; fn++)
+        known = emac_gpu_fold_supported(h->plan.dtype, EMAC_SUM, ns, fn, 0, sched[0], 1);
+    if (!known) return EMAC_ERR_UNSUPPORTED;
+    if (getenv("EXT_MPI_AMD_DEBUG_TUNE"))
+      fprintf(stderr, "ext_mpi_amd: EXT_MPI_AMD_FOLD_SCHEDULE %d has no kernel for this handle (%d leaves, fan %d): "
+                      "static pick kept\n", sched[0], h->nsrc, h->fan);
+    return 0;
   }
   sched[n++] = 2 | 1 << 4;
   sched[n++] = 4 | 1 << 4;
@@ -132,7 +151,11 @@ static int tune_candidates(const emac_handle *h, long vec, int *sched) {
       sched[n++] = 4 | (1 | 2 << 11) << 4;
     } else {
       sched[n++] = 4 | (1 | 1 << 11) << 4;
-      if (tree == 0) sched[n++] = 2 | (1 | 2 << 11 | 1 << 13) << 4; /* leaf-major groups: the linear fold's order only */
+      /* leaf-major groups (kLeafMajor): the linear fold and the compile-time chains; a chain keeps one
+         accumulator per open level, so it also gets the half group (U 2, 2 tiles: 94 VGPRs for
+         -2 -2 -2 against 218 at 4 tiles) */
+      sched[n++] = 2 | (1 | 2 << 11 | 1 << 13) << 4;
+      if (tree > 1) sched[n++] = 2 | (1 | 1 << 11 | 1 << 13) << 4;
     }
   }
   return n;
@@ -197,9 +220,10 @@ int upload_buckets(emac_handle *h, emac_bucket *b, int nb) {
     rc = emac_gpu_memcpy(h->d_edges, edges, sizeof(emac_edge) * (size_t)h->nedges);
   free(edges);
   for (i = 0; i < nb; i++) vec += b[i].nvec;
-  nc = rc ? 0 : tune_candidates(h, vec, sched);
-  if (nc < 0) return nc;
-  if (!nc || vec * 16 * (h->nsrc + (h->fan ? h->nsrc : 1)) < EMAC_TUNE_MIN_BYTES) return rc;
+  /* the size gate first: a handle too small to tune never looks at a forced schedule word */
+  if (rc || vec * 16 * (h->nsrc + (h->fan ? h->nsrc : 1)) < EMAC_TUNE_MIN_BYTES) return rc;
+  nc = tune_candidates(h, vec, sched);
+  if (nc <= 0) return nc;
   t->isolated = tune_isolated(h);
   shape_key(h, b, nb, &t->shape);
   if (cache_enabled() && (hit = cache_find(&t->shape)) != NULL) {

@@ -367,46 +367,127 @@ __device__ __forceinline__ void fold_group(const emac_bucket *b, long gbase, int
   }
 }
 
-// One leaf-major group (kLeafMajor): vector q of the group is lane vector q * EMAC_BLOCK + lane
-// from gbase (the KB tiles of U vectors are contiguous).
-template <typename T, int OP, int N, int U, int D, int ISSUE, bool ALL_FULL>
+// Leaf-major groups over a fold tree (kLeafMajor, round 5: any compile-time chain as well as the
+// linear fold). The tree's level l has lm_levels(CH, N) levels; level l groups lm_group(CH, N, l)
+// consecutive leaves (the linear fold: one level of N). Leaves arrive one after the other, so each
+// open level keeps one accumulator per vector: leaf t enters level 0 -- starting it when t opens a
+// level-0 group, else combined from the right -- and when t completes a level-(l-1) group that
+// partial enters level l the same way. These are chain_group's nested left folds in the same order,
+// so the bits are fold_leaves' (the linear fold: ((x0 + x1) + x2) + ...).
+constexpr int lm_levels(int ch) { return ch == 0 ? 1 : ch_levels(ch); }
+constexpr int lm_group(int ch, int n, int l) { return ch == 0 ? (l < 0 ? 1 : n) : ch_group(ch, l); }
+
+// leaf T has completed the level-(L-1) group it belongs to: that partial enters level L
+template <int OP, typename T, int N, int CH, int T_, int L, int Q, typename V>
+__device__ __forceinline__ void lm_close(V (&acc)[lm_levels(CH)][Q]) {
+  if constexpr (L < lm_levels(CH)) {
+    if constexpr ((T_ + 1) % lm_group(CH, N, L - 1) == 0) {
+      constexpr bool first = T_ % lm_group(CH, N, L) < lm_group(CH, N, L - 1);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) acc[L][q] = first ? acc[L - 1][q] : combine<OP, T>(acc[L][q], acc[L - 1][q]);
+      lm_close<OP, T, N, CH, T_, L + 1, Q>(acc);
+    }
+  }
+}
+
+// leaves S .. N-1 of the group, read leaf after leaf (each leaf's Q vectors per lane back to back).
+// BOUNDED (a group that reaches past its bucket's last vector): every leaf read is a buffer load
+// whose resource ends at the bucket's end, so loads past it return 0 instead of needing a guard;
+// the code stays straight-line (guarded loads and adds had made the compiler spill the
+// accumulators to scratch) and only the stores are guarded.
+template <typename T, int OP, int N, int CH, int Q, int ISSUE, bool BOUNDED, int S, typename V>
+__device__ __forceinline__ void lm_leaves(const emac_bucket *b, long gbase, unsigned bound, V (&acc)[lm_levels(CH)][Q]) {
+  typedef __attribute__((address_space(1))) V GV;
+  if constexpr (S < N) {
+    constexpr bool opens = S % lm_group(CH, N, 0) == 0;  // leaf S starts a level-0 group
+    const GV *src = (const GV *)b->src[S] + gbase;
+    V x[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const unsigned v = threadIdx.x + (unsigned)(q * EMAC_BLOCK);
+      V &dst = opens ? acc[0][q] : x[q];
+      if constexpr (BOUNDED) {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)src, 0, bound, 0x00020000);
+        dst = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, v * 16u, 0, kStreaming));
+      } else if constexpr ((ISSUE & kBufLoad) != 0) {
+        dst = nt_load16<V>((const void *)src, v * 16u);
+      } else {
+        dst = __builtin_nontemporal_load(src + v);
+      }
+    }
+    if constexpr (!opens) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) acc[0][q] = combine<OP, T>(acc[0][q], x[q]);
+    }
+    lm_close<OP, T, N, CH, S, 1, Q>(acc);
+    lm_leaves<T, OP, N, CH, Q, ISSUE, BOUNDED, S + 1>(b, gbase, bound, acc);
+  }
+}
+
+// ISSUE bit 16 (kLmPipe, with kLeafMajor): the leaves software-pipelined in the source -- leaf S + 1's
+// Q loads issued before leaf S is folded, a scheduling fence between the two -- so every wave keeps
+// Q to 2Q loads in flight whatever the fold tree (the compiler's own schedule of the chains drained
+// to vmcnt(0) between leaves).
+constexpr int kLmPipe = 1 << 16;
+
+template <typename T, int Q, bool BOUNDED, typename V>
+__device__ __forceinline__ void lm_load_leaf(const void *src_leaf, long gbase, unsigned bound, V (&x)[Q]) {
+  typedef __attribute__((address_space(1))) V GV;
+  const GV *src = (const GV *)src_leaf + gbase;
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const unsigned v = threadIdx.x + (unsigned)(q * EMAC_BLOCK);
+    if constexpr (BOUNDED) {
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)src, 0, bound, 0x00020000);
+      x[q] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, v * 16u, 0, kStreaming));
+    } else {
+      x[q] = __builtin_nontemporal_load(src + v);
+    }
+  }
+}
+
+template <typename T, int OP, int N, int CH, int Q, bool BOUNDED, int S, typename V>
+__device__ __forceinline__ void lm_pipe(const emac_bucket *b, long gbase, unsigned bound, V (&acc)[lm_levels(CH)][Q],
+                                        V (&cur)[Q], V (&nxt)[Q]) {
+  if constexpr (S < N) {
+    if constexpr (S + 1 < N) lm_load_leaf<T, Q, BOUNDED>(b->src[S + 1], gbase, bound, nxt);
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr bool opens = S % lm_group(CH, N, 0) == 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) acc[0][q] = opens ? cur[q] : combine<OP, T>(acc[0][q], cur[q]);
+    lm_close<OP, T, N, CH, S, 1, Q>(acc);
+    __builtin_amdgcn_sched_barrier(0);
+    lm_pipe<T, OP, N, CH, Q, BOUNDED, S + 1>(b, gbase, bound, acc, nxt, cur);
+  }
+}
+
+template <typename T, int OP, int N, int CH, int Q, int ISSUE, bool BOUNDED, typename V>
+__device__ __forceinline__ void lm_fold(const emac_bucket *b, long gbase, unsigned bound, V (&acc)[lm_levels(CH)][Q]) {
+  if constexpr ((ISSUE & kLmPipe) != 0) {
+    V xa[Q], xb[Q];
+    lm_load_leaf<T, Q, BOUNDED>(b->src[0], gbase, bound, xa);
+    lm_pipe<T, OP, N, CH, Q, BOUNDED, 0>(b, gbase, bound, acc, xa, xb);
+  } else {
+    lm_leaves<T, OP, N, CH, Q, ISSUE, BOUNDED, 0>(b, gbase, bound, acc);
+  }
+}
+
+// One leaf-major group: vector q of the group is lane vector q * EMAC_BLOCK + lane from gbase (the
+// KB tiles of U vectors are contiguous); no LDS.
+template <typename T, int OP, int N, int U, int CH, int D, int ISSUE, bool ALL_FULL>
 __device__ __forceinline__ void fold_group_leaf(const emac_bucket *b, long gbase, int nt) {
   typedef typename Lane<T>::V V;
   typedef __attribute__((address_space(1))) V GV;
   constexpr int Q = defer_tiles(ISSUE) * U;
-  const long left = ALL_FULL ? 0 : b->nvec - gbase;
-  auto in = [&](int q) {  // wave-uniform but for the bucket's last partial tile
-    return ALL_FULL || (q < nt * U && (long)(threadIdx.x + (unsigned)(q * EMAC_BLOCK)) < left);
-  };
-  V acc[Q];
-  {
-    const GV *src = (const GV *)b->src[0] + gbase;
-#pragma unroll
-    for (int q = 0; q < Q; ++q)
-      if (in(q)) {
-        const unsigned v = threadIdx.x + (unsigned)(q * EMAC_BLOCK);
-        if constexpr ((ISSUE & kBufLoad) != 0)
-          acc[q] = nt_load16<V>((const void *)src, v * 16u);
-        else
-          acc[q] = __builtin_nontemporal_load(src + v);
-      }
-  }
-#pragma unroll
-  for (int s = 1; s < N; ++s) {
-    const GV *src = (const GV *)b->src[s] + gbase;
-    V x[Q];
-#pragma unroll
-    for (int q = 0; q < Q; ++q)
-      if (in(q)) {
-        const unsigned v = threadIdx.x + (unsigned)(q * EMAC_BLOCK);
-        if constexpr ((ISSUE & kBufLoad) != 0)
-          x[q] = nt_load16<V>((const void *)src, v * 16u);
-        else
-          x[q] = __builtin_nontemporal_load(src + v);
-      }
-#pragma unroll
-    for (int q = 0; q < Q; ++q)
-      if (in(q)) acc[q] = combine<OP, T>(acc[q], x[q]);
+  constexpr int LV = lm_levels(CH);
+  static_assert(lm_group(CH, N, LV - 1) == N, "the fold tree spans the leaves");
+  // vectors of the group inside the bucket (a whole group unless it holds the bucket's last tile)
+  const long left = ALL_FULL ? (long)Q * EMAC_BLOCK : b->nvec - gbase;
+  V acc[LV][Q];
+  if (ALL_FULL || left >= (long)Q * EMAC_BLOCK) {
+    lm_fold<T, OP, N, CH, Q, ISSUE, false>(b, gbase, 0u, acc);
+  } else {
+    lm_fold<T, OP, N, CH, Q, ISSUE, true>(b, gbase, (unsigned)(left > 0 ? left * 16 : 0), acc);
   }
   // each group starts its stores at destination (group index mod D), so the groups in flight write
   // all D receive buffers at once rather than each in turn: 0.6-0.9 % faster at 16 MiB per rank,
@@ -417,9 +498,12 @@ __device__ __forceinline__ void fold_group_leaf(const emac_bucket *b, long gbase
     const int d = dd + d0 < D ? dd + d0 : dd + d0 - D;
     GV *dst = (GV *)b->dst[d] + gbase;
 #pragma unroll
-    for (int q = 0; q < Q; ++q)
-      if (in(q)) store_vec<V, ISSUE>(dst, threadIdx.x + (unsigned)(q * EMAC_BLOCK), acc[q]);
+    for (int q = 0; q < Q; ++q) {
+      const unsigned v = threadIdx.x + (unsigned)(q * EMAC_BLOCK);
+      if (ALL_FULL || (long)v < left) store_vec<V, ISSUE>(dst, v, acc[LV - 1][q]);
+    }
   }
+  (void)nt;
 }
 
 // The deferred-store schedule as a kernel of its own (equal buckets of tpb tiles: the tuner offers
@@ -429,7 +513,7 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_deferred_kernel(const emac_bu
                                                                    long ngroups, emac_codes codes) {
   typedef typename Lane<T>::V V;
   static_assert(N > 0 && (ISSUE & kRemote) == 0, "deferred stores: compile-time leaves, local memory");
-  static_assert((ISSUE & kLeafMajor) == 0 || CH == 0, "leaf-major groups: the linear fold's order");
+  static_assert((ISSUE & kLeafMajor) == 0 || CH != 1, "leaf-major groups: compile-time fold trees");
   constexpr int KB = defer_tiles(ISSUE);
   constexpr long TILE = (long)EMAC_BLOCK * U;
   constexpr bool LEAF = (ISSUE & kLeafMajor) != 0;
@@ -442,7 +526,7 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_deferred_kernel(const emac_bu
     const long t0 = (g - (long)bi * gpb) * KB;
     const int nt = tpb - t0 < KB ? (int)(tpb - t0) : KB;  // wave-uniform
     if constexpr (LEAF)
-      fold_group_leaf<T, OP, N, U, D, ISSUE, ALL_FULL>(bk + bi, t0 * TILE, nt);
+      fold_group_leaf<T, OP, N, U, CH, D, ISSUE, ALL_FULL>(bk + bi, t0 * TILE, nt);
     else
       fold_group<T, OP, N, U, CH, D, ISSUE, ALL_FULL>(bk + bi, t0 * TILE, nt, codes, res);
   }
@@ -768,7 +852,7 @@ int launch_one(const Launch &L) {
   constexpr int KB = defer_tiles(ISSUE);
   if (L.dry) return 0;
   if constexpr (KB > 1) {  // one workgroup per group of KB tiles
-    if (L.tpb <= 0) return launch_one<T, OP, N, U, CH, D, ISSUE & ~(3 << kDeferShift | kLeafMajor)>(L);  // unequal buckets
+    if (L.tpb <= 0) return launch_one<T, OP, N, U, CH, D, ISSUE & ~(3 << kDeferShift | kLeafMajor | kLmPipe)>(L);  // unequal buckets
     const long groups = (long)L.nb * ((L.tpb + KB - 1) / KB);
     const unsigned grid = (unsigned)(groups < 8192 ? groups : 8192);
     if (L.all_full && L.tpb % KB == 0)
@@ -813,8 +897,18 @@ int launch_sum(int unroll, const Launch &L) {
     if (unroll == sched(2, 1 | defer(4))) return launch_one<T, OP, N, 2, CH, D, 1 | defer(4)>(L);
     if (unroll == sched(4, 1 | defer(2))) return launch_one<T, OP, N, 4, CH, D, 1 | defer(2)>(L);
     if (unroll == sched(2, 1 | defer(8))) return launch_one<T, OP, N, 2, CH, D, 1 | defer(8)>(L);
-    if constexpr (CH == 0) {
-      if (unroll == sched(2, 1 | defer(4) | kLeafMajor)) return launch_one<T, OP, N, 2, CH, D, 1 | defer(4) | kLeafMajor>(L);
+    // leaf-major groups: the linear fold and the compile-time chains (CH == 1 took the branch above)
+    if (unroll == sched(2, 1 | defer(4) | kLeafMajor)) return launch_one<T, OP, N, 2, CH, D, 1 | defer(4) | kLeafMajor>(L);
+    if constexpr (CH > 1) {  // half the vectors per group: a chain keeps one accumulator per open level
+      if (unroll == sched(2, 1 | defer(2) | kLeafMajor)) return launch_one<T, OP, N, 2, CH, D, 1 | defer(2) | kLeafMajor>(L);
+    }
+    if constexpr (N == 8 && sizeof(T) == 4 && (T)0.5 != 0) {  // EXPERIMENT (float only): source-pipelined leaves
+      if (unroll == sched(2, 1 | defer(4) | kLeafMajor | kLmPipe))
+        return launch_one<T, OP, N, 2, CH, D, 1 | defer(4) | kLeafMajor | kLmPipe>(L);
+      if (unroll == sched(2, 1 | defer(2) | kLeafMajor | kLmPipe))
+        return launch_one<T, OP, N, 2, CH, D, 1 | defer(2) | kLeafMajor | kLmPipe>(L);
+      if (unroll == sched(1, 1 | defer(4) | kLeafMajor | kLmPipe))
+        return launch_one<T, OP, N, 1, CH, D, 1 | defer(4) | kLeafMajor | kLmPipe>(L);
     }
     if constexpr (N == 4 || N == 8) {  // the node fan-outs of 4 and 8 ranks: buffer loads, device-scope stores
       if (unroll == sched(4, 5 | kBufLoad)) return launch_one<T, OP, N, 4, CH, D, 5 | kBufLoad>(L);

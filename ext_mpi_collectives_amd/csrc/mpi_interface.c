@@ -66,7 +66,6 @@ static int cfg_ports_nodes = 0;      /* EXT_MPI_NUM_PORTS: its nodes (0 unset, -
 static int cfg_ports[EMAC_PORTS_MAX]; /* ... its 0-terminated port list (parse_ports) */
 static int cfg_blocking = 0;
 static int cfg_rccl = 0; /* EXT_MPI_AMD_TRANSPORT=rccl: legs over RCCL instead of hipIpc mappings */
-static int cfg_async_stage = 0; /* EXT_MPI_AMD_ASYNC_STAGE=1: blocking device staging on the handle's stream */
 /* Accepted as the reference reads them (ext_mpi.c:58-66, 88-116), with nothing to switch here:
    EXT_MPI_ALTERNATING -- the reference keeps two byte-code copies and swaps them per Start
    (ext_mpi_native.c:215-230, 554-617) so a Start's flags cannot meet the previous one's; here
@@ -168,7 +167,6 @@ static void read_env(void) {
     env_int("EXT_MPI_NUM_TASKS_PER_SOCKET", &cfg_tasks_per_socket);
     cfg_ports_nodes = parse_ports(getenv("EXT_MPI_NUM_PORTS"), cfg_ports); /* ext_mpi.c:124-157 */
     cfg_rccl = getenv("EXT_MPI_AMD_TRANSPORT") && !strcmp(getenv("EXT_MPI_AMD_TRANSPORT"), "rccl");
-    cfg_async_stage = getenv("EXT_MPI_AMD_ASYNC_STAGE") && atoi(getenv("EXT_MPI_AMD_ASYNC_STAGE")) > 0;
     if (env_int("EXT_MPI_NOT_RECURSIVE", &cfg_not_recursive))
       printf("# EXT_MPI not recursive = %d\n", cfg_not_recursive); /* ext_mpi.c:58-63 prints it always */
     if (env_int("EXT_MPI_FAST", &cfg_fast) && cfg_verbose) printf("# EXT_MPI fast %d\n", cfg_fast);
@@ -190,7 +188,6 @@ static void read_env(void) {
   PMPI_Bcast(&cfg_ports_nodes, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(cfg_ports, EMAC_PORTS_MAX, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_rccl, 1, MPI_INT, 0, MPI_COMM_WORLD);
-  PMPI_Bcast(&cfg_async_stage, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_alternating, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_fast, 1, MPI_INT, 0, MPI_COMM_WORLD);
   PMPI_Bcast(&cfg_not_recursive, 1, MPI_INT, 0, MPI_COMM_WORLD);
@@ -658,9 +655,11 @@ static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int
     }
     s = b->scratch;
     r = in_place ? b->scratch : (char *)b->scratch + stride;
-    /* a synchronous copy; with EXT_MPI_AMD_ASYNC_STAGE=1 device buffers are copied on the
-       handle's stream below instead */
-    if (!(on_dev && cfg_async_stage) && bytes && (rc = ext_mpi_amd_gpu_memcpy_hd((void *)s, sendbuf, bytes))) return rc;
+    /* synchronous copies in and out: stream-ordered ones on the handle's stream measured slower on
+       MI355X (2 and 4 ranks sharing one GPU, 1 KiB - 16 MiB: 83-169 us against 39-141 us per call,
+       profiles/r04/blocking_staging.txt): they go to a DMA engine, whose latency the synchronous
+       blit-kernel copies do not pay. (Round 4's opt-in for them was removed) */
+    if (bytes && (rc = ext_mpi_amd_gpu_memcpy_hd((void *)s, sendbuf, bytes))) return rc;
   }
   for (i = 0; i < BCACHE; i++) {
     e = &b->cache[i];
@@ -735,19 +734,6 @@ static int blocking_allreduce(const void *sendbuf, void *recvbuf, int count, int
   }
   e = &b->cache[slot];
   e->used = ++b->clock;
-  if (staged && on_dev && bytes && cfg_async_stage) {
-    /* EXT_MPI_AMD_ASYNC_STAGE=1: stage-in, the Allreduce and stage-out enqueued on the handle's
-       stream, one host wait at the end. Measured slower than the two synchronous copies on
-       MI355X (2 and 4 ranks sharing one GPU, 1 KiB - 16 MiB: 83-169 us against 39-141 us per
-       call, profiles/r04/blocking_staging.txt): the stream-ordered device copies go to a DMA
-       engine, whose latency the synchronous blit-kernel copies do not pay. Off by default. */
-    void *st = ext_mpi_amd_stream(e->handle);
-    if ((rc = ext_mpi_amd_gpu_after_default_stream(st)) || (rc = ext_mpi_amd_gpu_memcpy_async((void *)s, sendbuf, bytes, st)) ||
-        (rc = ext_mpi_amd_start(e->handle)) || (rc = ext_mpi_amd_gpu_memcpy_async(recvbuf, r, bytes, st)) ||
-        (rc = ext_mpi_amd_wait(e->handle)))
-      return rc;
-    return 0;
-  }
   if ((rc = ext_mpi_amd_start(e->handle)) || (rc = ext_mpi_amd_wait(e->handle))) return rc;
   if (staged && bytes && (rc = ext_mpi_amd_gpu_memcpy_dh(recvbuf, r, bytes))) return rc;
   return 0;

@@ -269,6 +269,10 @@ int ext_mpi_amd_node_shares(int nodes, const int *ports, int ranks_per_node, lon
 int ext_mpi_amd_set_num_sockets(int sockets);
 
 const char *ext_mpi_amd_version(void);
+/* "sha <commit>[+dirty] src <hash>": the commit and the hash of the product sources (csrc/,
+ * include/) this binary was built from (ext_mpi_collectives_amd/_stamp.py). No reference
+ * counterpart: it lets a test run state which build it exercised. */
+const char *ext_mpi_amd_build_info(void);
 
 #ifdef __cplusplus
 }

@@ -17,6 +17,7 @@ pytestmark = pytest.mark.gpu
 
 TORCH = {emac.FLOAT: torch.float32, emac.DOUBLE: torch.float64, emac.INT: torch.int32, emac.LONG: torch.int64}
 TUNE_STARTS = 1 + 3 * 3 * emac.TUNE_MAX + 1  # enough Starts for any handle's tuning to keep a schedule
+TUNE_1 = 1 + 3 * 3 + 1  # ... for a handle with one candidate (a forced schedule word)
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -445,8 +446,10 @@ def test_every_tuned_schedule_bitwise(oracle, code, copyin):
         assert any(t == 1 for _, _, t in seen), seen
         small = chunk * R * sends[0].itemsize < 8 << 20
         assert ((1, 1) in cands) == small, (chunk, cands)
-        leaf = (2, 1 | 2 << DEFER_SHIFT | LEAF_MAJOR)  # leaf-major groups: the linear fold only
-        assert (leaf in cands) == (copyin == "6;1 -8 8") and (4, 1 | 1 << DEFER_SHIFT) in cands, cands
+        leaf = (2, 1 | 2 << DEFER_SHIFT | LEAF_MAJOR)  # leaf-major groups: linear fold and compile-time chains
+        half = (2, 1 | 1 << DEFER_SHIFT | LEAF_MAJOR)  # ... and for a chain the half group
+        assert leaf in cands and (4, 1 | 1 << DEFER_SHIFT) in cands, cands
+        assert (half in cands) == (copyin != "6;1 -8 8"), cands
     # the local fold: one destination, one bucket
     n = 8 * 64000 + 40 if code == emac.FLOAT else 4 * 64000 + 20
     srcs_np = xorshift_inputs(R, n, code, seed_base=0x10CA1)
@@ -467,6 +470,50 @@ def test_every_tuned_schedule_bitwise(oracle, code, copyin):
             assert_bitwise([dst.cpu().numpy()], [lwant], f"local fold Start {k} {sc}")
     finally:
         emac.done(h)
+
+
+@pytest.mark.parametrize("copyin", ["6;1 -2 -2 -2 2 2 2", "6;1 -4 -2 2 4", "6;1 -2 -4 4 2", "6;1 -8 8", "6;1 -2 -2 2 2"])
+@pytest.mark.parametrize("kb", [4, 2])
+@pytest.mark.parametrize("code", [emac.FLOAT, emac.DOUBLE, emac.INT, emac.LONG])
+def test_leaf_major_chains_forced_bitwise(oracle, monkeypatch, code, kb, copyin):
+    """Leaf-major groups over the compile-time radix chains (round 5, fold_kernel.hpp lm_leaves: one
+    accumulator per open level, closed as the leaves complete their groups), forced as the only
+    schedule (EXT_MPI_AMD_FOLD_SCHEDULE): every Start bitwise against the oracle's fold order.
+    Sizes: whole groups (every bucket a multiple of the group), and a ragged one (partial last tile
+    and group: the bounded buffer loads), both above the tuning threshold so the forced word is
+    the handle's schedule; the linear fold's half group has no kernel (the word is skipped there)."""
+    R = 4 if copyin == "6;1 -2 -2 2 2" else 8
+    tsize = 4 if code in (emac.FLOAT, emac.INT) else 8
+    word = 2 | (1 | (2 if kb == 4 else 1) << DEFER_SHIFT | LEAF_MAJOR) << 4
+    if copyin == "6;1 -8 8" and kb == 2:
+        pytest.skip("the half leaf-major group is instantiated for the chains only")
+    monkeypatch.setenv("EXT_MPI_AMD_FOLD_SCHEDULE", str(word))
+    group = 256 * 2 * kb * 16 // tsize  # elements per group and leaf
+    m = max(8, (4 << 20) // (R * group * tsize))  # >= 4 MiB per rank: above the tuning threshold
+    for chunk in (m * group, m * group + 3 * group // 4 + 5):  # equal chunks: every bucket the same tiles
+        count = R * chunk
+        sends = xorshift_inputs(R, count, code, seed_base=0x1EAF + kb + chunk + 7 * R)
+        want = oracle.allreduce(sends, copyin)
+        dsend = [_dev(x) for x in sends]
+        drecv = [torch.full((count,), -1, dtype=TORCH[code], device="cuda") for _ in range(R)]
+        emac.tune_cache_clear()
+        h = emac.node_allreduce_init([t.data_ptr() for t in dsend], [t.data_ptr() for t in drecv], count, code, copyin)
+        dwant = [_dev(w) for w in want]
+        try:
+            assert emac.handle_candidates(h) == [(2, word >> 4)], emac.handle_candidates(h)
+            for k in range(TUNE_1):  # the static pick, the forced word's samples, then the word kept
+                for t in drecv:
+                    t.fill_(-1)
+                torch.cuda.synchronize()
+                emac.start(h)
+                emac.wait(h)
+                sc = emac.handle_schedule(h)
+                for r, (g, w) in enumerate(zip(drecv, dwant)):  # bitwise, compared on the device
+                    if not torch.equal(g.view(torch.uint8), w.view(torch.uint8)):
+                        assert_bitwise([t.cpu().numpy() for t in drecv], want, f"{copyin} kb {kb} chunk {chunk} Start {k} {sc}")
+            assert (sc["unroll"], sc["issue"], sc["tuned"]) == (2, word >> 4, 1), sc
+        finally:
+            emac.done(h)
 
 
 def run_comm_loopback(sends, code, copyin, host=False, in_place=False, phase=None, op=emac.SUM, repeats=1, nodes=1,

@@ -142,50 +142,49 @@ def test_comm_loopback_samples_time_the_fold_alone(oracle, fresh_tuner):
     sit in the 256 MiB Infinity Cache, the staged leaves freshly written by the reduce-scatter
     copies) the ranks' kept schedules differ from fold_init's by 4-20 % ties that move between
     ranks (measured: U 4 at 7.6 us on one rank, U 2 at 10.2 us for fold_init); the printout keeps
-    them beside each other."""
-    os.environ["EXT_MPI_AMD_TUNE_CACHE"] = "0"
+    them beside each other. The per-process schedule cache stays on: its key holds the handle's
+    form and how it is timed, so no COMM rank starts on the schedule fold_init kept for the same
+    launch shape -- each of them tunes."""
+    R, count, copyin = 8, (16 << 20) // 4, "6;1 -8 8"
+    ref_kept, ref = _tune_local_fold(R, count // R, emac.FLOAT, 0x10C0)
+    sends = xorshift_inputs(R, count, emac.FLOAT, seed_base=0x7A12)
+    want = oracle.allreduce(sends, copyin)
+    comms = emac.comm_init_loopback(R)
+    sbufs = [_dev(s) for s in sends]
+    rbufs = [torch.full((count,), -1.0, device="cuda") for _ in range(R)]
+    hs = []
     try:
-        R, count, copyin = 8, (16 << 20) // 4, "6;1 -8 8"
-        ref_kept, ref = _tune_local_fold(R, count // R, emac.FLOAT, 0x10C0)
-        sends = xorshift_inputs(R, count, emac.FLOAT, seed_base=0x7A12)
-        want = oracle.allreduce(sends, copyin)
-        comms = emac.comm_init_loopback(R)
-        sbufs = [_dev(s) for s in sends]
-        rbufs = [torch.full((count,), -1.0, device="cuda") for _ in range(R)]
-        hs = []
-        try:
-            for r in range(R):
-                hs.append(emac.allreduce_init(sbufs[r].data_ptr(), rbufs[r].data_ptr(), count, emac.FLOAT, comms[r],
-                                              copyin))
-            for rep in range(MAX_TUNE_STARTS):
-                for t in rbufs:
-                    t.fill_(-1.0)
-                torch.cuda.synchronize()
-                for leg in emac.lockstep_legs():
-                    if leg == emac.LEG_FOLD:  # one rank's fold at a time: alone on the GPU
-                        for h in hs:
-                            emac.start_legs(h, leg)
-                            emac.wait(h)
-                        continue
+        for r in range(R):
+            hs.append(emac.allreduce_init(sbufs[r].data_ptr(), rbufs[r].data_ptr(), count, emac.FLOAT, comms[r],
+                                          copyin))
+        for rep in range(MAX_TUNE_STARTS):
+            for t in rbufs:
+                t.fill_(-1.0)
+            torch.cuda.synchronize()
+            for leg in emac.lockstep_legs():
+                if leg == emac.LEG_FOLD:  # one rank's fold at a time: alone on the GPU
                     for h in hs:
                         emac.start_legs(h, leg)
-                    for h in hs:
                         emac.wait(h)
-                assert_bitwise([t.cpu().numpy() for t in rbufs], want, f"Start {rep}")
-            infos = [emac.handle_tune_info(h) for h in hs]
-            scheds = [emac.handle_schedule(h) for h in hs]
-        finally:
-            for h in hs:
-                emac.done(h)
-            for c in comms:
-                emac.comm_free(c)
+                    continue
+                for h in hs:
+                    emac.start_legs(h, leg)
+                for h in hs:
+                    emac.wait(h)
+            assert_bitwise([t.cpu().numpy() for t in rbufs], want, f"Start {rep}")
+        infos = [emac.handle_tune_info(h) for h in hs]
+        scheds = [emac.handle_schedule(h) for h in hs]
     finally:
-        del os.environ["EXT_MPI_AMD_TUNE_CACHE"]
+        for h in hs:
+            emac.done(h)
+        for c in comms:
+            emac.comm_free(c)
     print(f"fold_init kept {ref_kept}: {ref['schedules']} {ref['us']}")
     for r, (info, sc) in enumerate(zip(infos, scheds)):
         print(f"rank {r} kept {(sc['unroll'], sc['issue'])}: {info['us']} ops {info['ops_in_sample']}")
     for r, (info, sc) in enumerate(zip(infos, scheds)):
         assert sc["tuned"] == 1 and info["isolated"] == 1, (r, info)
+        assert info["cached"] == 0 and info["samples"] > 0, (r, info)  # not fold_init's kept schedule
         assert info["schedules"] == ref["schedules"], (r, info["schedules"], ref["schedules"])
         # one fold per timed Start in every sample: nothing else of the handle inside a timed span
         assert info["ops_in_sample"] == [info["timed_starts_per_sample"]] * (3 * info["candidates"]), (r, info)
@@ -254,6 +253,36 @@ def test_forced_schedule_refused_at_init(fresh_tuner, monkeypatch):
             emac.start(h)
             emac.wait(h)
         assert emac.handle_candidates(h) == [(4, 5)]
+        assert all(torch.equal(t, torch.full_like(t, float(R))) for t in drecv)
+    finally:
+        emac.done(h)
+
+
+def test_forced_schedule_other_shapes_keep_static_pick(fresh_tuner, monkeypatch):
+    """A forced word only some shapes have a kernel for (the leaf-major groups: node fan-outs only)
+    does not break other handles: a local fold of 8 leaves tuned by size keeps its
+    static pick, a handle under the tuning threshold never looks at the word, and both are exact."""
+    leaf_major = 2 | (1 | 2 << 11 | 1 << 13) << 4
+    monkeypatch.setenv("EXT_MPI_AMD_FOLD_SCHEDULE", str(leaf_major))
+    R, chunk = 8, (4 << 20) // 4  # 8 x 4 MiB -> 1: 36 MiB per launch, above the tuning threshold
+    srcs = [torch.full((chunk,), float(r + 1), device="cuda") for r in range(R)]
+    dst = torch.zeros(chunk, device="cuda")
+    h = emac.fold_init([t.data_ptr() for t in srcs], [dst.data_ptr()], chunk, emac.FLOAT)
+    try:
+        assert emac.handle_candidates(h) == []
+        emac.start(h)
+        emac.wait(h)
+        assert torch.equal(dst, torch.full_like(dst, R * (R + 1) / 2))
+    finally:
+        emac.done(h)
+    monkeypatch.setenv("EXT_MPI_AMD_FOLD_SCHEDULE", str(3 | 1 << 4))  # no kernel anywhere: U 3
+    small = 4096  # 8 x 16 KiB: below the tuning threshold, the word is never consulted
+    dsend = [torch.ones(small, device="cuda") for _ in range(R)]
+    drecv = [torch.zeros(small, device="cuda") for _ in range(R)]
+    h = emac.node_allreduce_init([t.data_ptr() for t in dsend], [t.data_ptr() for t in drecv], small, emac.FLOAT)
+    try:
+        emac.start(h)
+        emac.wait(h)
         assert all(torch.equal(t, torch.full_like(t, float(R))) for t in drecv)
     finally:
         emac.done(h)

@@ -185,4 +185,21 @@ void ceiling_gate_free(void *gate) {
   if (gate) (void)hipHostFree(gate);
 }
 
+/* Timing events without the system-scope fence a default event record carries (bench.py's
+   per-launch times: the fence would sit between the launches it brackets and change how they run) */
+void *ceiling_event_create(void) {
+  hipEvent_t e = nullptr;
+  return hipEventCreateWithFlags(&e, hipEventDisableSystemFence) == hipSuccess ? (void *)e : nullptr;
+}
+int ceiling_event_record(void *ev, void *stream) {
+  return hipEventRecord(static_cast<hipEvent_t>(ev), static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : -5;
+}
+int ceiling_event_ms(void *a, void *b, float *ms) {
+  if (hipEventSynchronize(static_cast<hipEvent_t>(b)) != hipSuccess) return -5;
+  return hipEventElapsedTime(ms, static_cast<hipEvent_t>(a), static_cast<hipEvent_t>(b)) == hipSuccess ? 0 : -5;
+}
+void ceiling_event_destroy(void *ev) {
+  if (ev) (void)hipEventDestroy(static_cast<hipEvent_t>(ev));
+}
+
 }  // extern "C"
