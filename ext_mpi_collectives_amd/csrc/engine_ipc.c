@@ -860,8 +860,9 @@ int ipc_allreduce_init(emac_handle *h, emac_comm *cm, const void *sendbuf, void 
   return rc;
 }
 
-unsigned *ipc_go(const emac_handle *h) {
-  return (unsigned *)((char *)g_comms[h->comm].sync + offsetof(emac_sync, go)) + h->slot;
+unsigned *ipc_go(const emac_handle *h) { return ipc_go_slot(h, h->slot); }
+unsigned *ipc_go_slot(const emac_handle *h, int slot) {
+  return (unsigned *)((char *)g_comms[h->comm].sync + offsetof(emac_sync, go)) + slot;
 }
 
 /* The end of a peer-mapped handle's set-up (after ipc_allreduce_init / node_ipc_init, whose
@@ -909,12 +910,17 @@ int ipc_barrier(emac_handle *h, int phase) {
    when the Start is waited for: the next Start on the handle synchronises normally */
 int ipc_status(const emac_handle *h) {
   volatile int *w;
-  int e;
+  int e, k;
   if (h->kind != KIND_IPC || !h->slot_held) return 0;
   w = (volatile int *)g_comms[h->comm].err + h->slot;
   e = *w;
-  if (!e) return 0;
   *w = 0;
+  for (k = 1; h->join && k < h->join->nparts; k++) { /* every part's slot (its first is h->slot) */
+    w = (volatile int *)g_comms[h->comm].err + h->join->slot[k];
+    e |= *w;
+    *w = 0;
+  }
+  if (!e) return 0;
   fprintf(stderr, "ext_mpi_amd: rank %d: node barrier failed:%s%s\n", g_comms[h->comm].rank,
           (e & EMAC_SYNC_ERR_TIMEOUT) ? " a peer did not arrive within EXT_MPI_AMD_BARRIER_TIMEOUT" : "",
           (e & EMAC_SYNC_ERR_ABORTED) ? " a peer gave up on this Allreduce" : "");

@@ -68,6 +68,46 @@ static int node_fold_codes(int n, int levels, int dtype, emac_codes *c) {
   return 0;
 }
 
+/* A bucket of the peer-mapped join before placement: pointers at message element 0, elements
+   [off, off + len) of the message */
+typedef struct {
+  emac_bucket b;
+  int nsrc;
+  long off, len;
+} jproto;
+
+/* the prototypes' elements inside [lo, hi), placed into b (pointers at their first element,
+   alignment split): the number of buckets */
+static int place_part(emac_bucket *b, const jproto *p, int n, long lo, long hi, long ts) {
+  int i, nb = 0;
+  for (i = 0; i < n; i++) {
+    const long a = p[i].off > lo ? p[i].off : lo, e = p[i].off + p[i].len < hi ? p[i].off + p[i].len : hi;
+    if (e <= a) continue;
+    b[nb] = p[i].b;
+    place_bucket(&b[nb], p[i].nsrc, a, e - a, (int)ts);
+    nb++;
+  }
+  return nb;
+}
+
+/* the parts of the pipelined join: EXT_MPI_AMD_JOIN_PARTS (1 = the serial join), else 4 from
+   EMAC_JOIN_MIN_BYTES per rank over several nodes */
+static int join_parts(const emac_handle *h, int nodes) {
+  const char *e = getenv("EXT_MPI_AMD_JOIN_PARTS");
+  int n = nodes > 1 && (long)h->bytes >= EMAC_JOIN_MIN_BYTES ? 4 : 1;
+  if (e && *e) n = atoi(e);
+  return n < 1 ? 1 : n > EMAC_JOIN_PARTS ? EMAC_JOIN_PARTS : n;
+}
+
+/* first element of part k of n over count elements: equal parts cut at 1024-element multiples (the
+   cuts keep every bucket's 16-byte phase), the last part to the end */
+static long join_cut(long count, int n, int k) {
+  long c;
+  if (k >= n) return count;
+  c = count / n * k / 1024 * 1024;
+  return c < count ? c : count;
+}
+
 /* The NODE form over peer-mapped nodes: node_comm_allreduce_init on an ext_mpi_amd_comm_init_ipc
    communicator -- one process per GPU, each member a node of R ranks whose buffers all live on
    its GPU. The inter-node schedule must be one reduce-scatter step over every node (EXT_MPI_NUM_PORTS
@@ -99,9 +139,10 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
   emac_share *sh[EMAC_MAX_RANKS] = {0};
   int nsh[EMAC_MAX_RANKS] = {0};
   emac_bucket *b = NULL;
+  jproto *pin = NULL, *psh = NULL, *ppl = NULL;
   const int N = cm->size, R = h->plan.nranks;
   const long ts = h->plan.tsize;
-  int attempt, r, k, me, i, slot, nb, pc;
+  int attempt, r, k, me, i, slot, pc, nparts, pslot[EMAC_JOIN_PARTS], nin = 0, nshr = 0, npl = 0;
   h->part_bytes = h->outbox_bytes = h->bytes > 16 ? h->bytes : 16;
   for (attempt = 0;; attempt++) {
     long lack = 0;
@@ -146,11 +187,29 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
     if (!peer_part[r] || !peer_out[r]) rc = EMAC_ERR_TRANSPORT;
   }
   if ((rc = ipc_agree(cm, rc == 0))) return rc;
-  for (slot = 0; slot < EMAC_SYNC_SLOTS; slot++) { /* the lowest slot free on every rank */
-    for (r = 0; r < N && (all[r].free_slots[slot >> 3] >> (slot & 7)) & 1; r++);
-    if (r == N) break;
+  /* the pipelined join (EXT_MPI_AMD_JOIN_PARTS, emac_join): the same part count on every rank (the
+     message size and the environment are the same), one slot per part */
+  nparts = join_parts(h, N);
+  for (k = 0, slot = 0; k < nparts; k++, slot++) { /* the lowest slots free on every rank */
+    for (; slot < EMAC_SYNC_SLOTS; slot++) {
+      for (r = 0; r < N && (all[r].free_slots[slot >> 3] >> (slot & 7)) & 1; r++);
+      if (r == N) break;
+    }
+    if (slot == EMAC_SYNC_SLOTS) return EMAC_ERR_MALLOC; /* the same verdict on every rank */
+    pslot[k] = slot;
   }
-  if (slot == EMAC_SYNC_SLOTS) return EMAC_ERR_MALLOC; /* the same verdict on every rank */
+  if (nparts > 1) {
+    if (!(h->join = (emac_join *)calloc(1, sizeof(emac_join)))) return EMAC_ERR_MALLOC; /* (all ranks: see above) */
+    h->join->nparts = nparts;
+    for (k = 0; k < nparts; k++) {
+      h->join->slot[k] = pslot[k];
+      cm->slot_used[pslot[k]] = 1;
+      cm->err[pslot[k]] = 0;
+      h->join->epoch[k][0] = cm->slot_epoch[pslot[k]][0];
+      h->join->epoch[k][1] = cm->slot_epoch[pslot[k]][1];
+    }
+  }
+  slot = pslot[0];
   h->slot = slot;
   cm->slot_used[slot] = 1;
   h->slot_held = 1;
@@ -181,59 +240,84 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
   for (me = 0, k = 0; me < R; me++) k += nsh[me];
   if (!rc) /* the halving flow folds log2 N levels of pairs, one step over every node a left fold */
     rc = node_fold_codes(N, N > 1 && emac_node_single(&h->ns) == 2 ? h->ns.nsteps : 1, h->plan.dtype, &h->xcodes);
-  if (!rc && !(b = (emac_bucket *)calloc((size_t)(k + h->plan.npieces * R) + 1, sizeof(emac_bucket)))) rc = EMAC_ERR_MALLOC;
+  if (!rc && (!(pin = (jproto *)calloc((size_t)h->plan.npieces * R + 1, sizeof(jproto))) ||
+              !(psh = (jproto *)calloc((size_t)k + 1, sizeof(jproto))) || !(ppl = (jproto *)calloc((size_t)k + 1, sizeof(jproto))) ||
+              !(b = (emac_bucket *)calloc((size_t)(k + h->plan.npieces * R) + 1, sizeof(emac_bucket)))))
+    rc = EMAC_ERR_MALLOC;
   /* 1. the copy-in: every owner chunk into this node's partial block (at its message offset) */
-  for (nb = 0, pc = 0; !rc && pc < h->plan.npieces; pc++)
+  for (pc = 0; !rc && pc < h->plan.npieces; pc++)
     for (i = 0; i < R; i++) {
       const long off = h->plan.chunk_off[(size_t)pc * R + i], len = h->plan.chunk_len[(size_t)pc * R + i];
-      emac_bucket *bk = &b[nb];
+      jproto *x = &pin[nin];
       int t;
       if (len <= 0) continue;
-      memset(bk, 0, sizeof(*bk));
-      for (t = 0; t < R; t++) bk->src[t] = h->dsend[h->plan.leaf_rank[i][t]];
-      bk->dst[0] = h->part;
-      bk->ndst = 1;
-      place_bucket(bk, R, off, len, ts);
-      nb++;
+      for (t = 0; t < R; t++) x->b.src[t] = h->dsend[h->plan.leaf_rank[i][t]];
+      x->b.dst[0] = h->part;
+      x->b.ndst = 1;
+      x->nsrc = R;
+      x->off = off;
+      x->len = len;
+      nin++;
     }
-  h->nsrc = R;
-  h->fan = 0;
-  if (!rc) rc = upload_buckets(h, b, nb);
   /* 2. this node's shares: the N partials in place, in the line's order, into the outbox */
-  for (nb = 0, me = 0; !rc && me < R; me++)
+  for (me = 0; !rc && me < R; me++)
     for (i = 0; i < nsh[me]; i++) {
       const emac_share *x = &sh[me][i];
-      emac_bucket *bk = &b[nb];
+      jproto *y = &psh[nshr];
       int l;
       if (x->node != cm->rank || x->len <= 0) continue;
-      memset(bk, 0, sizeof(*bk));
-      for (l = 0; l < x->nleaf; l++) bk->src[l] = peer_part[x->leaf_node[l]]; /* in h->xcodes' order */
-      bk->dst[0] = h->outbox;
-      bk->ndst = 1;
-      place_bucket(bk, x->nleaf, x->off, x->len, ts);
-      nb++;
+      for (l = 0; l < x->nleaf; l++) y->b.src[l] = peer_part[x->leaf_node[l]]; /* in h->xcodes' order */
+      y->b.dst[0] = h->outbox;
+      y->b.ndst = 1;
+      y->nsrc = x->nleaf;
+      y->off = x->off;
+      y->len = x->len;
+      nshr++;
     }
-  if (!rc) rc = upload_launch_fan(h, &h->xfold[0], b, nb, N, 2);
   /* 3. the pull, fused with the copy-out: every share read once from its node's outbox and stored
      into all R receive buffers, the nodes after this one first (their loads head for different
      GPUs' links), this node's own last */
-  for (nb = 0, k = 1; !rc && k <= N; k++) {
+  for (k = 1; !rc && k <= N; k++) {
     const int q = (cm->rank + k) % N;
     for (me = 0; me < R; me++)
       for (i = 0; i < nsh[me]; i++) {
         const emac_share *x = &sh[me][i];
-        emac_bucket *bk = &b[nb];
+        jproto *y = &ppl[npl];
         int d;
         if (x->node != q || x->len <= 0) continue;
-        memset(bk, 0, sizeof(*bk));
-        bk->src[0] = peer_out[q];
-        for (d = 0; d < R; d++) bk->dst[d] = h->drecv[d];
-        bk->ndst = R;
-        place_bucket(bk, 1, x->off, x->len, ts);
-        nb++;
+        y->b.src[0] = peer_out[q];
+        for (d = 0; d < R; d++) y->b.dst[d] = h->drecv[d];
+        y->b.ndst = R;
+        y->nsrc = 1;
+        y->off = x->off;
+        y->len = x->len;
+        npl++;
       }
   }
-  if (!rc) rc = upload_launch_fan(h, &h->pull, b, nb, 1, 2);
+  h->nsrc = R;
+  h->fan = 0;
+  if (!h->join) { /* the serial join: one launch per stage over every bucket */
+    if (!rc) rc = upload_buckets(h, b, place_part(b, pin, nin, 0, h->plan.count, ts)); /* tuned */
+    if (!rc) rc = upload_launch_fan(h, &h->xfold[0], b, place_part(b, psh, nshr, 0, h->plan.count, ts), N, 2);
+    if (!rc) rc = upload_launch_fan(h, &h->pull, b, place_part(b, ppl, npl, 0, h->plan.count, ts), 1, 2);
+  } else { /* part k: the buckets' elements inside [lo[k], lo[k + 1]) */
+    emac_join *J = h->join;
+    for (k = 0; k <= J->nparts; k++) J->lo[k] = join_cut(h->plan.count, J->nparts, k);
+    for (k = 0; !rc && k < J->nparts; k++) {
+      if (!rc) rc = upload_launch_as(h, &J->in[k], b, place_part(b, pin, nin, J->lo[k], J->lo[k + 1], ts), R,
+                                     emac_tree_kind(&h->plan.codes, h->plan.op) == 1);
+      if (!rc) rc = upload_launch_fan(h, &J->fold[k], b, place_part(b, psh, nshr, J->lo[k], J->lo[k + 1], ts), N, 2);
+      if (!rc) rc = upload_launch_fan(h, &J->pull[k], b, place_part(b, ppl, npl, J->lo[k], J->lo[k + 1], ts), 1, 2);
+      if (!rc) rc = emac_gpu_event_create(&J->ev_in[k]);
+      if (!rc) rc = emac_gpu_event_create(&J->ev_fold[k]);
+    }
+    if (!rc) rc = emac_gpu_event_create(&J->ev_done);
+    if (!rc) rc = emac_gpu_stream_create(&J->s_fold);
+    if (!rc) rc = emac_gpu_stream_create(&J->s_pull);
+  }
+  free(pin);
+  free(psh);
+  free(ppl);
   for (me = 0; me < R; me++) free(sh[me]);
   free(b);
   return rc;
@@ -433,4 +517,88 @@ int ext_mpi_amd_node_shares(int nodes, const int *ports, int ranks_per_node, lon
   free(sh);
   emac_plan_free(&p);
   return rc;
+}
+
+/* A Start of the pipelined peer-mapped join (emac_join): per part k,
+     copy-in stream (the handle's):  copy-in k -> [release] -> signal phase 0 of slot k -> event in[k]
+     fold stream:   wait in[k] -> wait phase 0 of slot k (go) -> share fold k -> signal phase 1 -> event fold[k]
+     pull stream:   wait fold[k] -> wait phase 1 of slot k -> pull + copy-out k (go)
+   and the handle's stream waits for the pull stream's last launch, so Test / Wait / the next Start
+   see the whole Allreduce. The local order between the stages of part k is the events'; the peers'
+   is the slot's flags, as in the serial join (ipc_sync.hpp), with the same timeout and abandon
+   rules per part: a part that times out costs the Start (every part's slot reports to Wait), and
+   the next Start synchronises normally on every slot. The next Start's copy-in of part k follows
+   this Start's last pull on the handle's stream, so no node overwrites its partial while a peer's
+   share fold of this Start may still read it (that peer signalled phase 1 of every part first). */
+int join_start(emac_handle *h) {
+  emac_comm *cm = &g_comms[h->comm];
+  emac_join *J = h->join;
+  const int N = cm->size;
+  int k, rc;
+  for (k = 0; k < J->nparts; k++) {
+    const emac_launch *I = &J->in[k], *X = &J->fold[k], *P = &J->pull[k];
+    const int slot = J->slot[k];
+    unsigned long e0, e1;
+    h->tune.ops++;
+    if ((I->nb || I->nedges) &&
+        (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, 0, I->unroll, &h->plan.codes, I->d_buckets, I->nb, I->ntiles,
+                            I->tiles_per_bucket, I->all_full, I->d_edges, I->nedges, h->stream)))
+      return rc;
+    if (h->ev_release && (rc = emac_gpu_event_record(h->ev_release, h->stream))) return rc; /* as ipc_barrier(h, 0) */
+    e0 = ++J->epoch[k][0];
+    e1 = ++J->epoch[k][1];
+    if ((rc = emac_gpu_node_signal((void *const *)cm->d_peer_sync, slot, 0, e0, N, cm->rank, h->stream)) ||
+        (rc = emac_gpu_event_record(J->ev_in[k], h->stream)) || (rc = emac_gpu_stream_wait(J->s_fold, J->ev_in[k])) ||
+        (rc = emac_gpu_node_wait(cm->sync, (void *const *)cm->d_peer_sync, slot, 0, e0, e1, N, cm->rank, cm->err + slot,
+                                 cm->timeout_ticks, J->s_fold)))
+      return rc;
+    if ((X->nb || X->nedges) &&
+        (rc = emac_gpu_fold_remote(h->plan.dtype, N > 1 ? h->plan.op : EMAC_SUM, N, X->unroll, &h->xcodes, X->d_buckets, X->nb,
+                                   X->ntiles, X->tiles_per_bucket, X->all_full, X->d_edges, X->nedges, ipc_go_slot(h, slot),
+                                   J->s_fold)))
+      return rc;
+    if ((rc = emac_gpu_node_signal((void *const *)cm->d_peer_sync, slot, 1, e1, N, cm->rank, J->s_fold)) ||
+        (rc = emac_gpu_event_record(J->ev_fold[k], J->s_fold)) || (rc = emac_gpu_stream_wait(J->s_pull, J->ev_fold[k])) ||
+        (rc = emac_gpu_node_wait(cm->sync, (void *const *)cm->d_peer_sync, slot, 1, e1, e1, N, cm->rank, cm->err + slot,
+                                 cm->timeout_ticks, J->s_pull)))
+      return rc;
+    if ((P->nb || P->nedges) &&
+        (rc = emac_gpu_copy_fan_remote(h->plan.tsize, h->plan.nranks, P->unroll, P->d_buckets, P->nb, P->ntiles,
+                                       P->tiles_per_bucket, P->all_full, P->d_edges, P->nedges, ipc_go_slot(h, slot),
+                                       J->s_pull)))
+      return rc;
+  }
+  if ((rc = emac_gpu_event_record(J->ev_done, J->s_pull))) return rc;
+  return emac_gpu_stream_wait(h->stream, J->ev_done);
+}
+
+/* the pipelined join's launches, streams and events; its slots (with their epochs) back to the
+   communicator */
+void join_free(emac_handle *h) {
+  emac_join *J = h->join;
+  int k;
+  if (!J) return;
+  if (J->s_fold) emac_gpu_stream_sync(J->s_fold);
+  if (J->s_pull) emac_gpu_stream_sync(J->s_pull);
+  for (k = 0; k < J->nparts; k++) {
+    emac_gpu_free(J->in[k].d_buckets);
+    emac_gpu_free(J->in[k].d_edges);
+    emac_gpu_free(J->fold[k].d_buckets);
+    emac_gpu_free(J->fold[k].d_edges);
+    emac_gpu_free(J->pull[k].d_buckets);
+    emac_gpu_free(J->pull[k].d_edges);
+    emac_gpu_event_destroy(J->ev_in[k]);
+    emac_gpu_event_destroy(J->ev_fold[k]);
+    if (h->slot_held) {
+      emac_comm *cm = &g_comms[h->comm];
+      cm->slot_used[J->slot[k]] = 0;
+      cm->slot_epoch[J->slot[k]][0] = J->epoch[k][0];
+      cm->slot_epoch[J->slot[k]][1] = J->epoch[k][1];
+    }
+  }
+  emac_gpu_event_destroy(J->ev_done);
+  if (J->s_fold) emac_gpu_stream_destroy(J->s_fold);
+  if (J->s_pull) emac_gpu_stream_destroy(J->s_pull);
+  free(J);
+  h->join = NULL;
 }

@@ -367,6 +367,10 @@ __device__ __forceinline__ void fold_group(const emac_bucket *b, long gbase, int
   }
 }
 
+// EXPERIMENT (bit 18, with kLeafMajor): every leaf loaded into fresh registers, a group's opening
+// leaf then copied into its level-0 accumulator behind an opaque asm barrier
+constexpr int kLmViaX = 1 << 18;
+
 // Leaf-major groups over a fold tree (kLeafMajor, round 5: any compile-time chain as well as the
 // linear fold). The tree's level l has lm_levels(CH, N) levels; level l groups lm_group(CH, N, l)
 // consecutive leaves (the linear fold: one level of N). Leaves arrive one after the other, so each
@@ -402,10 +406,11 @@ __device__ __forceinline__ void lm_leaves(const emac_bucket *b, long gbase, unsi
     constexpr bool opens = S % lm_group(CH, N, 0) == 0;  // leaf S starts a level-0 group
     const GV *src = (const GV *)b->src[S] + gbase;
     V x[Q];
+    constexpr bool VIA_X = (ISSUE & kLmViaX) != 0;
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const unsigned v = threadIdx.x + (unsigned)(q * EMAC_BLOCK);
-      V &dst = opens ? acc[0][q] : x[q];
+      V &dst = opens && !VIA_X ? acc[0][q] : x[q];
       if constexpr (BOUNDED) {
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)src, 0, bound, 0x00020000);
         dst = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, v * 16u, 0, kStreaming));
@@ -418,6 +423,12 @@ __device__ __forceinline__ void lm_leaves(const emac_bucket *b, long gbase, unsi
     if constexpr (!opens) {
 #pragma unroll
       for (int q = 0; q < Q; ++q) acc[0][q] = combine<OP, T>(acc[0][q], x[q]);
+    } else if constexpr (VIA_X) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        acc[0][q] = x[q];
+        asm volatile("" : "+v"(acc[0][q]));
+      }
     }
     lm_close<OP, T, N, CH, S, 1, Q>(acc);
     lm_leaves<T, OP, N, CH, Q, ISSUE, BOUNDED, S + 1>(b, gbase, bound, acc);
@@ -446,18 +457,29 @@ __device__ __forceinline__ void lm_load_leaf(const void *src_leaf, long gbase, u
   }
 }
 
-template <typename T, int OP, int N, int CH, int Q, bool BOUNDED, int S, typename V>
+// kLmInterleave (bit 17, with kLmPipe): inside each leaf's region one load of the next leaf after
+// every two VALU ops of this one (sched_group_barrier), a smooth issue rate instead of bursts
+constexpr int kLmInterleave = 1 << 17;
+
+template <typename T, int OP, int N, int CH, int Q, bool BOUNDED, bool IL, int S, typename V>
 __device__ __forceinline__ void lm_pipe(const emac_bucket *b, long gbase, unsigned bound, V (&acc)[lm_levels(CH)][Q],
                                         V (&cur)[Q], V (&nxt)[Q]) {
   if constexpr (S < N) {
     if constexpr (S + 1 < N) lm_load_leaf<T, Q, BOUNDED>(b->src[S + 1], gbase, bound, nxt);
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (!IL) __builtin_amdgcn_sched_barrier(0);
     constexpr bool opens = S % lm_group(CH, N, 0) == 0;
 #pragma unroll
     for (int q = 0; q < Q; ++q) acc[0][q] = opens ? cur[q] : combine<OP, T>(acc[0][q], cur[q]);
     lm_close<OP, T, N, CH, S, 1, Q>(acc);
+    if constexpr (IL && S + 1 < N) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // one VMEM read
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // two VALU
+      }
+    }
     __builtin_amdgcn_sched_barrier(0);
-    lm_pipe<T, OP, N, CH, Q, BOUNDED, S + 1>(b, gbase, bound, acc, nxt, cur);
+    lm_pipe<T, OP, N, CH, Q, BOUNDED, IL, S + 1>(b, gbase, bound, acc, nxt, cur);
   }
 }
 
@@ -466,7 +488,7 @@ __device__ __forceinline__ void lm_fold(const emac_bucket *b, long gbase, unsign
   if constexpr ((ISSUE & kLmPipe) != 0) {
     V xa[Q], xb[Q];
     lm_load_leaf<T, Q, BOUNDED>(b->src[0], gbase, bound, xa);
-    lm_pipe<T, OP, N, CH, Q, BOUNDED, 0>(b, gbase, bound, acc, xa, xb);
+    lm_pipe<T, OP, N, CH, Q, BOUNDED, (ISSUE & kLmInterleave) != 0, 0>(b, gbase, bound, acc, xa, xb);
   } else {
     lm_leaves<T, OP, N, CH, Q, ISSUE, BOUNDED, 0>(b, gbase, bound, acc);
   }
@@ -509,8 +531,8 @@ __device__ __forceinline__ void fold_group_leaf(const emac_bucket *b, long gbase
 // The deferred-store schedule as a kernel of its own (equal buckets of tpb tiles: the tuner offers
 // the schedule only then), so its code holds nothing of the per-tile loop's.
 template <typename T, int OP, int N, int U, int CH, int D, int ISSUE, bool ALL_FULL>
-__global__ __launch_bounds__(EMAC_BLOCK) void fold_deferred_kernel(const emac_bucket *__restrict__ bk, long tpb,
-                                                                   long ngroups, emac_codes codes) {
+__device__ __forceinline__ void deferred_body(const emac_bucket *__restrict__ bk, long tpb, long ngroups,
+                                              const emac_codes &codes) {
   typedef typename Lane<T>::V V;
   static_assert(N > 0 && (ISSUE & kRemote) == 0, "deferred stores: compile-time leaves, local memory");
   static_assert((ISSUE & kLeafMajor) == 0 || CH != 1, "leaf-major groups: compile-time fold trees");
@@ -530,6 +552,21 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_deferred_kernel(const emac_bu
     else
       fold_group<T, OP, N, U, CH, D, ISSUE, ALL_FULL>(bk + bi, t0 * TILE, nt, codes, res);
   }
+}
+
+template <typename T, int OP, int N, int U, int CH, int D, int ISSUE, bool ALL_FULL>
+__global__ __launch_bounds__(EMAC_BLOCK) void fold_deferred_kernel(const emac_bucket *__restrict__ bk, long tpb,
+                                                                   long ngroups, emac_codes codes) {
+  deferred_body<T, OP, N, U, CH, D, ISSUE, ALL_FULL>(bk, tpb, ngroups, codes);
+}
+
+// EXPERIMENT (bit 19): the same kernel compiled for at least W waves per SIMD (amdgpu_waves_per_eu):
+// the register budget then shapes the compiler's load schedule
+constexpr int kLmOcc = 1 << 19;
+template <typename T, int OP, int N, int U, int CH, int D, int ISSUE, bool ALL_FULL>
+__global__ __launch_bounds__(EMAC_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) void fold_deferred_kernel_w5(
+    const emac_bucket *__restrict__ bk, long tpb, long ngroups, emac_codes codes) {
+  deferred_body<T, OP, N, U, CH, D, ISSUE, ALL_FULL>(bk, tpb, ngroups, codes);
 }
 
 // ---- runtime leaf count (N = 0 in the templates below): MIN / MAX ----
@@ -852,10 +889,17 @@ int launch_one(const Launch &L) {
   constexpr int KB = defer_tiles(ISSUE);
   if (L.dry) return 0;
   if constexpr (KB > 1) {  // one workgroup per group of KB tiles
-    if (L.tpb <= 0) return launch_one<T, OP, N, U, CH, D, ISSUE & ~(3 << kDeferShift | kLeafMajor | kLmPipe)>(L);  // unequal buckets
+    if (L.tpb <= 0) return launch_one<T, OP, N, U, CH, D, ISSUE & ~(3 << kDeferShift | kLeafMajor | kLmPipe | kLmInterleave | kLmViaX | kLmOcc)>(L);  // unequal buckets
     const long groups = (long)L.nb * ((L.tpb + KB - 1) / KB);
     const unsigned grid = (unsigned)(groups < 8192 ? groups : 8192);
-    if (L.all_full && L.tpb % KB == 0)
+    if constexpr ((ISSUE & kLmOcc) != 0) {
+      if (L.all_full && L.tpb % KB == 0)
+        hipLaunchKernelGGL((fold_deferred_kernel_w5<T, OP, N, U, CH, D, ISSUE, true>), dim3(grid), dim3(EMAC_BLOCK), 0, L.s,
+                           L.b, L.tpb, groups, *L.c);
+      else
+        hipLaunchKernelGGL((fold_deferred_kernel_w5<T, OP, N, U, CH, D, ISSUE, false>), dim3(grid), dim3(EMAC_BLOCK), 0, L.s,
+                           L.b, L.tpb, groups, *L.c);
+    } else if (L.all_full && L.tpb % KB == 0)
       hipLaunchKernelGGL((fold_deferred_kernel<T, OP, N, U, CH, D, ISSUE, true>), dim3(grid), dim3(EMAC_BLOCK), 0, L.s, L.b,
                          L.tpb, groups, *L.c);
     else
@@ -909,6 +953,16 @@ int launch_sum(int unroll, const Launch &L) {
         return launch_one<T, OP, N, 2, CH, D, 1 | defer(2) | kLeafMajor | kLmPipe>(L);
       if (unroll == sched(1, 1 | defer(4) | kLeafMajor | kLmPipe))
         return launch_one<T, OP, N, 1, CH, D, 1 | defer(4) | kLeafMajor | kLmPipe>(L);
+      if (unroll == sched(2, 1 | defer(4) | kLeafMajor | kLmOcc))
+        return launch_one<T, OP, N, 2, CH, D, 1 | defer(4) | kLeafMajor | kLmOcc>(L);
+      if (unroll == sched(2, 1 | defer(4) | kLeafMajor | kLmViaX))
+        return launch_one<T, OP, N, 2, CH, D, 1 | defer(4) | kLeafMajor | kLmViaX>(L);
+      if (unroll == sched(2, 1 | defer(2) | kLeafMajor | kLmViaX))
+        return launch_one<T, OP, N, 2, CH, D, 1 | defer(2) | kLeafMajor | kLmViaX>(L);
+      if (unroll == sched(2, 1 | defer(4) | kLeafMajor | kLmPipe | kLmInterleave))
+        return launch_one<T, OP, N, 2, CH, D, 1 | defer(4) | kLeafMajor | kLmPipe | kLmInterleave>(L);
+      if (unroll == sched(2, 1 | defer(2) | kLeafMajor | kLmPipe | kLmInterleave))
+        return launch_one<T, OP, N, 2, CH, D, 1 | defer(2) | kLeafMajor | kLmPipe | kLmInterleave>(L);
     }
     if constexpr (N == 4 || N == 8) {  // the node fan-outs of 4 and 8 ranks: buffer loads, device-scope stores
       if (unroll == sched(4, 5 | kBufLoad)) return launch_one<T, OP, N, 4, CH, D, 5 | kBufLoad>(L);

@@ -123,6 +123,13 @@ int emac_gpu_event_create_release(void **ev);
 /* node barrier `phase` of the Start tagged `tag` (its phase-1 epoch) on `stream`: one wave */
 int emac_gpu_node_barrier(void *self, void *const *d_peers, int slot, int phase, unsigned long epoch, unsigned long tag,
                           int nranks, int me, int *err, long timeout_ticks, void *stream);
+/* the two halves of a node barrier (the pipelined node join, engine_join.c), one wave each: signal
+   phase `phase` with `epoch` to every peer; wait for every peer's signal (phase 0: and leave the
+   verdict in go[slot] for the fold launch behind it, marking the Start abandoned in the peers'
+   blocks on a timeout; phase 1: report a timeout or a peer that gave up, as the whole barrier) */
+int emac_gpu_node_signal(void *const *d_peers, int slot, int phase, unsigned long epoch, int nranks, int me, void *stream);
+int emac_gpu_node_wait(void *self, void *const *d_peers, int slot, int phase, unsigned long epoch, unsigned long tag,
+                       int nranks, int me, int *err, long timeout_ticks, void *stream);
 /* the whole peer-mapped Allreduce (barrier, fold, barrier, pull) in one launch, small messages.
    The grid is kept small (as many workgroups as tiles, at most 64): every workgroup spins while a
    peer is late, and a wide grid would hold that many CUs from the rank's other streams. */

@@ -62,6 +62,22 @@ __global__ __launch_bounds__(64) void node_barrier_kernel(emac::NodeSync ns, int
   }
 }
 
+// The split barrier of the pipelined node join: the signal on the stream that produced the data,
+// the wait on the stream that consumes it (ipc_sync.hpp; phase 0's wait leaves go[slot]).
+__global__ __launch_bounds__(64) void node_signal_kernel(emac::NodeSync ns, int phase, unsigned long epoch) {
+  emac::wave_signal(ns, phase, epoch);
+}
+
+__global__ __launch_bounds__(64) void node_wait_kernel(emac::NodeSync ns, int phase, unsigned long epoch) {
+  if (phase == 0) {
+    const bool ok = emac::wave_phase0(ns, epoch, false);
+    if (threadIdx.x == 0) __hip_atomic_store(&ns.self->go[ns.slot], ok ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+    const bool in_time = emac::wave_wait(ns, 1, epoch);
+    emac::wave_report(ns, (in_time ? 0 : EMAC_SYNC_ERR_TIMEOUT) | (emac::peer_gave_up(ns) ? EMAC_SYNC_ERR_ABORTED : 0));
+  }
+}
+
 // Byte probes of the IPC set-up (engine.c ipc_exchange): one lane per byte. Stores are
 // published with a system-scope release (L2 write-back of this XCD); loads follow a system-scope
 // acquire (L2 invalidate), so both see memory as the other processes left it.
@@ -293,6 +309,20 @@ int emac_gpu_node_barrier(void *self, void *const *d_peers, int slot, int phase,
   const emac::NodeSync ns = {static_cast<emac_sync *>(self), reinterpret_cast<emac_sync *const *>(d_peers), slot,
                              nranks, me, err, timeout_ticks, tag};
   hipLaunchKernelGGL(node_barrier_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), ns, phase, epoch);
+  return ok(hipGetLastError());
+}
+
+int emac_gpu_node_signal(void *const *d_peers, int slot, int phase, unsigned long epoch, int nranks, int me, void *stream) {
+  const emac::NodeSync ns = {nullptr, reinterpret_cast<emac_sync *const *>(d_peers), slot, nranks, me, nullptr, 0, 0};
+  hipLaunchKernelGGL(node_signal_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), ns, phase, epoch);
+  return ok(hipGetLastError());
+}
+
+int emac_gpu_node_wait(void *self, void *const *d_peers, int slot, int phase, unsigned long epoch, unsigned long tag,
+                       int nranks, int me, int *err, long timeout_ticks, void *stream) {
+  const emac::NodeSync ns = {static_cast<emac_sync *>(self), reinterpret_cast<emac_sync *const *>(d_peers), slot,
+                             nranks, me, err, timeout_ticks, tag};
+  hipLaunchKernelGGL(node_wait_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), ns, phase, epoch);
   return ok(hipGetLastError());
 }
 

@@ -12,6 +12,7 @@ line per case. Exit status 0 iff every case matched.
 """
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -66,6 +67,47 @@ def unsupported(N):
     if N == 4:
         out += [(emac.FLOAT, 1000, 2, "6;1 -2 2", [3], emac.SUM)]  # '4(3)': the allgather steps reduce
     return out
+
+
+def timeout_recovery(node, N, dev):
+    """A late node costs one Start, not the communicator (ipc_sync.hpp), in the serial and in the
+    pipelined join (every part's slot): on a communicator with a 0.3 s barrier timeout node 1 starts
+    its second Allreduce 1 s late. Every node must report that Start as failed (ERROR_TRANSPORT) and
+    the next Start on the same handle must be bit-exact again."""
+    saved = os.environ.get("EXT_MPI_AMD_BARRIER_TIMEOUT")
+    os.environ["EXT_MPI_AMD_BARRIER_TIMEOUT"] = "0.3"
+    comm = emac.comm_init_ipc(node, N, emac.torch_allgather(), dev)
+    os.environ["EXT_MPI_AMD_BARRIER_TIMEOUT"] = saved if saved is not None else ""
+    if saved is None:
+        del os.environ["EXT_MPI_AMD_BARRIER_TIMEOUT"]
+    emac.comm_set_nodes(comm, N, [-(N - 1), N - 1])
+    R, count = 2, 1 << 20  # 4 MiB per rank: the pipelined join's size by default
+    sbufs = [torch.full((count,), float(node * R + me + 1), device="cuda") for me in range(R)]
+    rbufs = [torch.empty_like(s) for s in sbufs]
+    want = float(N * R * (N * R + 1) // 2)
+    h = emac.node_comm_allreduce_init([s.data_ptr() for s in sbufs], [r.data_ptr() for r in rbufs], count, emac.FLOAT,
+                                      comm, "6;1 -2 2")
+    verdicts = []
+    for it in range(3):
+        dist.barrier()
+        for r in rbufs:
+            r.fill_(-1.0)
+        torch.cuda.synchronize()
+        if it == 1 and node == 1:
+            time.sleep(1.0)
+        try:
+            emac.start(h)
+            emac.wait(h)
+            verdicts.append("ok" if all(bool((r == want).all()) for r in rbufs) else "wrong")
+        except emac.ExtMpiError as e:
+            verdicts.append("failed" if e.code == emac.ERROR_TRANSPORT else str(e))
+    dist.barrier()
+    emac.done(h)
+    emac.comm_free(comm)
+    ok = verdicts == ["ok", "failed", "ok"]
+    print(f"NODEIPC node {node}/{N} timeout recovery (join parts {os.environ.get('EXT_MPI_AMD_JOIN_PARTS', 'default')}): "
+          f"{'ok' if ok else verdicts}", flush=True)
+    return ok
 
 
 def main():
@@ -138,6 +180,8 @@ def main():
         failures += not ok
         print(f"NODEIPC node {node}/{N} refusal {k} op {op} ports {ports}: {'ok' if ok else res}", flush=True)
     emac.comm_free(comm)
+    if os.environ.get("NODEIPC_RECOVERY"):
+        failures += not timeout_recovery(node, N, dev)
     dist.barrier()
     dist.destroy_process_group()
     sys.exit(1 if failures else 0)

@@ -30,12 +30,12 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run_nodes(nodes, budget=180):
+def _run_nodes(nodes, budget=180, **extra_env):
     port = _port()
     procs, logs = [], []
     for r in range(nodes):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(nodes), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), IPC_DEVICE="0", EXT_MPI_AMD_BARRIER_TIMEOUT="20")
+                   MASTER_PORT=str(port), IPC_DEVICE="0", EXT_MPI_AMD_BARRIER_TIMEOUT="20", **extra_env)
         logs.append(tempfile.TemporaryFile(mode="w+"))
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "node_ipc_worker.py")],
                                       env=env, stdout=logs[-1], stderr=subprocess.STDOUT, text=True))
@@ -65,4 +65,14 @@ def _run_nodes(nodes, budget=180):
 
 @pytest.mark.parametrize("nodes", [2, 3, 4, 8])
 def test_node_form_over_peer_mapped_nodes(nodes):
+    """the default join: serial below EMAC_JOIN_MIN_BYTES per rank, pipelined by 4 parts above"""
     _run_nodes(nodes, budget=300 if nodes >= 8 else 180)
+
+
+@pytest.mark.parametrize("parts", ["1", "3"])
+@pytest.mark.parametrize("nodes", [2, 3, 4, 8])
+def test_node_join_serial_and_pipelined(nodes, parts):
+    """every case with the join forced serial (EXT_MPI_AMD_JOIN_PARTS=1) or pipelined by 3 parts at
+    every size (parts of no element, buckets cut inside their tiles), plus the timeout recovery of a
+    late node over every part's slot"""
+    _run_nodes(nodes, budget=300 if nodes >= 8 else 180, EXT_MPI_AMD_JOIN_PARTS=parts, NODEIPC_RECOVERY="1")
