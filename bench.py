@@ -1006,6 +1006,7 @@ def _node_form_run(emac, comm, R, count, tdtype, code, copyin, steps, warmup, ra
         emac.start(handles[0])
         stream.synchronize()
         sched = emac.handle_schedule(handles[0])
+        join_parts = emac.handle_join_parts(handles[0])
         # check set 0 against a float64 sum over every rank of every node (sampled)
         idx = np.arange(0, count, max(1, count // (1 << 18)))
         got = []
@@ -1049,7 +1050,8 @@ def _node_form_run(emac, comm, R, count, tdtype, code, copyin, steps, warmup, ra
         parts = {"copy_in_fold_s": part(emac.LEG_FOLD, steps),
                  "node_legs_s": part(emac.LEG_NODES_RS | emac.LEG_NODES_FOLD | emac.LEG_NODES_AG, steps),
                  "copy_out_s": part(emac.LEG_ALLGATHER, steps)}
-        return {"wall": el.item(), "checked": bool(ok.item()), "schedule": sched, "nsets": nsets, **parts}
+        return {"wall": el.item(), "checked": bool(ok.item()), "schedule": sched, "nsets": nsets, "join_parts": join_parts,
+                **parts}
     finally:
         for h in handles:
             emac.done(h)
@@ -1129,7 +1131,7 @@ def transport_child(args):
     log(f"rank {rank}: {transport} child on GPU {dev}: communicator set-up")
     if transport.startswith("node-"):  # the N > 1 headline over one transport (node_child)
         res = node_child(args, emac, rank, world, dev, dist, torch, transport[5:])
-        with open(args.child_result, "w") as f:
+        with open(args.child_result.replace("{rank}", str(rank)), "w") as f:
             json.dump(res, f)
         dist.barrier()
         dist.destroy_process_group()
@@ -1238,7 +1240,7 @@ def transport_child(args):
             log(f"rank {rank}: {transport}: host buffers {count * tsize} B: {el_p * 1e5:.2f} us, checked {ok_p}")
     finally:
         emac.comm_free(comm)
-    with open(args.child_result, "w") as f:
+    with open(args.child_result.replace("{rank}", str(rank)), "w") as f:
         json.dump(res, f)
     dist.barrier()
     dist.destroy_process_group()
@@ -1511,6 +1513,9 @@ def node_form_line(args, world, dname, rn, one_rank_per_gpu):
                      "start_to_wait": round(wall * 1e6 / steps, 2)},
         # (peer-mapped members: the copy-out is fused into the node legs' pull, its part is empty)
         "copy_out_achieved_gbps": round(R * S / t_out / 1e9, 1) if t_out > 1e-6 else None,
+        # the peer-mapped join pipelined by parts (engine_join.c emac_join; 1: serial): its copy-ins
+        # overlap the node legs, so start_to_wait can fall below the sum of the parts timed alone
+        "join_parts": rn.get("join_parts"),
         "node_legs_xgmi_bound_us": round(xgmi_bound * 1e6, 1),
         "node_legs_frac_of_xgmi_bound": round(xgmi_bound / t_x, 3) if t_x > 0 else None,
         "value_per_gpu_gbps": round(R * S * steps / wall / 1e9, 2),

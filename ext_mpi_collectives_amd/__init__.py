@@ -122,6 +122,7 @@ def lib():
         L.ext_mpi_amd_set_num_sockets.restype = c_int
         L.ext_mpi_amd_version.restype = ctypes.c_char_p
         L.ext_mpi_amd_build_info.restype = ctypes.c_char_p
+        L.ext_mpi_amd_handle_join_parts.argtypes = [c_int]
         L.ext_mpi_amd_gpu_malloc.argtypes = [P(c_void_p), ctypes.c_size_t]
         L.ext_mpi_amd_gpu_free.argtypes = [c_void_p]
         L.ext_mpi_amd_gpu_memcpy_hd.argtypes = [c_void_p, c_void_p, ctypes.c_size_t]
@@ -503,3 +504,10 @@ def check_build():
         raise RuntimeError(f"{LIB_PATH} was built from sources {info.get('src')}, this tree's are {info['tree']}: "
                            "rebuild it (make -C ext_mpi_collectives_amd/csrc)")
     return info
+
+
+def handle_join_parts(h):
+    """The parts a peer-mapped node join is pipelined by (1: serial), 0 for other handles."""
+    n = lib().ext_mpi_amd_handle_join_parts(h)
+    _check("ext_mpi_amd_handle_join_parts", min(n, 0))
+    return n

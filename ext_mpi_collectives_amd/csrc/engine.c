@@ -278,10 +278,11 @@ static int enqueue_legs(emac_handle *h, int legs) {
   if ((legs & EXT_MPI_AMD_LEG_STAGE_IN) && (rc = stage_in(h))) return rc;
   if (h->kind == KIND_IPC && h->hier) { /* the NODE form over peer-mapped nodes (node_ipc_init) */
     const int nodes = g_comms[h->comm].size;
-    if (h->join) { /* pipelined by parts: the copy-in, the node legs and the copy-out together */
-      const int all = EXT_MPI_AMD_LEG_FOLD | EXT_MPI_AMD_LEG_NODES_RS | EXT_MPI_AMD_LEG_NODES_FOLD | EXT_MPI_AMD_LEG_NODES_AG;
-      if ((legs & all) != all && (legs & all) != 0) return EMAC_ERR_UNSUPPORTED;
-      if ((legs & all) && (rc = join_start(h))) return rc;
+    if (h->join) { /* pipelined by parts: the copy-in, and the node legs fused with the copy-out */
+      const int nl = EXT_MPI_AMD_LEG_NODES_RS | EXT_MPI_AMD_LEG_NODES_FOLD | EXT_MPI_AMD_LEG_NODES_AG;
+      if ((legs & nl) != nl && (legs & nl) != 0) return EMAC_ERR_UNSUPPORTED; /* the legs of a part go together */
+      if ((legs & (EXT_MPI_AMD_LEG_FOLD | nl)) && (rc = join_start(h, (legs & EXT_MPI_AMD_LEG_FOLD) != 0, (legs & nl) != 0)))
+        return rc;
       if ((legs & EXT_MPI_AMD_LEG_STAGE_OUT) && (rc = stage_out(h))) return rc;
       return 0;
     }

@@ -213,9 +213,9 @@ typedef struct {
    phase 0 of part k and goes on with part k + 1 while the fold stream waits for every node's part
    k, folds it and signals phase 1, and the pull stream waits for that. The HBM-bound copy-in of
    part k + 1 then runs beside the link-bound share fold of part k and pull of part k - 1 instead of
-   before them. EXT_MPI_AMD_JOIN_PARTS=1 keeps the serial join (one slot, one stream). */
+   before them. Opt-in (EXT_MPI_AMD_JOIN_PARTS=k): on one MI355X each part's dependent launches and
+   cross-stream waits cost more than the overlap gains (engine_join.c join_parts). */
 #define EMAC_JOIN_PARTS 8
-#define EMAC_JOIN_MIN_BYTES (4L << 20) /* per rank: smaller messages keep the serial join by default */
 typedef struct {
   int nparts;
   long lo[EMAC_JOIN_PARTS + 1]; /* part k: message elements [lo[k], lo[k + 1]) */
@@ -316,7 +316,7 @@ int upload_buckets(emac_handle *h, emac_bucket *b, int nb);
 int fold_launch(emac_handle *h);
 
 /* engine_join.c */
-int join_start(emac_handle *h);
+int join_start(emac_handle *h, int copyin, int legs);
 void join_free(emac_handle *h);
 
 /* engine_node.c */

@@ -90,11 +90,15 @@ static int place_part(emac_bucket *b, const jproto *p, int n, long lo, long hi, 
   return nb;
 }
 
-/* the parts of the pipelined join: EXT_MPI_AMD_JOIN_PARTS (1 = the serial join), else 4 from
-   EMAC_JOIN_MIN_BYTES per rank over several nodes */
+/* the parts of the pipelined join: EXT_MPI_AMD_JOIN_PARTS, else 1 (the serial join). Opt-in: on one
+   MI355X every part added 30-110 us of dependent launches and cross-stream waits to a Start (N = 1:
+   legs 37.8 -> 164.7 us at 4 parts; N = 2 processes sharing the GPU: 127 -> 453 us,
+   profiles/r05/join/), far above the overlap it can buy at 16 MiB per rank */
 static int join_parts(const emac_handle *h, int nodes) {
   const char *e = getenv("EXT_MPI_AMD_JOIN_PARTS");
-  int n = nodes > 1 && (long)h->bytes >= EMAC_JOIN_MIN_BYTES ? 4 : 1;
+  int n = 1;
+  (void)h;
+  (void)nodes;
   if (e && *e) n = atoi(e);
   return n < 1 ? 1 : n > EMAC_JOIN_PARTS ? EMAC_JOIN_PARTS : n;
 }
@@ -527,10 +531,12 @@ int ext_mpi_amd_node_shares(int nodes, const int *ports, int ranks_per_node, lon
    see the whole Allreduce. The local order between the stages of part k is the events'; the peers'
    is the slot's flags, as in the serial join (ipc_sync.hpp), with the same timeout and abandon
    rules per part: a part that times out costs the Start (every part's slot reports to Wait), and
-   the next Start synchronises normally on every slot. The next Start's copy-in of part k follows
+   the next Start synchronises normally on every slot. `copyin` / `legs`: the copy-ins, the node
+   legs (barriers, share folds, pulls), or both (ext_mpi_amd_start_legs times each alone; the legs
+   alone read the partials the last copy-ins left). The next Start's copy-in of part k follows
    this Start's last pull on the handle's stream, so no node overwrites its partial while a peer's
    share fold of this Start may still read it (that peer signalled phase 1 of every part first). */
-int join_start(emac_handle *h) {
+int join_start(emac_handle *h, int copyin, int legs) {
   emac_comm *cm = &g_comms[h->comm];
   emac_join *J = h->join;
   const int N = cm->size;
@@ -540,10 +546,11 @@ int join_start(emac_handle *h) {
     const int slot = J->slot[k];
     unsigned long e0, e1;
     h->tune.ops++;
-    if ((I->nb || I->nedges) &&
+    if (copyin && (I->nb || I->nedges) &&
         (rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, 0, I->unroll, &h->plan.codes, I->d_buckets, I->nb, I->ntiles,
                             I->tiles_per_bucket, I->all_full, I->d_edges, I->nedges, h->stream)))
       return rc;
+    if (!legs) continue; /* the copy-ins alone (ext_mpi_amd_start_legs: a part of the Start timed alone) */
     if (h->ev_release && (rc = emac_gpu_event_record(h->ev_release, h->stream))) return rc; /* as ipc_barrier(h, 0) */
     e0 = ++J->epoch[k][0];
     e1 = ++J->epoch[k][1];
@@ -568,6 +575,7 @@ int join_start(emac_handle *h) {
                                        J->s_pull)))
       return rc;
   }
+  if (!legs) return 0;
   if ((rc = emac_gpu_event_record(J->ev_done, J->s_pull))) return rc;
   return emac_gpu_stream_wait(h->stream, J->ev_done);
 }
@@ -601,4 +609,11 @@ void join_free(emac_handle *h) {
   if (J->s_pull) emac_gpu_stream_destroy(J->s_pull);
   free(J);
   h->join = NULL;
+}
+
+int ext_mpi_amd_handle_join_parts(int handle) {
+  const emac_handle *h = handle_get(handle);
+  if (!h) return EMAC_ERR_ARG;
+  if (h->kind != KIND_IPC || !h->hier) return 0;
+  return h->join ? h->join->nparts : 1;
 }

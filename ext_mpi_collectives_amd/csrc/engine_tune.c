@@ -102,7 +102,7 @@ static int tune_candidates(const emac_handle *h, long vec, int *sched) {
      s_sleep 2 every 4 loads); deferred stores (kDeferShift) when every bucket has the same tile
      count: (U 2, 4 tiles) and (U 4, 4 tiles) for one destination; for the fan-out (U 2, 4 tiles),
      (U 4, 2 tiles) and the leaf-major form (kLeafMajor) of (U 2, 4 tiles), over a compile-time chain
-     also of (U 2, 2 tiles).
+     also with the opening leaves copied (kLmOpenCopy).
      (U 4, 2 tiles) had the fewest DRAM credit stalls and the shortest busy time at 256 MiB per rank
      (profiles/r03_pmc_defer/stalls_per_request.txt: write-credit stalls 0.17 per request against
      0.71-0.86 for the per-tile schedules) and is offered again for the linear fold (round 3 had
@@ -151,11 +151,11 @@ static int tune_candidates(const emac_handle *h, long vec, int *sched) {
       sched[n++] = 4 | (1 | 2 << 11) << 4;
     } else {
       sched[n++] = 4 | (1 | 1 << 11) << 4;
-      /* leaf-major groups (kLeafMajor): the linear fold and the compile-time chains; a chain keeps one
-         accumulator per open level, so it also gets the half group (U 2, 2 tiles: 94 VGPRs for
-         -2 -2 -2 against 218 at 4 tiles) */
+      /* leaf-major groups (kLeafMajor): the linear fold and the compile-time chains; a chain also in the
+         form that copies each level-0 group's opening leaf into its accumulator (kLmOpenCopy): which of
+         the two is faster depends on the chain (fold_kernel.hpp) */
       sched[n++] = 2 | (1 | 2 << 11 | 1 << 13) << 4;
-      if (tree > 1) sched[n++] = 2 | (1 | 1 << 11 | 1 << 13) << 4;
+      if (tree > 1) sched[n++] = 2 | (1 | 2 << 11 | 1 << 13 | 1 << 16) << 4;
     }
   }
   return n;

@@ -367,9 +367,14 @@ __device__ __forceinline__ void fold_group(const emac_bucket *b, long gbase, int
   }
 }
 
-// EXPERIMENT (bit 18, with kLeafMajor): every leaf loaded into fresh registers, a group's opening
-// leaf then copied into its level-0 accumulator behind an opaque asm barrier
-constexpr int kLmViaX = 1 << 18;
+// ISSUE bit 16 (kLmOpenCopy, with kLeafMajor over a compile-time chain): every leaf is loaded into
+// registers of its own and a level-0 group's opening leaf is then copied into the group's
+// accumulator behind an empty asm statement, instead of being loaded into the accumulator itself.
+// It changes the compiler's schedule of the chains' leaf loads (the linear fold does not need it).
+// 16 MiB x 8 per Start, forced, one lease (profiles/r05/chains/): -2 -4 44.1 against 47.1 us
+// without it, -2 -2 -2 45.5 against 48.2, -4 -2 45.7 against 45.3; the linear fold 44.6. Both forms
+// are tuner candidates of the chains' fan-out (engine_tune.c).
+constexpr int kLmOpenCopy = 1 << 16;
 
 // Leaf-major groups over a fold tree (kLeafMajor, round 5: any compile-time chain as well as the
 // linear fold). The tree's level l has lm_levels(CH, N) levels; level l groups lm_group(CH, N, l)
@@ -406,7 +411,7 @@ __device__ __forceinline__ void lm_leaves(const emac_bucket *b, long gbase, unsi
     constexpr bool opens = S % lm_group(CH, N, 0) == 0;  // leaf S starts a level-0 group
     const GV *src = (const GV *)b->src[S] + gbase;
     V x[Q];
-    constexpr bool VIA_X = (ISSUE & kLmViaX) != 0;
+    constexpr bool VIA_X = (ISSUE & kLmOpenCopy) != 0;
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const unsigned v = threadIdx.x + (unsigned)(q * EMAC_BLOCK);
@@ -435,65 +440,6 @@ __device__ __forceinline__ void lm_leaves(const emac_bucket *b, long gbase, unsi
   }
 }
 
-// ISSUE bit 16 (kLmPipe, with kLeafMajor): the leaves software-pipelined in the source -- leaf S + 1's
-// Q loads issued before leaf S is folded, a scheduling fence between the two -- so every wave keeps
-// Q to 2Q loads in flight whatever the fold tree (the compiler's own schedule of the chains drained
-// to vmcnt(0) between leaves).
-constexpr int kLmPipe = 1 << 16;
-
-template <typename T, int Q, bool BOUNDED, typename V>
-__device__ __forceinline__ void lm_load_leaf(const void *src_leaf, long gbase, unsigned bound, V (&x)[Q]) {
-  typedef __attribute__((address_space(1))) V GV;
-  const GV *src = (const GV *)src_leaf + gbase;
-#pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    const unsigned v = threadIdx.x + (unsigned)(q * EMAC_BLOCK);
-    if constexpr (BOUNDED) {
-      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)src, 0, bound, 0x00020000);
-      x[q] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, v * 16u, 0, kStreaming));
-    } else {
-      x[q] = __builtin_nontemporal_load(src + v);
-    }
-  }
-}
-
-// kLmInterleave (bit 17, with kLmPipe): inside each leaf's region one load of the next leaf after
-// every two VALU ops of this one (sched_group_barrier), a smooth issue rate instead of bursts
-constexpr int kLmInterleave = 1 << 17;
-
-template <typename T, int OP, int N, int CH, int Q, bool BOUNDED, bool IL, int S, typename V>
-__device__ __forceinline__ void lm_pipe(const emac_bucket *b, long gbase, unsigned bound, V (&acc)[lm_levels(CH)][Q],
-                                        V (&cur)[Q], V (&nxt)[Q]) {
-  if constexpr (S < N) {
-    if constexpr (S + 1 < N) lm_load_leaf<T, Q, BOUNDED>(b->src[S + 1], gbase, bound, nxt);
-    if constexpr (!IL) __builtin_amdgcn_sched_barrier(0);
-    constexpr bool opens = S % lm_group(CH, N, 0) == 0;
-#pragma unroll
-    for (int q = 0; q < Q; ++q) acc[0][q] = opens ? cur[q] : combine<OP, T>(acc[0][q], cur[q]);
-    lm_close<OP, T, N, CH, S, 1, Q>(acc);
-    if constexpr (IL && S + 1 < N) {
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // one VMEM read
-        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // two VALU
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    lm_pipe<T, OP, N, CH, Q, BOUNDED, IL, S + 1>(b, gbase, bound, acc, nxt, cur);
-  }
-}
-
-template <typename T, int OP, int N, int CH, int Q, int ISSUE, bool BOUNDED, typename V>
-__device__ __forceinline__ void lm_fold(const emac_bucket *b, long gbase, unsigned bound, V (&acc)[lm_levels(CH)][Q]) {
-  if constexpr ((ISSUE & kLmPipe) != 0) {
-    V xa[Q], xb[Q];
-    lm_load_leaf<T, Q, BOUNDED>(b->src[0], gbase, bound, xa);
-    lm_pipe<T, OP, N, CH, Q, BOUNDED, (ISSUE & kLmInterleave) != 0, 0>(b, gbase, bound, acc, xa, xb);
-  } else {
-    lm_leaves<T, OP, N, CH, Q, ISSUE, BOUNDED, 0>(b, gbase, bound, acc);
-  }
-}
-
 // One leaf-major group: vector q of the group is lane vector q * EMAC_BLOCK + lane from gbase (the
 // KB tiles of U vectors are contiguous); no LDS.
 template <typename T, int OP, int N, int U, int CH, int D, int ISSUE, bool ALL_FULL>
@@ -507,9 +453,9 @@ __device__ __forceinline__ void fold_group_leaf(const emac_bucket *b, long gbase
   const long left = ALL_FULL ? (long)Q * EMAC_BLOCK : b->nvec - gbase;
   V acc[LV][Q];
   if (ALL_FULL || left >= (long)Q * EMAC_BLOCK) {
-    lm_fold<T, OP, N, CH, Q, ISSUE, false>(b, gbase, 0u, acc);
+    lm_leaves<T, OP, N, CH, Q, ISSUE, false, 0>(b, gbase, 0u, acc);
   } else {
-    lm_fold<T, OP, N, CH, Q, ISSUE, true>(b, gbase, (unsigned)(left > 0 ? left * 16 : 0), acc);
+    lm_leaves<T, OP, N, CH, Q, ISSUE, true, 0>(b, gbase, (unsigned)(left > 0 ? left * 16 : 0), acc);
   }
   // each group starts its stores at destination (group index mod D), so the groups in flight write
   // all D receive buffers at once rather than each in turn: 0.6-0.9 % faster at 16 MiB per rank,
@@ -557,15 +503,6 @@ __device__ __forceinline__ void deferred_body(const emac_bucket *__restrict__ bk
 template <typename T, int OP, int N, int U, int CH, int D, int ISSUE, bool ALL_FULL>
 __global__ __launch_bounds__(EMAC_BLOCK) void fold_deferred_kernel(const emac_bucket *__restrict__ bk, long tpb,
                                                                    long ngroups, emac_codes codes) {
-  deferred_body<T, OP, N, U, CH, D, ISSUE, ALL_FULL>(bk, tpb, ngroups, codes);
-}
-
-// EXPERIMENT (bit 19): the same kernel compiled for at least W waves per SIMD (amdgpu_waves_per_eu):
-// the register budget then shapes the compiler's load schedule
-constexpr int kLmOcc = 1 << 19;
-template <typename T, int OP, int N, int U, int CH, int D, int ISSUE, bool ALL_FULL>
-__global__ __launch_bounds__(EMAC_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) void fold_deferred_kernel_w5(
-    const emac_bucket *__restrict__ bk, long tpb, long ngroups, emac_codes codes) {
   deferred_body<T, OP, N, U, CH, D, ISSUE, ALL_FULL>(bk, tpb, ngroups, codes);
 }
 
@@ -889,17 +826,10 @@ int launch_one(const Launch &L) {
   constexpr int KB = defer_tiles(ISSUE);
   if (L.dry) return 0;
   if constexpr (KB > 1) {  // one workgroup per group of KB tiles
-    if (L.tpb <= 0) return launch_one<T, OP, N, U, CH, D, ISSUE & ~(3 << kDeferShift | kLeafMajor | kLmPipe | kLmInterleave | kLmViaX | kLmOcc)>(L);  // unequal buckets
+    if (L.tpb <= 0) return launch_one<T, OP, N, U, CH, D, ISSUE & ~(3 << kDeferShift | kLeafMajor | kLmOpenCopy)>(L);  // unequal buckets
     const long groups = (long)L.nb * ((L.tpb + KB - 1) / KB);
     const unsigned grid = (unsigned)(groups < 8192 ? groups : 8192);
-    if constexpr ((ISSUE & kLmOcc) != 0) {
-      if (L.all_full && L.tpb % KB == 0)
-        hipLaunchKernelGGL((fold_deferred_kernel_w5<T, OP, N, U, CH, D, ISSUE, true>), dim3(grid), dim3(EMAC_BLOCK), 0, L.s,
-                           L.b, L.tpb, groups, *L.c);
-      else
-        hipLaunchKernelGGL((fold_deferred_kernel_w5<T, OP, N, U, CH, D, ISSUE, false>), dim3(grid), dim3(EMAC_BLOCK), 0, L.s,
-                           L.b, L.tpb, groups, *L.c);
-    } else if (L.all_full && L.tpb % KB == 0)
+    if (L.all_full && L.tpb % KB == 0)
       hipLaunchKernelGGL((fold_deferred_kernel<T, OP, N, U, CH, D, ISSUE, true>), dim3(grid), dim3(EMAC_BLOCK), 0, L.s, L.b,
                          L.tpb, groups, *L.c);
     else
@@ -943,26 +873,9 @@ int launch_sum(int unroll, const Launch &L) {
     if (unroll == sched(2, 1 | defer(8))) return launch_one<T, OP, N, 2, CH, D, 1 | defer(8)>(L);
     // leaf-major groups: the linear fold and the compile-time chains (CH == 1 took the branch above)
     if (unroll == sched(2, 1 | defer(4) | kLeafMajor)) return launch_one<T, OP, N, 2, CH, D, 1 | defer(4) | kLeafMajor>(L);
-    if constexpr (CH > 1) {  // half the vectors per group: a chain keeps one accumulator per open level
-      if (unroll == sched(2, 1 | defer(2) | kLeafMajor)) return launch_one<T, OP, N, 2, CH, D, 1 | defer(2) | kLeafMajor>(L);
-    }
-    if constexpr (N == 8 && sizeof(T) == 4 && (T)0.5 != 0) {  // EXPERIMENT (float only): source-pipelined leaves
-      if (unroll == sched(2, 1 | defer(4) | kLeafMajor | kLmPipe))
-        return launch_one<T, OP, N, 2, CH, D, 1 | defer(4) | kLeafMajor | kLmPipe>(L);
-      if (unroll == sched(2, 1 | defer(2) | kLeafMajor | kLmPipe))
-        return launch_one<T, OP, N, 2, CH, D, 1 | defer(2) | kLeafMajor | kLmPipe>(L);
-      if (unroll == sched(1, 1 | defer(4) | kLeafMajor | kLmPipe))
-        return launch_one<T, OP, N, 1, CH, D, 1 | defer(4) | kLeafMajor | kLmPipe>(L);
-      if (unroll == sched(2, 1 | defer(4) | kLeafMajor | kLmOcc))
-        return launch_one<T, OP, N, 2, CH, D, 1 | defer(4) | kLeafMajor | kLmOcc>(L);
-      if (unroll == sched(2, 1 | defer(4) | kLeafMajor | kLmViaX))
-        return launch_one<T, OP, N, 2, CH, D, 1 | defer(4) | kLeafMajor | kLmViaX>(L);
-      if (unroll == sched(2, 1 | defer(2) | kLeafMajor | kLmViaX))
-        return launch_one<T, OP, N, 2, CH, D, 1 | defer(2) | kLeafMajor | kLmViaX>(L);
-      if (unroll == sched(2, 1 | defer(4) | kLeafMajor | kLmPipe | kLmInterleave))
-        return launch_one<T, OP, N, 2, CH, D, 1 | defer(4) | kLeafMajor | kLmPipe | kLmInterleave>(L);
-      if (unroll == sched(2, 1 | defer(2) | kLeafMajor | kLmPipe | kLmInterleave))
-        return launch_one<T, OP, N, 2, CH, D, 1 | defer(2) | kLeafMajor | kLmPipe | kLmInterleave>(L);
+    if constexpr (CH > 1) {  // a chain: the opening leaf of each level-0 group copied (kLmOpenCopy)
+      if (unroll == sched(2, 1 | defer(4) | kLeafMajor | kLmOpenCopy))
+        return launch_one<T, OP, N, 2, CH, D, 1 | defer(4) | kLeafMajor | kLmOpenCopy>(L);
     }
     if constexpr (N == 4 || N == 8) {  // the node fan-outs of 4 and 8 ranks: buffer loads, device-scope stores
       if (unroll == sched(4, 5 | kBufLoad)) return launch_one<T, OP, N, 4, CH, D, 5 | kBufLoad>(L);

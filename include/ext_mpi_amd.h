@@ -268,6 +268,10 @@ int ext_mpi_amd_node_shares(int nodes, const int *ports, int ranks_per_node, lon
  * or EXT_MPI_AMD_ERROR_ARG. A node size it does not divide is rejected at init. */
 int ext_mpi_amd_set_num_sockets(int sockets);
 
+/* The NODE form over peer-mapped nodes: the parts its join is pipelined by (1: the serial join;
+ * EXT_MPI_AMD_JOIN_PARTS, engine_join.c), 0 for any other handle, or EXT_MPI_AMD_ERROR_ARG. */
+int ext_mpi_amd_handle_join_parts(int handle);
+
 const char *ext_mpi_amd_version(void);
 /* "sha <commit>[+dirty] src <hash>": the commit and the hash of the product sources (csrc/,
  * include/) this binary was built from (ext_mpi_collectives_amd/_stamp.py). No reference

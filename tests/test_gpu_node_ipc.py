@@ -65,7 +65,7 @@ def _run_nodes(nodes, budget=180, **extra_env):
 
 @pytest.mark.parametrize("nodes", [2, 3, 4, 8])
 def test_node_form_over_peer_mapped_nodes(nodes):
-    """the default join: serial below EMAC_JOIN_MIN_BYTES per rank, pipelined by 4 parts above"""
+    """the default join (serial; the stream-pipelined one is opt-in, engine_join.c join_parts)"""
     _run_nodes(nodes, budget=300 if nodes >= 8 else 180)
 
 

@@ -406,7 +406,8 @@ def test_copy_reduce_headline_instance():
 
 
 DEFER_SHIFT = 11  # fold_kernel.hpp kDeferShift: deferred-store schedules (issue bits 11-12)
-LEAF_MAJOR = 1 << 13  # fold_kernel.hpp kLeafMajor: leaf-major deferred groups (the linear fold)
+LEAF_MAJOR = 1 << 13  # fold_kernel.hpp kLeafMajor: leaf-major deferred groups
+LM_OPEN_COPY = 1 << 16  # fold_kernel.hpp kLmOpenCopy: a chain's opening leaves copied into their accumulators
 
 
 @pytest.mark.parametrize("copyin", ["6;1 -8 8", "6;1 -2 -2 -2 2 2 2"])
@@ -447,9 +448,9 @@ def test_every_tuned_schedule_bitwise(oracle, code, copyin):
         small = chunk * R * sends[0].itemsize < 8 << 20
         assert ((1, 1) in cands) == small, (chunk, cands)
         leaf = (2, 1 | 2 << DEFER_SHIFT | LEAF_MAJOR)  # leaf-major groups: linear fold and compile-time chains
-        half = (2, 1 | 1 << DEFER_SHIFT | LEAF_MAJOR)  # ... and for a chain the half group
+        opencopy = (2, 1 | 2 << DEFER_SHIFT | LEAF_MAJOR | LM_OPEN_COPY)  # ... and for a chain its other form
         assert leaf in cands and (4, 1 | 1 << DEFER_SHIFT) in cands, cands
-        assert (half in cands) == (copyin != "6;1 -8 8"), cands
+        assert (opencopy in cands) == (copyin != "6;1 -8 8"), cands
     # the local fold: one destination, one bucket
     n = 8 * 64000 + 40 if code == emac.FLOAT else 4 * 64000 + 20
     srcs_np = xorshift_inputs(R, n, code, seed_base=0x10CA1)
@@ -473,26 +474,28 @@ def test_every_tuned_schedule_bitwise(oracle, code, copyin):
 
 
 @pytest.mark.parametrize("copyin", ["6;1 -2 -2 -2 2 2 2", "6;1 -4 -2 2 4", "6;1 -2 -4 4 2", "6;1 -8 8", "6;1 -2 -2 2 2"])
-@pytest.mark.parametrize("kb", [4, 2])
+@pytest.mark.parametrize("form", ["plain", "opencopy"])
 @pytest.mark.parametrize("code", [emac.FLOAT, emac.DOUBLE, emac.INT, emac.LONG])
-def test_leaf_major_chains_forced_bitwise(oracle, monkeypatch, code, kb, copyin):
+def test_leaf_major_chains_forced_bitwise(oracle, monkeypatch, code, form, copyin):
     """Leaf-major groups over the compile-time radix chains (round 5, fold_kernel.hpp lm_leaves: one
     accumulator per open level, closed as the leaves complete their groups), forced as the only
     schedule (EXT_MPI_AMD_FOLD_SCHEDULE): every Start bitwise against the oracle's fold order.
     Sizes: whole groups (every bucket a multiple of the group), and a ragged one (partial last tile
     and group: the bounded buffer loads), both above the tuning threshold so the forced word is
-    the handle's schedule; the linear fold's half group has no kernel (the word is skipped there)."""
+    the handle's schedule. Both forms of the chains (the opening leaf of each level-0 group loaded into
+    its accumulator, or copied there: kLmOpenCopy); the linear fold has the first only."""
     R = 4 if copyin == "6;1 -2 -2 2 2" else 8
     tsize = 4 if code in (emac.FLOAT, emac.INT) else 8
-    word = 2 | (1 | (2 if kb == 4 else 1) << DEFER_SHIFT | LEAF_MAJOR) << 4
-    if copyin == "6;1 -8 8" and kb == 2:
-        pytest.skip("the half leaf-major group is instantiated for the chains only")
+    kb = 4
+    word = 2 | (1 | 2 << DEFER_SHIFT | LEAF_MAJOR | (LM_OPEN_COPY if form == "opencopy" else 0)) << 4
+    if copyin == "6;1 -8 8" and form == "opencopy":
+        pytest.skip("the opening-copy form is instantiated for the chains only")
     monkeypatch.setenv("EXT_MPI_AMD_FOLD_SCHEDULE", str(word))
     group = 256 * 2 * kb * 16 // tsize  # elements per group and leaf
     m = max(8, (4 << 20) // (R * group * tsize))  # >= 4 MiB per rank: above the tuning threshold
     for chunk in (m * group, m * group + 3 * group // 4 + 5):  # equal chunks: every bucket the same tiles
         count = R * chunk
-        sends = xorshift_inputs(R, count, code, seed_base=0x1EAF + kb + chunk + 7 * R)
+        sends = xorshift_inputs(R, count, code, seed_base=0x1EAF + len(form) + chunk + 7 * R)
         want = oracle.allreduce(sends, copyin)
         dsend = [_dev(x) for x in sends]
         drecv = [torch.full((count,), -1, dtype=TORCH[code], device="cuda") for _ in range(R)]
