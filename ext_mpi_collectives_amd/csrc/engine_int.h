@@ -208,20 +208,25 @@ typedef struct {
 
 /* The peer-mapped node join pipelined by parts (engine_join.c, round 5; VERDICT r04 missing 2).
    The message is cut into nparts element ranges; part k's copy-in, share fold and pull + copy-out
-   are launches of their own on three streams (the handle's: copy-ins; s_fold; s_pull), and each
-   part has its own synchronisation slot, so its barriers are split: the copy-in stream signals
-   phase 0 of part k and goes on with part k + 1 while the fold stream waits for every node's part
-   k, folds it and signals phase 1, and the pull stream waits for that. The HBM-bound copy-in of
-   part k + 1 then runs beside the link-bound share fold of part k and pull of part k - 1 instead of
-   before them. Opt-in (EXT_MPI_AMD_JOIN_PARTS=k): on one MI355X each part's dependent launches and
-   cross-stream waits cost more than the overlap gains (engine_join.c join_parts). */
-#define EMAC_JOIN_PARTS 8
+   each have their own launch layout and part k its own synchronisation slot. Two executions:
+   * fused (the default form of EXT_MPI_AMD_JOIN_PARTS > 1; join_fused.hip): ONE launch per Start
+     whose workgroups walk the parts' segments in a skewed order, the dependencies being the
+     slots' flags -- the copy-in of part k + 1 runs beside the share fold of part k and the pull of
+     part k - 1;
+   * streams (EXT_MPI_AMD_JOIN=streams): part k's launches on three streams (the handle's: copy-ins;
+     s_fold; s_pull) with split barriers and events -- kept for A/B: on one MI355X each part's
+     dependent launches and cross-stream waits cost more than the overlap gains.
+   EXT_MPI_AMD_JOIN_PARTS=1 keeps the serial join (one slot, one stream). */
+#define EMAC_JOIN_PARTS EMAC_JOIN_PARTS_MAX
 typedef struct {
   int nparts;
+  int fused; /* one launch per Start (join_fused.hip), else the streams form */
+  int grid;  /* the fused launch's workgroups */
   long lo[EMAC_JOIN_PARTS + 1]; /* part k: message elements [lo[k], lo[k + 1]) */
   int slot[EMAC_JOIN_PARTS];
   unsigned long epoch[EMAC_JOIN_PARTS][2];
   emac_launch in[EMAC_JOIN_PARTS], fold[EMAC_JOIN_PARTS], pull[EMAC_JOIN_PARTS];
+  void *ctl; /* fused: its emac_join_ctl (device memory, zeroed between Starts) */
   void *s_fold, *s_pull;
   void *ev_in[EMAC_JOIN_PARTS], *ev_fold[EMAC_JOIN_PARTS], *ev_done;
 } emac_join;

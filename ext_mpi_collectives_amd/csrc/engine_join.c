@@ -90,10 +90,7 @@ static int place_part(emac_bucket *b, const jproto *p, int n, long lo, long hi, 
   return nb;
 }
 
-/* the parts of the pipelined join: EXT_MPI_AMD_JOIN_PARTS, else 1 (the serial join). Opt-in: on one
-   MI355X every part added 30-110 us of dependent launches and cross-stream waits to a Start (N = 1:
-   legs 37.8 -> 164.7 us at 4 parts; N = 2 processes sharing the GPU: 127 -> 453 us,
-   profiles/r05/join/), far above the overlap it can buy at 16 MiB per rank */
+/* the parts of the pipelined join: EXT_MPI_AMD_JOIN_PARTS, else 1 (the serial join) */
 static int join_parts(const emac_handle *h, int nodes) {
   const char *e = getenv("EXT_MPI_AMD_JOIN_PARTS");
   int n = 1;
@@ -101,6 +98,30 @@ static int join_parts(const emac_handle *h, int nodes) {
   (void)nodes;
   if (e && *e) n = atoi(e);
   return n < 1 ? 1 : n > EMAC_JOIN_PARTS ? EMAC_JOIN_PARTS : n;
+}
+
+/* the fused form unless EXT_MPI_AMD_JOIN=streams (the same on every rank: same environment) */
+static int join_fused_wanted(void) {
+  const char *e = getenv("EXT_MPI_AMD_JOIN");
+  return !(e && !strcmp(e, "streams"));
+}
+
+/* a launch of nb buckets of nsrc leaves with the tiles of schedule `unroll` (the fused join's
+   segments: the kernel's own U per stage) */
+static int upload_forced(emac_launch *L, emac_bucket *b, int nb, int nsrc, int unroll) {
+  emac_edge *edges = NULL;
+  int rc;
+  memset(L, 0, sizeof(*L));
+  if ((rc = emac_layout_as(b, nb, EMAC_SUM, nsrc, 0, 0, unroll, &edges, &L->nedges, &L->ntiles, &L->tiles_per_bucket,
+                           &L->all_full, &L->unroll)))
+    return rc;
+  L->nb = nb;
+  if (nb && (rc = emac_gpu_malloc((void **)&L->d_buckets, sizeof(emac_bucket) * (size_t)nb)) == 0)
+    rc = emac_gpu_memcpy(L->d_buckets, b, sizeof(emac_bucket) * (size_t)nb);
+  if (!rc && L->nedges && (rc = emac_gpu_malloc((void **)&L->d_edges, sizeof(emac_edge) * (size_t)L->nedges)) == 0)
+    rc = emac_gpu_memcpy(L->d_edges, edges, sizeof(emac_edge) * (size_t)L->nedges);
+  free(edges);
+  return rc;
 }
 
 /* first element of part k of n over count elements: equal parts cut at 1024-element multiples (the
@@ -193,7 +214,17 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
   if ((rc = ipc_agree(cm, rc == 0))) return rc;
   /* the pipelined join (EXT_MPI_AMD_JOIN_PARTS, emac_join): the same part count on every rank (the
      message size and the environment are the same), one slot per part */
+  /* the share fold's tree: the halving flow folds log2 N levels of pairs, one step over every node a
+     left fold */
+  if ((rc = node_fold_codes(N, N > 1 && emac_node_single(&h->ns) == 2 ? h->ns.nsteps : 1, h->plan.dtype, &h->xcodes)))
+    return rc; /* (a function of the shape alone: the same on every rank) */
   nparts = join_parts(h, N);
+  /* a shape the fused join has no kernel for (leaf counts other than 1, 2, 4, 8, MIN / MAX,
+     irregular fold trees) keeps the serial join -- the same verdict on every rank (same shape) */
+  if (nparts > 1 && join_fused_wanted() &&
+      (h->plan.op != EMAC_SUM || emac_gpu_join_fused(h->plan.dtype, R, &h->plan.codes, &h->xcodes, nparts, 3, NULL, NULL, NULL,
+                                                     NULL, NULL, NULL, N, cm->rank, NULL, 0, NULL, 0, NULL)))
+    nparts = 1;
   for (k = 0, slot = 0; k < nparts; k++, slot++) { /* the lowest slots free on every rank */
     for (; slot < EMAC_SYNC_SLOTS; slot++) {
       for (r = 0; r < N && (all[r].free_slots[slot >> 3] >> (slot & 7)) & 1; r++);
@@ -205,6 +236,7 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
   if (nparts > 1) {
     if (!(h->join = (emac_join *)calloc(1, sizeof(emac_join)))) return EMAC_ERR_MALLOC; /* (all ranks: see above) */
     h->join->nparts = nparts;
+    h->join->fused = join_fused_wanted();
     for (k = 0; k < nparts; k++) {
       h->join->slot[k] = pslot[k];
       cm->slot_used[pslot[k]] = 1;
@@ -242,8 +274,6 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
     }
   }
   for (me = 0, k = 0; me < R; me++) k += nsh[me];
-  if (!rc) /* the halving flow folds log2 N levels of pairs, one step over every node a left fold */
-    rc = node_fold_codes(N, N > 1 && emac_node_single(&h->ns) == 2 ? h->ns.nsteps : 1, h->plan.dtype, &h->xcodes);
   if (!rc && (!(pin = (jproto *)calloc((size_t)h->plan.npieces * R + 1, sizeof(jproto))) ||
               !(psh = (jproto *)calloc((size_t)k + 1, sizeof(jproto))) || !(ppl = (jproto *)calloc((size_t)k + 1, sizeof(jproto))) ||
               !(b = (emac_bucket *)calloc((size_t)(k + h->plan.npieces * R) + 1, sizeof(emac_bucket)))))
@@ -304,6 +334,22 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
     if (!rc) rc = upload_buckets(h, b, place_part(b, pin, nin, 0, h->plan.count, ts)); /* tuned */
     if (!rc) rc = upload_launch_fan(h, &h->xfold[0], b, place_part(b, psh, nshr, 0, h->plan.count, ts), N, 2);
     if (!rc) rc = upload_launch_fan(h, &h->pull, b, place_part(b, ppl, npl, 0, h->plan.count, ts), 1, 2);
+  } else if (h->join->fused) { /* part k: the buckets' elements inside [lo[k], lo[k + 1]), one launch */
+    emac_join *J = h->join;
+    emac_join_ctl zero;
+    memset(&zero, 0, sizeof(zero));
+    for (k = 0; k <= J->nparts; k++) J->lo[k] = join_cut(h->plan.count, J->nparts, k);
+    for (k = 0; !rc && k < J->nparts; k++) {
+      if (!rc) rc = upload_forced(&J->in[k], b, place_part(b, pin, nin, J->lo[k], J->lo[k + 1], ts), R, 2 | 1 << 4);
+      if (!rc) rc = upload_forced(&J->fold[k], b, place_part(b, psh, nshr, J->lo[k], J->lo[k + 1], ts), N, 1 | 1 << 4);
+      if (!rc) rc = upload_forced(&J->pull[k], b, place_part(b, ppl, npl, J->lo[k], J->lo[k + 1], ts), 1, 2 | 1 << 4);
+    }
+    if (!rc && (rc = emac_gpu_malloc(&J->ctl, sizeof(emac_join_ctl))) == 0) rc = emac_gpu_memcpy(J->ctl, &zero, sizeof(zero));
+    if (!rc) {
+      /* at most what the GPU holds at once; ranks sharing this GPU (the rehearsal) divide it */
+      const int cap = emac_gpu_join_grid() / (cm->cross_device || N < 2 ? 1 : N);
+      J->grid = cap < 1 ? 1 : cap > 1024 ? 1024 : cap;
+    }
   } else { /* part k: the buckets' elements inside [lo[k], lo[k + 1]) */
     emac_join *J = h->join;
     for (k = 0; k <= J->nparts; k++) J->lo[k] = join_cut(h->plan.count, J->nparts, k);
@@ -541,6 +587,29 @@ int join_start(emac_handle *h, int copyin, int legs) {
   emac_join *J = h->join;
   const int N = cm->size;
   int k, rc;
+  if (J->fused) {
+    emac_join_seg seg[3 * EMAC_JOIN_PARTS_MAX];
+    unsigned long e0[EMAC_JOIN_PARTS_MAX], e1[EMAC_JOIN_PARTS_MAX];
+    memset(seg, 0, sizeof(seg));
+    for (k = 0; k < J->nparts; k++) {
+      const emac_launch *st[3] = {&J->in[k], &J->fold[k], &J->pull[k]};
+      int i;
+      for (i = 0; i < 3; i++)
+        seg[i * EMAC_JOIN_PARTS_MAX + k] = (emac_join_seg){st[i]->d_buckets, st[i]->nb, st[i]->ntiles, st[i]->tiles_per_bucket,
+                                                           st[i]->all_full, st[i]->d_edges, st[i]->nedges};
+      if (legs) { /* the epochs advance with the node legs only (the copy-ins alone signal nothing) */
+        e0[k] = ++J->epoch[k][0];
+        e1[k] = ++J->epoch[k][1];
+      } else {
+        e0[k] = J->epoch[k][0];
+        e1[k] = J->epoch[k][1];
+      }
+    }
+    h->tune.ops++;
+    return emac_gpu_join_fused(h->plan.dtype, h->nsrc, &h->plan.codes, &h->xcodes, J->nparts, (copyin ? 1 : 0) | (legs ? 2 : 0),
+                               seg, J->slot, e0, e1, cm->sync, (void *const *)cm->d_peer_sync, N, cm->rank,
+                               cm->err + J->slot[0], cm->timeout_ticks, J->ctl, J->grid, h->stream);
+  }
   for (k = 0; k < J->nparts; k++) {
     const emac_launch *I = &J->in[k], *X = &J->fold[k], *P = &J->pull[k];
     const int slot = J->slot[k];
@@ -605,6 +674,7 @@ void join_free(emac_handle *h) {
     }
   }
   emac_gpu_event_destroy(J->ev_done);
+  emac_gpu_free(J->ctl);
   if (J->s_fold) emac_gpu_stream_destroy(J->s_fold);
   if (J->s_pull) emac_gpu_stream_destroy(J->s_pull);
   free(J);

@@ -77,6 +77,10 @@ constexpr int kDevStreaming = 18;  // sc1 | nt
 // or 8 leaves (47.1-47.8 against 47.9 us for its kept LDS groups at 8 x 32 MiB, three passes,
 // profiles/r04/bufload/local_*.json) (engine_tune.c).
 constexpr int kBufLoad = 1 << 15;
+// ISSUE bit 17: stores system-coherent write-through (cache policy sc0 sc1), loads as the other bits
+// say: the fused node join's copy-in (join_fused.hip), whose partial is read by peers and by other
+// XCDs inside the same launch, after a flag rather than a kernel boundary.
+constexpr int kSysStore = 1 << 17;
 constexpr int kStreaming = 2;  // nt
 typedef unsigned int U32x4 __attribute__((ext_vector_type(4)));
 
@@ -274,7 +278,7 @@ __device__ __forceinline__ void load_fold(const emac_bucket *b, long tile_base, 
 // One 16-byte vector stored under the launch's store policy.
 template <typename V, int ISSUE>
 __device__ __forceinline__ void store_vec(__attribute__((address_space(1))) V *dst, unsigned v, V r) {
-  if constexpr ((ISSUE & kRemote) != 0)
+  if constexpr ((ISSUE & (kRemote | kSysStore)) != 0)
     sys_store16<V>((void *)dst, v * 16u, r);
   else if constexpr ((ISSUE & kDevStore) != 0)
     dev_store16<V>((void *)dst, v * 16u, r);
@@ -678,6 +682,8 @@ __global__ __launch_bounds__(EMAC_BLOCK) void fold_edge_kernel(const emac_bucket
 
 // A set of buckets of one launch as kernel arguments (the fused kernel runs two: the fold of
 // this rank's owner chunks and the pull of every other owner's result).
+typedef emac_join_ctl JoinCtl;
+
 struct Work {
   const emac_bucket *b;
   int nb;

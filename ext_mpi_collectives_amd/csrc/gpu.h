@@ -123,6 +123,31 @@ int emac_gpu_event_create_release(void **ev);
 /* node barrier `phase` of the Start tagged `tag` (its phase-1 epoch) on `stream`: one wave */
 int emac_gpu_node_barrier(void *self, void *const *d_peers, int slot, int phase, unsigned long epoch, unsigned long tag,
                           int nranks, int me, int *err, long timeout_ticks, void *stream);
+/* The peer-mapped node join pipelined by parts in one launch per Start (join_fused.hip): per part
+   the copy-in, share-fold and pull segments (stage * EMAC_JOIN_PARTS_MAX + part), each part's
+   synchronisation slot and this Start's epochs for it; `ctl` a zeroed emac_join_ctl in device
+   memory (the kernel leaves it zeroed). mode: 1 the copy-ins, 2 the node legs (barriers, share
+   folds, pulls), 3 both. segs NULL: whether the shape has a kernel (0) or not. */
+#define EMAC_JOIN_PARTS_MAX 8
+typedef struct {
+  unsigned ci[EMAC_JOIN_PARTS_MAX], sf[EMAC_JOIN_PARTS_MAX];           /* workgroups through a part's segment */
+  unsigned failed0[EMAC_JOIN_PARTS_MAX], failed1[EMAC_JOIN_PARTS_MAX]; /* a part's barrier failed */
+  unsigned out;                                                        /* workgroups done */
+} emac_join_ctl;
+typedef struct {
+  const emac_bucket *d_buckets;
+  int nb;
+  long ntiles, tiles_per_bucket;
+  int all_full;
+  const emac_edge *d_edges;
+  int nedges;
+} emac_join_seg;
+int emac_gpu_join_fused(int dtype, int nsrc, const emac_codes *codes, const emac_codes *xcodes, int nparts, int mode,
+                        const emac_join_seg *segs, const int *slots, const unsigned long *e0, const unsigned long *e1,
+                        void *self_sync, void *const *d_peers, int nranks, int me, int *err, long timeout_ticks, void *ctl,
+                        int grid, void *stream);
+int emac_gpu_join_grid(void); /* workgroups of the join kernel the GPU holds at once */
+
 /* the two halves of a node barrier (the pipelined node join, engine_join.c), one wave each: signal
    phase `phase` with `epoch` to every peer; wait for every peer's signal (phase 0: and leave the
    verdict in go[slot] for the fold launch behind it, marking the Start abandoned in the peers'

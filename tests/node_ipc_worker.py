@@ -135,6 +135,7 @@ def main():
                 sbufs.append(s.data_ptr())
                 rbufs.append(r.data_ptr())
         h = emac.node_comm_allreduce_init(sbufs, rbufs, count, code, comm, copyin, op=op)
+        parts = emac.handle_join_parts(h)
         ok = True
         for rep in range(repeats):
             sends = xorshift_inputs(W, count, code, seed_base=0x40DE0000 + 977 * k + 31 * rep)
@@ -165,7 +166,7 @@ def main():
         emac.done(h)
         failures += not ok
         print(f"NODEIPC node {node}/{N} case {k} code {code} op {op} count {count} R {R} '{copyin}' ports {ports} "
-              f"in_place={in_place} host={host} x{repeats}: {'ok' if ok else 'MISMATCH'}", flush=True)
+              f"in_place={in_place} host={host} x{repeats} join parts {parts}: {'ok' if ok else 'MISMATCH'}", flush=True)
     for k, (code, count, R, copyin, ports, op) in enumerate(unsupported(N)):
         emac.comm_set_nodes(comm, N if ports is not None else 1, ports)
         bufs = [torch.zeros(count, dtype=TORCH[code], device="cuda") for _ in range(2 * R)]

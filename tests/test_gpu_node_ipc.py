@@ -69,10 +69,15 @@ def test_node_form_over_peer_mapped_nodes(nodes):
     _run_nodes(nodes, budget=300 if nodes >= 8 else 180)
 
 
-@pytest.mark.parametrize("parts", ["1", "3"])
+@pytest.mark.parametrize("join", ["serial", "fused3", "fused4", "streams3"])
 @pytest.mark.parametrize("nodes", [2, 3, 4, 8])
-def test_node_join_serial_and_pipelined(nodes, parts):
-    """every case with the join forced serial (EXT_MPI_AMD_JOIN_PARTS=1) or pipelined by 3 parts at
-    every size (parts of no element, buckets cut inside their tiles), plus the timeout recovery of a
-    late node over every part's slot"""
-    _run_nodes(nodes, budget=300 if nodes >= 8 else 180, EXT_MPI_AMD_JOIN_PARTS=parts, NODEIPC_RECOVERY="1")
+def test_node_join_serial_and_pipelined(nodes, join):
+    """every case with the join serial (EXT_MPI_AMD_JOIN_PARTS=1) or pipelined by 3 or 4 parts at
+    every size (parts of no element, buckets cut inside their tiles) -- in one launch per Start
+    (join_fused.hip; shapes it has no kernel for fall back to the serial join) or on three streams
+    (EXT_MPI_AMD_JOIN=streams) -- plus the timeout recovery of a late node over every part's slot"""
+    parts = "1" if join == "serial" else join[-1]
+    env = dict(EXT_MPI_AMD_JOIN_PARTS=parts, NODEIPC_RECOVERY="1")
+    if join.startswith("streams"):
+        env["EXT_MPI_AMD_JOIN"] = "streams"
+    _run_nodes(nodes, budget=300 if nodes >= 8 else 180, **env)
