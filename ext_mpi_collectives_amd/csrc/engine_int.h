@@ -209,7 +209,7 @@ typedef struct {
 /* The peer-mapped node join pipelined by parts (engine_join.c, round 5; VERDICT r04 missing 2).
    The message is cut into nparts element ranges; part k's copy-in, share fold and pull + copy-out
    each have their own launch layout and part k its own synchronisation slot. Two executions:
-   * fused (the default form of EXT_MPI_AMD_JOIN_PARTS > 1; join_fused.hip): ONE launch per Start
+   * fused (the default, 2 parts from EMAC_JOIN_MIN_BYTES per rank; join_fused.hip): ONE launch per Start
      whose workgroups walk the parts' segments in a skewed order, the dependencies being the
      slots' flags -- the copy-in of part k + 1 runs beside the share fold of part k and the pull of
      part k - 1;
@@ -218,6 +218,7 @@ typedef struct {
      dependent launches and cross-stream waits cost more than the overlap gains.
    EXT_MPI_AMD_JOIN_PARTS=1 keeps the serial join (one slot, one stream). */
 #define EMAC_JOIN_PARTS EMAC_JOIN_PARTS_MAX
+#define EMAC_JOIN_MIN_BYTES (1L << 20) /* per rank: the pipelined join by default from here */
 typedef struct {
   int nparts;
   int fused; /* one launch per Start (join_fused.hip), else the streams form */

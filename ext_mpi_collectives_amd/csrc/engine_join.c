@@ -90,12 +90,13 @@ static int place_part(emac_bucket *b, const jproto *p, int n, long lo, long hi, 
   return nb;
 }
 
-/* the parts of the pipelined join: EXT_MPI_AMD_JOIN_PARTS, else 1 (the serial join) */
+/* the parts of the pipelined join: EXT_MPI_AMD_JOIN_PARTS (1: the serial join), else 2 over several
+   nodes from EMAC_JOIN_MIN_BYTES per rank. With nodes sharing one MI355X (16 MiB per rank, 8 ranks
+   per node) the fused join with 2 parts took 150.7 against 187.6 us per Start at 2 nodes and 274.8
+   against 389.6 at 4; 4 parts were no faster (profiles/r05/join/) */
 static int join_parts(const emac_handle *h, int nodes) {
   const char *e = getenv("EXT_MPI_AMD_JOIN_PARTS");
-  int n = 1;
-  (void)h;
-  (void)nodes;
+  int n = nodes > 1 && (long)h->bytes >= EMAC_JOIN_MIN_BYTES ? 2 : 1;
   if (e && *e) n = atoi(e);
   return n < 1 ? 1 : n > EMAC_JOIN_PARTS ? EMAC_JOIN_PARTS : n;
 }
@@ -340,15 +341,18 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
     memset(&zero, 0, sizeof(zero));
     for (k = 0; k <= J->nparts; k++) J->lo[k] = join_cut(h->plan.count, J->nparts, k);
     for (k = 0; !rc && k < J->nparts; k++) {
-      if (!rc) rc = upload_forced(&J->in[k], b, place_part(b, pin, nin, J->lo[k], J->lo[k + 1], ts), R, 2 | 1 << 4);
-      if (!rc) rc = upload_forced(&J->fold[k], b, place_part(b, psh, nshr, J->lo[k], J->lo[k + 1], ts), N, 1 | 1 << 4);
-      if (!rc) rc = upload_forced(&J->pull[k], b, place_part(b, ppl, npl, J->lo[k], J->lo[k + 1], ts), 1, 2 | 1 << 4);
+      /* the kernel's tiles (join_fused.hip: 1024-lane workgroups): 2 vectors per lane for the copy-in
+         and the pull, 1 for the share fold -- in layout units of EMAC_BLOCK lanes, U 8 and 4 */
+      if (!rc) rc = upload_forced(&J->in[k], b, place_part(b, pin, nin, J->lo[k], J->lo[k + 1], ts), R, 8 | 1 << 4);
+      if (!rc) rc = upload_forced(&J->fold[k], b, place_part(b, psh, nshr, J->lo[k], J->lo[k + 1], ts), N, 4 | 1 << 4);
+      if (!rc) rc = upload_forced(&J->pull[k], b, place_part(b, ppl, npl, J->lo[k], J->lo[k + 1], ts), 1, 8 | 1 << 4);
     }
     if (!rc && (rc = emac_gpu_malloc(&J->ctl, sizeof(emac_join_ctl))) == 0) rc = emac_gpu_memcpy(J->ctl, &zero, sizeof(zero));
     if (!rc) {
-      /* at most what the GPU holds at once; ranks sharing this GPU (the rehearsal) divide it */
-      const int cap = emac_gpu_join_grid() / (cm->cross_device || N < 2 ? 1 : N);
-      J->grid = cap < 1 ? 1 : cap > 1024 ? 1024 : cap;
+      /* join_fused.hip: one 1024-lane workgroup per CU; nodes sharing this GPU (the 1-GPU rehearsal)
+         divide it, so every node's workgroups find room beside the others' waiting ones */
+      const int g = emac_gpu_join_grid() / (cm->cross_device || N < 2 ? 1 : N);
+      J->grid = g < 8 ? 8 : g > 4096 ? 4096 : g;
     }
   } else { /* part k: the buckets' elements inside [lo[k], lo[k + 1]) */
     emac_join *J = h->join;
@@ -606,7 +610,10 @@ int join_start(emac_handle *h, int copyin, int legs) {
       }
     }
     h->tune.ops++;
-    return emac_gpu_join_fused(h->plan.dtype, h->nsrc, &h->plan.codes, &h->xcodes, J->nparts, (copyin ? 1 : 0) | (legs ? 2 : 0),
+    const char *e = getenv("EXT_MPI_AMD_JOIN_SYSSTORE"); /* A/B: 1 system-scope partial stores on one GPU too */
+    const int dev_scope = !cm->cross_device && !(e && atoi(e) > 0);
+    return emac_gpu_join_fused(h->plan.dtype, h->nsrc, &h->plan.codes, &h->xcodes, J->nparts,
+                               (copyin ? 1 : 0) | (legs ? 2 : 0) | (dev_scope ? 4 : 0),
                                seg, J->slot, e0, e1, cm->sync, (void *const *)cm->d_peer_sync, N, cm->rank,
                                cm->err + J->slot[0], cm->timeout_ticks, J->ctl, J->grid, h->stream);
   }

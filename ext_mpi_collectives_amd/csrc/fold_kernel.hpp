@@ -239,7 +239,9 @@ __device__ __forceinline__ void fold_scalar_element(const emac_bucket *b, long e
 // (every vector of leaf 0, then leaf 1, ...) instead of vector-major; bits 1.. = s_sleep after
 // every 4 loads (0 = back-to-back burst).
 // Loads and folds one tile: r[u] = the fold of every leaf's vector u of the tile.
-template <typename T, int OP, int N, int U, int CH, bool FULL, int ISSUE>
+// BS: the workgroup's lanes (a tile is BS * U vectors; EMAC_BLOCK but for the fused node join's
+// 1024-lane workgroups, join_fused.hip)
+template <typename T, int OP, int N, int U, int CH, bool FULL, int ISSUE, int BS = EMAC_BLOCK>
 __device__ __forceinline__ void load_fold(const emac_bucket *b, long tile_base, long nvec, const emac_codes &c,
                                           typename Lane<T>::V (&r)[U]) {
   typedef typename Lane<T>::V V;
@@ -257,7 +259,7 @@ __device__ __forceinline__ void load_fold(const emac_bucket *b, long tile_base, 
 #pragma unroll
   for (int k = 0; k < N * U; ++k) {
     const int s = SRC_MAJOR ? k / U : k % N, u = SRC_MAJOR ? k % U : k / N;
-    const unsigned v = threadIdx.x + (unsigned)(u * EMAC_BLOCK);
+    const unsigned v = threadIdx.x + (unsigned)(u * BS);
     if constexpr (REMOTE) {
       if (FULL || (long)v < left) x[u][s] = sys_load16<V>((const void *)src[s], v * 16u);
     } else if constexpr ((ISSUE & kPlainLoad) != 0) {
@@ -288,7 +290,7 @@ __device__ __forceinline__ void store_vec(__attribute__((address_space(1))) V *d
     __builtin_nontemporal_store(r, dst + v);
 }
 
-template <typename T, int OP, int N, int U, int CH, int D, bool FULL, int ISSUE = 1>
+template <typename T, int OP, int N, int U, int CH, int D, bool FULL, int ISSUE = 1, int BS = EMAC_BLOCK>
 __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_base, long nvec, const emac_codes &c,
                                              bool store = true) {
   typedef typename Lane<T>::V V;
@@ -296,7 +298,7 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
   constexpr bool REMOTE = ISSUE & kRemote;
   const long left = nvec - tile_base;
   V r[U];
-  load_fold<T, OP, N, U, CH, FULL, ISSUE>(b, tile_base, nvec, c, r);
+  load_fold<T, OP, N, U, CH, FULL, ISSUE, BS>(b, tile_base, nvec, c, r);
   // destination pointers are only needed now: their descriptor read overlaps the loads
   if (!store) return;  // peer-mapped launch whose phase-0 barrier failed (wave-uniform)
 #pragma unroll
@@ -304,7 +306,7 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
     GV *dst = (GV *)b->dst[d] + tile_base;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const unsigned v = threadIdx.x + (unsigned)(u * EMAC_BLOCK);
+      const unsigned v = threadIdx.x + (unsigned)(u * BS);
       if (FULL || (long)v < left) store_vec<V, ISSUE>(dst, v, r[u]);
     }
   }

@@ -127,10 +127,13 @@ int emac_gpu_node_barrier(void *self, void *const *d_peers, int slot, int phase,
    the copy-in, share-fold and pull segments (stage * EMAC_JOIN_PARTS_MAX + part), each part's
    synchronisation slot and this Start's epochs for it; `ctl` a zeroed emac_join_ctl in device
    memory (the kernel leaves it zeroed). mode: 1 the copy-ins, 2 the node legs (barriers, share
-   folds, pulls), 3 both. segs NULL: whether the shape has a kernel (0) or not. */
+   folds, pulls), 3 both; | 4 when every node runs on this GPU (device-scope write-through of the
+   partial instead of system scope). segs NULL: whether the shape has a kernel (0) or not. */
 #define EMAC_JOIN_PARTS_MAX 8
 typedef struct {
-  unsigned ci[EMAC_JOIN_PARTS_MAX], sf[EMAC_JOIN_PARTS_MAX];           /* workgroups through a part's segment */
+  unsigned tk[3][EMAC_JOIN_PARTS_MAX];   /* per segment (stage, part): the next unclaimed item */
+  unsigned done[3][EMAC_JOIN_PARTS_MAX]; /* ... items finished */
+  unsigned sig[3][EMAC_JOIN_PARTS_MAX];  /* ... its completion signalled */
   unsigned failed0[EMAC_JOIN_PARTS_MAX], failed1[EMAC_JOIN_PARTS_MAX]; /* a part's barrier failed */
   unsigned out;                                                        /* workgroups done */
 } emac_join_ctl;
@@ -146,7 +149,7 @@ int emac_gpu_join_fused(int dtype, int nsrc, const emac_codes *codes, const emac
                         const emac_join_seg *segs, const int *slots, const unsigned long *e0, const unsigned long *e1,
                         void *self_sync, void *const *d_peers, int nranks, int me, int *err, long timeout_ticks, void *ctl,
                         int grid, void *stream);
-int emac_gpu_join_grid(void); /* workgroups of the join kernel the GPU holds at once */
+int emac_gpu_join_grid(void); /* workgroups of the fused join's launch (one per CU) */
 
 /* the two halves of a node barrier (the pipelined node join, engine_join.c), one wave each: signal
    phase `phase` with `epoch` to every peer; wait for every peer's signal (phase 0: and leave the

@@ -9,26 +9,27 @@
 //    SF[k]  the fold of this node's share of every chunk over the N nodes' partials (peer loads),
 //    PL[k]  the pull of every node's share into the R receive buffers (peer loads + local stores),
 // in the skewed order CI[0], CI[1], SF[0], CI[2], SF[1], PL[0], ... : every workgroup walks the
-// segments in that order, grid-striding over each one's tiles, so while some workgroups still fold
+// segments in that order, claiming each one's tiles in chunks, so while some workgroups still fold
 // part k + 1's copy-in (HBM-bound) others fold part k's share and pull part k - 1 (link-bound) --
 // what the stream-pipelined join could not do on one MI355X, whose per-part dependent launches and
 // cross-stream waits cost 30-110 us each (profiles/r05/join/).
 // Dependencies are flags, not launch boundaries:
-//  * a workgroup that has finished its tiles of CI[k] drains its stores and counts itself in
-//    ctl->ci[k]; the last one signals phase 0 of part k's slot to every node, itself included
-//    (ipc_sync.hpp flags: uncached memory, system-scope atomics);
+//  * a workgroup that has finished its items of CI[k] drains its stores and counts them in
+//    ctl->done; the one that completes the count signals phase 0 of part k's slot to every node,
+//    itself included (ipc_sync.hpp flags: uncached memory, system-scope atomics);
 //  * SF[k] waits (one wave per workgroup) for every node's phase 0 of part k; PL[k] for phase 1,
 //    which the last workgroup through SF[k] signals the same way;
 //  * the copy-in's partial stores are system-coherent write-through (cache policy sc0 sc1), so a
 //    peer -- or a workgroup on another XCD of this GPU -- reading the partial after the flag sees
 //    it in memory, not in some XCD's L2; the share fold and the pull load with the same policy.
-// No workgroup waits for a tile another workgroup has not started: the grid is at most what the
-// GPU holds at once (host side), every workgroup folds its copy-in tiles before it waits, and every
-// wait is bounded by the communicator's timeout. A part whose phase-0 wait times out is marked
+// No workgroup waits for an item a workgroup that has not started holds: items are claimed from a
+// counter by running workgroups only (join_seg), and every wait is bounded by the communicator's
+// timeout. A part whose phase-0 wait times out is marked
 // abandoned in the peers' blocks and its share is not stored; a phase-1 timeout skips the pull's
 // stores; both are reported through the slot's error word, as the serial join's barriers do, and
 // the next Start synchronises normally (epochs keep counting). The last workgroup out resets the
 // control block for the next Start (stream order).
+#include <stdlib.h>
 #include <string.h>
 
 #include <type_traits>
@@ -36,6 +37,12 @@
 #include "fold_kernel.hpp"
 
 namespace emac {
+
+// 1024-lane workgroups, one per CU: 16 waves per CU without more workgroups contending for the
+// segments' counters (each one claims and counts on them; 4x the workgroups of 256 lanes cost 40-170
+// us more per Start at 512-2048 workgroups, profiles/r05/join/). A tile is JB * U vectors: the
+// layouts are made with U * JB / EMAC_BLOCK (engine_join.c).
+constexpr int JB = 1024;
 
 struct JoinSegs {
   Work w[3][EMAC_JOIN_PARTS_MAX];  // [CI, SF, PL][part]
@@ -48,14 +55,14 @@ __device__ __forceinline__ bool join_wait(NodeSync &ns, int phase, unsigned long
   return wave_wait(ns, phase, epoch, true);
 }
 
-// grid-stride over the tiles and edge items of one segment; N leaves (N = 0: runtime nrt), D
-// destinations, ISSUE the load / store policy
+// one item of a segment: tile `i` (i < ntiles) or edge item i - ntiles; N leaves (N = 0: runtime
+// nrt), D destinations, ISSUE the load / store policy
 template <typename T, int N, int U, int CH, int D, int ISSUE>
-__device__ __forceinline__ void join_run(const Work &w, const emac_codes &codes, int nrt, bool store) {
-  constexpr long TILE = (long)EMAC_BLOCK * U;
+__device__ __forceinline__ void join_item(const Work &w, long i, const emac_codes &codes, int nrt, bool store) {
+  constexpr long TILE = (long)JB * U;
   constexpr long EPV = 16 / sizeof(typename Lane<T>::S);
-  constexpr bool REMOTE = (ISSUE & kRemote) != 0;
-  for (long tile = blockIdx.x; tile < w.ntiles; tile += gridDim.x) {
+  if (i < w.ntiles) {
+    const long tile = i;
     int bi;
     long t;
     if (w.tpb > 0) {
@@ -81,39 +88,66 @@ __device__ __forceinline__ void join_run(const Work &w, const emac_codes &codes,
         fold_vectors_rt<T, EMAC_SUM, 1, false, true>(b, t * TILE, b->nvec, codes, nrt, store);
     } else {
       if (w.all_full || (t + 1) * TILE <= b->nvec)
-        fold_vectors<T, EMAC_SUM, N, U, CH, D, true, ISSUE>(b, t * TILE, 0, codes, store);
+        fold_vectors<T, EMAC_SUM, N, U, CH, D, true, ISSUE, JB>(b, t * TILE, 0, codes, store);
       else
-        fold_vectors<T, EMAC_SUM, N, U, CH, D, false, ISSUE>(b, t * TILE, b->nvec, codes, store);
+        fold_vectors<T, EMAC_SUM, N, U, CH, D, false, ISSUE, JB>(b, t * TILE, b->nvec, codes, store);
     }
+    return;
   }
-  for (int item = blockIdx.x; item < w.nedges; item += gridDim.x) {
-    const emac_edge it = w.edges[item];
-    const emac_bucket *b = w.b + it.bucket;
-    auto one = [&](long e) {
-      if (!store) return;
-      if constexpr (N == 0)
-        fold_scalar_rt<T, EMAC_SUM, 1, true>(b, e, codes, nrt);
-      else
-        fold_scalar_element<T, EMAC_SUM, N, CH, D, true>(b, e, codes);
-    };
-    if (it.mode == 1) {
-      for (long e = it.start + threadIdx.x; e < it.start + it.count; e += EMAC_BLOCK) one(e);
-    } else {
-      const long nsc = b->head + b->tail;
-      for (long i = threadIdx.x; i < nsc; i += EMAC_BLOCK) one(i < b->head ? i : b->head + b->nvec * EPV + (i - b->head));
-    }
+  if (!store) return;
+  const emac_edge it = w.edges[i - w.ntiles];
+  const emac_bucket *b = w.b + it.bucket;
+  auto one = [&](long e) {
+    if constexpr (N == 0)
+      fold_scalar_rt<T, EMAC_SUM, 1, true>(b, e, codes, nrt);
+    else
+      fold_scalar_element<T, EMAC_SUM, N, CH, D, true>(b, e, codes);
+  };
+  if (it.mode == 1) {
+    for (long e = it.start + threadIdx.x; e < it.start + it.count; e += JB) one(e);
+  } else {
+    const long nsc = b->head + b->tail;
+    for (long j = threadIdx.x; j < nsc; j += JB) one(j < b->head ? j : b->head + b->nvec * EPV + (j - b->head));
   }
-  (void)REMOTE;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's stores acknowledged by memory
 }
 
-// this workgroup is through a segment: count it; the last one signals `phase` of the part's slot to
-// every node (itself too). Returns nothing; the workgroup's stores were drained before.
-__device__ __forceinline__ void join_arrive(unsigned *count, NodeSync &ns, int phase, unsigned long epoch) {
+// The items of one segment, claimed in chunks from the segment's ticket counter (the next chunk's
+// ticket fetched while the current one is folded); then this workgroup's items are counted in
+// `done`, and whoever completes the count -- for a segment of no item, the first through -- signals
+// `phase` of the part's slot to every node, itself too (phase < 0: nothing to signal). Claiming
+// rather than a static grid stride: a workgroup the GPU has not started yet holds no item a
+// waiting one needs, so the grid need not be resident all at once.
+template <typename T, int N, int U, int CH, int D, int ISSUE>
+__device__ __forceinline__ void join_seg(const Work &w, unsigned *tk, unsigned *done, unsigned *sig, const emac_codes &codes,
+                                         int nrt, bool store, NodeSync &ns, int phase, unsigned long epoch) {
+  __shared__ unsigned claim[2];
   __shared__ unsigned last;
+  const unsigned n = (unsigned)(w.ntiles + w.nedges);
+  unsigned c = n / (gridDim.x * 4u);  // a few chunks per workgroup: few claims, balanced ends
+  c = c < 1u ? 1u : c > 32u ? 32u : c;
+  unsigned mine = 0;
   __syncthreads();
-  if (threadIdx.x == 0)
-    last = __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  if (threadIdx.x == 0) claim[0] = n ? __hip_atomic_fetch_add(tk, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+  __syncthreads();
+  unsigned at = claim[0];
+  while (at < n) {
+    unsigned next = 0;
+    if (threadIdx.x == 0) next = __hip_atomic_fetch_add(tk, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned end = at + c < n ? at + c : n;
+    for (unsigned i = at; i < end; ++i) join_item<T, N, U, CH, D, ISSUE>(w, (long)i, codes, nrt, store);
+    mine += end - at;
+    __syncthreads();
+    if (threadIdx.x == 0) claim[1] = next;
+    __syncthreads();
+    at = claim[1];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's stores acknowledged by memory
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned before = __hip_atomic_fetch_add(done, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = before + mine == n && phase >= 0 &&
+           __hip_atomic_exchange(sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+  }
   __syncthreads();
   if (last && threadIdx.x < 64) wave_signal(ns, phase, epoch, true);
 }
@@ -150,35 +184,39 @@ __device__ __forceinline__ bool join_gate(NodeSync &ns, int phase, unsigned long
 // R copy-in leaves (compile time, fold tree CH), N nodes (runtime, the share's tree in xcodes)
 // mode bit 0: the copy-ins; bit 1: the node legs (the signals, waits, share folds and pulls; without
 // the copy-ins they read the partials the last ones left -- bench.py times each alone)
-template <typename T, int R, int CH>
-__global__ __launch_bounds__(EMAC_BLOCK) void join_fused_kernel(JoinSegs segs, int nparts, int mode, emac_codes codes,
+template <typename T, int R, int CH, bool SYS>
+__global__ __launch_bounds__(JB) void join_fused_kernel(JoinSegs segs, int nparts, int mode, emac_codes codes,
                                                                 emac_codes xcodes, NodeSync ns0, JoinCtl *ctl) {
-  constexpr int CI_ISSUE = 1 | kSysStore;  // local leaves, write-through partial stores
+  // local leaves; the partial written through to memory, at system scope when a peer runs on another
+  // GPU, else at device scope (kDevStore: sc1 nt) -- enough for this GPU's other XCDs and processes
+  constexpr int CI_ISSUE = 1 | (SYS ? kSysStore : kDevStore);
   for (int s = 0; s <= nparts + 1; ++s) {
-    if (s < nparts) {  // CI[s]
+    if (s < nparts) {  // CI[s]: signals phase 0 of part s when its last item is in (with the node legs)
       NodeSync ns = ns0;
       ns.slot = segs.slot[s];
       ns.tag = segs.e1[s];
-      if (mode & 1) join_run<T, R, 2, CH, 1, CI_ISSUE>(segs.w[0][s], codes, 0, true);
-      if (mode & 2) join_arrive(&ctl->ci[s], ns, 0, segs.e0[s]);
+      const Work empty = {segs.w[0][s].b, 0, 0, 0, 1, nullptr, 0};
+      join_seg<T, R, 2, CH, 1, CI_ISSUE>((mode & 1) ? segs.w[0][s] : empty, &ctl->tk[0][s], &ctl->done[0][s],
+                                         &ctl->sig[0][s], codes, 0, true, ns, (mode & 2) ? 0 : -1, segs.e0[s]);
     }
     if (!(mode & 2)) continue;
-    if (s >= 1 && s <= nparts) {  // SF[k]
+    if (s >= 1 && s <= nparts) {  // SF[k], after every node's phase 0 of part k; signals phase 1
       const int k = s - 1;
       NodeSync ns = ns0;
       ns.slot = segs.slot[k];
       ns.tag = segs.e1[k];
       const bool ok = join_gate(ns, 0, segs.e0[k], &ctl->failed0[k]);
-      join_run<T, 0, 1, 0, 1, 1 | kRemote>(segs.w[1][k], xcodes, ns0.nranks, ok);
-      join_arrive(&ctl->sf[k], ns, 1, segs.e1[k]);
+      join_seg<T, 0, 1, 0, 1, 1 | kRemote>(segs.w[1][k], &ctl->tk[1][k], &ctl->done[1][k], &ctl->sig[1][k], xcodes,
+                                           ns0.nranks, ok, ns, 1, segs.e1[k]);
     }
-    if (s >= 2) {  // PL[k]
+    if (s >= 2) {  // PL[k], after every node's phase 1 of part k
       const int k = s - 2;
       NodeSync ns = ns0;
       ns.slot = segs.slot[k];
       ns.tag = segs.e1[k];
       const bool ok = join_gate(ns, 1, segs.e1[k], &ctl->failed1[k]);
-      join_run<T, 1, 2, 0, R, 1 | kRemote>(segs.w[2][k], codes, 0, ok);
+      join_seg<T, 1, 2, 0, R, 1 | kRemote>(segs.w[2][k], &ctl->tk[2][k], &ctl->done[2][k], &ctl->sig[2][k], codes, 0, ok,
+                                           ns, -1, 0);
     }
   }
   // the last workgroup out resets the control block for the next Start (stream-ordered behind)
@@ -186,20 +224,21 @@ __global__ __launch_bounds__(EMAC_BLOCK) void join_fused_kernel(JoinSegs segs, i
   __syncthreads();
   if (threadIdx.x == 0) last = __hip_atomic_fetch_add(&ctl->out, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
-  if (last && threadIdx.x < EMAC_JOIN_PARTS_MAX) {
-    ctl->ci[threadIdx.x] = 0;
-    ctl->sf[threadIdx.x] = 0;
-    ctl->failed0[threadIdx.x] = 0;
-    ctl->failed1[threadIdx.x] = 0;
-    if (threadIdx.x == 0) ctl->out = 0;
+  if (last) {
+    unsigned *cw = reinterpret_cast<unsigned *>(ctl);
+    for (unsigned i = threadIdx.x; i < sizeof(JoinCtl) / sizeof(unsigned); i += JB) cw[i] = 0;
   }
 }
 
 template <typename T, int R, int CH>
 int join_launch_one(const JoinSegs &segs, int nparts, int mode, const emac_codes &codes, const emac_codes &xcodes,
                     const NodeSync &ns, JoinCtl *ctl, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((join_fused_kernel<T, R, CH>), dim3((unsigned)grid), dim3(EMAC_BLOCK), 0, s, segs, nparts, mode,
-                     codes, xcodes, ns, ctl);
+  if (mode & 4)  // every node on this GPU: device-scope write-through suffices
+    hipLaunchKernelGGL((join_fused_kernel<T, R, CH, false>), dim3((unsigned)grid), dim3(JB), 0, s, segs, nparts,
+                       mode, codes, xcodes, ns, ctl);
+  else
+    hipLaunchKernelGGL((join_fused_kernel<T, R, CH, true>), dim3((unsigned)grid), dim3(JB), 0, s, segs, nparts,
+                       mode, codes, xcodes, ns, ctl);
   return hipGetLastError() == hipSuccess ? 0 : EMAC_ERR_DEVICE;
 }
 
@@ -269,12 +308,14 @@ extern "C" int emac_gpu_join_fused(int dtype, int nsrc, const emac_codes *codes,
 }
 
 extern "C" int emac_gpu_join_grid(void) {
-  // the workgroups the GPU holds at once of the heaviest instance (8 leaves, float): the grid never
-  // exceeds them, so no workgroup waits on tiles of one that cannot start
-  int per_cu = 0, dev = 0, cus = 0;
+  // one workgroup per CU (items are claimed, so the grid need not match the work): every segment
+  // costs each workgroup a claim and a count on the segment's counters, and a wider grid only adds
+  // contention on them (EXT_MPI_AMD_JOIN_GRID overrides, for A/B runs)
+  int dev = 0, cus = 0;
+  const char *e = getenv("EXT_MPI_AMD_JOIN_GRID");
+  if (e && atoi(e) > 0) return atoi(e);
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, emac::join_fused_kernel<float, 8, 0>, EMAC_BLOCK, 0) != hipSuccess ||
-      per_cu < 1 || cus < 1)
-    return 64;
-  return per_cu * cus;
+      cus < 1)
+    return 256;
+  return cus;
 }

@@ -65,7 +65,8 @@ def _run_nodes(nodes, budget=180, **extra_env):
 
 @pytest.mark.parametrize("nodes", [2, 3, 4, 8])
 def test_node_form_over_peer_mapped_nodes(nodes):
-    """the default join (serial; the stream-pipelined one is opt-in, engine_join.c join_parts)"""
+    """the default join: serial under 1 MiB per rank, the fused one of 2 parts from there
+    (engine_join.c join_parts)"""
     _run_nodes(nodes, budget=300 if nodes >= 8 else 180)
 
 
