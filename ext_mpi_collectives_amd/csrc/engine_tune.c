@@ -122,9 +122,12 @@ static int tune_candidates(const emac_handle *h, long vec, int *sched) {
     /* a word some other tuned shape has a kernel for (a fan-out-only schedule met by a local fold, a
        width-specific one by another leaf count): this handle keeps its static pick; a word no shape
        has a kernel for is a mistake, refused at init */
+    static const int chains[] = EMAC_CHAINS;
+    int c;
     for (ns = 2; ns <= 8 && !known; ns++)
       for (fn = 0; fn <= 1 && !known; fn++)
-        known = emac_gpu_fold_supported(h->plan.dtype, EMAC_SUM, ns, fn, 0, sched[0], 1);
+        for (c = -1; c < (int)(sizeof(chains) / sizeof(chains[0])) && !known; c++) /* the linear fold, then the chains */
+          known = emac_gpu_fold_supported(h->plan.dtype, EMAC_SUM, ns, fn, c < 0 ? 0 : chains[c], sched[0], 1);
     if (!known) return EMAC_ERR_UNSUPPORTED;
     if (getenv("EXT_MPI_AMD_DEBUG_TUNE"))
       fprintf(stderr, "ext_mpi_amd: EXT_MPI_AMD_FOLD_SCHEDULE %d has no kernel for this handle (%d leaves, fan %d): "
