@@ -148,6 +148,12 @@ static int tune_candidates(const emac_handle *h, long vec, int *sched) {
     sched[n++] = 4 | (5 | 1 << 15) << 4;
   }
   if (small) sched[n++] = 1 | 1 << 4;
+  /* unequal buckets (the -k fractions), at most EMAC_GROUP_MAP_MAX: the fan-out's leaf-major groups
+     through the layout's bucket map (layout.c; the other deferred schedules need equal buckets) */
+  if (h->tiles_per_bucket <= 0 && h->fan && h->nb > 0 && h->nb <= EMAC_GROUP_MAP_MAX) {
+    sched[n++] = 2 | (1 | 2 << 11 | 1 << 13) << 4;
+    if (tree > 1) sched[n++] = 2 | (1 | 2 << 11 | 1 << 13 | 1 << 16) << 4;
+  }
   if (h->tiles_per_bucket > 0) {
     sched[n++] = 2 | (1 | 2 << 11) << 4;
     if (!h->fan) {

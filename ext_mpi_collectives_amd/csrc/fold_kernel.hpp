@@ -480,11 +480,15 @@ __device__ __forceinline__ void fold_group_leaf(const emac_bucket *b, long gbase
   (void)nt;
 }
 
-// The deferred-store schedule as a kernel of its own (equal buckets of tpb tiles: the tuner offers
-// the schedule only then), so its code holds nothing of the per-tile loop's.
-template <typename T, int OP, int N, int U, int CH, int D, int ISSUE, bool ALL_FULL>
+// The deferred-store schedule as a kernel of its own, so its code holds nothing of the per-tile
+// loop's: equal buckets of tpb tiles, or (MAP, round 5) up to EMAC_GROUP_MAP_MAX buckets of any
+// tile counts whose first groups the layout wrote into their tile0 (layout.c): the workgroup loads
+// those starts into LDS once, and a group's bucket is the number of starts at or below it, one
+// ballot over the table (the `-k` fractions' few short chunks beside a long one get the leaf-major
+// and LDS groups instead of the per-tile loop).
+template <typename T, int OP, int N, int U, int CH, int D, int ISSUE, bool ALL_FULL, bool MAP = false>
 __device__ __forceinline__ void deferred_body(const emac_bucket *__restrict__ bk, long tpb, long ngroups,
-                                              const emac_codes &codes) {
+                                              const emac_codes &codes, int nb = 0) {
   typedef typename Lane<T>::V V;
   static_assert(N > 0 && (ISSUE & kRemote) == 0, "deferred stores: compile-time leaves, local memory");
   static_assert((ISSUE & kLeafMajor) == 0 || CH != 1, "leaf-major groups: compile-time fold trees");
@@ -494,11 +498,29 @@ __device__ __forceinline__ void deferred_body(const emac_bucket *__restrict__ bk
   __shared__ V res[LEAF ? 1 : KB * U * EMAC_BLOCK];
   // groups per bucket (the last one may hold fewer tiles); group counts fit 32 bits (< 2^31 groups
   // of >= 8 KiB), and 32-bit division is a short sequence ahead of the group's first load
-  const unsigned gpb = (unsigned)((tpb + KB - 1) / KB);
+  const unsigned gpb = MAP ? 1u : (unsigned)((tpb + KB - 1) / KB);
+  __shared__ unsigned g0[MAP ? EMAC_GROUP_MAP_MAX : 1];
+  if constexpr (MAP) {
+    static_assert(!ALL_FULL, "bucket-mapped groups check their bucket's end");
+    static_assert(EMAC_GROUP_MAP_MAX <= 64, "one ballot over the table");
+    if (threadIdx.x < EMAC_GROUP_MAP_MAX) g0[threadIdx.x] = threadIdx.x < (unsigned)nb ? (unsigned)bk[threadIdx.x].tile0 : ~0u;
+    __syncthreads();
+  }
   for (long g = blockIdx.x; g < ngroups; g += gridDim.x) {
-    const int bi = (int)((unsigned)g / gpb);
-    const long t0 = (g - (long)bi * gpb) * KB;
-    const int nt = tpb - t0 < KB ? (int)(tpb - t0) : KB;  // wave-uniform
+    int bi;
+    long t0;
+    int nt;
+    if constexpr (MAP) {
+      const unsigned lane = threadIdx.x & 63u;
+      bi = __popcll(__ballot(g0[lane] <= (unsigned)g)) - 1;  // starts ascend: the last one <= g
+      t0 = (g - (long)g0[bi]) * KB;
+      const long tb = (bk[bi].nvec + TILE - 1) / TILE;  // the bucket's tiles
+      nt = tb - t0 < KB ? (int)(tb - t0) : KB;
+    } else {
+      bi = (int)((unsigned)g / gpb);
+      t0 = (g - (long)bi * gpb) * KB;
+      nt = tpb - t0 < KB ? (int)(tpb - t0) : KB;  // wave-uniform
+    }
     if constexpr (LEAF)
       fold_group_leaf<T, OP, N, U, CH, D, ISSUE, ALL_FULL>(bk + bi, t0 * TILE, nt);
     else
@@ -510,6 +532,12 @@ template <typename T, int OP, int N, int U, int CH, int D, int ISSUE, bool ALL_F
 __global__ __launch_bounds__(EMAC_BLOCK) void fold_deferred_kernel(const emac_bucket *__restrict__ bk, long tpb,
                                                                    long ngroups, emac_codes codes) {
   deferred_body<T, OP, N, U, CH, D, ISSUE, ALL_FULL>(bk, tpb, ngroups, codes);
+}
+
+template <typename T, int OP, int N, int U, int CH, int D, int ISSUE>
+__global__ __launch_bounds__(EMAC_BLOCK) void fold_deferred_map_kernel(const emac_bucket *__restrict__ bk, int nb,
+                                                                       long ngroups, emac_codes codes) {
+  deferred_body<T, OP, N, U, CH, D, ISSUE, false, true>(bk, -1, ngroups, codes, nb);
 }
 
 // ---- runtime leaf count (N = 0 in the templates below): MIN / MAX ----
@@ -834,10 +862,19 @@ int launch_one(const Launch &L) {
   constexpr int KB = defer_tiles(ISSUE);
   if (L.dry) return 0;
   if constexpr (KB > 1) {  // one workgroup per group of KB tiles
-    if (L.tpb <= 0) return launch_one<T, OP, N, U, CH, D, ISSUE & ~(3 << kDeferShift | kLeafMajor | kLmOpenCopy)>(L);  // unequal buckets
-    const long groups = (long)L.nb * ((L.tpb + KB - 1) / KB);
+    constexpr bool MAPPED = (ISSUE & kLeafMajor) != 0;  // bucket-mapped groups: the leaf-major ones only
+    if (L.tpb == 0 || (L.tpb < 0 && !MAPPED))  // unequal buckets: the per-tile loop
+      return launch_one<T, OP, N, U, CH, D, ISSUE & ~(3 << kDeferShift | kLeafMajor | kLmOpenCopy)>(L);
+    const long groups = L.tpb < 0 ? L.ntiles : (long)L.nb * ((L.tpb + KB - 1) / KB);
     const unsigned grid = (unsigned)(groups < 8192 ? groups : 8192);
-    if (L.all_full && L.tpb % KB == 0)
+    if (L.tpb < 0) {  // unequal buckets, their first groups in tile0 (layout.c)
+      if constexpr (MAPPED) {
+        if (L.nb > EMAC_GROUP_MAP_MAX) return EMAC_ERR_ARG;
+        if (grid > 0)
+          hipLaunchKernelGGL((fold_deferred_map_kernel<T, OP, N, U, CH, D, ISSUE>), dim3(grid), dim3(EMAC_BLOCK), 0, L.s, L.b,
+                             L.nb, groups, *L.c);
+      }
+    } else if (L.all_full && L.tpb % KB == 0)
       hipLaunchKernelGGL((fold_deferred_kernel<T, OP, N, U, CH, D, ISSUE, true>), dim3(grid), dim3(EMAC_BLOCK), 0, L.s, L.b,
                          L.tpb, groups, *L.c);
     else

@@ -41,6 +41,9 @@ typedef struct {
 #define EMAC_EDGE_RANGE 65536
 
 #define EMAC_BLOCK 256
+/* deferred-store launches over buckets of unequal tile counts: at most this many buckets, whose
+   first groups the kernel keeps in LDS (layout.c emac_layout_as; tiles_per_bucket -1 marks them) */
+#define EMAC_GROUP_MAP_MAX 64
 
 int emac_gpu_device_count(void);
 int emac_gpu_get_device(int *dev);

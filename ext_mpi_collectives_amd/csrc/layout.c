@@ -108,6 +108,24 @@ int emac_layout_as(emac_bucket *b, int nb, int op, int nsrc, int tree, int fan, 
   *nedges = ne;
   *ntiles_out = tiles;
   *tpb_out = uniform > 0 ? uniform : 0;
+  {
+    /* a leaf-major deferred-store schedule (fold_kernel.hpp kDeferShift: groups of kb tiles of one bucket) over
+       buckets of unequal tile counts, at most EMAC_GROUP_MAP_MAX of them (the `-k` fractions: a few
+       short chunks beside one long one): each bucket's tile0 becomes its first GROUP, ntiles the
+       groups of the launch and tiles_per_bucket -1 -- the kernel finds a group's bucket in a table
+       of these starts it keeps in LDS, instead of falling back to the per-tile loop */
+    const int issue = unroll >> 4, kd = (issue >> 11) & 3;
+    const long kb = kd ? 1L << kd : 1;
+    if (kb > 1 && (issue & (1 << 13)) && *tpb_out == 0 && nb > 0 && nb <= EMAC_GROUP_MAP_MAX) { /* leaf-major (kLeafMajor) */
+      long g = 0;
+      for (i = 0; i < nb; i++) {
+        b[i].tile0 = g;
+        g += ((b[i].nvec + tv - 1) / tv + kb - 1) / kb;
+      }
+      *ntiles_out = g;
+      *tpb_out = -1;
+    }
+  }
   *all_full_out = all_full;
   *unroll_out = unroll;
   return 0;
