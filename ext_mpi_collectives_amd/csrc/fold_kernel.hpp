@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "gpu.h"
 #include "ipc_sync.hpp"
 
@@ -465,7 +467,9 @@ __device__ __forceinline__ void fold_group_leaf(const emac_bucket *b, long gbase
   }
   // each group starts its stores at destination (group index mod D), so the groups in flight write
   // all D receive buffers at once rather than each in turn: 0.6-0.9 % faster at 16 MiB per rank,
-  // three passes (profiles/r04/leafshape/rotdst_*.json); the same values land in every buffer
+  // three passes (profiles/r04/leafshape/rotdst_*.json); the same values land in every buffer. (One
+  // guarded store loop: a second, unguarded one for whole groups took the partial-group kernels
+  // from 112 to 255 VGPRs and the -64 fractions from 46.1 to 49.5 us, profiles/r05/chains/.)
   const int d0 = (int)((unsigned long)gbase / (unsigned long)(Q * EMAC_BLOCK) % (unsigned)D);
 #pragma unroll
   for (int dd = 0; dd < D; ++dd) {
