@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round 5: the driver's GPU suite, smoke(), the default bench (N = 1), then the lease fingerprint of
+# the 256 MiB point (tools/gpu_r05_lease.sh). Usage: gpu_r05_full.sh <tag>
+cd "$GRAFT_REPO_ROOT"
+tag=${1:-full}
+O=gpurun_out/r05/$tag
+mkdir -p $O
+timeout -k 10 1200 python -u -m pytest tests -x -q -m gpu --timeout 400 --timeout-method thread --durations=15 > $O/gpu_tests.log 2>&1
+rc=$?
+tail -25 $O/gpu_tests.log
+[ $rc -ne 0 ] && { echo "GPU SUITE rc=$rc"; exit $rc; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
+tail -2 $O/smoke.log
+timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python3 - "$O/bench.json" <<'PY'
+import json, sys
+d = json.load(open(sys.argv[1])); e = d['extras']
+print('headline', d['ms_per_step'], d['roofline']['frac'], d['config']['fold_schedules_per_set'])
+print('256', {k: e['point_256MiB'].get(k) for k in ('median_launch_us', 'min_launch_us', 'max_launch_us', 'frac_of_peak_at_median', 'schedules_per_set')})
+print('local', {k: e['local_fold_256MiB'].get(k) for k in ('median_launch_us', 'min_launch_us', 'max_launch_us', 'frac_of_peak_at_median')})
+print('chains', {k: (v['avg_launch_us'], v['vs_linear']) for k, v in e['radix_chains_16MiB'].items()})
+print('int/long', {k: v['avg_launch_us'] for k, v in e['config3_int_long_4MiB'].items()})
+PY
+bash tools/gpu_r05_lease.sh $tag

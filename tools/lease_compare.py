@@ -1,0 +1,82 @@
+"""The 256 MiB point's lease fingerprints side by side (tools/gpu_r05_lease.sh): per lease, the node
+launch's event time under its usual kept schedule and under leaf-major groups, the best 1:1 copy of
+its 4 GiB, and, per kernel, the DRAM credit stall cycles and L2->memory cycles in flight per request
+(the counters round 4 found bounding the fold), next to the busy time. Sorted by the node launch's
+time, so the counters of slow and fast leases line up.
+Usage: lease_compare.py <gpurun_out/r05/lease> [--json OUT]"""
+import glob
+import json
+import os
+import sys
+
+CLOCK_GHZ = 2.4  # GRBM_GUI_ACTIVE counts engine cycles on each of the 8 XCDs
+
+
+def merged(path):
+    """{kernel: {counter: median}} over every pass directory of one pmc_*.json"""
+    out = {}
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return out
+    for per_dir in d.values():
+        for k, cs in per_dir.items():
+            out.setdefault(k, {}).update(cs)
+    return out
+
+
+def per_request(cs):
+    rd, wr = cs.get("TCC_EA0_RDREQ_sum"), cs.get("TCC_EA0_WRREQ_sum")
+    f = {}
+    if rd:
+        if "TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum" in cs:
+            f["rd_credit_stall_per_req"] = round(cs["TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum"] / rd, 3)
+        if "TCC_EA0_RDREQ_LEVEL_sum" in cs:
+            f["rd_level_per_req"] = round(cs["TCC_EA0_RDREQ_LEVEL_sum"] / rd, 1)
+        f["rd_mib"] = round(rd * 128 / 2 ** 20, 1)
+    if wr:
+        if "TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum" in cs:
+            f["wr_credit_stall_per_req"] = round(cs["TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum"] / wr, 3)
+        if "TCC_EA0_WRREQ_LEVEL_sum" in cs:
+            f["wr_level_per_req"] = round(cs["TCC_EA0_WRREQ_LEVEL_sum"] / wr, 1)
+        f["wr_mib"] = round(wr * 64 / 2 ** 20, 1)
+    if "GRBM_GUI_ACTIVE" in cs:
+        f["busy_us"] = round(cs["GRBM_GUI_ACTIVE"] / 8 / CLOCK_GHZ / 1e3, 1)
+    return f
+
+
+def lease(d):
+    out = {"lease": os.path.basename(d)}
+    try:
+        out["host"] = open(os.path.join(d, "host.txt")).read().strip()
+    except OSError:
+        pass
+    try:
+        t = json.load(open(os.path.join(d, "time_node256.json")))
+        out["node256_us"] = {w: v["avg_launch_us"] for w, v in t["by_schedule"].items()}
+    except (OSError, ValueError, KeyError):
+        return None
+    try:
+        out["copy256_us"] = json.load(open(os.path.join(d, "time_copy256.json")))["avg_launch_us"]
+    except (OSError, ValueError, KeyError):
+        pass
+    out["fold_pmc"] = {k: per_request(cs) for k, cs in merged(os.path.join(d, "pmc_fold.json")).items()}
+    out["copy_pmc"] = {k: per_request(cs) for k, cs in merged(os.path.join(d, "pmc_copy.json")).items()}
+    return out
+
+
+def main():
+    root = sys.argv[1]
+    rows = [r for r in (lease(d) for d in sorted(glob.glob(os.path.join(root, "*")))) if r]
+    rows.sort(key=lambda r: min(r["node256_us"].values()))
+    for r in rows:
+        fold = next(iter(r["fold_pmc"].values()), {})
+        copy = {k: v for k, v in r["copy_pmc"].items() if "phased" in k}
+        copy = next(iter(copy.values()), {})
+        print(f"{r['lease']:>12} node {r['node256_us']} copy {r.get('copy256_us')} | fold {fold} | phased copy {copy}")
+    if "--json" in sys.argv:
+        json.dump(rows, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
