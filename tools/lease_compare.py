@@ -4,24 +4,45 @@ its 4 GiB, and, per kernel, the DRAM credit stall cycles and L2->memory cycles i
 (the counters round 4 found bounding the fold), next to the busy time. Sorted by the node launch's
 time, so the counters of slow and fast leases line up.
 Usage: lease_compare.py <gpurun_out/r05/lease> [--json OUT]"""
+import csv
 import glob
 import json
 import os
+import re
 import sys
 
 CLOCK_GHZ = 2.4  # GRBM_GUI_ACTIVE counts engine cycles on each of the 8 XCDs
 
 
-def merged(path):
-    """{kernel: {counter: median}} over every pass directory of one pmc_*.json"""
-    out = {}
-    try:
-        d = json.load(open(path))
-    except (OSError, ValueError):
-        return out
-    for per_dir in d.values():
-        for k, cs in per_dir.items():
-            out.setdefault(k, {}).update(cs)
+def label(name):
+    """a short kernel label: the fold's template arguments, or which copy ceiling kernel"""
+    if "copy_phased" in name:
+        return "copy phased"
+    if "copy_k4<true>" in name:
+        return "copy nt"
+    if "copy_k4<false>" in name:
+        return "copy plain"
+    m = re.search(r"(fold_\w*kernel<[^>]*>)", name)
+    return m.group(1) if m else None
+
+
+def merged(d, prefix):
+    """{kernel label: {counter: median}} over the lease's PMC pass directories <prefix>_*"""
+    vals = {}
+    for path in glob.glob(os.path.join(d, prefix + "_*", "**", "*counter_collection*.csv"), recursive=True):
+        for row in csv.DictReader(open(path)):
+            k = label(row.get("Kernel_Name", ""))
+            if k:
+                vals.setdefault(k, {}).setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+    out = {k: {c: sorted(v)[len(v) // 2] for c, v in cs.items()} for k, cs in vals.items()}
+    if not out:  # a lease whose large CSVs were dropped: the medians tools/pmc_counters.py kept
+        try:
+            for per_dir in json.load(open(os.path.join(d, "pmc_fold.json" if prefix == "node256" else "pmc_copy.json"))).values():
+                for k, cs in per_dir.items():
+                    if label(k):
+                        out.setdefault(label(k), {}).update(cs)
+        except (OSError, ValueError):
+            pass
     return out
 
 
@@ -60,8 +81,8 @@ def lease(d):
         out["copy256_us"] = json.load(open(os.path.join(d, "time_copy256.json")))["avg_launch_us"]
     except (OSError, ValueError, KeyError):
         pass
-    out["fold_pmc"] = {k: per_request(cs) for k, cs in merged(os.path.join(d, "pmc_fold.json")).items()}
-    out["copy_pmc"] = {k: per_request(cs) for k, cs in merged(os.path.join(d, "pmc_copy.json")).items()}
+    out["fold_pmc"] = {k: per_request(cs) for k, cs in merged(d, "node256").items()}
+    out["copy_pmc"] = {k: per_request(cs) for k, cs in merged(d, "copy256").items()}
     return out
 
 
@@ -71,8 +92,7 @@ def main():
     rows.sort(key=lambda r: min(r["node256_us"].values()))
     for r in rows:
         fold = next(iter(r["fold_pmc"].values()), {})
-        copy = {k: v for k, v in r["copy_pmc"].items() if "phased" in k}
-        copy = next(iter(copy.values()), {})
+        copy = r["copy_pmc"].get("copy phased", {})
         print(f"{r['lease']:>12} node {r['node256_us']} copy {r.get('copy256_us')} | fold {fold} | phased copy {copy}")
     if "--json" in sys.argv:
         json.dump(rows, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
