@@ -224,11 +224,13 @@ def rotation_sets(read_bytes_per_set, set_bytes=None):
 
 
 def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * MIB, host=False, alloc="torch",
-             pool=None, launch_times=False):
+             pool=None, launch_times=False, isolate=False):
     """Time `steps` node-form Allreduces (R ranks in this GPU). Returns dict of timings. `pool`: a
     dict that keeps the device buffer sets for the next call of the same shape (freed by the caller,
     free_pool) instead of making and filling them again. `launch_times`: also each Start's own time,
-    between fence-free events recorded before and after every launch ("launch_us")."""
+    between fence-free events recorded before and after every launch ("launch_us"). `isolate`: the
+    host waits for each Start before queuing the next, so no launch overlaps its neighbours' head or
+    tail (the lease fingerprint's isolated times)."""
     import torch
     import ext_mpi_collectives_amd as emac
     tsize = torch.empty((), dtype=tdtype).element_size()
@@ -318,11 +320,13 @@ def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * 
         evs = []
 
     def one(k):
-        if evs and k == 0:
-            C.ceiling_event_record(evs[0], stream.cuda_stream)
+        if evs and (k == 0 or isolate):
+            C.ceiling_event_record(evs[k], stream.cuda_stream)
         emac.start(handles[k % nsets])
         if evs:
             C.ceiling_event_record(evs[k + 1], stream.cuda_stream)
+        if isolate:
+            stream.synchronize()
 
     gate = StreamGate(stream.cuda_stream)
     try:
@@ -1656,8 +1660,13 @@ def shape_only(args):
             free_pool(pool)
             r = {"by_schedule": r}
         else:
-            x = node_run(8, MB // ts, td, cd, args.copyin or "6;1 -8 8", steps, 5, alloc="hip")
-            r = {"avg_launch_us": round(x["event_ms"] * 1e3 / steps, 2), "checked": x["checked"], "schedule": x["schedule"]}
+            x = node_run(8, MB // ts, td, cd, args.copyin or "6;1 -8 8", steps, 5, alloc="hip", launch_times=True)
+            r = {"avg_launch_us": round(x["event_ms"] * 1e3 / steps, 2), "checked": x["checked"], "schedule": x["schedule"],
+                 **launch_stats(x["launch_us"])}
+            if os.environ.get("EXT_MPI_AMD_BENCH_ISOLATED"):  # each launch alone (lease fingerprint)
+                y = node_run(8, MB // ts, td, cd, args.copyin or "6;1 -8 8", 20, 5, alloc="hip", launch_times=True,
+                             isolate=True)
+                r["isolated"] = launch_stats(y["launch_us"])
     emit({"shape": args.shape, **r})
 
 

@@ -78,6 +78,12 @@ def lease(d):
     except (OSError, ValueError, KeyError):
         return None
     try:
+        t = json.load(open(os.path.join(d, "time_node256_iso.json")))
+        out["node256_back_to_back_median_us"] = t.get("median_launch_us")
+        out["node256_isolated_median_us"] = t.get("isolated", {}).get("median_launch_us")
+    except (OSError, ValueError):
+        pass
+    try:
         out["copy256_us"] = json.load(open(os.path.join(d, "time_copy256.json")))["avg_launch_us"]
     except (OSError, ValueError, KeyError):
         pass
@@ -93,7 +99,8 @@ def main():
     for r in rows:
         fold = next(iter(r["fold_pmc"].values()), {})
         copy = r["copy_pmc"].get("copy phased", {})
-        print(f"{r['lease']:>12} node {r['node256_us']} copy {r.get('copy256_us')} | fold {fold} | phased copy {copy}")
+        print(f"{r['lease']:>12} node {r['node256_us']} b2b/isolated {r.get('node256_back_to_back_median_us')} / "
+              f"{r.get('node256_isolated_median_us')} copy {r.get('copy256_us')} | fold {fold} | phased copy {copy}")
     if "--json" in sys.argv:
         json.dump(rows, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
 
