@@ -1660,13 +1660,17 @@ def shape_only(args):
             free_pool(pool)
             r = {"by_schedule": r}
         else:
-            x = node_run(8, MB // ts, td, cd, args.copyin or "6;1 -8 8", steps, 5, alloc="hip", launch_times=True)
+            pool = {}  # the isolated run reuses the buffer sets (filling 8 GiB from host takes minutes)
+            x = node_run(8, MB // ts, td, cd, args.copyin or "6;1 -8 8", steps, 5, alloc="hip", launch_times=True,
+                         pool=pool)
             r = {"avg_launch_us": round(x["event_ms"] * 1e3 / steps, 2), "checked": x["checked"], "schedule": x["schedule"],
                  **launch_stats(x["launch_us"])}
+            log(f"{args.shape}: back to back {r}")
             if os.environ.get("EXT_MPI_AMD_BENCH_ISOLATED"):  # each launch alone (lease fingerprint)
                 y = node_run(8, MB // ts, td, cd, args.copyin or "6;1 -8 8", 20, 5, alloc="hip", launch_times=True,
-                             isolate=True)
+                             isolate=True, pool=pool)
                 r["isolated"] = launch_stats(y["launch_us"])
+            free_pool(pool)
     emit({"shape": args.shape, **r})
 
 
