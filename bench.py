@@ -331,7 +331,7 @@ def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * 
     gate = StreamGate(stream.cuda_stream)
     try:
         e0.record(stream)
-        pre = min(2, steps)
+        pre = 0 if isolate else min(2, steps)  # (isolated launches wait for each other: nothing behind the gate)
         for k in range(pre):
             one(k)
     finally:  # a held stream must never outlive an error

@@ -141,7 +141,10 @@ __device__ __forceinline__ void join_seg(const Work &w, unsigned *tk, unsigned *
     __syncthreads();
     at = claim[1];
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's stores acknowledged by memory
+  // a segment whose completion is signalled: this workgroup's stores acknowledged by memory before
+  // it counts them (the pull's segments signal nothing: their stores complete with the launch, and
+  // the workgroup goes on without waiting for them)
+  if (phase >= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned before = __hip_atomic_fetch_add(done, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
