@@ -257,9 +257,12 @@ def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * 
             np_dtype = {torch.float32: np.float32, torch.float64: np.float64, torch.int32: np.int32,
                         torch.int64: np.int64}[tdtype]
             sends, recvs = [], []
+            # EXT_MPI_AMD_BENCH_FAST_FILL (the lease fingerprint's placement runs): one random array
+            # for every buffer of the set, so fresh allocations cost a copy, not a generation each
+            same = host_random(count, np_dtype, 0x5EED0000 + 97 * s) if os.environ.get("EXT_MPI_AMD_BENCH_FAST_FILL") else None
             for r in range(R):
                 b = DevBuf(count * tsize)
-                b.upload(host_random(count, np_dtype, 0x5EED0000 + 97 * s + r))
+                b.upload(same if same is not None else host_random(count, np_dtype, 0x5EED0000 + 97 * s + r))
                 sends.append(b)
                 recvs.append(DevBuf(count * tsize))
         else:
@@ -1671,6 +1674,12 @@ def shape_only(args):
                              isolate=True, pool=pool)
                 r["isolated"] = launch_stats(y["launch_us"])
             free_pool(pool)
+            # EXT_MPI_AMD_BENCH_PLACEMENTS=k: k more runs, each on freshly allocated buffer sets (the
+            # lease fingerprint: does the time move with the allocation inside one lease?)
+            for i in range(int(os.environ.get("EXT_MPI_AMD_BENCH_PLACEMENTS", "0"))):
+                z = node_run(8, MB // ts, td, cd, args.copyin or "6;1 -8 8", 20, 5, alloc="hip", launch_times=True)
+                r.setdefault("placements", []).append(launch_stats(z["launch_us"]).get("median_launch_us"))
+                log(f"{args.shape}: placement {i}: {r['placements'][-1]}")
     emit({"shape": args.shape, **r})
 
 

@@ -16,8 +16,9 @@ hostname > $O/host.txt
 timeout -k 10 300 python3 bench.py --shape node256 --schedules $W > $O/time_node256.json 2> $O/time_node256.err || exit $?
 echo "time node256 $(cat $O/time_node256.json)"
 # the kept schedule's launches back to back and each alone (the host waits between them)
-EXT_MPI_AMD_FOLD_SCHEDULE=786452 EXT_MPI_AMD_BENCH_ISOLATED=1 timeout -k 10 300 python3 bench.py --shape node256 \
-  > $O/time_node256_iso.json 2> $O/time_node256_iso.err || exit $?
+# ... and on 4 more freshly allocated buffer sets (the placement inside one lease)
+EXT_MPI_AMD_FOLD_SCHEDULE=786452 EXT_MPI_AMD_BENCH_ISOLATED=1 EXT_MPI_AMD_BENCH_PLACEMENTS=4 EXT_MPI_AMD_BENCH_FAST_FILL=1 \
+  timeout -k 10 400 python3 bench.py --shape node256 > $O/time_node256_iso.json 2> $O/time_node256_iso.err || exit $?
 echo "time node256 back to back / isolated $(cat $O/time_node256_iso.json)"
 timeout -k 10 300 python3 bench.py --shape copy256 > $O/time_copy256.json 2> $O/time_copy256.err || exit $?
 echo "time copy256 $(cat $O/time_copy256.json)"

@@ -81,6 +81,7 @@ def lease(d):
         t = json.load(open(os.path.join(d, "time_node256_iso.json")))
         out["node256_back_to_back_median_us"] = t.get("median_launch_us")
         out["node256_isolated_median_us"] = t.get("isolated", {}).get("median_launch_us")
+        out["node256_placements_median_us"] = t.get("placements")
     except (OSError, ValueError):
         pass
     try:
@@ -100,7 +101,8 @@ def main():
         fold = next(iter(r["fold_pmc"].values()), {})
         copy = r["copy_pmc"].get("copy phased", {})
         print(f"{r['lease']:>12} node {r['node256_us']} b2b/isolated {r.get('node256_back_to_back_median_us')} / "
-              f"{r.get('node256_isolated_median_us')} copy {r.get('copy256_us')} | fold {fold} | phased copy {copy}")
+              f"{r.get('node256_isolated_median_us')} fresh allocations {r.get('node256_placements_median_us')} "
+              f"copy {r.get('copy256_us')} | fold {fold} | phased copy {copy}")
     if "--json" in sys.argv:
         json.dump(rows, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
 
