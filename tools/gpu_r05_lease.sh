@@ -12,7 +12,13 @@ O=gpurun_out/r05/lease/$1
 mkdir -p $O
 export TMPDIR=/tmp
 W=786452,196626  # (4 | (1 | kDevStore | kBufLoad) << 4), leaf-major (U 2, 4 tiles)
-hostname > $O/host.txt
+# which GPU (uuid, PCI location) and its clocks at the time (read-only queries)
+timeout -k 5 60 python3 -c "
+import torch
+p = torch.cuda.get_device_properties(0)
+print('uuid', getattr(p, 'uuid', '?'), 'pci', getattr(p, 'pci_bus_id', '?'), getattr(p, 'pci_device_id', '?'),
+      'cus', p.multi_processor_count, 'mem', p.total_memory)" > $O/host.txt 2>/dev/null
+timeout -k 5 60 rocm-smi --showclocks >> $O/host.txt 2>&1 || true
 timeout -k 10 300 python3 bench.py --shape node256 --schedules $W > $O/time_node256.json 2> $O/time_node256.err || exit $?
 echo "time node256 $(cat $O/time_node256.json)"
 # the kept schedule's launches back to back and each alone (the host waits between them)
