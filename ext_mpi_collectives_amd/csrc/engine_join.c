@@ -343,11 +343,7 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
     for (k = 0; !rc && k < J->nparts; k++) {
       /* the kernel's tiles (join_fused.hip: 1024-lane workgroups): 2 vectors per lane for the copy-in
          and the pull, 1 for the share fold -- in layout units of EMAC_BLOCK lanes, U 8 and 4 */
-      /* part 0's copy-in is a launch of its own ahead of the fused one: the handle's main fold, tuned
-         like any copy-in (fold_launch), streaming at the tuned rate while no link is busy yet; the
-         later parts' copy-ins run inside the fused launch, beside the links */
-      if (!rc && k == 0) rc = upload_buckets(h, b, place_part(b, pin, nin, J->lo[0], J->lo[1], ts));
-      if (!rc && k > 0) rc = upload_forced(&J->in[k], b, place_part(b, pin, nin, J->lo[k], J->lo[k + 1], ts), R, 8 | 1 << 4);
+      if (!rc) rc = upload_forced(&J->in[k], b, place_part(b, pin, nin, J->lo[k], J->lo[k + 1], ts), R, 8 | 1 << 4);
       if (!rc) rc = upload_forced(&J->fold[k], b, place_part(b, psh, nshr, J->lo[k], J->lo[k + 1], ts), N, 4 | 1 << 4);
       if (!rc) rc = upload_forced(&J->pull[k], b, place_part(b, ppl, npl, J->lo[k], J->lo[k + 1], ts), 1, 8 | 1 << 4);
     }
@@ -613,11 +609,6 @@ int join_start(emac_handle *h, int copyin, int legs) {
         e1[k] = J->epoch[k][1];
       }
     }
-    /* part 0's copy-in (J->in[0] is empty): the tuned fold, then -- when a peer runs on another GPU
-       -- a system-scope release of its partial; the fused launch's CI[0] segment holds no item and
-       signals part 0's phase 0 as soon as a workgroup starts */
-    if (copyin && (rc = fold_launch(h))) return rc;
-    if (legs && h->ev_release && (rc = emac_gpu_event_record(h->ev_release, h->stream))) return rc;
     h->tune.ops++;
     const char *e = getenv("EXT_MPI_AMD_JOIN_SYSSTORE"); /* A/B: 1 system-scope partial stores on one GPU too */
     const int dev_scope = !cm->cross_device && !(e && atoi(e) > 0);
