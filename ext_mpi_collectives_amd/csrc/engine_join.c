@@ -341,9 +341,9 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
     memset(&zero, 0, sizeof(zero));
     for (k = 0; k <= J->nparts; k++) J->lo[k] = join_cut(h->plan.count, J->nparts, k);
     for (k = 0; !rc && k < J->nparts; k++) {
-      /* the kernel's tiles (join_fused.hip): the copy-in's waves fold tiles of 256 vectors (U 1); the
-         1024-lane workgroups fold the share's (1 vector per lane: U 4) and pull 2048 (U 8) */
-      if (!rc) rc = upload_forced(&J->in[k], b, place_part(b, pin, nin, J->lo[k], J->lo[k + 1], ts), R, 1 | 1 << 4);
+      /* the kernel's tiles (join_fused.hip: 1024-lane workgroups): 2 vectors per lane for the copy-in
+         and the pull, 1 for the share fold -- in layout units of EMAC_BLOCK lanes, U 8 and 4 */
+      if (!rc) rc = upload_forced(&J->in[k], b, place_part(b, pin, nin, J->lo[k], J->lo[k + 1], ts), R, 8 | 1 << 4);
       if (!rc) rc = upload_forced(&J->fold[k], b, place_part(b, psh, nshr, J->lo[k], J->lo[k + 1], ts), N, 4 | 1 << 4);
       if (!rc) rc = upload_forced(&J->pull[k], b, place_part(b, ppl, npl, J->lo[k], J->lo[k + 1], ts), 1, 8 | 1 << 4);
     }

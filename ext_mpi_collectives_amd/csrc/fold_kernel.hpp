@@ -412,11 +412,9 @@ __device__ __forceinline__ void lm_close(V (&acc)[lm_levels(CH)][Q]) {
 // whose resource ends at the bucket's end, so loads past it return 0 instead of needing a guard;
 // the code stays straight-line (guarded loads and adds had made the compiler spill the
 // accumulators to scratch) and only the stores are guarded.
-// BS: the lanes that share the group (EMAC_BLOCK; 64 for one wave's own group, join_fused.hip)
-template <typename T, int OP, int N, int CH, int Q, int ISSUE, bool BOUNDED, int S, typename V, int BS = EMAC_BLOCK>
+template <typename T, int OP, int N, int CH, int Q, int ISSUE, bool BOUNDED, int S, typename V>
 __device__ __forceinline__ void lm_leaves(const emac_bucket *b, long gbase, unsigned bound, V (&acc)[lm_levels(CH)][Q]) {
   typedef __attribute__((address_space(1))) V GV;
-  const unsigned lane = BS == EMAC_BLOCK ? threadIdx.x : threadIdx.x % (unsigned)BS;
   if constexpr (S < N) {
     constexpr bool opens = S % lm_group(CH, N, 0) == 0;  // leaf S starts a level-0 group
     const GV *src = (const GV *)b->src[S] + gbase;
@@ -424,7 +422,7 @@ __device__ __forceinline__ void lm_leaves(const emac_bucket *b, long gbase, unsi
     constexpr bool VIA_X = (ISSUE & kLmOpenCopy) != 0;
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-      const unsigned v = lane + (unsigned)(q * BS);
+      const unsigned v = threadIdx.x + (unsigned)(q * EMAC_BLOCK);
       V &dst = opens && !VIA_X ? acc[0][q] : x[q];
       if constexpr (BOUNDED) {
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)src, 0, bound, 0x00020000);
@@ -446,7 +444,7 @@ __device__ __forceinline__ void lm_leaves(const emac_bucket *b, long gbase, unsi
       }
     }
     lm_close<OP, T, N, CH, S, 1, Q>(acc);
-    lm_leaves<T, OP, N, CH, Q, ISSUE, BOUNDED, S + 1, V, BS>(b, gbase, bound, acc);
+    lm_leaves<T, OP, N, CH, Q, ISSUE, BOUNDED, S + 1>(b, gbase, bound, acc);
   }
 }
 

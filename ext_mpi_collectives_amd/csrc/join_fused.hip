@@ -155,92 +155,6 @@ __device__ __forceinline__ void join_seg(const Work &w, unsigned *tk, unsigned *
   if (last && threadIdx.x < 64) wave_signal(ns, phase, epoch, true);
 }
 
-// The copy-in segment, one wave at a time: every wave claims CW tiles of 256 vectors (the layout's U
-// 1) at a time and folds each leaf after leaf, 4 vectors per lane (lm_leaves over 64 lanes), into
-// the partial. The waves of a workgroup never wait for each other here -- in step, the 16 waves of
-// a workgroup loaded, folded and stored together and the copy-in streamed at 3.6 TB/s -- and count
-// their items in LDS; the last wave of the workgroup adds the workgroup's total to the segment's
-// count (after every wave drained its stores), so the counters see one atomic per workgroup.
-template <typename T, int R, int CH, int ISSUE>
-__device__ __forceinline__ void join_ci_waves(const Work &w, unsigned *tk, unsigned *done, unsigned *sig, const emac_codes &codes,
-                                              NodeSync &ns, int phase, unsigned long epoch, unsigned *lds_items,
-                                              unsigned *lds_waves) {
-  typedef typename Lane<T>::V V;
-  typedef __attribute__((address_space(1))) V GV;
-  constexpr int Q = 4, LV = lm_levels(CH);
-  constexpr long TILE = 4L * 64;  // vectors: one layout tile of U 1
-  constexpr unsigned CW = 4;
-  constexpr long EPV = 16 / sizeof(typename Lane<T>::S);
-  const unsigned lane = threadIdx.x & 63u, waves = blockDim.x / 64u;
-  const unsigned n = (unsigned)(w.ntiles + w.nedges);
-  unsigned mine = 0;
-  for (;;) {
-    unsigned at = 0;
-    if (lane == 0) at = __hip_atomic_fetch_add(tk, CW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    at = __builtin_amdgcn_readfirstlane(at);
-    if (at >= n) break;
-    const unsigned end = at + CW < n ? at + CW : n;
-    for (unsigned i = at; i < end; ++i) {
-      if (i < (unsigned)w.ntiles) {
-        const long tile = i;
-        int bi;
-        long t;
-        if (w.tpb > 0) {
-          bi = (int)((unsigned)tile / (unsigned)w.tpb);
-          t = tile - (long)bi * w.tpb;
-        } else {
-          int lo = 0, hi = w.nb - 1;
-          while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (w.b[mid].tile0 <= tile)
-              lo = mid;
-            else
-              hi = mid - 1;
-          }
-          bi = lo;
-          t = tile - w.b[lo].tile0;
-        }
-        const emac_bucket *b = w.b + bi;
-        const long gbase = t * TILE;
-        const long left = w.all_full ? TILE : b->nvec - gbase;
-        V acc[LV][Q];
-        if (left >= TILE)
-          lm_leaves<T, EMAC_SUM, R, CH, Q, ISSUE, false, 0, V, 64>(b, gbase, 0u, acc);
-        else
-          lm_leaves<T, EMAC_SUM, R, CH, Q, ISSUE, true, 0, V, 64>(b, gbase, (unsigned)(left > 0 ? left * 16 : 0), acc);
-        GV *dst = (GV *)b->dst[0] + gbase;
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-          const unsigned v = lane + (unsigned)(q * 64);
-          if ((long)v < left) store_vec<V, ISSUE>(dst, v, acc[LV - 1][q]);
-        }
-      } else {
-        const emac_edge it = w.edges[i - w.ntiles];
-        const emac_bucket *b = w.b + it.bucket;
-        auto one = [&](long e) { fold_scalar_element<T, EMAC_SUM, R, CH, 1, true>(b, e, codes); };
-        if (it.mode == 1) {
-          for (long e = it.start + lane; e < it.start + it.count; e += 64) one(e);
-        } else {
-          const long nsc = b->head + b->tail;
-          for (long j = lane; j < nsc; j += 64) one(j < b->head ? j : b->head + b->nvec * EPV + (j - b->head));
-        }
-      }
-    }
-    mine += end - at;
-  }
-  if (phase >= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores acknowledged
-  unsigned last = 0;
-  if (lane == 0) {
-    __hip_atomic_fetch_add(lds_items, mine, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (__hip_atomic_fetch_add(lds_waves, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == waves - 1) {
-      const unsigned total = __hip_atomic_load(lds_items, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const unsigned before = __hip_atomic_fetch_add(done, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = before + total == n && phase >= 0 && __hip_atomic_exchange(sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
-    }
-  }
-  if (__builtin_amdgcn_readfirstlane(last)) wave_signal(ns, phase, epoch, true);
-}
-
 // wait (one wave) for every node's `phase` of the part; the verdict for the whole workgroup. A
 // part some workgroup already found failed is not waited for again (ctl failed word).
 __device__ __forceinline__ bool join_gate(NodeSync &ns, int phase, unsigned long epoch, unsigned *failed) {
@@ -279,17 +193,14 @@ __global__ __launch_bounds__(JB) void join_fused_kernel(JoinSegs segs, int npart
   // local leaves; the partial written through to memory, at system scope when a peer runs on another
   // GPU, else at device scope (kDevStore: sc1 nt) -- enough for this GPU's other XCDs and processes
   constexpr int CI_ISSUE = 1 | (SYS ? kSysStore : kDevStore);
-  __shared__ unsigned ci_items[EMAC_JOIN_PARTS_MAX], ci_waves[EMAC_JOIN_PARTS_MAX];  // join_ci_waves' counts
-  if (threadIdx.x < EMAC_JOIN_PARTS_MAX) ci_items[threadIdx.x] = ci_waves[threadIdx.x] = 0;
-  __syncthreads();
   for (int s = 0; s <= nparts + 1; ++s) {
     if (s < nparts) {  // CI[s]: signals phase 0 of part s when its last item is in (with the node legs)
       NodeSync ns = ns0;
       ns.slot = segs.slot[s];
       ns.tag = segs.e1[s];
       const Work empty = {segs.w[0][s].b, 0, 0, 0, 1, nullptr, 0};
-      join_ci_waves<T, R, CH, CI_ISSUE>((mode & 1) ? segs.w[0][s] : empty, &ctl->tk[0][s], &ctl->done[0][s], &ctl->sig[0][s],
-                                        codes, ns, (mode & 2) ? 0 : -1, segs.e0[s], &ci_items[s], &ci_waves[s]);
+      join_seg<T, R, 2, CH, 1, CI_ISSUE>((mode & 1) ? segs.w[0][s] : empty, &ctl->tk[0][s], &ctl->done[0][s],
+                                         &ctl->sig[0][s], codes, 0, true, ns, (mode & 2) ? 0 : -1, segs.e0[s]);
     }
     if (!(mode & 2)) continue;
     if (s >= 1 && s <= nparts) {  // SF[k], after every node's phase 0 of part k; signals phase 1
