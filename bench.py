@@ -223,7 +223,7 @@ def rotation_sets(read_bytes_per_set, set_bytes=None):
     return 1 + math.ceil(READ_REUSE_BYTES / max(1, read_bytes_per_set))
 
 
-def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * MIB, host=False, alloc="torch",
+def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * MIB, host=False, alloc="torch", hold=None,
              pool=None, launch_times=False, isolate=False):
     """Time `steps` node-form Allreduces (R ranks in this GPU). Returns dict of timings. `pool`: a
     dict that keeps the device buffer sets for the next call of the same shape (freed by the caller,
@@ -334,11 +334,17 @@ def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * 
             stream.synchronize()
 
     gate = StreamGate(stream.cuda_stream)
+    host_us = None
     try:
         e0.record(stream)
-        pre = 0 if isolate else min(2, steps)  # (isolated launches wait for each other: nothing behind the gate)
+        # (isolated launches wait for each other: nothing behind the gate; the latency sweeps hold 2
+        # launches only, so their wall clock keeps the host's cost of each Start)
+        pre = 0 if isolate else min(GATE_HOLD if hold is None else hold, steps)
+        h0 = time.perf_counter()
         for k in range(pre):
             one(k, isolate and bool(evs))
+        if pre and gate.g:
+            host_us = (time.perf_counter() - h0) / pre * 1e6
     finally:  # a held stream must never outlive an error
         t0 = time.perf_counter()
         gate.open()
@@ -348,10 +354,17 @@ def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * 
     stream.synchronize()
     t1 = time.perf_counter()
     gate.free()
-    if evs and not isolate:  # the per-launch pass
-        for k in range(steps):
+    if evs and not isolate:  # the per-launch pass, held the same way
+        gate = StreamGate(stream.cuda_stream)
+        try:
+            for k in range(min(GATE_HOLD, steps)):
+                one(k, True)
+        finally:
+            gate.open()
+        for k in range(min(GATE_HOLD, steps), steps):
             one(k, True)
         stream.synchronize()
+        gate.free()
     launch_us = []
     if evs:
         ms = ctypes.c_float()
@@ -366,7 +379,8 @@ def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * 
         free_sets(sets)
     del sets
     return {"wall_s": t1 - t0, "event_ms": e0.elapsed_time(e1), "nsets": nsets, "checked": checked,
-            "set_bytes": set_bytes, "schedule": sched, "schedules": scheds, "launch_us": launch_us}
+            "set_bytes": set_bytes, "schedule": sched, "schedules": scheds, "launch_us": launch_us,
+            "host_start_us": None if host_us is None else round(host_us, 2)}
 
 
 def launch_stats(us):
@@ -406,11 +420,18 @@ def comm_shape_fold(R, chunk, tdtype, code, steps, launch_times=False):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     stream.synchronize()
     sched = emac.handle_schedule(handles[0])
-    e0.record(stream)
-    for k in range(steps):
+    gate = StreamGate(stream.cuda_stream)
+    try:
+        e0.record(stream)
+        for k in range(min(GATE_HOLD, steps)):
+            emac.start(handles[k % nsets])
+    finally:
+        gate.open()
+    for k in range(min(GATE_HOLD, steps), steps):
         emac.start(handles[k % nsets])
     e1.record(stream)
     stream.synchronize()
+    gate.free()
     t = e0.elapsed_time(e1) * 1e-3 / steps
     # then (launch_times) the same launches again, each between its own fence-free events: an event
     # record between two launches adds about a microsecond to the pair, so the average above is
@@ -422,11 +443,19 @@ def comm_shape_fold(R, chunk, tdtype, code, steps, launch_times=False):
             C.ceiling_event_destroy(ev)
         evs = []
     if evs:
-        C.ceiling_event_record(evs[0], stream.cuda_stream)
-        for k in range(steps):
+        gate = StreamGate(stream.cuda_stream)
+        try:
+            C.ceiling_event_record(evs[0], stream.cuda_stream)
+            for k in range(min(GATE_HOLD, steps)):
+                emac.start(handles[k % nsets])
+                C.ceiling_event_record(evs[k + 1], stream.cuda_stream)
+        finally:
+            gate.open()
+        for k in range(min(GATE_HOLD, steps), steps):
             emac.start(handles[k % nsets])
             C.ceiling_event_record(evs[k + 1], stream.cuda_stream)
         stream.synchronize()
+        gate.free()
     launch_us = []
     if evs:
         ms = ctypes.c_float()
@@ -476,6 +505,12 @@ def _ceiling_lib():
     L.ceiling_malloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
     L.ceiling_free.argtypes = [ctypes.c_void_p]
     return L
+
+
+# launches enqueued behind the gate before it opens: all of a timed region's (up to this many), so
+# the GPU never waits for the host's next Start (a Start costs the host several microseconds:
+# `host_start_us`; configs[2]'s launch is only 11 us) -- well below the stream's packet ring
+GATE_HOLD = 64
 
 
 class StreamGate:
@@ -712,6 +747,9 @@ def single_gpu(args):
                      "avg_launch_us": round(kernel_s * 1e6, 2),
                      "guide_measured_copy": HBM_GUIDE_COPY_GBPS,
                      "frac_of_guide_measured_copy": round(achieved / HBM_GUIDE_COPY_GBPS, 4)},
+        # the timed region's Starts are enqueued behind a stream gate and run back to back once it opens
+        # (StreamGate); host_start_us is what one Start cost the host meanwhile
+        "timing": {"launches_held_behind_gate": min(GATE_HOLD, args.steps), "host_start_us": main["host_start_us"]},
     }
     if not args.no_extras:
         extras = {}
@@ -770,7 +808,7 @@ def single_gpu(args):
             st = 200 if nbytes <= (1 << 20) else 40 if nbytes <= (64 << 20) else 5
             r = node_run(R, cnt, tdtype, code, copyin, st, 2 if nbytes > (64 << 20) else 5,
                          min_set_bytes=0 if nbytes < (16 << 20) or nbytes > (64 << 20) else 640 * MIB,
-                         alloc=args.alloc)
+                         alloc=args.alloc, hold=2)
             sweep.append({"bytes_per_rank": cnt * tsize, "us_per_allreduce": round(r["wall_s"] * 1e6 / st, 2),
                           "gpu_us_per_allreduce": round(r["event_ms"] * 1e3 / st, 2),
                           "gbps_reduced": round(R * cnt * tsize * st / r["wall_s"] / 1e9, 2),
@@ -784,7 +822,7 @@ def single_gpu(args):
                 cnt = max(1, nbytes // tsize)
                 st = 200 if nbytes <= (1 << 20) else 40
                 r = node_run(R, cnt, tdtype, code, cp, st, 5, min_set_bytes=0 if nbytes < (16 << 20) else 640 * MIB,
-                             alloc=args.alloc)
+                             alloc=args.alloc, hold=2)
                 rsweep.append({"copyin": cp, "bytes_per_rank": cnt * tsize,
                                "us_per_allreduce": round(r["wall_s"] * 1e6 / st, 2),
                                "gpu_us_per_allreduce": round(r["event_ms"] * 1e3 / st, 2), "checked": r["checked"]})
@@ -820,11 +858,11 @@ def single_gpu(args):
         if "read_ceiling_gbps" in extras:
             lf["frac_of_measured_read_ceiling"] = round(lf["achieved_gbps"] / extras["read_ceiling_gbps"], 4)
         extras["local_fold_256MiB"] = lf
-        hst = node_run(R, count, tdtype, code, copyin, 10, 3, host=True)
+        hst = node_run(R, count, tdtype, code, copyin, 10, 3, host=True, hold=2)
         os.environ["EXT_MPI_AMD_HOST_DIRECT"] = "0"  # staged through device mirrors, for comparison
-        hst0 = node_run(R, count, tdtype, code, copyin, 10, 3, host=True)
+        hst0 = node_run(R, count, tdtype, code, copyin, 10, 3, host=True, hold=2)
         os.environ["EXT_MPI_AMD_PIPELINE"] = "1"  # the opt-in pipelined staging
-        hst1 = node_run(R, count, tdtype, code, copyin, 10, 3, host=True)
+        hst1 = node_run(R, count, tdtype, code, copyin, 10, 3, host=True, hold=2)
         del os.environ["EXT_MPI_AMD_PIPELINE"], os.environ["EXT_MPI_AMD_HOST_DIRECT"]
         extras["host_buffers_pcie_inclusive"] = {
             "gbps_reduced": round(R * S * 10 / hst["wall_s"] / 1e9, 2),
@@ -844,14 +882,15 @@ def single_gpu(args):
             r = node_run(R, (4 * MIB) // ts, td, cd, copyin, 50, 5, alloc=args.alloc)
             k = r["event_ms"] * 1e-3 / 50
             ints[dn] = {"gbps_reduced": round(R * 4 * MIB / k / 1e9, 1), "avg_launch_us": round(k * 1e6, 2),
-                        "achieved_gbps": round(2 * R * 4 * MIB / k / 1e9, 1), "bitexact": r["checked"]}
+                        "achieved_gbps": round(2 * R * 4 * MIB / k / 1e9, 1), "bitexact": r["checked"],
+                        "host_start_us": r["host_start_us"]}
         extras["config3_int_long_4MiB"] = ints
         # BASELINE configs[0] shape (tests/benchmark.c: 4 ranks, 64 KiB float, '6;1 -4 4') on this path
         c0 = (64 << 10) // 4
-        d0 = node_run(4, c0, torch.float32, emac.FLOAT, "6;1 -4 4", 400, 20, min_set_bytes=0, alloc=args.alloc)
-        h0 = node_run(4, c0, torch.float32, emac.FLOAT, "6;1 -4 4", 200, 20, host=True)
+        d0 = node_run(4, c0, torch.float32, emac.FLOAT, "6;1 -4 4", 400, 20, min_set_bytes=0, alloc=args.alloc, hold=2)
+        h0 = node_run(4, c0, torch.float32, emac.FLOAT, "6;1 -4 4", 200, 20, host=True, hold=2)
         os.environ["EXT_MPI_AMD_HOST_DIRECT"] = "0"
-        h1 = node_run(4, c0, torch.float32, emac.FLOAT, "6;1 -4 4", 200, 20, host=True)
+        h1 = node_run(4, c0, torch.float32, emac.FLOAT, "6;1 -4 4", 200, 20, host=True, hold=2)
         del os.environ["EXT_MPI_AMD_HOST_DIRECT"]
         extras["config0_64KiB_4ranks"] = {
             "device_us_per_allreduce": round(d0["wall_s"] * 1e6 / 400, 2),
