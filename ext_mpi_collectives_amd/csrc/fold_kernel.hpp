@@ -279,6 +279,10 @@ __device__ __forceinline__ void load_fold(const emac_bucket *b, long tile_base, 
   for (int u = 0; u < U; ++u) r[u] = fold_leaves<OP, T, N, CH>(x[u], c);
 }
 
+// ISSUE bit 19 (with kRemote): no store drain after each tile (fold_vectors); the fused node join
+// drains once per segment, before it counts the segment's items (join_fused.hip join_seg)
+constexpr int kNoDrain = 1 << 19;
+
 // One 16-byte vector stored under the launch's store policy.
 template <typename V, int ISSUE>
 __device__ __forceinline__ void store_vec(__attribute__((address_space(1))) V *dst, unsigned v, V r) {
@@ -313,8 +317,9 @@ __device__ __forceinline__ void fold_vectors(const emac_bucket *b, long tile_bas
     }
   }
   // a peer-mapped launch's stores are acknowledged by the owners' memory before the wave ends,
-  // so the barrier launch after it can signal without a release fence
-  if constexpr (REMOTE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // so the barrier launch after it can signal without a release fence (kNoDrain: the caller
+  // drains once for many items, join_fused.hip)
+  if constexpr (REMOTE && (ISSUE & kNoDrain) == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ISSUE bits 11-12 (kDeferShift): deferred stores. A workgroup takes KB = 2^k consecutive tiles

@@ -209,7 +209,7 @@ __global__ __launch_bounds__(JB) void join_fused_kernel(JoinSegs segs, int npart
       ns.slot = segs.slot[k];
       ns.tag = segs.e1[k];
       const bool ok = join_gate(ns, 0, segs.e0[k], &ctl->failed0[k]);
-      join_seg<T, 0, 1, 0, 1, 1 | kRemote>(segs.w[1][k], &ctl->tk[1][k], &ctl->done[1][k], &ctl->sig[1][k], xcodes,
+      join_seg<T, 0, 1, 0, 1, 1 | kRemote | kNoDrain>(segs.w[1][k], &ctl->tk[1][k], &ctl->done[1][k], &ctl->sig[1][k], xcodes,
                                            ns0.nranks, ok, ns, 1, segs.e1[k]);
     }
     if (s >= 2) {  // PL[k], after every node's phase 1 of part k
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(JB) void join_fused_kernel(JoinSegs segs, int npart
       ns.slot = segs.slot[k];
       ns.tag = segs.e1[k];
       const bool ok = join_gate(ns, 1, segs.e1[k], &ctl->failed1[k]);
-      join_seg<T, 1, 2, 0, R, 1 | kRemote>(segs.w[2][k], &ctl->tk[2][k], &ctl->done[2][k], &ctl->sig[2][k], codes, 0, ok,
+      join_seg<T, 1, 2, 0, R, 1 | kRemote | kNoDrain>(segs.w[2][k], &ctl->tk[2][k], &ctl->done[2][k], &ctl->sig[2][k], codes, 0, ok,
                                            ns, -1, 0);
     }
   }

@@ -2,8 +2,9 @@
 # Round 5: the fused join (1024-lane workgroups) at N = 1, 2 and 4 (processes sharing the GPU)
 # against the serial join, parts 2 and 4; EXT_MPI_AMD_JOIN_GRID = per-process workgroups before
 # the shared-GPU division. One line per run.
+# Usage: gpu_r05_join_sweep.sh [tag] ["N:parts:grid ..."] (default: the full sweep)
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r05/join_sweep2
+O=gpurun_out/r05/${1:-join_sweep2}
 mkdir -p $O
 port=29900
 run() {  # N parts grid
@@ -16,6 +17,10 @@ run() {  # N parts grid
 import json; d=json.load(open('$O/${tag}_r0.json'))
 print('$tag', 'start_to_wait %.1f' % (d['wall']*1e6/20), 'copy_in %.1f' % (d['copy_in_fold_s']*1e6), 'legs %.1f' % (d['node_legs_s']*1e6), 'checked', d['checked'])" | tee -a $O/summary.txt
 }
+if [ -n "$2" ]; then
+  for c in $2; do IFS=: read -r N p g <<< "$c"; run $N $p $g || exit 1; done
+  exit 0
+fi
 for N in 1 2 4; do
   run $N 1 256 || exit 1
   for g in 256 128; do for p in 2 4; do run $N $p $g || exit 1; done; done
