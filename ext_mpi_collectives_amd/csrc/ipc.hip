@@ -199,6 +199,18 @@ int emac_gpu_device_uuid(unsigned char *uuid) {
     return EMAC_ERR_DEVICE;
   }
   memcpy(uuid, u.bytes, 16);
+  // a runtime that reports no UUID (all zero) would make every GPU look alike, and the peer-mapped
+  // forms would then keep device-scope stores across GPUs: identify the device by its PCI location
+  static const unsigned char zero[16] = {0};
+  if (!memcmp(uuid, zero, 16)) {
+    int loc[3] = {-1, -1, -1};
+    (void)hipDeviceGetAttribute(&loc[0], hipDeviceAttributePciDomainID, dev);
+    (void)hipDeviceGetAttribute(&loc[1], hipDeviceAttributePciBusId, dev);
+    (void)hipDeviceGetAttribute(&loc[2], hipDeviceAttributePciDeviceId, dev);
+    clear_error("emac_gpu_device_uuid: PCI location");
+    uuid[0] = 0xff;  // never a real all-zero UUID
+    memcpy(uuid + 4, loc, sizeof(loc));
+  }
   return 0;
 }
 
