@@ -1064,6 +1064,9 @@ def _node_form_run(emac, comm, R, count, tdtype, code, copyin, steps, warmup, ra
         stream.synchronize()
         sched = emac.handle_schedule(handles[0])
         join_parts = emac.handle_join_parts(handles[0])
+        # how many distinct GPUs the nodes ran on (1 in the shared-GPU rehearsal; N on a real node)
+        devs = [None] * world
+        dist.all_gather_object(devs, str(torch.cuda.get_device_properties(torch.cuda.current_device()).uuid))
         # check set 0 against a float64 sum over every rank of every node (sampled)
         idx = np.arange(0, count, max(1, count // (1 << 18)))
         got = []
@@ -1108,7 +1111,7 @@ def _node_form_run(emac, comm, R, count, tdtype, code, copyin, steps, warmup, ra
                  "node_legs_s": part(emac.LEG_NODES_RS | emac.LEG_NODES_FOLD | emac.LEG_NODES_AG, steps),
                  "copy_out_s": part(emac.LEG_ALLGATHER, steps)}
         return {"wall": el.item(), "checked": bool(ok.item()), "schedule": sched, "nsets": nsets, "join_parts": join_parts,
-                **parts}
+                "distinct_devices": len(set(devs)), **parts}
     finally:
         for h in handles:
             emac.done(h)
@@ -1573,6 +1576,7 @@ def node_form_line(args, world, dname, rn, one_rank_per_gpu):
         # the peer-mapped join pipelined by parts (engine_join.c emac_join; 1: serial): its copy-ins
         # overlap the node legs, so start_to_wait can fall below the sum of the parts timed alone
         "join_parts": rn.get("join_parts"),
+        "distinct_devices": rn.get("distinct_devices"),
         "node_legs_xgmi_bound_us": round(xgmi_bound * 1e6, 1),
         "node_legs_frac_of_xgmi_bound": round(xgmi_bound / t_x, 3) if t_x > 0 else None,
         "value_per_gpu_gbps": round(R * S * steps / wall / 1e9, 2),
