@@ -491,9 +491,9 @@ __device__ __forceinline__ void fold_group_leaf(const emac_bucket *b, long gbase
 
 // The deferred-store schedule as a kernel of its own, so its code holds nothing of the per-tile
 // loop's: equal buckets of tpb tiles, or (MAP, round 5) up to EMAC_GROUP_MAP_MAX buckets of any
-// tile counts whose first groups the layout wrote into their tile0 (layout.c): the workgroup loads
-// those starts into LDS once, and a group's bucket is the number of starts at or below it, one
-// ballot over the table (the `-k` fractions' few short chunks beside a long one get the leaf-major
+// tile counts whose first groups the layout wrote into their tile0 (layout.c): each wave loads
+// those starts into its registers once, and a group's bucket is the number of starts at or below it,
+// one ballot (the `-k` fractions' few short chunks beside a long one get the leaf-major
 // and LDS groups instead of the per-tile loop).
 template <typename T, int OP, int N, int U, int CH, int D, int ISSUE, bool ALL_FULL, bool MAP = false>
 __device__ __forceinline__ void deferred_body(const emac_bucket *__restrict__ bk, long tpb, long ngroups,
@@ -508,21 +508,22 @@ __device__ __forceinline__ void deferred_body(const emac_bucket *__restrict__ bk
   // groups per bucket (the last one may hold fewer tiles); group counts fit 32 bits (< 2^31 groups
   // of >= 8 KiB), and 32-bit division is a short sequence ahead of the group's first load
   const unsigned gpb = MAP ? 1u : (unsigned)((tpb + KB - 1) / KB);
-  __shared__ unsigned g0[MAP ? EMAC_GROUP_MAP_MAX : 1];
+  // the bucket map in each wave's own registers: lane i holds bucket i's first group (no LDS table,
+  // no barrier ahead of the first leaf load)
+  unsigned gt = ~0u;
   if constexpr (MAP) {
     static_assert(!ALL_FULL, "bucket-mapped groups check their bucket's end");
-    static_assert(EMAC_GROUP_MAP_MAX <= 64, "one ballot over the table");
-    if (threadIdx.x < EMAC_GROUP_MAP_MAX) g0[threadIdx.x] = threadIdx.x < (unsigned)nb ? (unsigned)bk[threadIdx.x].tile0 : ~0u;
-    __syncthreads();
+    static_assert(EMAC_GROUP_MAP_MAX <= 64, "one lane per bucket of the map");
+    const unsigned lane = threadIdx.x & 63u;
+    if (lane < (unsigned)nb) gt = (unsigned)bk[lane].tile0;
   }
   for (long g = blockIdx.x; g < ngroups; g += gridDim.x) {
     int bi;
     long t0;
     int nt;
     if constexpr (MAP) {
-      const unsigned lane = threadIdx.x & 63u;
-      bi = __popcll(__ballot(g0[lane] <= (unsigned)g)) - 1;  // starts ascend: the last one <= g
-      t0 = (g - (long)g0[bi]) * KB;
+      bi = __popcll(__ballot(gt <= (unsigned)g)) - 1;  // starts ascend: the last one <= g
+      t0 = (g - (long)(unsigned)__builtin_amdgcn_readlane((int)gt, bi)) * KB;
       const long tb = (bk[bi].nvec + TILE - 1) / TILE;  // the bucket's tiles
       nt = tb - t0 < KB ? (int)(tb - t0) : KB;
     } else {
