@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--transport", default="ipc", choices=["ipc", "rccl"],
                     help="N > 1: peer-mapped hipIpc form (default) or RCCL point-to-point legs")
     ap.add_argument("--shape", default=None, choices=["local256", "node16", "node64", "node256", "node512", "copy256",
-                                                      "int4", "long4", "small"],
+                                                      "int4", "long4", "small", "joinci"],
                     help="profiling: run only this fold shape (40 launches) and exit (PMC passes, tools/gpu_pmc_r02.sh)")
     ap.add_argument("--schedules", default=None,
                     help="--shape node* / local256: comma-separated fold schedule words (U | issue << 4) to run in turn")
@@ -861,18 +861,14 @@ def single_gpu(args):
         hst = node_run(R, count, tdtype, code, copyin, 10, 3, host=True, hold=2)
         os.environ["EXT_MPI_AMD_HOST_DIRECT"] = "0"  # staged through device mirrors, for comparison
         hst0 = node_run(R, count, tdtype, code, copyin, 10, 3, host=True, hold=2)
-        os.environ["EXT_MPI_AMD_PIPELINE"] = "1"  # the opt-in pipelined staging
-        hst1 = node_run(R, count, tdtype, code, copyin, 10, 3, host=True, hold=2)
-        del os.environ["EXT_MPI_AMD_PIPELINE"], os.environ["EXT_MPI_AMD_HOST_DIRECT"]
+        del os.environ["EXT_MPI_AMD_HOST_DIRECT"]
         extras["host_buffers_pcie_inclusive"] = {
             "gbps_reduced": round(R * S * 10 / hst["wall_s"] / 1e9, 2),
             "ms_per_step": round(hst["wall_s"] * 1e3 / 10, 3),
-            "checked": hst["checked"] and hst0["checked"] and hst1["checked"],
+            "checked": hst["checked"] and hst0["checked"],
             "staged_gbps_reduced": round(R * S * 10 / hst0["wall_s"] / 1e9, 2),
-            "pipelined_gbps_reduced": round(R * S * 10 / hst1["wall_s"] / 1e9, 2),
             "note": "pinned host send/recv buffers read and written by the fold kernel over PCIe (default); "
-                    "staged: EXT_MPI_AMD_HOST_DIRECT=0, H2D -> fold -> D2H on one stream; pipelined: staged + "
-                    "EXT_MPI_AMD_PIPELINE=1, 8 element ranges on three streams, 3 warm-up Starts"}
+                    "staged: EXT_MPI_AMD_HOST_DIRECT=0, H2D -> fold -> D2H on one stream, 3 warm-up Starts"}
         # BASELINE configs[2]: int and long, 4 MiB per rank, 8 ranks; integer sums are exact in any
         # order, so the check against the float64 sum of the inputs is bit-exact (|values| <= 2^20
         # int, 2^40 long: every partial sum is exact in float64)
@@ -1657,6 +1653,58 @@ def small_sweep(emac, torch):
     return out
 
 
+def join_copyin_alone(emac, torch, steps=40):
+    """The peer-mapped node join's copy-in alone on a one-node communicator (configs[1]'s node, 8 ranks
+    x 16 MiB): the fused join's (join_fused_kernel, mode 1: CI segments only; EXT_MPI_AMD_JOIN_PARTS,
+    default 2) beside the serial join's tuned fold over the same bytes. Rotated buffer sets as the
+    headline. For rocprofv3 PMC passes every join_fused_kernel dispatch of this run is a copy-in."""
+    R, count = 8, 16 * MIB // 4
+    parts = os.environ.get("EXT_MPI_AMD_JOIN_PARTS", "2")
+    comm = emac.comm_init_ipc(0, 1, lambda p: [p], torch.cuda.current_device())
+    out = {}
+    try:
+        for label, p in (("fused", parts), ("serial", "1")):
+            os.environ["EXT_MPI_AMD_JOIN_PARTS"] = p
+            nsets = rotation_sets(R * count * 4, 2 * R * count * 4)
+            stream = torch.cuda.Stream()
+            sets, handles = [], []
+            for s in range(nsets):
+                sends = [DevBuf(count * 4) for _ in range(R)]
+                recvs = [DevBuf(count * 4) for _ in range(R)]
+                for r, b in enumerate(sends):
+                    b.upload(host_random(count, np.float32, 0x5EED0000 + 4099 * s + r))
+                h = emac.node_comm_allreduce_init([b.data_ptr() for b in sends], [b.data_ptr() for b in recvs], count,
+                                                  emac.FLOAT, comm, "6;1 -8 8")
+                emac.set_stream(h, stream.cuda_stream)
+                sets.append(sends + recvs)
+                handles.append(h)
+            try:
+                for k in range(nsets * TUNE_STARTS):  # the serial join's fold past its tuning
+                    emac.start_legs(handles[k % nsets], emac.LEG_FOLD)
+                stream.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for k in range(steps):
+                    emac.start_legs(handles[k % nsets], emac.LEG_FOLD)
+                e1.record(stream)
+                stream.synchronize()
+                us = e0.elapsed_time(e1) * 1e3 / steps
+                out[label] = {"join_parts": emac.handle_join_parts(handles[0]), "avg_launch_us": round(us, 2),
+                              "achieved_gbps": round((R + 1) * count * 4 / (us * 1e-6) / 1e9, 1),
+                              "schedule": emac.handle_schedule(handles[0])}
+                log(f"joinci {label}: {out[label]}")
+            finally:
+                for h in handles:
+                    emac.done(h)
+                for bs in sets:
+                    for b in bs:
+                        b.free()
+    finally:
+        os.environ["EXT_MPI_AMD_JOIN_PARTS"] = parts
+        emac.comm_free(comm)
+    return {"bytes_per_launch": (R + 1) * count * 4, **out}
+
+
 def shape_only(args):
     """One fold shape alone (for rocprofv3 PMC passes): the local fold (8 x 32 MiB -> 1) or the
     node-form Allreduce at 256 / 16 MiB per rank, 40 launches after warm-up."""
@@ -1678,6 +1726,8 @@ def shape_only(args):
         r = comm_shape_fold(8, MB // 8 // 4, torch.float32, emac.FLOAT, 40)
     elif args.shape == "small":
         r = small_sweep(emac, torch)
+    elif args.shape == "joinci":
+        r = join_copyin_alone(emac, torch)
     elif args.shape == "copy256":  # the node256 launch's bytes as a 1:1 copy (tools/ceiling.hip), same lease
         L = _ceiling_lib()
         n = 8 * MB  # 2 GiB read + 2 GiB written per launch, 3 buffer pairs rotated

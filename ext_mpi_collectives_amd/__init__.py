@@ -123,6 +123,7 @@ def lib():
         L.ext_mpi_amd_version.restype = ctypes.c_char_p
         L.ext_mpi_amd_build_info.restype = ctypes.c_char_p
         L.ext_mpi_amd_handle_join_parts.argtypes = [c_int]
+        L.ext_mpi_amd_handle_ipc_flags.argtypes = [c_int]
         L.ext_mpi_amd_gpu_malloc.argtypes = [P(c_void_p), ctypes.c_size_t]
         L.ext_mpi_amd_gpu_free.argtypes = [c_void_p]
         L.ext_mpi_amd_gpu_memcpy_hd.argtypes = [c_void_p, c_void_p, ctypes.c_size_t]
@@ -510,4 +511,14 @@ def handle_join_parts(h):
     """The parts a peer-mapped node join is pipelined by (1: serial), 0 for other handles."""
     n = lib().ext_mpi_amd_handle_join_parts(h)
     _check("ext_mpi_amd_handle_join_parts", min(n, 0))
+    return n
+
+
+IPC_CROSS_DEVICE, IPC_RELEASE_EVENT, IPC_SYS_STORES, IPC_DEV_STORES = 1, 2, 4, 8
+
+
+def handle_ipc_flags(h):
+    """A peer-mapped handle's cross-GPU settings (IPC_* bits, include/ext_mpi_amd.h), 0 for others."""
+    n = lib().ext_mpi_amd_handle_ipc_flags(h)
+    _check("ext_mpi_amd_handle_ipc_flags", min(n, 0))
     return n

@@ -49,7 +49,6 @@ void handle_release(emac_handle *h) {
     emac_gpu_stream_sync(h->stream);
     if (h->own_stream) emac_gpu_stream_destroy(h->stream);
   }
-  pipe_free(h->pipe);
   emac_gpu_free(h->d_buckets);
   emac_gpu_free(h->d_edges);
   emac_gpu_free(h->pull.d_buckets);
@@ -404,7 +403,6 @@ int ext_mpi_amd_start_legs(int handle, int legs) {
   int rc, key;
   if (!h) return EMAC_ERR_ARG;
   if (emac_gpu_set_device(h->device)) return EMAC_ERR_DEVICE;
-  if (h->pipe && (legs & EXT_MPI_AMD_LEG_ALL) == EXT_MPI_AMD_LEG_ALL) return pipe_start(h);
   key = legs & EXT_MPI_AMD_LEG_ALL;
   if (legs >> EMAC_LEG_STEP_SHIFT) { /* one node step alone (loopback lock-step): never captured */
     if ((rc = enqueue_legs(h, legs))) return rc;

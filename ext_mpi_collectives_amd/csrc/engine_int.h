@@ -6,8 +6,7 @@
  *   engine.c       handle table, buffer mapping, bucket upload, Start / Test / Wait / Done
  *   engine_tune.c  per-handle launch-schedule tuning of the fold, and the per-process cache of
  *                  tuned schedules shared by handles of one shape
- *   engine_node.c  NODE form (every node rank in this process), pipelined host staging, the
- *                  layout self-check
+ *   engine_node.c  NODE form (every node rank in this process), the layout self-check
  *   engine_comm.c  COMM form over RCCL (and the loopback test transport), the point-to-point legs
  *   engine_ipc.c   peer-mapped form (hipIpc over xGMI): mappings, the arena, node barriers
  *   engine_join.c  NODE form over several nodes (RCCL legs or peer-mapped shares)
@@ -101,7 +100,13 @@ typedef struct {
   unsigned long slot_epoch[EMAC_SYNC_SLOTS][2]; /* a slot's epochs continue across its handles */
   ipc_mirror *mirrors;
   int nmirrors;
-  int cross_device; /* some peer runs on another device: release to system scope before phase 0 */
+  int cross_device; /* some peer runs on another device: release to system scope before phase 0,
+                       system-scope partial stores in the fused node join. Agreed at set-up from
+                       the exchanged device UUIDs (or forced on every rank by
+                       EXT_MPI_AMD_TEST_CROSS_DEVICE=1 on any rank: the cross-GPU code paths on one
+                       GPU, tests/test_gpu_node_ipc.py) */
+  int same_device;  /* ranks of the communicator on this rank's device (itself included), from the
+                       UUIDs: the fused node join divides its grid by it */
   /* the arena (library memory the peers read: outboxes, send-buffer mirrors), ipc_allreduce_init */
   arena_seg seg[EMAC_ARENA_SEGS]; /* this rank's segments */
   int nseg;
@@ -121,8 +126,8 @@ typedef struct {
   int handle[EMAC_MAX_RANKS][MAX_LOOP_HANDLES];
 } loop_group;
 
-/* one fold launch over a set of device-resident buckets (a handle's main launch, or one part of
-   a pipelined host-staged NODE handle) */
+/* one fold launch over a set of device-resident buckets (a handle's main launch, or one stage of
+   one part of the pipelined node join) */
 typedef struct {
   emac_bucket *d_buckets;
   int nb;
@@ -193,19 +198,6 @@ typedef struct {
   int span_ops[EMAC_TUNE_SAMPLES];  /* the handle's operations inside each sample's timed span(s) */
 } emac_tune;
 
-/* NODE form with host buffers: the message is staged in EMAC_PIPE_PARTS element ranges so that
-   the H2D copies of part p+1, the fold of part p and the D2H copies of part p-1 overlap
-   (three streams, events between them) */
-#define EMAC_PIPE_PARTS 8
-#define EMAC_PIPE_MIN_BYTES (4L << 20) /* per rank */
-typedef struct {
-  int nparts;
-  long off[EMAC_PIPE_PARTS + 1]; /* element ranges */
-  emac_launch part[EMAC_PIPE_PARTS];
-  void *s_in, *s_out;
-  void *ev_start, *ev_in[EMAC_PIPE_PARTS], *ev_fold[EMAC_PIPE_PARTS], *ev_done;
-} emac_pipe;
-
 /* The peer-mapped node join pipelined by parts (engine_join.c, round 5; VERDICT r04 missing 2).
    The message is cut into nparts element ranges; part k's copy-in, share fold and pull + copy-out
    each have their own launch layout and part k its own synchronisation slot. Two executions:
@@ -222,6 +214,7 @@ typedef struct {
 typedef struct {
   int nparts;
   int fused; /* one launch per Start (join_fused.hip), else the streams form */
+  int sys_stores; /* fused: the copy-in's partials written through at system scope (a node on another GPU) */
   int grid;  /* the fused launch's workgroups */
   long lo[EMAC_JOIN_PARTS + 1]; /* part k: message elements [lo[k], lo[k + 1]) */
   int slot[EMAC_JOIN_PARTS];
@@ -282,7 +275,6 @@ typedef struct {
   emac_launch xfold[2 * EMAC_MAX_NODE_STEPS]; /* ... and, per exchange step, the fold of the lines' partials */
   void *graph[EXT_MPI_AMD_LEG_ALL + 1]; /* COMM form: captured legs, per subset of EXT_MPI_AMD_LEG_* */
   unsigned char graph_failed[EXT_MPI_AMD_LEG_ALL + 1];
-  emac_pipe *pipe; /* pipelined host staging (NODE form), or NULL */
   emac_tune tune;  /* launch-schedule tuning of the fold */
   /* NODE form over several nodes (ext_mpi_amd_node_comm_allreduce_init): every rank of this node
      in this process, the communicator's members being the nodes */
@@ -324,10 +316,6 @@ int fold_launch(emac_handle *h);
 /* engine_join.c */
 int join_start(emac_handle *h, int copyin, int legs);
 void join_free(emac_handle *h);
-
-/* engine_node.c */
-void pipe_free(emac_pipe *pp);
-int pipe_start(emac_handle *h);
 
 /* engine_comm.c */
 int node_radix(const emac_node_sched *ns, int st);

@@ -157,6 +157,7 @@ typedef struct {
   long len;      /* bytes the peers access (the sample spans them) */
   unsigned char sample[EMAC_SAMPLE_BYTES]; /* the exporter's own read of the buffer (ipc_exchange) */
   unsigned char uuid[16];                  /* communicator set-up: the exporter's device */
+  int force_cross; /* communicator set-up: EXT_MPI_AMD_TEST_CROSS_DEVICE=1 on the exporter */
   unsigned char free_slots[EMAC_SYNC_SLOTS / 8]; /* handle set-up: slots this rank can use */
 } ipc_export;
 
@@ -200,14 +201,30 @@ static int ipc_sync_exchange(emac_comm *cm, int rc, ipc_export *all) {
       mine.extent = emac_gpu_alloc_extent(cm->sync, &b0);
       mine.buf_id = emac_gpu_buffer_id(b0);
     }
+    /* a device this rank cannot identify fails the set-up on every rank: taken for the same device
+       as a peer on another GPU, it would keep device-scope stores between GPUs */
+    if (!rc) rc = emac_gpu_device_uuid(mine.uuid);
+    {
+      const char *fc = getenv("EXT_MPI_AMD_TEST_CROSS_DEVICE");
+      mine.force_cross = fc && atoi(fc) > 0;
+    }
     mine.status = rc == 0;
-    if (!rc) emac_gpu_device_uuid(mine.uuid);
     if (cm->ag(cm->ag_ctx, &mine, all, (long)sizeof(ipc_export))) return EMAC_ERR_TRANSPORT;
     for (r = 0; r < R; r++)
       if (!all[r].status) rc = rc ? rc : EMAC_ERR_TRANSPORT;
+    /* the same verdict on every rank: every rank sees every UUID and every test flag. A forced
+       verdict runs the cross-GPU code (system-scope release, system-scope partial stores of the
+       fused node join) with every rank on one GPU; same_device still counts the ranks really
+       sharing this device, so the fused join's grid stays divided among them */
     cm->cross_device = 0;
-    for (r = 0; !rc && r < R; r++)
-      if (memcmp(all[r].uuid, mine.uuid, 16)) cm->cross_device = 1;
+    cm->same_device = 0;
+    for (r = 0; !rc && r < R; r++) {
+      if (memcmp(all[r].uuid, mine.uuid, 16))
+        cm->cross_device = 1;
+      else
+        cm->same_device++;
+      if (all[r].force_cross) cm->cross_device = 1;
+    }
     for (r = 0; !rc && r < R; r++) {
       if (r == cm->rank) {
         cm->peer_sync[r] = cm->sync;
@@ -925,4 +942,15 @@ int ipc_status(const emac_handle *h) {
           (e & EMAC_SYNC_ERR_TIMEOUT) ? " a peer did not arrive within EXT_MPI_AMD_BARRIER_TIMEOUT" : "",
           (e & EMAC_SYNC_ERR_ABORTED) ? " a peer gave up on this Allreduce" : "");
   return EMAC_ERR_TRANSPORT;
+}
+
+int ext_mpi_amd_handle_ipc_flags(int handle) {
+  const emac_handle *h = handle_get(handle);
+  int f = 0;
+  if (!h) return EMAC_ERR_ARG;
+  if (h->kind != KIND_IPC) return 0;
+  if (g_comms[h->comm].cross_device) f |= EXT_MPI_AMD_IPC_CROSS_DEVICE;
+  if (h->ev_release) f |= EXT_MPI_AMD_IPC_RELEASE_EVENT;
+  if (h->join && h->join->fused) f |= h->join->sys_stores ? EXT_MPI_AMD_IPC_SYS_STORES : EXT_MPI_AMD_IPC_DEV_STORES;
+  return f;
 }

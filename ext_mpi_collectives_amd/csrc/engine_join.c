@@ -90,21 +90,32 @@ static int place_part(emac_bucket *b, const jproto *p, int n, long lo, long hi, 
   return nb;
 }
 
-/* the parts of the pipelined join: EXT_MPI_AMD_JOIN_PARTS (1: the serial join), else 2 over several
-   nodes from EMAC_JOIN_MIN_BYTES per rank. With nodes sharing one MI355X (16 MiB per rank, 8 ranks
-   per node) the fused join with 2 parts took 150.7 against 187.6 us per Start at 2 nodes and 274.8
-   against 389.6 at 4; 4 parts were no faster (profiles/r05/join/) */
-static int join_parts(const emac_handle *h, int nodes) {
-  const char *e = getenv("EXT_MPI_AMD_JOIN_PARTS");
-  int n = nodes > 1 && (long)h->bytes >= EMAC_JOIN_MIN_BYTES ? 2 : 1;
-  if (e && *e) n = atoi(e);
-  return n < 1 ? 1 : n > EMAC_JOIN_PARTS ? EMAC_JOIN_PARTS : n;
+/* The join's settings from this rank's environment; node_ipc_init takes rank 0's for every rank (the
+   ranks must run the same slot and epoch protocol, whatever their environments say):
+   EXT_MPI_AMD_JOIN_PARTS (0: unset), EXT_MPI_AMD_JOIN=streams, EXT_MPI_AMD_JOIN_SYSSTORE=1 (A/B:
+   system-scope partial stores in the fused join with every node on one GPU too) */
+typedef struct {
+  int parts, streams, sys_stores;
+} join_env;
+
+static join_env join_env_local(void) {
+  const char *p = getenv("EXT_MPI_AMD_JOIN_PARTS"), *j = getenv("EXT_MPI_AMD_JOIN"), *y = getenv("EXT_MPI_AMD_JOIN_SYSSTORE");
+  join_env e;
+  e.parts = p && *p ? atoi(p) : 0;
+  if (p && *p && e.parts < 1) e.parts = 1;
+  e.streams = j && !strcmp(j, "streams");
+  e.sys_stores = y && atoi(y) > 0;
+  return e;
 }
 
-/* the fused form unless EXT_MPI_AMD_JOIN=streams (the same on every rank: same environment) */
-static int join_fused_wanted(void) {
-  const char *e = getenv("EXT_MPI_AMD_JOIN");
-  return !(e && !strcmp(e, "streams"));
+/* the parts of the pipelined join: the agreed EXT_MPI_AMD_JOIN_PARTS (1: the serial join), else 2
+   over several nodes from EMAC_JOIN_MIN_BYTES per rank. With nodes sharing one MI355X (16 MiB per
+   rank, 8 ranks per node) the fused join with 2 parts took 150.7 against 187.6 us per Start at 2
+   nodes and 274.8 against 389.6 at 4; 4 parts were no faster (profiles/r05/join/) */
+static int join_parts(const emac_handle *h, int nodes, int env_parts) {
+  int n = nodes > 1 && (long)h->bytes >= EMAC_JOIN_MIN_BYTES ? 2 : 1;
+  if (env_parts > 0) n = env_parts;
+  return n < 1 ? 1 : n > EMAC_JOIN_PARTS ? EMAC_JOIN_PARTS : n;
 }
 
 /* a launch of nb buckets of nsrc leaves with the tiles of schedule `unroll` (the fused join's
@@ -158,6 +169,7 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
     int status;
     int seg[2];
     long offset[2];
+    join_env env; /* rank 0's is every rank's */
     unsigned char free_slots[EMAC_SYNC_SLOTS / 8];
   } nx_export;
   nx_export mine, all[EMAC_MAX_RANKS];
@@ -168,8 +180,12 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
   jproto *pin = NULL, *psh = NULL, *ppl = NULL;
   const int N = cm->size, R = h->plan.nranks;
   const long ts = h->plan.tsize;
+  emac_join *J = NULL;
+  join_env env;
   int attempt, r, k, me, i, slot, pc, nparts, pslot[EMAC_JOIN_PARTS], nin = 0, nshr = 0, npl = 0;
   h->part_bytes = h->outbox_bytes = h->bytes > 16 ? h->bytes : 16;
+  /* the pipelined join's state, before the exchange: a failure here is in its verdict */
+  if (!rc && !(J = (emac_join *)calloc(1, sizeof(emac_join)))) rc = EMAC_ERR_MALLOC;
   for (attempt = 0;; attempt++) {
     long lack = 0;
     int grow = 0;
@@ -189,19 +205,24 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
       }
     }
     mine.lack = rc ? 0 : lack;
+    mine.env = join_env_local();
     mine.status = rc == 0;
     for (r = 0; r < EMAC_SYNC_SLOTS; r++)
       if (!cm->slot_used[r]) mine.free_slots[r >> 3] |= (unsigned char)(1u << (r & 7));
-    if (cm->ag(cm->ag_ctx, &mine, all, (long)sizeof(mine))) return EMAC_ERR_TRANSPORT;
-    for (r = 0; r < N; r++) {
-      if (!all[r].status && !rc) rc = EMAC_ERR_TRANSPORT;
+    if (cm->ag(cm->ag_ctx, &mine, all, (long)sizeof(mine))) rc = EMAC_ERR_TRANSPORT;
+    for (r = 0; !rc && r < N; r++) {
+      if (!all[r].status) rc = EMAC_ERR_TRANSPORT;
       if (all[r].lack > 0) grow = 1;
     }
-    if (rc) return rc; /* the same verdict on every rank */
-    if (!grow) break;
-    if (attempt == EMAC_IPC_ATTEMPTS - 1) return EMAC_ERR_MALLOC;
-    if ((rc = arena_grow(cm, 0, lack))) return rc;
+    if (!rc && grow && attempt == EMAC_IPC_ATTEMPTS - 1) rc = EMAC_ERR_MALLOC;
+    if (!rc && grow) rc = arena_grow(cm, 0, lack);
+    if (rc || !grow) break; /* the same verdict on every rank */
   }
+  if (rc) {
+    free(J);
+    return rc;
+  }
+  env = all[0].env;
   for (r = 0; r < N; r++) {
     if (r == cm->rank) {
       peer_part[r] = h->part;
@@ -212,17 +233,22 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
     peer_out[r] = all[r].seg[1] < cm->peer_nseg[r] ? (char *)cm->peer_seg[r][all[r].seg[1]] + all[r].offset[1] : NULL;
     if (!peer_part[r] || !peer_out[r]) rc = EMAC_ERR_TRANSPORT;
   }
-  if ((rc = ipc_agree(cm, rc == 0))) return rc;
-  /* the pipelined join (EXT_MPI_AMD_JOIN_PARTS, emac_join): the same part count on every rank (the
-     message size and the environment are the same), one slot per part */
+  if ((rc = ipc_agree(cm, rc == 0))) {
+    free(J);
+    return rc;
+  }
+  /* the pipelined join (emac_join): the same part count on every rank (the message size and rank
+     0's environment), one slot per part */
   /* the share fold's tree: the halving flow folds log2 N levels of pairs, one step over every node a
      left fold */
-  if ((rc = node_fold_codes(N, N > 1 && emac_node_single(&h->ns) == 2 ? h->ns.nsteps : 1, h->plan.dtype, &h->xcodes)))
+  if ((rc = node_fold_codes(N, N > 1 && emac_node_single(&h->ns) == 2 ? h->ns.nsteps : 1, h->plan.dtype, &h->xcodes))) {
+    free(J);
     return rc; /* (a function of the shape alone: the same on every rank) */
-  nparts = join_parts(h, N);
+  }
+  nparts = join_parts(h, N, env.parts);
   /* a shape the fused join has no kernel for (leaf counts other than 1, 2, 4, 8, MIN / MAX,
      irregular fold trees) keeps the serial join -- the same verdict on every rank (same shape) */
-  if (nparts > 1 && join_fused_wanted() &&
+  if (nparts > 1 && !env.streams &&
       (h->plan.op != EMAC_SUM || emac_gpu_join_fused(h->plan.dtype, R, &h->plan.codes, &h->xcodes, nparts, 3, NULL, NULL, NULL,
                                                      NULL, NULL, NULL, N, cm->rank, NULL, 0, NULL, 0, NULL)))
     nparts = 1;
@@ -231,13 +257,19 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
       for (r = 0; r < N && (all[r].free_slots[slot >> 3] >> (slot & 7)) & 1; r++);
       if (r == N) break;
     }
-    if (slot == EMAC_SYNC_SLOTS) return EMAC_ERR_MALLOC; /* the same verdict on every rank */
+    if (slot == EMAC_SYNC_SLOTS) {
+      free(J);
+      return EMAC_ERR_MALLOC; /* the same verdict on every rank */
+    }
     pslot[k] = slot;
   }
   if (nparts > 1) {
-    if (!(h->join = (emac_join *)calloc(1, sizeof(emac_join)))) return EMAC_ERR_MALLOC; /* (all ranks: see above) */
+    h->join = J;
     h->join->nparts = nparts;
-    h->join->fused = join_fused_wanted();
+    h->join->fused = !env.streams;
+    /* the copy-in's partials go to memory at system scope when some node runs on another GPU
+       (every rank has the same cross_device verdict), else at device scope */
+    h->join->sys_stores = cm->cross_device || env.sys_stores;
     for (k = 0; k < nparts; k++) {
       h->join->slot[k] = pslot[k];
       cm->slot_used[pslot[k]] = 1;
@@ -245,6 +277,8 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
       h->join->epoch[k][0] = cm->slot_epoch[pslot[k]][0];
       h->join->epoch[k][1] = cm->slot_epoch[pslot[k]][1];
     }
+  } else {
+    free(J);
   }
   slot = pslot[0];
   h->slot = slot;
@@ -349,9 +383,10 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
     }
     if (!rc && (rc = emac_gpu_malloc(&J->ctl, sizeof(emac_join_ctl))) == 0) rc = emac_gpu_memcpy(J->ctl, &zero, sizeof(zero));
     if (!rc) {
-      /* join_fused.hip: one 1024-lane workgroup per CU; nodes sharing this GPU (the 1-GPU rehearsal)
-         divide it, so every node's workgroups find room beside the others' waiting ones */
-      const int g = emac_gpu_join_grid() / (cm->cross_device || N < 2 ? 1 : N);
+      /* join_fused.hip: one 1024-lane workgroup per CU; the nodes sharing this GPU (by UUID: the
+         1-GPU rehearsal, or a mixed placement) divide it, so every node's workgroups find room
+         beside the others' waiting ones */
+      const int g = emac_gpu_join_grid() / (cm->same_device > 1 ? cm->same_device : 1);
       J->grid = g < 8 ? 8 : g > 4096 ? 4096 : g;
     }
   } else { /* part k: the buckets' elements inside [lo[k], lo[k + 1]) */
@@ -610,8 +645,7 @@ int join_start(emac_handle *h, int copyin, int legs) {
       }
     }
     h->tune.ops++;
-    const char *e = getenv("EXT_MPI_AMD_JOIN_SYSSTORE"); /* A/B: 1 system-scope partial stores on one GPU too */
-    const int dev_scope = !cm->cross_device && !(e && atoi(e) > 0);
+    const int dev_scope = !J->sys_stores;
     return emac_gpu_join_fused(h->plan.dtype, h->nsrc, &h->plan.codes, &h->xcodes, J->nparts,
                                (copyin ? 1 : 0) | (legs ? 2 : 0) | (dev_scope ? 4 : 0),
                                seg, J->slot, e0, e1, cm->sync, (void *const *)cm->d_peer_sync, N, cm->rank,

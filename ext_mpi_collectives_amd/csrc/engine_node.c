@@ -1,7 +1,6 @@
 /*
  * engine_node.c -- the NODE form: every node rank's buffers in this process on one device, one
- * fold launch per Start (copy-in and copy-out fused); pipelined staging of host buffers; the
- * host-side layout self-check of the planner / layout pair (engine_int.h).
+ * fold launch per Start (copy-in and copy-out fused); the host-side layout self-check of the planner / layout pair (engine_int.h).
  */
 #include "engine_int.h"
 
@@ -26,55 +25,6 @@ static int node_buckets(const emac_handle *h, long lo, long hi, emac_bucket *b) 
     }
   }
   return nb;
-}
-
-/* Pipelined staging of a NODE handle whose buffers are mirrored host memory: the message in
-   EMAC_PIPE_PARTS element ranges, each its own fold launch between its copies (ext_mpi_amd_start). */
-static int node_pipe_init(emac_handle *h) {
-  emac_pipe *pp;
-  emac_bucket *pb;
-  const long count = (long)(h->bytes / (size_t)h->plan.tsize);
-  long step;
-  int r, p, any = 0, rc = 0;
-  for (r = 0; r < h->nbuf; r++) any |= h->send_mirror[r] | h->recv_mirror[r];
-  /* opt-in (EXT_MPI_AMD_PIPELINE=1): +12-25 % in a process with few streams, but down to -8 % in
-     one that has made many (hardware-queue sharing) */
-  if (!any || (long)h->bytes < EMAC_PIPE_MIN_BYTES || !getenv("EXT_MPI_AMD_PIPELINE") ||
-      atoi(getenv("EXT_MPI_AMD_PIPELINE")) <= 0)
-    return 0;
-  pp = (emac_pipe *)calloc(1, sizeof(emac_pipe));
-  pb = (emac_bucket *)calloc((size_t)h->plan.npieces * (size_t)h->plan.nranks, sizeof(emac_bucket));
-  if (!pp || !pb) {
-    free(pp);
-    free(pb);
-    return EMAC_ERR_MALLOC;
-  }
-  h->pipe = pp;
-  {
-    const char *np = getenv("EXT_MPI_AMD_PIPE_PARTS");
-    pp->nparts = np ? atoi(np) : EMAC_PIPE_PARTS;
-    if (pp->nparts < 1 || pp->nparts > EMAC_PIPE_PARTS) pp->nparts = EMAC_PIPE_PARTS;
-  }
-  step = ((count + pp->nparts - 1) / pp->nparts + 4095) / 4096 * 4096; /* 16-byte aligned ranges, any type */
-  for (p = 0; p < pp->nparts; p++) pp->off[p] = (long)p * step < count ? (long)p * step : count;
-  pp->off[pp->nparts] = count;
-  for (p = 0; p < pp->nparts && !rc; p++) {
-    const int n = node_buckets(h, pp->off[p], pp->off[p + 1], pb);
-    rc = upload_launch(h, &pp->part[p], pb, n);
-    if (!rc) rc = emac_gpu_event_create(&pp->ev_in[p]);
-    if (!rc) rc = emac_gpu_event_create(&pp->ev_fold[p]);
-  }
-  free(pb);
-  if (!rc) rc = emac_gpu_event_create(&pp->ev_start);
-  if (!rc) rc = emac_gpu_event_create(&pp->ev_done);
-  /* The copy streams get an explicit (least) priority: streams of the default priority share the
-     process's few hardware queues round-robin, and a copy stream that landed on the fold
-     stream's queue serialised the pipeline (8 x 16 MiB pinned: 20-22 GB/s reduced against 25-26
-     unpipelined, depending on how many streams the process had made before); on a priority's own
-     queues it ran at 29-31 GB/s whatever came before (profiles/r01_host_pipeline_priority.json). */
-  if (!rc) rc = emac_gpu_stream_create_priority(&pp->s_in, 0);
-  if (!rc) rc = emac_gpu_stream_create_priority(&pp->s_out, 0);
-  return rc;
 }
 
 int ext_mpi_amd_node_allreduce_init(int nranks, const void *const *sendbufs, void *const *recvbufs, long count,
@@ -105,7 +55,6 @@ int ext_mpi_amd_node_allreduce_init(int nranks, const void *const *sendbufs, voi
     goto fail;
   }
   nb = node_buckets(h, 0, count, b);
-  if ((rc = node_pipe_init(h))) goto fail; /* first: a pipelined handle's main fold is never tuned */
   if ((rc = upload_buckets(h, b, nb))) goto fail;
   free(b);
   b = NULL;
@@ -156,65 +105,6 @@ int ext_mpi_amd_fold_init(int nsrc, const void *const *srcs, int ndst, void *con
 fail:
   handle_release(h);
   return rc;
-}
-
-void pipe_free(emac_pipe *pp) {
-  int p;
-  if (!pp) return;
-  if (pp->s_in) emac_gpu_stream_sync(pp->s_in);
-  if (pp->s_out) emac_gpu_stream_sync(pp->s_out);
-  for (p = 0; p < pp->nparts; p++) {
-    emac_gpu_free(pp->part[p].d_buckets);
-    emac_gpu_free(pp->part[p].d_edges);
-    emac_gpu_event_destroy(pp->ev_in[p]);
-    emac_gpu_event_destroy(pp->ev_fold[p]);
-  }
-  emac_gpu_event_destroy(pp->ev_start);
-  emac_gpu_event_destroy(pp->ev_done);
-  if (pp->s_in) emac_gpu_stream_destroy(pp->s_in);
-  if (pp->s_out) emac_gpu_stream_destroy(pp->s_out);
-  free(pp);
-}
-
-/* A pipelined NODE Start: H2D of every part on s_in, the part's fold on the handle's stream
-   after its copies, its D2H on s_out after its fold; the handle's stream then waits for the
-   last D2H, so Wait / Test and the next Start see the whole Allreduce. */
-int pipe_start(emac_handle *h) {
-  emac_pipe *pp = h->pipe;
-  const size_t ts = (size_t)h->plan.tsize;
-  int p, r, rc;
-  /* the caller's earlier work on the handle's stream (and the previous Start) comes first */
-  if ((rc = emac_gpu_event_record(pp->ev_start, h->stream)) || (rc = emac_gpu_stream_wait(pp->s_in, pp->ev_start)))
-    return rc;
-  for (p = 0; p < pp->nparts; p++) {
-    const size_t o = (size_t)pp->off[p] * ts, n = (size_t)(pp->off[p + 1] - pp->off[p]) * ts;
-    for (r = 0; r < h->nbuf && n; r++) {
-      const void *src = h->send_mirror[r] ? h->user_send[r]
-                                          : (h->recv_mirror[r] && h->dsend[r] == h->drecv[r] ? h->user_recv[r] : NULL);
-      if (src && (rc = emac_gpu_memcpy_async((char *)h->dsend[r] + o, (const char *)src + o, n, pp->s_in))) return rc;
-    }
-    if ((rc = emac_gpu_event_record(pp->ev_in[p], pp->s_in))) return rc;
-  }
-  for (p = 0; p < pp->nparts; p++) {
-    const emac_launch *L = &pp->part[p];
-    if ((rc = emac_gpu_stream_wait(h->stream, pp->ev_in[p]))) return rc;
-    if ((rc = emac_gpu_fold(h->plan.dtype, h->plan.op, h->nsrc, h->fan, L->unroll, &h->plan.codes, L->d_buckets, L->nb,
-                            L->ntiles, L->tiles_per_bucket, L->all_full, L->d_edges, L->nedges, h->stream)))
-      return rc;
-    if ((rc = emac_gpu_event_record(pp->ev_fold[p], h->stream))) return rc;
-  }
-  for (p = 0; p < pp->nparts; p++) {
-    const size_t o = (size_t)pp->off[p] * ts, n = (size_t)(pp->off[p + 1] - pp->off[p]) * ts;
-    if ((rc = emac_gpu_stream_wait(pp->s_out, pp->ev_fold[p]))) return rc;
-    for (r = 0; r < h->nbuf && n; r++)
-      if (h->recv_mirror[r] &&
-          (rc = emac_gpu_memcpy_async((char *)h->user_recv[r] + o, (const char *)h->drecv[r] + o, n, pp->s_out)))
-        return rc;
-  }
-  if ((rc = emac_gpu_event_record(pp->ev_done, pp->s_out)) || (rc = emac_gpu_stream_wait(h->stream, pp->ev_done)))
-    return rc;
-  h->started = 1;
-  return 0;
 }
 
 /* ---- layout self-check (host only, no device): the NODE form's buckets and launch layout for

@@ -94,9 +94,8 @@ static int tune_candidates(const emac_handle *h, long vec, int *sched) {
   const char *g = getenv("EXT_MPI_AMD_GRAPH"); /* captured Starts replay one schedule */
   const int tree = emac_tree_kind(&h->plan.codes, h->plan.op);
   int n = 0;
-  /* (the pipelined host-staged NODE handle never launches its main fold: pipe_start folds parts) */
   if ((e && atoi(e) <= 0) || (h->kind == KIND_COMM && g && atoi(g) > 0) || h->plan.op != EMAC_SUM || h->nsrc < 2 ||
-      h->nsrc > 8 || h->host_direct || h->pipe || tree == 1 || (h->fan != 0 && h->fan != 1))
+      h->nsrc > 8 || h->host_direct || tree == 1 || (h->fan != 0 && h->fan != 1))
     return 0;
   /* fold_kernel.hpp instantiation policy: (U 2, burst), (U 4, burst), for the node fan-out (U 4,
      s_sleep 2 every 4 loads); deferred stores (kDeferShift) when every bucket has the same tile

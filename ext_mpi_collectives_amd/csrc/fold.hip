@@ -276,17 +276,6 @@ int emac_gpu_stream_create(void **stream) {
   *stream = s;
   return 0;
 }
-int emac_gpu_stream_create_priority(void **stream, int high) {
-  hipStream_t s;
-  int lo = 0, hi = 0;
-  if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) {
-    clear_error("emac_gpu_stream_create_priority");
-    return emac_gpu_stream_create(stream);
-  }
-  if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? hi : lo) != hipSuccess) return EMAC_ERR_DEVICE;
-  *stream = s;
-  return 0;
-}
 int emac_gpu_stream_destroy(void *stream) { return ok(hipStreamDestroy(static_cast<hipStream_t>(stream))); }
 int emac_gpu_stream_sync(void *stream) { return ok(hipStreamSynchronize(static_cast<hipStream_t>(stream))); }
 int emac_gpu_stream_query(void *stream) {

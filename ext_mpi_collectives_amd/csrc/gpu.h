@@ -58,7 +58,6 @@ int emac_gpu_pinned_view(const void *p, void **dev); /* page-locked host memory:
 int emac_gpu_host_register(void *p, size_t bytes);
 int emac_gpu_host_unregister(void *p);
 int emac_gpu_stream_create(void **stream);
-int emac_gpu_stream_create_priority(void **stream, int high); /* non-blocking, greatest / least priority */
 int emac_gpu_stream_destroy(void *stream);
 int emac_gpu_stream_sync(void *stream);
 int emac_gpu_stream_query(void *stream); /* 1 idle, 0 busy, <0 error */

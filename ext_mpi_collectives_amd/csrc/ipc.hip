@@ -204,10 +204,13 @@ int emac_gpu_device_uuid(unsigned char *uuid) {
   static const unsigned char zero[16] = {0};
   if (!memcmp(uuid, zero, 16)) {
     int loc[3] = {-1, -1, -1};
-    (void)hipDeviceGetAttribute(&loc[0], hipDeviceAttributePciDomainID, dev);
-    (void)hipDeviceGetAttribute(&loc[1], hipDeviceAttributePciBusId, dev);
-    (void)hipDeviceGetAttribute(&loc[2], hipDeviceAttributePciDeviceId, dev);
-    clear_error("emac_gpu_device_uuid: PCI location");
+    if (hipDeviceGetAttribute(&loc[0], hipDeviceAttributePciDomainID, dev) != hipSuccess ||
+        hipDeviceGetAttribute(&loc[1], hipDeviceAttributePciBusId, dev) != hipSuccess ||
+        hipDeviceGetAttribute(&loc[2], hipDeviceAttributePciDeviceId, dev) != hipSuccess) {
+      // no identity at all: every GPU would look alike (the caller fails the set-up)
+      clear_error("emac_gpu_device_uuid: PCI location");
+      return EMAC_ERR_DEVICE;
+    }
     uuid[0] = 0xff;  // never a real all-zero UUID
     memcpy(uuid + 4, loc, sizeof(loc));
   }

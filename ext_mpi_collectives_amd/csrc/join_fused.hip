@@ -29,6 +29,11 @@
 // stores; both are reported through the slot's error word, as the serial join's barriers do, and
 // the next Start synchronises normally (epochs keep counting). The last workgroup out resets the
 // control block for the next Start (stream order).
+// One relaxation of the serial join's rule (a rank that times out in phase 0 folds nothing): here the
+// verdict is per workgroup. A workgroup that passed the phase-0 gate before another one timed out
+// and published the abandon marks still folds and stores its share items. Nothing is corrupted --
+// those stores go only to this node's own outbox, and the Start is reported failed on every node
+// through the marks and the slot's error word -- but part of a failed Start's share may be stored.
 #include <stdlib.h>
 #include <string.h>
 

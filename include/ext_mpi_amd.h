@@ -272,6 +272,17 @@ int ext_mpi_amd_set_num_sockets(int sockets);
  * EXT_MPI_AMD_JOIN_PARTS, engine_join.c), 0 for any other handle, or EXT_MPI_AMD_ERROR_ARG. */
 int ext_mpi_amd_handle_join_parts(int handle);
 
+/* A peer-mapped handle's cross-GPU settings (diagnostics for tests; no reference counterpart), as
+ * EXT_MPI_AMD_IPC_* bits: the communicator's agreed verdict that some rank runs on another device
+ * (device UUIDs exchanged at ext_mpi_amd_comm_init_ipc, or EXT_MPI_AMD_TEST_CROSS_DEVICE=1 on any
+ * rank), a system-scope release recorded before every phase-0 barrier, and the fused node join's
+ * partial stores at system or device scope. 0 for other handles, EXT_MPI_AMD_ERROR_ARG for none. */
+#define EXT_MPI_AMD_IPC_CROSS_DEVICE 1
+#define EXT_MPI_AMD_IPC_RELEASE_EVENT 2
+#define EXT_MPI_AMD_IPC_SYS_STORES 4
+#define EXT_MPI_AMD_IPC_DEV_STORES 8
+int ext_mpi_amd_handle_ipc_flags(int handle);
+
 const char *ext_mpi_amd_version(void);
 /* "sha <commit>[+dirty] src <hash>": the commit and the hash of the product sources (csrc/,
  * include/) this binary was built from (ext_mpi_collectives_amd/_stamp.py). No reference

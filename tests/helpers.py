@@ -50,3 +50,21 @@ def replay_plan(sends, code, copyin, sockets=1):
                         cur = acc[lvl]
             out[seg] = cur
     return out
+
+
+def ipc_flags_problem(h, world, join_parts=None):
+    """None if the peer-mapped handle `h` runs the cross-GPU code exactly when the communicator was
+    told to (EXT_MPI_AMD_TEST_CROSS_DEVICE=1: tests on one GPU, whose device UUIDs all match), else
+    what differs. The flags (emac.handle_ipc_flags): the agreed cross-device verdict, the
+    system-scope release before every phase 0 (engine_ipc.c, engine_join.c), and -- for a fused
+    node join (`join_parts` > 1 without EXT_MPI_AMD_JOIN=streams) -- system-scope partial stores,
+    i.e. the join_fused_kernel<..., true> instantiation (join_fused.hip)."""
+    import os
+    cross = os.environ.get("EXT_MPI_AMD_TEST_CROSS_DEVICE", "0") not in ("", "0")
+    f = emac.handle_ipc_flags(h)
+    want = emac.IPC_CROSS_DEVICE if cross else 0
+    if world > 1 and (cross or os.environ.get("EXT_MPI_AMD_IPC_RELEASE", "0") not in ("", "0")):
+        want |= emac.IPC_RELEASE_EVENT
+    if join_parts and join_parts > 1 and os.environ.get("EXT_MPI_AMD_JOIN") != "streams":
+        want |= emac.IPC_SYS_STORES if cross else emac.IPC_DEV_STORES
+    return None if f == want else f"ipc flags {f:#x}, want {want:#x}"

@@ -20,7 +20,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import ext_mpi_collectives_amd as emac  # noqa: E402
-from helpers import xorshift_inputs  # noqa: E402
+from helpers import ipc_flags_problem, xorshift_inputs  # noqa: E402
 from oracle import oracle  # noqa: E402
 
 TORCH = {emac.FLOAT: torch.float32, emac.DOUBLE: torch.float64, emac.INT: torch.int32, emac.LONG: torch.int64}
@@ -207,6 +207,10 @@ def main():
             recv = send if in_place else torch.full((count,), -1, dtype=TORCH[code], device="cuda")
             h = emac.allreduce_init(send.data_ptr(), recv.data_ptr(), count, code, comm, copyin, op=op)
         ok = True
+        why = ipc_flags_problem(h, world)
+        if why:
+            print(f"IPC rank {rank}/{world} case {k}: {why}", flush=True)
+            ok = False
         for _ in range(repeats):
             if raw:
                 src = np.ascontiguousarray(sends[rank])

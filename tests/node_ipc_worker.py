@@ -23,7 +23,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import ext_mpi_collectives_amd as emac  # noqa: E402
-from helpers import xorshift_inputs  # noqa: E402
+from helpers import ipc_flags_problem, xorshift_inputs  # noqa: E402
 from oracle import oracle  # noqa: E402
 
 TORCH = {emac.FLOAT: torch.float32, emac.DOUBLE: torch.float64, emac.INT: torch.int32, emac.LONG: torch.int64}
@@ -87,7 +87,9 @@ def timeout_recovery(node, N, dev):
     want = float(N * R * (N * R + 1) // 2)
     h = emac.node_comm_allreduce_init([s.data_ptr() for s in sbufs], [r.data_ptr() for r in rbufs], count, emac.FLOAT,
                                       comm, "6;1 -2 2")
-    verdicts = []
+    parts = emac.handle_join_parts(h)
+    why = ipc_flags_problem(h, N, parts)
+    verdicts = [why] if why else []
     for it in range(3):
         dist.barrier()
         for r in rbufs:
@@ -105,7 +107,7 @@ def timeout_recovery(node, N, dev):
     emac.done(h)
     emac.comm_free(comm)
     ok = verdicts == ["ok", "failed", "ok"]
-    print(f"NODEIPC node {node}/{N} timeout recovery (join parts {os.environ.get('EXT_MPI_AMD_JOIN_PARTS', 'default')}): "
+    print(f"NODEIPC node {node}/{N} timeout recovery (join parts {parts}): "
           f"{'ok' if ok else verdicts}", flush=True)
     return ok
 
@@ -137,6 +139,10 @@ def main():
         h = emac.node_comm_allreduce_init(sbufs, rbufs, count, code, comm, copyin, op=op)
         parts = emac.handle_join_parts(h)
         ok = True
+        why = ipc_flags_problem(h, N, parts)
+        if why:
+            print(f"node {node}/{N} case {k}: {why}", flush=True)
+            ok = False
         for rep in range(repeats):
             sends = xorshift_inputs(W, count, code, seed_base=0x40DE0000 + 977 * k + 31 * rep)
             want = oracle.allreduce_nodes(sends, copyin, N, ports=ports if ports is not None else

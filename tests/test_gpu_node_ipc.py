@@ -30,12 +30,15 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run_nodes(nodes, budget=180, **extra_env):
+def _run_nodes(nodes, budget=180, rank_env=None, **extra_env):
+    """Run `nodes` node_ipc_worker processes (rank_env(r): extra environment of node r only); every
+    case line of every node must end in ': ok'. Returns node 0's case lines."""
     port = _port()
     procs, logs = [], []
     for r in range(nodes):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(nodes), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), IPC_DEVICE="0", EXT_MPI_AMD_BARRIER_TIMEOUT="20", **extra_env)
+        env.update(rank_env(r) if rank_env else {})
         logs.append(tempfile.TemporaryFile(mode="w+"))
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "node_ipc_worker.py")],
                                       env=env, stdout=logs[-1], stderr=subprocess.STDOUT, text=True))
@@ -61,6 +64,10 @@ def _run_nodes(nodes, budget=180, **extra_env):
     lines = [l for o in outs for l in o.splitlines() if l.startswith("NODEIPC")]
     assert lines and len(lines) == nodes * sum(1 for l in lines if l.startswith("NODEIPC node 0/")), tails
     print("\n".join(l for l in lines if l.startswith("NODEIPC node 0/")))
+    for r in range(1, nodes):  # every node ran every case with the same join (parts agreed on rank 0's)
+        assert [l.split("join parts")[-1] for l in lines if l.startswith(f"NODEIPC node {r}/") and "join parts" in l] == \
+            [l.split("join parts")[-1] for l in lines if l.startswith("NODEIPC node 0/") and "join parts" in l], tails
+    return [l for l in lines if l.startswith("NODEIPC node 0/")]
 
 
 @pytest.mark.parametrize("nodes", [2, 3, 4, 8])
@@ -82,3 +89,28 @@ def test_node_join_serial_and_pipelined(nodes, join):
     if join.startswith("streams"):
         env["EXT_MPI_AMD_JOIN"] = "streams"
     _run_nodes(nodes, budget=300 if nodes >= 8 else 180, **env)
+
+
+@pytest.mark.parametrize("join", ["default", "serial", "fused3", "fused4"])
+@pytest.mark.parametrize("nodes", [2, 4, 8])
+def test_node_join_cross_device_code(nodes, join):
+    """The code an 8-GPU node runs, on one GPU: EXT_MPI_AMD_TEST_CROSS_DEVICE=1 makes the
+    communicator's agreed verdict 'some node is on another device' (engine_ipc.c) while the nodes
+    still share this GPU, so every Start records the system-scope release before phase 0 and the
+    fused join runs join_fused_kernel<..., true> (system-scope partial stores), its grid still
+    divided among the nodes on this GPU (by UUID). Every case bitwise against the oracle; every
+    handle's flags (tests/helpers.py ipc_flags_problem) say the cross-GPU code ran; plus the
+    timeout recovery over every part's slot. Reference synchronisation replaced:
+    ext_mpi_native_exec.c:21-84, cuda_shmem.c:218-299."""
+    env = dict(EXT_MPI_AMD_TEST_CROSS_DEVICE="1", NODEIPC_RECOVERY="1")
+    if join != "default":
+        env["EXT_MPI_AMD_JOIN_PARTS"] = "1" if join == "serial" else join[-1]
+    _run_nodes(nodes, budget=300 if nodes >= 8 else 180, **env)
+
+
+def test_node_join_settings_follow_rank0():
+    """The join's settings are rank 0's: node 0 asks for 3 parts, the others for the
+    serial join; every node must run 3 parts from 1 MiB per rank (and the same join on every case),
+    bitwise -- a disagreement would run different slot protocols and time out every Start."""
+    lines = _run_nodes(4, rank_env=lambda r: {"EXT_MPI_AMD_JOIN_PARTS": "3" if r == 0 else "1"})
+    assert any(l.endswith("join parts 3: ok") for l in lines), lines

@@ -199,15 +199,14 @@ def test_pinned_host_buffers(oracle, monkeypatch, direct, code, R, count, copyin
 
 
 @pytest.mark.parametrize("code,R,count,copyin,in_place", [
-    (emac.FLOAT, 8, (4 << 20) + 7, "6;1 -8 8", False),            # pipelined: 8 element ranges
+    (emac.FLOAT, 8, (4 << 20) + 7, "6;1 -8 8", False),
     (emac.DOUBLE, 4, (1 << 20) + 1001, "6;1 -2 -2 2 2", True),
     (emac.INT, 3, 3 << 20, "6;3 -3 3", False),                    # pieces clipped by the ranges
     (emac.LONG, 8, 1 << 20, "6;-64 -8 8", False)])
-def test_host_buffers_pipelined(oracle, monkeypatch, code, R, count, copyin, in_place):
-    """Host buffers of >= 4 MiB per rank with EXT_MPI_AMD_PIPELINE=1: H2D, fold and D2H overlap in
-    element-range parts on three streams; repeated Starts reuse the parts (the previous Start's
-    copies come first)."""
-    monkeypatch.setenv("EXT_MPI_AMD_PIPELINE", "1")
+def test_host_buffers_staged(oracle, monkeypatch, code, R, count, copyin, in_place):
+    """Host buffers of >= 4 MiB per rank staged through device mirrors (EXT_MPI_AMD_HOST_DIRECT=0:
+    H2D, fold, D2H on the handle's stream); repeated Starts restage every time."""
+    monkeypatch.setenv("EXT_MPI_AMD_HOST_DIRECT", "0")
     sends = xorshift_inputs(R, count, code, seed_base=0x9191 + count)
     recvs = [s.copy() for s in sends] if in_place else [np.full(count, -1, dtype=s.dtype) for s in sends]
     h = emac.node_allreduce_init([(r if in_place else s).ctypes.data for s, r in zip(sends, recvs)],
@@ -219,7 +218,7 @@ def test_host_buffers_pipelined(oracle, monkeypatch, code, R, count, copyin, in_
                     r[:] = s
             emac.start(h)
             emac.wait(h)
-            assert_bitwise(recvs, oracle.allreduce(sends, copyin, in_place=in_place), "host pipelined")
+            assert_bitwise(recvs, oracle.allreduce(sends, copyin, in_place=in_place), "host staged")
     finally:
         emac.done(h)
 

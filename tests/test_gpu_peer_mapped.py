@@ -116,3 +116,12 @@ def test_ipc_forced_mirror(world):
     report = _run_world(world, {"EXT_MPI_AMD_IPC_FORCE_MIRROR": "1", "IPC_FUZZ": "4",
                                 "IPC_SECTIONS": "realloc,newdata,concurrent,recycle"})
     assert "re-placing send" in report  # the forced round was taken (EXT_MPI_AMD_DEBUG_IPC)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_ipc_cross_device_code(world):
+    """EXT_MPI_AMD_TEST_CROSS_DEVICE=1: the ranks' agreed verdict is 'some peer on another device'
+    though all share this GPU, so every Start records the system-scope release before phase 0 (the
+    code one rank per GPU runs, engine_ipc.c); every case bitwise against the oracle and every
+    handle's flags checked (ipc_worker.py), timeout recovery included."""
+    _run_world(world, {"EXT_MPI_AMD_TEST_CROSS_DEVICE": "1"})

@@ -288,23 +288,6 @@ def test_forced_schedule_other_shapes_keep_static_pick(fresh_tuner, monkeypatch)
         emac.done(h)
 
 
-def test_pipelined_host_handle_not_tuned(fresh_tuner, monkeypatch):
-    """A pipelined host-staged NODE handle (EXT_MPI_AMD_PIPELINE=1) never launches its main fold
-    (pipe_start folds parts): it gets no tuner uploads or events."""
-    monkeypatch.setenv("EXT_MPI_AMD_PIPELINE", "1")
-    R, count = 8, (8 << 20) // 4
-    sends = [np.full(count, r + 1, dtype=np.float32) for r in range(R)]
-    recvs = [np.zeros(count, dtype=np.float32) for _ in range(R)]
-    h = emac.node_allreduce_init([s.ctypes.data for s in sends], [r.ctypes.data for r in recvs], count, emac.FLOAT)
-    try:
-        assert emac.handle_tune_info(h)["candidates"] == 0
-        emac.start(h)
-        emac.wait(h)
-        assert all(np.all(r == R * (R + 1) / 2) for r in recvs)
-    finally:
-        emac.done(h)
-
-
 DEV_STORE = 1 << 14  # fold_kernel.hpp kDevStore: device-scope streaming stores (cache policy sc1 nt)
 BUF_LOAD = 1 << 15  # fold_kernel.hpp kBufLoad: leaf loads as buffer loads
 

@@ -2,7 +2,8 @@
 
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half of the bytes of a
 wide (16 B/lane) coalesced streaming read -> doubled; WRITE_SIZE is exact for 16-B stores.
-Both counters are in KiB. Usage: pmc_traffic.py <fetch_dir> <write_dir> <out.json> <tag>"""
+Both counters are in KiB. Usage: pmc_traffic.py <fetch_dir> <write_dir> <out.json> <tag> [kernel regex]
+(default: the fold kernels; e.g. 'join_fused_kernel<' for the fused node join)"""
 import csv
 import glob
 import json
@@ -12,19 +13,20 @@ import sys
 FOLD = re.compile(r"\bfold_(deferred_)?kernel<")  # the per-tile loop or the deferred-store kernel
 
 
-def per_dispatch(d, counter):
+def per_dispatch(d, counter, kern=FOLD):
     vals = []
     for path in glob.glob(f"{d}/**/*counter_collection*.csv", recursive=True):
         for row in csv.DictReader(open(path)):
-            if FOLD.search(row.get("Kernel_Name", "")) and row.get("Counter_Name") == counter:
+            if kern.search(row.get("Kernel_Name", "")) and row.get("Counter_Name") == counter:
                 vals.append(float(row["Counter_Value"]))
     return vals
 
 
 def main():
     fetch_dir, write_dir, out, tag = sys.argv[1:5]
-    f = per_dispatch(fetch_dir, "FETCH_SIZE")
-    w = per_dispatch(write_dir, "WRITE_SIZE")
+    kern = re.compile(sys.argv[5]) if len(sys.argv) > 5 else FOLD
+    f = per_dispatch(fetch_dir, "FETCH_SIZE", kern)
+    w = per_dispatch(write_dir, "WRITE_SIZE", kern)
     if not f or not w:
         print("no fold_kernel counter rows found", file=sys.stderr)
         sys.exit(1)
@@ -32,7 +34,7 @@ def main():
     w.sort()
     fetch = f[len(f) // 2] * 1024 * 2  # median dispatch, KiB -> B, x2 gfx950 correction
     write = w[len(w) // 2] * 1024
-    res = {"tag": tag, "kernel": "fold_kernel / fold_deferred_kernel", "dispatches": [len(f), len(w)],
+    res = {"tag": tag, "kernel": kern.pattern, "dispatches": [len(f), len(w)],
            "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
            "hbm_bytes_per_launch": fetch + write,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; median dispatch; "
