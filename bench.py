@@ -814,11 +814,13 @@ def single_gpu(args):
                           "gbps_reduced": round(R * cnt * tsize * st / r["wall_s"] / 1e9, 2),
                           "checked": r["checked"], "fold_schedule": r.get("schedule")})
         extras["sweep_node_form"] = sweep
-        # BASELINE configs[4]'s EXT_MPI_COPYIN radix sweep on the node form (8 ranks in this GPU):
-        # the radix chains and the small-message -64 fractions from latency to bandwidth sizes
+        # BASELINE configs[4]'s EXT_MPI_COPYIN radix sweep on the node form (8 ranks in this GPU): the
+        # linear fold, the radix chains and the -64 fractions -- which the reference offers for small
+        # messages (reduce_copyin.c:410-425) -- from latency to bandwidth sizes, each point against the
+        # linear fold measured in the same sweep, and each variant's latency -> bandwidth crossover
         rsweep = []
-        for cp in ("6;1 -2 -2 -2 2 2 2", "6;1 -4 -2 2 4", "6;-64 -8 8"):
-            for nbytes in (8, 64 << 10, 1 << 20, 16 << 20):
+        for cp in (copyin,) + RADIX_VARIANTS.get(R, ()):
+            for nbytes in RADIX_SWEEP_BYTES:
                 cnt = max(1, nbytes // tsize)
                 st = 200 if nbytes <= (1 << 20) else 40
                 r = node_run(R, cnt, tdtype, code, cp, st, 5, min_set_bytes=0 if nbytes < (16 << 20) else 640 * MIB,
@@ -826,12 +828,14 @@ def single_gpu(args):
                 rsweep.append({"copyin": cp, "bytes_per_rank": cnt * tsize,
                                "us_per_allreduce": round(r["wall_s"] * 1e6 / st, 2),
                                "gpu_us_per_allreduce": round(r["event_ms"] * 1e3 / st, 2), "checked": r["checked"]})
+        radix_vs_linear(rsweep, copyin, "gpu_us_per_allreduce")
+        extras["radix_crossover_node_form"] = radix_crossovers(rsweep, "gpu_us_per_allreduce", R)
         extras["radix_sweep_node_form"] = rsweep
         # radix chains (compile-time fold trees) against the linear fold, measured alike and
         # alternated twice (median of each), so a drifting clock does not favour either
         chains, runs = {}, {}
         for rep in range(2):
-            for cp in (copyin, "6;1 -2 -2 -2 2 2 2", "6;1 -4 -2 2 4", "6;1 -2 -4 4 2", "6;-64 -8 8"):
+            for cp in (copyin, "6;1 -2 -2 -2 2 2 2", "6;1 -4 -2 2 4", "6;1 -2 -4 4 2"):  # (-k: small messages only)
                 r = node_run(R, count, tdtype, code, cp, args.steps, args.warmup, alloc=args.alloc)
                 runs.setdefault(cp, []).append((r["event_ms"] * 1e-3 / args.steps, r["checked"]))
         lin = min(t for t, _ in runs[copyin])
@@ -1266,22 +1270,22 @@ def transport_child(args):
                               "algbw_gbps": round(cnt * tsz * st / el_p / 1e9, 2), "checked": ok_p})
                 log(f"rank {rank}: {transport}: sweep {dname_p} {cnt * tsz} B: {el_p * 1e6 / st:.2f} us, checked {ok_p}")
             res["sweep"] = sweep
-            # BASELINE configs[4]: EXT_MPI_COPYIN radix variants of this node size (radix chains
-            # and the small-message -64 fraction) at a latency, a middle and a bandwidth point
-            variants = {8: ["6;1 -2 -2 -2 2 2 2", "6;1 -4 -2 2 4", "6;-64 -8 8"], 4: ["6;1 -2 -2 2 2", "6;-64 -4 4"],
-                        2: ["6;-64 -2 2"]}.get(world, [])
+            # BASELINE configs[4]: EXT_MPI_COPYIN radix variants of this node size (radix chains and
+            # the small-message -64 fraction) beside the linear fold, latency to bandwidth sizes
             radix = []
-            for cp in variants:
-                for nbytes in (64 << 10, 1 << 20, 16 << 20):
-                    cnt, st = nbytes // tsize, 100 if nbytes <= (1 << 20) else 20
+            for cp in (copyin,) + RADIX_VARIANTS.get(world, ()):
+                for nbytes in RADIX_SWEEP_BYTES:
+                    cnt, st = max(1, nbytes // tsize), 100 if nbytes <= (1 << 20) else 20
                     hp, sb, rb, _, el_p, ok_p = _comm_run(emac, comm, cnt, tdtype, code, dname, cp, st, 3, rank, world,
                                                           dist, torch)
                     emac.done(hp)
                     sb.free()
                     rb.free()
-                    radix.append({"copyin": cp, "bytes_per_rank": nbytes, "us_per_allreduce": round(el_p * 1e6 / st, 2),
-                                  "algbw_gbps": round(nbytes * st / el_p / 1e9, 2), "checked": ok_p})
+                    radix.append({"copyin": cp, "bytes_per_rank": cnt * tsize, "us_per_allreduce": round(el_p * 1e6 / st, 2),
+                                  "algbw_gbps": round(cnt * tsize * st / el_p / 1e9, 2), "checked": ok_p})
                     log(f"rank {rank}: {transport}: '{cp}' {nbytes} B: {el_p * 1e6 / st:.2f} us, checked {ok_p}")
+            radix_vs_linear(radix, copyin, "us_per_allreduce")
+            res["radix_crossover"] = radix_crossovers(radix, "us_per_allreduce", world)
             res["radix_sweep"] = radix
             # the path's real start and end: page-locked host send / receive buffers, staged through
             # device mirrors on each rank's own PCIe link (H2D, legs, D2H on the handle's stream)
@@ -1480,6 +1484,7 @@ def multi_gpu_line(args, world, dname, S, copyin, rn, results, order, gpus_visib
         extras["transport"] = primary
         extras["sweep"] = r.get("sweep", [])
         extras["radix_sweep"] = r.get("radix_sweep", [])
+        extras["radix_crossover"] = r.get("radix_crossover", {})
         extras["local_fold_rate_retained"] = r.get("local_fold")
         extras["host_buffers_pcie_inclusive"] = r.get("host_buffers")
         chunk = S / world
@@ -1604,6 +1609,39 @@ def node_form_line(args, world, dname, rn, one_rank_per_gpu):
     }
 
 
+# BASELINE configs[4]'s EXT_MPI_COPYIN variants per node size (beside the linear '6;1 -R R'), and the
+# sizes per rank they are swept at: the -k fractions are the reference's small-message split
+RADIX_VARIANTS = {8: ("6;1 -2 -2 -2 2 2 2", "6;1 -4 -2 2 4", "6;-64 -8 8"), 4: ("6;1 -2 -2 2 2", "6;-64 -4 4"),
+                  2: ("6;-64 -2 2",)}
+RADIX_SWEEP_BYTES = (8, 1 << 10, 64 << 10, 1 << 20, 16 << 20)
+
+
+def radix_vs_linear(points, linear, key):
+    """Each point's time against the linear fold's at the same size (linear / variant: > 1 faster)."""
+    lin = {p["bytes_per_rank"]: p[key] for p in points if p["copyin"] == linear}
+    for p in points:
+        if p["bytes_per_rank"] in lin and p[key] > 0:
+            p["vs_linear"] = round(lin[p["bytes_per_rank"]] / p[key], 4)
+
+
+def radix_crossovers(points, key, R):
+    """Per EXT_MPI_COPYIN variant, its latency -> bandwidth crossover: the fixed cost (the shortest time
+    of the points up to 1 KiB per rank), the streaming rate (GB/s reduced between the two largest
+    points) and the size per rank at which streaming time equals the fixed cost."""
+    out = {}
+    for cp in dict.fromkeys(p["copyin"] for p in points):
+        pts = sorted((p["bytes_per_rank"], p[key]) for p in points if p["copyin"] == cp)
+        small = sorted(t for b, t in pts if b <= 1024)
+        if len(pts) < 3 or not small or pts[-1][1] <= pts[-2][1]:
+            continue
+        fixed = small[0]
+        (b1, t1), (b2, t2) = pts[-2], pts[-1]
+        rate = R * (b2 - b1) / ((t2 - t1) * 1e-6)  # bytes reduced per second
+        out[cp] = {"fixed_us": round(fixed, 2), "streaming_gbps_reduced": round(rate / 1e9, 1),
+                   "crossover_bytes_per_rank": int(fixed * 1e-6 * rate / R)}
+    return out
+
+
 def _fit_line(xs, ys):
     """least-squares y = a + b x: (a, b)"""
     n = len(xs)
@@ -1723,7 +1761,7 @@ def shape_only(args):
         del os.environ["EXT_MPI_AMD_FOLD_SCHEDULE"]
         r = {"by_schedule": r}
     elif args.shape == "local256":
-        r = comm_shape_fold(8, MB // 8 // 4, torch.float32, emac.FLOAT, 40)
+        r = comm_shape_fold(8, MB // 8 // 4, torch.float32, emac.FLOAT, 40, launch_times=True)
     elif args.shape == "small":
         r = small_sweep(emac, torch)
     elif args.shape == "joinci":

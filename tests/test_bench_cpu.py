@@ -173,3 +173,23 @@ def test_rotation_keeps_every_read_in_hbm(monkeypatch, read_mib):
     assert legacy == max(2, -(-640 * bench.MIB // (2 * rd)))
     if read_mib == 16 * 8:  # the headline: 6 sets now, 3 before
         assert (n, legacy) == (6, 3)
+
+
+def test_radix_crossover_and_vs_linear():
+    """bench.py's configs[4] summary: each point against the linear fold at the same size, and each
+    variant's fixed cost, streaming rate and latency -> bandwidth crossover from synthetic times
+    t = fixed + R * bytes / rate."""
+    sys.path.insert(0, ROOT)
+    import bench
+    R, pts = 8, []
+    for cp, fixed, rate in (("6;1 -8 8", 3.0, 3.0e12), ("6;-64 -8 8", 4.0, 2.0e12)):
+        for b in bench.RADIX_SWEEP_BYTES:
+            pts.append({"copyin": cp, "bytes_per_rank": b, "us": fixed + R * b / rate * 1e6})
+    bench.radix_vs_linear(pts, "6;1 -8 8", "us")
+    assert all(p["vs_linear"] == 1.0 for p in pts if p["copyin"] == "6;1 -8 8")
+    assert [p["vs_linear"] for p in pts if p["copyin"] != "6;1 -8 8"][0] == 0.75  # 3 / 4 us at 8 B
+    x = bench.radix_crossovers(pts, "us", R)
+    assert x["6;1 -8 8"]["fixed_us"] == 3.0 and x["6;1 -8 8"]["streaming_gbps_reduced"] == 3000.0
+    # fixed cost == streaming time at 3 us * 3 TB/s / 8 ranks per rank
+    assert abs(x["6;1 -8 8"]["crossover_bytes_per_rank"] - 3e-6 * 3e12 / 8) < 16
+    assert abs(x["6;-64 -8 8"]["crossover_bytes_per_rank"] - 4e-6 * 2e12 / 8) < 16

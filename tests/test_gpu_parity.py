@@ -201,9 +201,9 @@ def test_pinned_host_buffers(oracle, monkeypatch, direct, code, R, count, copyin
 @pytest.mark.parametrize("code,R,count,copyin,in_place", [
     (emac.FLOAT, 8, (4 << 20) + 7, "6;1 -8 8", False),
     (emac.DOUBLE, 4, (1 << 20) + 1001, "6;1 -2 -2 2 2", True),
-    (emac.INT, 3, 3 << 20, "6;3 -3 3", False),                    # pieces clipped by the ranges
+    (emac.INT, 3, 3 << 20, "6;3 -3 3", False),                    # three pieces per chunk
     (emac.LONG, 8, 1 << 20, "6;-64 -8 8", False)])
-def test_host_buffers_staged(oracle, monkeypatch, code, R, count, copyin, in_place):
+def test_host_buffers_staged_large(oracle, monkeypatch, code, R, count, copyin, in_place):
     """Host buffers of >= 4 MiB per rank staged through device mirrors (EXT_MPI_AMD_HOST_DIRECT=0:
     H2D, fold, D2H on the handle's stream); repeated Starts restage every time."""
     monkeypatch.setenv("EXT_MPI_AMD_HOST_DIRECT", "0")

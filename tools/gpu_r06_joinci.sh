@@ -4,12 +4,14 @@
 # copy-in alone (bench.py --shape joinci) and the whole Start with N processes sharing the GPU
 # (bench.py --child-transport node-ipc, as tools/gpu_r05_join_sweep.sh). One line per run.
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r06/joinci
+O=gpurun_out/r06/joinci${TAG:+_$TAG}
 mkdir -p $O
-EXT_MPI_AMD_JOIN_CI_U=4 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
-  tests/test_gpu_node_ipc.py -k "serial_and_pipelined and (fused3 or fused4) or over_peer_mapped" > $O/tests_ciu4.log 2>&1
-rc=$?; tail -n 3 $O/tests_ciu4.log; [ $rc -ne 0 ] && exit $rc
-for p in 2 4; do for u in 2 3 4; do
+CIUS=${CIUS:-2 3 4}
+TESTU=${TESTU:-4}
+EXT_MPI_AMD_JOIN_CI_U=$TESTU timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+  tests/test_gpu_node_ipc.py -k "serial_and_pipelined and (fused3 or fused4) or over_peer_mapped" > $O/tests_ciu$TESTU.log 2>&1
+rc=$?; tail -n 3 $O/tests_ciu$TESTU.log; [ $rc -ne 0 ] && exit $rc
+for p in 2 4; do for u in $CIUS; do
   EXT_MPI_AMD_JOIN_PARTS=$p EXT_MPI_AMD_JOIN_CI_U=$u timeout -k 10 240 python3 bench.py --shape joinci > $O/joinci_p${p}_u$u.json 2> $O/joinci_p${p}_u$u.err || { tail -5 $O/joinci_p${p}_u$u.err; exit 1; }
   python3 -c "
 import json; d=json.loads(open('$O/joinci_p${p}_u$u.json').read())
@@ -28,6 +30,6 @@ print('$tag', 'start_to_wait %.1f' % (d['wall']*1e6/20), 'copy_in %.1f' % (d['co
 }
 for N in 1 2 4; do
   run $N 1 2 || exit 1
-  for c in 2:2 2:3 2:4 4:4 4:2; do IFS=: read -r p u <<< "$c"; run $N $p $u || exit 1; done
+  for c in ${RUNS:-2:2 2:3 2:4 4:4 4:2}; do IFS=: read -r p u <<< "$c"; run $N $p $u || exit 1; done
 done
 exit 0
