@@ -215,7 +215,6 @@ typedef struct {
   int nparts;
   int fused; /* one launch per Start (join_fused.hip), else the streams form */
   int sys_stores; /* fused: the copy-in's partials written through at system scope (a node on another GPU) */
-  int ci_u;       /* fused: the copy-in tile's vectors per lane and leaf (join_fused.hip CIU) */
   int grid;  /* the fused launch's workgroups */
   long lo[EMAC_JOIN_PARTS + 1]; /* part k: message elements [lo[k], lo[k + 1]) */
   int slot[EMAC_JOIN_PARTS];

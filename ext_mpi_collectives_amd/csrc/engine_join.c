@@ -95,7 +95,7 @@ static int place_part(emac_bucket *b, const jproto *p, int n, long lo, long hi, 
    EXT_MPI_AMD_JOIN_PARTS (0: unset), EXT_MPI_AMD_JOIN=streams, EXT_MPI_AMD_JOIN_SYSSTORE=1 (A/B:
    system-scope partial stores in the fused join with every node on one GPU too) */
 typedef struct {
-  int parts, streams, sys_stores, ci_u;
+  int parts, streams, sys_stores;
 } join_env;
 
 static join_env join_env_local(void) {
@@ -105,12 +105,6 @@ static join_env join_env_local(void) {
   if (p && *p && e.parts < 1) e.parts = 1;
   e.streams = j && !strcmp(j, "streams");
   e.sys_stores = y && atoi(y) > 0;
-  {
-    /* A/B: EXT_MPI_AMD_JOIN_CI_U = the fused join's copy-in tile, vectors per lane and leaf (2, or 3 / 4
-       where join_fused.hip has the kernel) */
-    const char *u = getenv("EXT_MPI_AMD_JOIN_CI_U");
-    e.ci_u = u && atoi(u) >= 1 && atoi(u) <= 4 ? atoi(u) : 2;
-  }
   return e;
 }
 
@@ -276,12 +270,6 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
     /* the copy-in's partials go to memory at system scope when some node runs on another GPU
        (every rank has the same cross_device verdict), else at device scope */
     h->join->sys_stores = cm->cross_device || env.sys_stores;
-    /* the copy-in tile (a shape without that kernel keeps 2: the same verdict on every rank) */
-    h->join->ci_u = env.ci_u;
-    if (h->join->fused && env.ci_u != 2 &&
-        emac_gpu_join_fused(h->plan.dtype, R, &h->plan.codes, &h->xcodes, nparts, 3 | env.ci_u << 8, NULL, NULL, NULL, NULL,
-                            NULL, NULL, N, cm->rank, NULL, 0, NULL, 0, NULL))
-      h->join->ci_u = 2;
     for (k = 0; k < nparts; k++) {
       h->join->slot[k] = pslot[k];
       cm->slot_used[pslot[k]] = 1;
@@ -387,11 +375,9 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
     memset(&zero, 0, sizeof(zero));
     for (k = 0; k <= J->nparts; k++) J->lo[k] = join_cut(h->plan.count, J->nparts, k);
     for (k = 0; !rc && k < J->nparts; k++) {
-      /* the kernel's tiles (join_fused.hip: 1024-lane workgroups): ci_u vectors per lane for the
-         copy-in (default 2), 2 for the pull, 1 for the share fold -- in layout units of EMAC_BLOCK
-         lanes (U 4 * ci_u, 16 written as 0; 8; 4) */
-      if (!rc)
-        rc = upload_forced(&J->in[k], b, place_part(b, pin, nin, J->lo[k], J->lo[k + 1], ts), R, ((4 * J->ci_u) & 15) | 1 << 4);
+      /* the kernel's tiles (join_fused.hip: 1024-lane workgroups): 2 vectors per lane for the copy-in
+         and the pull, 1 for the share fold -- in layout units of EMAC_BLOCK lanes, U 8 and 4 */
+      if (!rc) rc = upload_forced(&J->in[k], b, place_part(b, pin, nin, J->lo[k], J->lo[k + 1], ts), R, 8 | 1 << 4);
       if (!rc) rc = upload_forced(&J->fold[k], b, place_part(b, psh, nshr, J->lo[k], J->lo[k + 1], ts), N, 4 | 1 << 4);
       if (!rc) rc = upload_forced(&J->pull[k], b, place_part(b, ppl, npl, J->lo[k], J->lo[k + 1], ts), 1, 8 | 1 << 4);
     }
@@ -661,7 +647,7 @@ int join_start(emac_handle *h, int copyin, int legs) {
     h->tune.ops++;
     const int dev_scope = !J->sys_stores;
     return emac_gpu_join_fused(h->plan.dtype, h->nsrc, &h->plan.codes, &h->xcodes, J->nparts,
-                               (copyin ? 1 : 0) | (legs ? 2 : 0) | (dev_scope ? 4 : 0) | J->ci_u << 8,
+                               (copyin ? 1 : 0) | (legs ? 2 : 0) | (dev_scope ? 4 : 0),
                                seg, J->slot, e0, e1, cm->sync, (void *const *)cm->d_peer_sync, N, cm->rank,
                                cm->err + J->slot[0], cm->timeout_ticks, J->ctl, J->grid, h->stream);
   }

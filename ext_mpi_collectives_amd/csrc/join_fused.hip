@@ -122,13 +122,13 @@ __device__ __forceinline__ void join_item(const Work &w, long i, const emac_code
 // `phase` of the part's slot to every node, itself too (phase < 0: nothing to signal). Claiming
 // rather than a static grid stride: a workgroup the GPU has not started yet holds no item a
 // waiting one needs, so the grid need not be resident all at once.
-template <typename T, int N, int U, int CH, int D, int ISSUE, unsigned DIV = 4>
+template <typename T, int N, int U, int CH, int D, int ISSUE>
 __device__ __forceinline__ void join_seg(const Work &w, unsigned *tk, unsigned *done, unsigned *sig, const emac_codes &codes,
                                          int nrt, bool store, NodeSync &ns, int phase, unsigned long epoch) {
   __shared__ unsigned claim[2];
   __shared__ unsigned last;
   const unsigned n = (unsigned)(w.ntiles + w.nedges);
-  unsigned c = n / (gridDim.x * DIV);  // DIV chunks per workgroup: few claims, balanced ends
+  unsigned c = n / (gridDim.x * 4u);  // a few chunks per workgroup: few claims, balanced ends
   c = c < 1u ? 1u : c > 32u ? 32u : c;
   unsigned mine = 0;
   __syncthreads();
@@ -193,9 +193,11 @@ __device__ __forceinline__ bool join_gate(NodeSync &ns, int phase, unsigned long
 // R copy-in leaves (compile time, fold tree CH), N nodes (runtime, the share's tree in xcodes)
 // mode bit 0: the copy-ins; bit 1: the node legs (the signals, waits, share folds and pulls; without
 // the copy-ins they read the partials the last ones left -- bench.py times each alone)
-// CIU: vectors per lane and leaf of a copy-in tile (JB * CIU vectors of one bucket; the layouts of
-// engine_join.c are made to match)
-template <typename T, int R, int CH, bool SYS, int CIU>
+// The copy-in's tiles are JB * 2 vectors of one bucket (engine_join.c lays them out so). Wider and
+// narrower ones were measured on configs[1]'s node, the copy-ins alone (bench.py --shape joinci,
+// profiles/r06/joinci/): 2 parts, 39.3 us at 2 vectors per lane, 40.6 at 1 (one claim per workgroup
+// and part), 41.8 at 3, 46.9 at 4 -- more loads in flight per wave made it slower.
+template <typename T, int R, int CH, bool SYS>
 __global__ __launch_bounds__(JB) void join_fused_kernel(JoinSegs segs, int nparts, int mode, emac_codes codes,
                                                                 emac_codes xcodes, NodeSync ns0, JoinCtl *ctl) {
   // local leaves; the partial written through to memory, at system scope when a peer runs on another
@@ -207,7 +209,7 @@ __global__ __launch_bounds__(JB) void join_fused_kernel(JoinSegs segs, int npart
       ns.slot = segs.slot[s];
       ns.tag = segs.e1[s];
       const Work empty = {segs.w[0][s].b, 0, 0, 0, 1, nullptr, 0};
-      join_seg<T, R, CIU, CH, 1, CI_ISSUE, CIU == 1 ? 1u : 4u>((mode & 1) ? segs.w[0][s] : empty, &ctl->tk[0][s], &ctl->done[0][s],
+      join_seg<T, R, 2, CH, 1, CI_ISSUE>((mode & 1) ? segs.w[0][s] : empty, &ctl->tk[0][s], &ctl->done[0][s],
                                          &ctl->sig[0][s], codes, 0, true, ns, (mode & 2) ? 0 : -1, segs.e0[s]);
     }
     if (!(mode & 2)) continue;
@@ -241,40 +243,23 @@ __global__ __launch_bounds__(JB) void join_fused_kernel(JoinSegs segs, int npart
   }
 }
 
-template <typename T, int R, int CH, int CIU>
+template <typename T, int R, int CH>
 int join_launch_one(const JoinSegs &segs, int nparts, int mode, const emac_codes &codes, const emac_codes &xcodes,
                     const NodeSync &ns, JoinCtl *ctl, int grid, hipStream_t s) {
   if (mode & 4)  // every node on this GPU: device-scope write-through suffices
-    hipLaunchKernelGGL((join_fused_kernel<T, R, CH, false, CIU>), dim3((unsigned)grid), dim3(JB), 0, s, segs, nparts,
+    hipLaunchKernelGGL((join_fused_kernel<T, R, CH, false>), dim3((unsigned)grid), dim3(JB), 0, s, segs, nparts,
                        mode, codes, xcodes, ns, ctl);
   else
-    hipLaunchKernelGGL((join_fused_kernel<T, R, CH, true, CIU>), dim3((unsigned)grid), dim3(JB), 0, s, segs, nparts,
+    hipLaunchKernelGGL((join_fused_kernel<T, R, CH, true>), dim3((unsigned)grid), dim3(JB), 0, s, segs, nparts,
                        mode, codes, xcodes, ns, ctl);
   return hipGetLastError() == hipSuccess ? 0 : EMAC_ERR_DEVICE;
-}
-
-// the copy-in tile's CIU (mode bits 8-11; 0: 2): 2 for every shape; 1, 3 and 4 (A/B,
-// EXT_MPI_AMD_JOIN_CI_U) for configs[1]'s node (float, 8 leaves, linear) only. CIU 1 claims one
-// chunk of its share per workgroup and part (its tiles back to back, no barrier between them)
-template <typename T, int R, int CH>
-int join_launch_u(const JoinSegs &segs, int nparts, int mode, const emac_codes &codes, const emac_codes &xcodes,
-                  const NodeSync &ns, JoinCtl *ctl, int grid, hipStream_t s, bool dry) {
-  const int ciu = (mode >> 8) & 15;
-  if (ciu == 0 || ciu == 2)
-    return dry ? 0 : join_launch_one<T, R, CH, 2>(segs, nparts, mode, codes, xcodes, ns, ctl, grid, s);
-  if constexpr (std::is_same<T, float>::value && R == 8 && CH == 0) {
-    if (ciu == 1) return dry ? 0 : join_launch_one<T, R, CH, 1>(segs, nparts, mode, codes, xcodes, ns, ctl, grid, s);
-    if (ciu == 3) return dry ? 0 : join_launch_one<T, R, CH, 3>(segs, nparts, mode, codes, xcodes, ns, ctl, grid, s);
-    if (ciu == 4) return dry ? 0 : join_launch_one<T, R, CH, 4>(segs, nparts, mode, codes, xcodes, ns, ctl, grid, s);
-  }
-  return EMAC_ERR_UNSUPPORTED;
 }
 
 template <typename T, int R>
 int join_launch_ch(int ch, const JoinSegs &segs, int nparts, int mode, const emac_codes &codes, const emac_codes &xcodes,
                    const NodeSync &ns, JoinCtl *ctl, int grid, hipStream_t s, bool dry) {
   auto go = [&](auto chc) -> int {
-    return join_launch_u<T, R, decltype(chc)::value>(segs, nparts, mode, codes, xcodes, ns, ctl, grid, s, dry);
+    return dry ? 0 : join_launch_one<T, R, decltype(chc)::value>(segs, nparts, mode, codes, xcodes, ns, ctl, grid, s);
   };
   if (ch == 0) return go(std::integral_constant<int, 0>{});
   if constexpr (R == 4) {

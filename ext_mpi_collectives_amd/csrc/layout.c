@@ -71,7 +71,7 @@ int emac_layout_as(emac_bucket *b, int nb, int op, int nsrc, int tree, int fan, 
   emac_edge *edges;
   for (i = 0; i < nb; i++) total += b[i].nvec;
   unroll = forced > 0 ? forced : emac_gpu_pick_unroll(op, nsrc, tree, fan, total); /* U | ISSUE << 4 */
-  tv = (long)EMAC_BLOCK * ((unroll & 15) ? (unroll & 15) : 16); /* (U field 0: 16, the fused join's 1024 x 4 tiles) */
+  tv = (long)EMAC_BLOCK * (unroll & 15);
   for (i = 0; i < nb; i++) {
     long t = (b[i].nvec + tv - 1) / tv;
     b[i].tile0 = tiles;
