@@ -60,7 +60,7 @@ def parse():
                     help="N > 1: peer-mapped hipIpc form (default) or RCCL point-to-point legs")
     ap.add_argument("--shape", default=None, choices=["local256", "node16", "node64", "node256", "node512", "copy256",
                                                       "int4", "long4", "small", "joinci"],
-                    help="profiling: run only this fold shape (40 launches) and exit (PMC passes, tools/gpu_pmc_r02.sh)")
+                    help="profiling: run only this fold shape (40 launches) and exit (PMC passes, tools/gpu_r06_localfp.sh)")
     ap.add_argument("--schedules", default=None,
                     help="--shape node* / local256: comma-separated fold schedule words (U | issue << 4) to run in turn")
     ap.add_argument("--child-transport", default=None, choices=["ipc", "rccl", "node-ipc", "node-rccl"],

@@ -14,7 +14,7 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# EXT_MPI_AMD_LIB: another build of the same library (A/B runs of build options, tools/ab/)
+# EXT_MPI_AMD_LIB: another build of the same library (A/B runs of build options)
 LIB_PATH = os.environ.get("EXT_MPI_AMD_LIB") or os.path.join(HERE, "libext_mpi_amd.so")
 MPI_LIB_PATH = os.path.join(HERE, "libext_mpi_collectives.so")
 

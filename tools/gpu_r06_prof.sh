@@ -1,11 +1,12 @@
 #!/bin/bash
-# Round-4 closing evidence: PMC traffic (FETCH_SIZE / WRITE_SIZE, separate passes, gfx950
-# correction in tools/pmc_traffic.py) of the bench's node16 launch, the node256 / local256 / int4
-# shapes, then the driver's own bench command under rocprofv3 --kernel-trace --stats (its kept
-# fold kernel's mean must agree with roofline.avg_launch_us).
+# Round-6 closing evidence, part 2: PMC traffic (FETCH_SIZE / WRITE_SIZE, separate passes, gfx950
+# correction in tools/pmc_traffic.py) of the bench's node16 launch and the node256 / local256
+# shapes, then the driver's own bench command under rocprofv3 --kernel-trace --stats (its kept fold
+# kernel's mean must agree with roofline.avg_launch_us). Usage: gpu_r06_prof.sh <tag>
 set -u
-cd "$GRAFT_REPO_ROOT"; R=$PWD; mkdir -p gpurun_out/fin4; export TMPDIR=/tmp
-O=gpurun_out/fin4
+cd "$GRAFT_REPO_ROOT"; R=$PWD; export TMPDIR=/tmp
+O=gpurun_out/r06/${1:-prof}
+mkdir -p $O
 pass() {  # tag counter bench-args...
   local tag=$1 c=$2; shift 2
   rm -rf $O/pmc_${tag}_$c
@@ -26,8 +27,8 @@ rm -rf $O/prof
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run --output-format csv -- \
   python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_prof.json 2> $O/bench_prof.err || exit $?
 tail -c 1500 $O/bench_prof.json
-f=$(find $O/prof -name "*kernel_stats.csv" | head -1); cp "$f" $O/bench_kernel_stats.csv; grep -E "fold_(deferred_)?kernel<" "$f" | head
-t=$(find $O/prof -name "*kernel_trace.csv" | head -1); python3 tools/prof_dispatches.py "$t" "fold_(deferred_)?kernel<" 5 > $O/bench_dispatches.txt
+f=$(find $O/prof -name "*kernel_stats.csv" | head -1); cp "$f" $O/bench_kernel_stats.csv; grep -E "fold_\w*kernel<" "$f" | head
+t=$(find $O/prof -name "*kernel_trace.csv" | head -1); python3 tools/prof_dispatches.py "$t" "fold_\w*kernel<" 5 > $O/bench_dispatches.txt
 head -30 $O/bench_dispatches.txt
 find $O -name "*.csv" -size +4M -delete
 exit 0
