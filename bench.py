@@ -371,30 +371,6 @@ def node_run(R, count, tdtype, code, copyin, steps, warmup, min_set_bytes=640 * 
         for k in range(steps):
             if C.ceiling_event_ms(evs[k], evs[k + 1], ctypes.byref(ms)) == 0:
                 launch_us.append(ms.value * 1e3)
-    # and (launch_times) a third pass in blocks of BLOCK launches back to back, a fence-free event
-    # only between blocks: the per-launch events above add about a microsecond to each launch they
-    # separate (DESIGN.md section 5), which this pass spreads over BLOCK launches
-    block_us = []
-    BLOCK = 5
-    if evs and steps >= 2 * BLOCK:
-        nb = steps // BLOCK
-        gate = StreamGate(stream.cuda_stream)
-        try:
-            C.ceiling_event_record(evs[0], stream.cuda_stream)
-            for j in range(nb):
-                for k in range(j * BLOCK, (j + 1) * BLOCK):
-                    emac.start(handles[k % nsets])
-                C.ceiling_event_record(evs[j + 1], stream.cuda_stream)
-                if j + 1 == min(nb, GATE_HOLD // BLOCK):
-                    gate.open()
-        finally:
-            gate.open()
-        stream.synchronize()
-        gate.free()
-        ms = ctypes.c_float()
-        for j in range(nb):
-            if C.ceiling_event_ms(evs[j], evs[j + 1], ctypes.byref(ms)) == 0:
-                block_us.append(ms.value * 1e3 / BLOCK)
     for ev in evs:
         C.ceiling_event_destroy(ev)
     for h in handles:
@@ -486,8 +462,32 @@ def comm_shape_fold(R, chunk, tdtype, code, steps, launch_times=False):
         for k in range(steps):
             if C.ceiling_event_ms(evs[k], evs[k + 1], ctypes.byref(ms)) == 0:
                 launch_us.append(ms.value * 1e3)
-        for ev in evs:
-            C.ceiling_event_destroy(ev)
+    # and (launch_times) a third pass in blocks of BLOCK launches back to back, a fence-free event
+    # only between blocks: the per-launch events above add about a microsecond to each launch they
+    # separate (DESIGN.md section 5), which this pass spreads over BLOCK launches
+    block_us = []
+    BLOCK = 5
+    if evs and steps >= 2 * BLOCK:
+        nb = steps // BLOCK
+        gate = StreamGate(stream.cuda_stream)
+        try:
+            C.ceiling_event_record(evs[0], stream.cuda_stream)
+            for j in range(nb):
+                for k in range(j * BLOCK, (j + 1) * BLOCK):
+                    emac.start(handles[k % nsets])
+                C.ceiling_event_record(evs[j + 1], stream.cuda_stream)
+                if j + 1 == min(nb, GATE_HOLD // BLOCK):
+                    gate.open()
+        finally:
+            gate.open()
+        stream.synchronize()
+        gate.free()
+        ms = ctypes.c_float()
+        for j in range(nb):
+            if C.ceiling_event_ms(evs[j], evs[j + 1], ctypes.byref(ms)) == 0:
+                block_us.append(ms.value * 1e3 / BLOCK)
+    for ev in evs:
+        C.ceiling_event_destroy(ev)
     scheds = [emac.handle_schedule(h) for h in handles]
     for h in handles:
         emac.done(h)
