@@ -374,16 +374,10 @@ static int node_ipc_init(emac_handle *h, emac_comm *cm, int rc) {
     emac_join_ctl zero;
     memset(&zero, 0, sizeof(zero));
     for (k = 0; k <= J->nparts; k++) J->lo[k] = join_cut(h->plan.count, J->nparts, k);
-    /* part 0's copy-in is the handle's own (tuned) fold launch ahead of the fused one, whose CI[0]
-       segment is then empty (its first workgroup through signals phase 0 of part 0): nothing can
-       overlap part 0's copy-in anyway, and inside the fused launch -- one 32 KiB-per-leaf tile per
-       workgroup and part, 16 waves in lock step -- a copy-in streams at 3.8 TB/s against the tuned
-       fold's 6.2 (bench.py --shape joinci, profiles/r06/joinci/) */
-    if (!rc) rc = upload_buckets(h, b, place_part(b, pin, nin, J->lo[0], J->lo[1], ts)); /* tuned */
     for (k = 0; !rc && k < J->nparts; k++) {
       /* the kernel's tiles (join_fused.hip: 1024-lane workgroups): 2 vectors per lane for the copy-in
          and the pull, 1 for the share fold -- in layout units of EMAC_BLOCK lanes, U 8 and 4 */
-      if (!rc) rc = upload_forced(&J->in[k], b, k ? place_part(b, pin, nin, J->lo[k], J->lo[k + 1], ts) : 0, R, 8 | 1 << 4);
+      if (!rc) rc = upload_forced(&J->in[k], b, place_part(b, pin, nin, J->lo[k], J->lo[k + 1], ts), R, 8 | 1 << 4);
       if (!rc) rc = upload_forced(&J->fold[k], b, place_part(b, psh, nshr, J->lo[k], J->lo[k + 1], ts), N, 4 | 1 << 4);
       if (!rc) rc = upload_forced(&J->pull[k], b, place_part(b, ppl, npl, J->lo[k], J->lo[k + 1], ts), 1, 8 | 1 << 4);
     }
@@ -634,12 +628,6 @@ int join_start(emac_handle *h, int copyin, int legs) {
   int k, rc;
   if (J->fused) {
     emac_join_seg seg[3 * EMAC_JOIN_PARTS_MAX];
-    /* part 0's copy-in, the tuned fold (node_ipc_init); with a node on another GPU its partial is
-       released to system scope before the fused launch signals it (as ipc_barrier(h, 0)) */
-    if (copyin && (h->nb || h->nedges)) {
-      if ((rc = fold_launch(h))) return rc;
-      if (legs && h->ev_release && (rc = emac_gpu_event_record(h->ev_release, h->stream))) return rc;
-    }
     unsigned long e0[EMAC_JOIN_PARTS_MAX], e1[EMAC_JOIN_PARTS_MAX];
     memset(seg, 0, sizeof(seg));
     for (k = 0; k < J->nparts; k++) {
