@@ -9,7 +9,7 @@ mkdir -p $O
 CIUS=${CIUS:-2 3 4}
 TESTU=${TESTU:-4}
 EXT_MPI_AMD_JOIN_CI_U=$TESTU timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
-  tests/test_gpu_node_ipc.py -k "serial_and_pipelined and (fused3 or fused4) or over_peer_mapped" > $O/tests_ciu$TESTU.log 2>&1
+  tests/test_gpu_node_ipc.py -k "${TESTK:-serial_and_pipelined and (fused3 or fused4) or over_peer_mapped}" > $O/tests_ciu$TESTU.log 2>&1
 rc=$?; tail -n 3 $O/tests_ciu$TESTU.log; [ $rc -ne 0 ] && exit $rc
 for p in 2 4; do for u in $CIUS; do
   EXT_MPI_AMD_JOIN_PARTS=$p EXT_MPI_AMD_JOIN_CI_U=$u timeout -k 10 240 python3 bench.py --shape joinci > $O/joinci_p${p}_u$u.json 2> $O/joinci_p${p}_u$u.err || { tail -5 $O/joinci_p${p}_u$u.err; exit 1; }
