@@ -34,8 +34,10 @@
 // and published the abandon marks still folds and stores its share items. Nothing is corrupted --
 // those stores go only to this node's own outbox, and the Start is reported failed on every node
 // through the marks and the slot's error word -- but part of a failed Start's share may be stored.
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <type_traits>
 
@@ -53,7 +55,15 @@ struct JoinSegs {
   Work w[3][EMAC_JOIN_PARTS_MAX];  // [CI, SF, PL][part]
   int slot[EMAC_JOIN_PARTS_MAX];
   unsigned long e0[EMAC_JOIN_PARTS_MAX], e1[EMAC_JOIN_PARTS_MAX];  // this Start's epochs per part
+  unsigned long *trace;  // diagnostics (EXT_MPI_AMD_JOIN_TRACE): kTraceSlots per workgroup, or null
 };
+
+// Diagnostics: with EXT_MPI_AMD_JOIN_TRACE=<path> every workgroup's thread 0 records the wall clock
+// (100 MHz) when it starts, leaves each segment or passes a gate, and ends, as
+// (clock << 16) | (items << 8) | tag, tag = stage << 4 | part (stage 0 CI, 1 SF gate, 2 SF, 3 PL gate,
+// 4 PL; 14 start, 15 end); the host appends each launch's records to <path>.<pid> before the next
+// launch (which then waits for it: a diagnostic of one launch's timeline, not of Start-to-Start overlap)
+constexpr int kTraceSlots = 32;
 
 // a wave waits for every node's (itself included) flag of `phase` in slot s to reach `epoch`
 __device__ __forceinline__ bool join_wait(NodeSync &ns, int phase, unsigned long epoch) {
@@ -123,8 +133,8 @@ __device__ __forceinline__ void join_item(const Work &w, long i, const emac_code
 // rather than a static grid stride: a workgroup the GPU has not started yet holds no item a
 // waiting one needs, so the grid need not be resident all at once.
 template <typename T, int N, int U, int CH, int D, int ISSUE>
-__device__ __forceinline__ void join_seg(const Work &w, unsigned *tk, unsigned *done, unsigned *sig, const emac_codes &codes,
-                                         int nrt, bool store, NodeSync &ns, int phase, unsigned long epoch) {
+__device__ __forceinline__ unsigned join_seg(const Work &w, unsigned *tk, unsigned *done, unsigned *sig, const emac_codes &codes,
+                                             int nrt, bool store, NodeSync &ns, int phase, unsigned long epoch) {
   __shared__ unsigned claim[2];
   __shared__ unsigned last;
   const unsigned n = (unsigned)(w.ntiles + w.nedges);
@@ -150,7 +160,7 @@ __device__ __forceinline__ void join_seg(const Work &w, unsigned *tk, unsigned *
   // it counts them. A segment that signals nothing (the pulls; the copy-ins timed alone) is not
   // counted at all: its stores complete with the launch, and the workgroup goes on at once
   // instead of waiting for a counter's round trip
-  if (phase < 0) return;
+  if (phase < 0) return mine;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -159,6 +169,7 @@ __device__ __forceinline__ void join_seg(const Work &w, unsigned *tk, unsigned *
   }
   __syncthreads();
   if (last && threadIdx.x < 64) wave_signal(ns, phase, epoch, true);
+  return mine;
 }
 
 // wait (one wave) for every node's `phase` of the part; the verdict for the whole workgroup. A
@@ -203,14 +214,23 @@ __global__ __launch_bounds__(JB) void join_fused_kernel(JoinSegs segs, int npart
   // local leaves; the partial written through to memory, at system scope when a peer runs on another
   // GPU, else at device scope (kDevStore: sc1 nt) -- enough for this GPU's other XCDs and processes
   constexpr int CI_ISSUE = 1 | (SYS ? kSysStore : kDevStore);
+  unsigned long *const tr = segs.trace ? segs.trace + (size_t)blockIdx.x * kTraceSlots : nullptr;
+  int ev = 0;
+  auto mark = [&](unsigned tag, unsigned items) {  // (wave-uniform branch on tr)
+    if (tr && threadIdx.x == 0 && ev < kTraceSlots)
+      tr[ev] = (unsigned long)wall_clock64() << 16 | (unsigned long)(items > 255u ? 255u : items) << 8 | tag;
+    ++ev;
+  };
+  mark(14u << 4, 0);
   for (int s = 0; s <= nparts + 1; ++s) {
     if (s < nparts) {  // CI[s]: signals phase 0 of part s when its last item is in (with the node legs)
       NodeSync ns = ns0;
       ns.slot = segs.slot[s];
       ns.tag = segs.e1[s];
       const Work empty = {segs.w[0][s].b, 0, 0, 0, 1, nullptr, 0};
-      join_seg<T, R, 2, CH, 1, CI_ISSUE>((mode & 1) ? segs.w[0][s] : empty, &ctl->tk[0][s], &ctl->done[0][s],
+      const unsigned it = join_seg<T, R, 2, CH, 1, CI_ISSUE>((mode & 1) ? segs.w[0][s] : empty, &ctl->tk[0][s], &ctl->done[0][s],
                                          &ctl->sig[0][s], codes, 0, true, ns, (mode & 2) ? 0 : -1, segs.e0[s]);
+      mark(0u << 4 | s, it);
     }
     if (!(mode & 2)) continue;
     if (s >= 1 && s <= nparts) {  // SF[k], after every node's phase 0 of part k; signals phase 1
@@ -219,8 +239,10 @@ __global__ __launch_bounds__(JB) void join_fused_kernel(JoinSegs segs, int npart
       ns.slot = segs.slot[k];
       ns.tag = segs.e1[k];
       const bool ok = join_gate(ns, 0, segs.e0[k], &ctl->failed0[k]);
-      join_seg<T, 0, 1, 0, 1, 1 | kRemote | kNoDrain>(segs.w[1][k], &ctl->tk[1][k], &ctl->done[1][k], &ctl->sig[1][k], xcodes,
-                                           ns0.nranks, ok, ns, 1, segs.e1[k]);
+      mark(1u << 4 | k, 0);
+      const unsigned it = join_seg<T, 0, 1, 0, 1, 1 | kRemote | kNoDrain>(segs.w[1][k], &ctl->tk[1][k], &ctl->done[1][k],
+                                                                        &ctl->sig[1][k], xcodes, ns0.nranks, ok, ns, 1, segs.e1[k]);
+      mark(2u << 4 | k, it);
     }
     if (s >= 2) {  // PL[k], after every node's phase 1 of part k
       const int k = s - 2;
@@ -228,10 +250,13 @@ __global__ __launch_bounds__(JB) void join_fused_kernel(JoinSegs segs, int npart
       ns.slot = segs.slot[k];
       ns.tag = segs.e1[k];
       const bool ok = join_gate(ns, 1, segs.e1[k], &ctl->failed1[k]);
-      join_seg<T, 1, 2, 0, R, 1 | kRemote | kNoDrain>(segs.w[2][k], &ctl->tk[2][k], &ctl->done[2][k], &ctl->sig[2][k], codes, 0, ok,
-                                           ns, -1, 0);
+      mark(3u << 4 | k, 0);
+      const unsigned it = join_seg<T, 1, 2, 0, R, 1 | kRemote | kNoDrain>(segs.w[2][k], &ctl->tk[2][k], &ctl->done[2][k],
+                                                                        &ctl->sig[2][k], codes, 0, ok, ns, -1, 0);
+      mark(4u << 4 | k, it);
     }
   }
+  mark(15u << 4, 0);
   // the last workgroup out resets the control block for the next Start (stream-ordered behind)
   __shared__ unsigned last;
   __syncthreads();
@@ -286,6 +311,47 @@ int join_launch_t(int nsrc, int ch, const JoinSegs &segs, int nparts, int mode, 
 
 }  // namespace emac
 
+namespace {
+// EXT_MPI_AMD_JOIN_TRACE (see kTraceSlots): the previous launch's records appended to the file, this
+// launch's buffer cleared; null when off
+unsigned long *join_trace_next(int grid, int mode, hipStream_t s) {
+  using namespace emac;
+  static int on = -1, prev_grid = 0, prev_mode = 0;
+  static long launches = 0;
+  static unsigned long *d = nullptr, *h = nullptr;
+  static FILE *f = nullptr;
+  constexpr int kMaxGrid = 4096;
+  if (on < 0) {
+    const char *e = getenv("EXT_MPI_AMD_JOIN_TRACE");
+    on = e && *e;
+    if (on) {
+      char path[512];
+      snprintf(path, sizeof(path), "%s.%d", e, (int)getpid());
+      f = fopen(path, "a");
+      h = static_cast<unsigned long *>(malloc(sizeof(unsigned long) * kMaxGrid * kTraceSlots));
+      if (!f || !h || hipMalloc(reinterpret_cast<void **>(&d), sizeof(unsigned long) * kMaxGrid * kTraceSlots) != hipSuccess)
+        on = 0;
+    }
+  }
+  if (!on || grid > kMaxGrid) return nullptr;
+  if (launches > 0 && hipStreamSynchronize(s) == hipSuccess &&
+      hipMemcpy(h, d, sizeof(unsigned long) * prev_grid * kTraceSlots, hipMemcpyDeviceToHost) == hipSuccess) {
+    fprintf(f, "launch %ld mode %d grid %d\n", launches - 1, prev_mode, prev_grid);
+    for (int g = 0; g < prev_grid; ++g) {
+      fprintf(f, "%d", g);
+      for (int k = 0; k < kTraceSlots && h[(size_t)g * kTraceSlots + k]; ++k) fprintf(f, " %lu", h[(size_t)g * kTraceSlots + k]);
+      fprintf(f, "\n");
+    }
+    fflush(f);
+  }
+  (void)hipMemsetAsync(d, 0, sizeof(unsigned long) * grid * kTraceSlots, s);
+  prev_grid = grid;
+  prev_mode = mode;
+  ++launches;
+  return d;
+}
+}  // namespace
+
 extern "C" int emac_gpu_join_fused(int dtype, int nsrc, const emac_codes *codes, const emac_codes *xcodes, int nparts,
                                    int mode, const emac_join_seg *segs, const int *slots, const unsigned long *e0,
                                    const unsigned long *e1, void *self_sync, void *const *d_peers, int nranks, int me,
@@ -310,6 +376,7 @@ extern "C" int emac_gpu_join_fused(int dtype, int nsrc, const emac_codes *codes,
   const NodeSync ns = {static_cast<emac_sync *>(self_sync), reinterpret_cast<emac_sync *const *>(d_peers), 0, nranks, me,
                        err, timeout_ticks, 0};
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (!dry) S.trace = join_trace_next(grid, mode, s);
   JoinCtl *c = static_cast<JoinCtl *>(ctl);
   switch (dtype) {
   case EMAC_FLOAT: return join_launch_t<float>(nsrc, ch, S, nparts, mode, *codes, *xcodes, ns, c, grid, s, dry);
