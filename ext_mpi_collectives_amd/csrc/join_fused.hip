@@ -127,7 +127,7 @@ __device__ __forceinline__ void join_item(const Work &w, long i, const emac_code
 }
 
 // The items of one segment, claimed in chunks from the segment's ticket counter (the next chunk's
-// ticket fetched while the current one is folded); then this workgroup's items are counted in
+// ticket fetched while the current one is folded, where that cannot starve another workgroup); then this workgroup's items are counted in
 // `done`, and whoever completes the count -- for a segment of no item, the first through -- signals
 // `phase` of the part's slot to every node, itself too (phase < 0: nothing to signal). Claiming
 // rather than a static grid stride: a workgroup the GPU has not started yet holds no item a
@@ -147,9 +147,15 @@ __device__ __forceinline__ unsigned join_seg(const Work &w, unsigned *tk, unsign
   unsigned at = claim[0];
   while (at < n) {
     unsigned next = 0;
-    if (threadIdx.x == 0) next = __hip_atomic_fetch_add(tk, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the next chunk is fetched while this one is folded only while more than a grid's worth of
+    // chunks follows it: fetched early in a segment of about one chunk per workgroup, it let the
+    // first workgroups take two chunks each and left others none -- two tiles in series on the
+    // critical path (join_trace_summary.py: items per workgroup 0-2 in a segment of grid items)
+    const bool ahead = (unsigned long)at + (unsigned long)c * gridDim.x < n;
+    if (threadIdx.x == 0 && ahead) next = __hip_atomic_fetch_add(tk, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned end = at + c < n ? at + c : n;
     for (unsigned i = at; i < end; ++i) join_item<T, N, U, CH, D, ISSUE>(w, (long)i, codes, nrt, store);
+    if (threadIdx.x == 0 && !ahead) next = __hip_atomic_fetch_add(tk, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     mine += end - at;
     __syncthreads();
     if (threadIdx.x == 0) claim[1] = next;
