@@ -169,9 +169,20 @@ __device__ __forceinline__ unsigned join_seg(const Work &w, unsigned *tk, unsign
   if (phase < 0) return mine;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  // (one counter per segment for the whole grid: its atomics serialise -- a segment of no item, where
+  // every workgroup once added 0 and exchanged the flag, took 5-8 us (join_trace_summary.py) -- so
+  // a workgroup of no item does not count, and with no item at all the flag is read before it is
+  // taken: only the first workgroups through try the exchange)
   if (threadIdx.x == 0) {
-    const unsigned before = __hip_atomic_fetch_add(done, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = before + mine == n && __hip_atomic_exchange(sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+    if (n == 0) {
+      last = __hip_atomic_load(sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+             __hip_atomic_exchange(sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+    } else if (mine) {
+      const unsigned before = __hip_atomic_fetch_add(done, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = before + mine == n && __hip_atomic_exchange(sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+    } else {
+      last = false;  // the workgroup that completes the count holds items
+    }
   }
   __syncthreads();
   if (last && threadIdx.x < 64) wave_signal(ns, phase, epoch, true);
