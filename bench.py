@@ -1432,6 +1432,14 @@ def multi_gpu(args):
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return bool(t.item())
 
+    # ranks sharing a GPU (a rehearsal on fewer GPUs than ranks): at HIP's default of 4 hardware queues
+    # per process, 8 processes oversubscribe the GPU's queue slots and the scheduler time-slices them,
+    # ~22.5 ms per Allreduce whatever its size; 2 queues each keep every queue resident
+    # (profiles/r06/rehearsal/: 22.9 ms against 0.50 ms per Start). One process per GPU is untouched.
+    shared_hwq = None
+    if torch.cuda.device_count() < world and "GPU_MAX_HW_QUEUES" not in os.environ:
+        shared_hwq = "2"
+
     def run_child(i, transport, full, share):
         out = os.path.join("/tmp", f"emac_bench_{base_port}_{i}_{rank}.json")
         if os.path.exists(out):
@@ -1444,6 +1452,8 @@ def multi_gpu(args):
                "--child-deadline", str(int(budget))] + (["--child-full"] if full else []) + \
               (["--copyin", args.copyin] if args.copyin else [])
         env = dict(os.environ, MASTER_PORT=str(base_port + 101 + i))
+        if shared_hwq:
+            env["GPU_MAX_HW_QUEUES"] = shared_hwq
         env.pop("TORCHELASTIC_USE_AGENT_STORE", None)  # the children's rank 0 hosts their own store
         rc, elapsed, tail = run_child_process(cmd, env, budget + 20)  # the child's watchdog fires first
         result = None
@@ -1481,8 +1491,11 @@ def multi_gpu(args):
     allf = [None] * world
     dist.all_gather_object(allf, failures)
     if rank == 0:
-        emit(multi_gpu_line(args, world, dname, S, copyin, rn, results, order, torch.cuda.device_count(),
-                            [f for fs in allf for f in fs]))
+        line = multi_gpu_line(args, world, dname, S, copyin, rn, results, order, torch.cuda.device_count(),
+                              [f for fs in allf for f in fs])
+        if shared_hwq:
+            line.setdefault("extras", {})["gpu_max_hw_queues_per_process"] = int(shared_hwq)
+        emit(line)
     dist.barrier()
     dist.destroy_process_group()
 
