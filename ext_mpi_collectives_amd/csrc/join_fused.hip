@@ -132,40 +132,17 @@ __device__ __forceinline__ void join_item(const Work &w, long i, const emac_code
 // `phase` of the part's slot to every node, itself too (phase < 0: nothing to signal). Claiming
 // rather than a static grid stride: a workgroup the GPU has not started yet holds no item a
 // waiting one needs, so the grid need not be resident all at once.
-// a segment's chunk of items per claim: a few chunks per workgroup -- few claims, balanced ends
-__device__ __forceinline__ unsigned join_chunk(unsigned n) {
-  const unsigned c = n / (gridDim.x * 4u);
-  return c < 1u ? 1u : c > 32u ? 32u : c;
-}
-
-constexpr unsigned kNoTicket = ~0u;
-// the segment this workgroup walks after the current one: its ticket counter (null: none, or no
-// item) and chunk. A workgroup leaving a segment claims its first chunk there together with the
-// current segment's last claim or count -- two atomics in one round trip instead of two: each is
-// resolved at the memory side on this 8-XCD chip, 2-3 us under the grid's contention
-// (join_trace_summary.py)
-struct NextClaim {
-  unsigned *tk;
-  unsigned c;
-};
-
 template <typename T, int N, int U, int CH, int D, int ISSUE>
 __device__ __forceinline__ unsigned join_seg(const Work &w, unsigned *tk, unsigned *done, unsigned *sig, const emac_codes &codes,
-                                             int nrt, bool store, NodeSync &ns, int phase, unsigned long epoch,
-                                             unsigned &pre, NextClaim nx) {
+                                             int nrt, bool store, NodeSync &ns, int phase, unsigned long epoch) {
   __shared__ unsigned claim[2];
   __shared__ unsigned last;
   const unsigned n = (unsigned)(w.ntiles + w.nedges);
-  const unsigned c = join_chunk(n);
+  unsigned c = n / (gridDim.x * 4u);  // a few chunks per workgroup: few claims, balanced ends
+  c = c < 1u ? 1u : c > 32u ? 32u : c;
   unsigned mine = 0;
-  // (thread 0 only) a ticket of the next segment, claimed beside this segment's last claim or count
-  unsigned held = kNoTicket;
-  auto claim_next = [&]() {
-    if (nx.tk && held == kNoTicket) held = __hip_atomic_fetch_add(nx.tk, nx.c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
   __syncthreads();
-  if (threadIdx.x == 0)
-    claim[0] = pre != kNoTicket ? pre : n ? __hip_atomic_fetch_add(tk, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+  if (threadIdx.x == 0) claim[0] = n ? __hip_atomic_fetch_add(tk, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
   __syncthreads();
   unsigned at = claim[0];
   while (at < n) {
@@ -178,10 +155,7 @@ __device__ __forceinline__ unsigned join_seg(const Work &w, unsigned *tk, unsign
     if (threadIdx.x == 0 && ahead) next = __hip_atomic_fetch_add(tk, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned end = at + c < n ? at + c : n;
     for (unsigned i = at; i < end; ++i) join_item<T, N, U, CH, D, ISSUE>(w, (long)i, codes, nrt, store);
-    if (threadIdx.x == 0 && !ahead) {
-      next = __hip_atomic_fetch_add(tk, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      claim_next();  // (issued before `next` is waited for)
-    }
+    if (threadIdx.x == 0 && !ahead) next = __hip_atomic_fetch_add(tk, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     mine += end - at;
     __syncthreads();
     if (threadIdx.x == 0) claim[1] = next;
@@ -192,10 +166,7 @@ __device__ __forceinline__ unsigned join_seg(const Work &w, unsigned *tk, unsign
   // it counts them. A segment that signals nothing (the pulls; the copy-ins timed alone) is not
   // counted at all: its stores complete with the launch, and the workgroup goes on at once
   // instead of waiting for a counter's round trip
-  if (phase < 0) {
-    pre = held;
-    return mine;
-  }
+  if (phase < 0) return mine;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   // (one counter per segment for the whole grid: its atomics serialise -- a segment of no item, where
@@ -204,12 +175,10 @@ __device__ __forceinline__ unsigned join_seg(const Work &w, unsigned *tk, unsign
   // taken: only the first workgroups through try the exchange)
   if (threadIdx.x == 0) {
     if (n == 0) {
-      const unsigned taken = __hip_atomic_load(sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      claim_next();
-      last = taken == 0u && __hip_atomic_exchange(sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+      last = __hip_atomic_load(sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+             __hip_atomic_exchange(sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
     } else if (mine) {
       const unsigned before = __hip_atomic_fetch_add(done, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      claim_next();
       last = before + mine == n && __hip_atomic_exchange(sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
     } else {
       last = false;  // the workgroup that completes the count holds items
@@ -217,7 +186,6 @@ __device__ __forceinline__ unsigned join_seg(const Work &w, unsigned *tk, unsign
   }
   __syncthreads();
   if (last && threadIdx.x < 64) wave_signal(ns, phase, epoch, true);
-  pre = held;
   return mine;
 }
 
@@ -271,29 +239,6 @@ __global__ __launch_bounds__(JB) void join_fused_kernel(JoinSegs segs, int npart
     ++ev;
   };
   mark(14u << 4, 0);
-  const bool legs = (mode & 2) != 0;
-  // the walk: step s runs CI[s] (s < nparts), SF[s - 1] (legs, 1 <= s <= nparts), PL[s - 2] (legs, s >= 2)
-  auto items_of = [&](int stage, int part) -> unsigned {
-    if (stage == 0 && !(mode & 1)) return 0u;
-    return (unsigned)(segs.w[stage][part].ntiles + segs.w[stage][part].nedges);
-  };
-  auto first_of_step = [&](int t, int &stage, int &part) {
-    stage = -1;
-    if (t > nparts + 1) return;
-    if (t < nparts) { stage = 0; part = t; }
-    else if (legs && t >= 1 && t <= nparts) { stage = 1; part = t - 1; }
-    else if (legs && t >= 2) { stage = 2; part = t - 2; }
-  };
-  auto next_after = [&](int s, int stage) -> NextClaim {  // the segment after (step s, stage)
-    int st = -1, pt = 0;
-    if (stage == 0 && legs && s >= 1 && s <= nparts) { st = 1; pt = s - 1; }
-    else if (stage <= 1 && legs && s >= 2) { st = 2; pt = s - 2; }
-    else first_of_step(s + 1, st, pt);
-    if (st < 0) return NextClaim{nullptr, 0u};
-    const unsigned n = items_of(st, pt);
-    return n ? NextClaim{&ctl->tk[st][pt], join_chunk(n)} : NextClaim{nullptr, 0u};
-  };
-  unsigned pre = kNoTicket;  // (thread 0) a ticket of the segment walked next, claimed in advance
   for (int s = 0; s <= nparts + 1; ++s) {
     if (s < nparts) {  // CI[s]: signals phase 0 of part s when its last item is in (with the node legs)
       NodeSync ns = ns0;
@@ -301,8 +246,7 @@ __global__ __launch_bounds__(JB) void join_fused_kernel(JoinSegs segs, int npart
       ns.tag = segs.e1[s];
       const Work empty = {segs.w[0][s].b, 0, 0, 0, 1, nullptr, 0};
       const unsigned it = join_seg<T, R, 2, CH, 1, CI_ISSUE>((mode & 1) ? segs.w[0][s] : empty, &ctl->tk[0][s], &ctl->done[0][s],
-                                         &ctl->sig[0][s], codes, 0, true, ns, (mode & 2) ? 0 : -1, segs.e0[s], pre,
-                                         next_after(s, 0));
+                                         &ctl->sig[0][s], codes, 0, true, ns, (mode & 2) ? 0 : -1, segs.e0[s]);
       mark(0u << 4 | s, it);
     }
     if (!(mode & 2)) continue;
@@ -314,8 +258,7 @@ __global__ __launch_bounds__(JB) void join_fused_kernel(JoinSegs segs, int npart
       const bool ok = join_gate(ns, 0, segs.e0[k], &ctl->failed0[k]);
       mark(1u << 4 | k, 0);
       const unsigned it = join_seg<T, 0, 1, 0, 1, 1 | kRemote | kNoDrain>(segs.w[1][k], &ctl->tk[1][k], &ctl->done[1][k],
-                                                                        &ctl->sig[1][k], xcodes, ns0.nranks, ok, ns, 1, segs.e1[k],
-                                                                        pre, next_after(s, 1));
+                                                                        &ctl->sig[1][k], xcodes, ns0.nranks, ok, ns, 1, segs.e1[k]);
       mark(2u << 4 | k, it);
     }
     if (s >= 2) {  // PL[k], after every node's phase 1 of part k
@@ -326,8 +269,7 @@ __global__ __launch_bounds__(JB) void join_fused_kernel(JoinSegs segs, int npart
       const bool ok = join_gate(ns, 1, segs.e1[k], &ctl->failed1[k]);
       mark(3u << 4 | k, 0);
       const unsigned it = join_seg<T, 1, 2, 0, R, 1 | kRemote | kNoDrain>(segs.w[2][k], &ctl->tk[2][k], &ctl->done[2][k],
-                                                                        &ctl->sig[2][k], codes, 0, ok, ns, -1, 0, pre,
-                                                                        next_after(s, 2));
+                                                                        &ctl->sig[2][k], codes, 0, ok, ns, -1, 0);
       mark(4u << 4 | k, it);
     }
   }
