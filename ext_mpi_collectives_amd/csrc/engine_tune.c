@@ -133,7 +133,13 @@ static int tune_candidates(const emac_handle *h, long vec, int *sched) {
                       "static pick kept\n", sched[0], h->nsrc, h->fan);
     return 0;
   }
-  sched[n++] = 2 | 1 << 4;
+  /* one destination, 4 or 8 leaves, from 8 MiB per leaf (the local fold of SURVEY 8(d), the serial
+     node join's copy-in): forced one at a time on the local fold, 8 x 32 MiB -> 1, two leases, six
+     passes (profiles/r06/localab/), (U 2, burst) ran 49.8-50.6 us and (U 4, 4 tiles) 48.2-49.4
+     against 47.3-48.1 for the other candidates, yet the tuner had kept (U 4, 4 tiles) on two of
+     four handles of one lease; they are not offered there, (U 4, 2 tiles) is (47.6-47.9 us) */
+  const int big1 = !h->fan && !small && (h->nsrc == 4 || h->nsrc == 8);
+  if (!big1) sched[n++] = 2 | 1 << 4;
   sched[n++] = 4 | 1 << 4;
   /* the node fan-outs of 4 and 8 ranks: (U 4, staggered) with buffer loads (fold_kernel.hpp
      kBufLoad), and from 32 MiB per leaf (U 4, burst) with buffer loads and device-scope streaming
@@ -156,7 +162,7 @@ static int tune_candidates(const emac_handle *h, long vec, int *sched) {
   if (h->tiles_per_bucket > 0) {
     sched[n++] = 2 | (1 | 2 << 11) << 4;
     if (!h->fan) {
-      sched[n++] = 4 | (1 | 2 << 11) << 4;
+      sched[n++] = big1 ? 4 | (1 | 1 << 11) << 4 : 4 | (1 | 2 << 11) << 4;
     } else {
       sched[n++] = 4 | (1 | 1 << 11) << 4;
       /* leaf-major groups (kLeafMajor): the linear fold and the compile-time chains; a chain also in the

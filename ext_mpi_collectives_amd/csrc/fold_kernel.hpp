@@ -945,12 +945,10 @@ int launch_sum(int unroll, const Launch &L) {
     if (unroll == sched(4, 1 | defer(4))) return launch_one<T, OP, N, 4, CH, D, 1 | defer(4)>(L);
     if constexpr (N == 4 || N == 8) {  // one destination of 4 or 8 leaves: (U 4, staggered) with buffer loads
       if (unroll == sched(4, 5 | kBufLoad)) return launch_one<T, OP, N, 4, CH, D, 5 | kBufLoad>(L);
-      // round 6, A/B of the local fold (EXT_MPI_AMD_FOLD_SCHEDULE; not tuner candidates): the LDS
-      // groups with buffer loads, two and eight tiles
-      if (unroll == sched(2, 1 | defer(4) | kBufLoad)) return launch_one<T, OP, N, 2, CH, D, 1 | defer(4) | kBufLoad>(L);
-      if (unroll == sched(4, 1 | defer(4) | kBufLoad)) return launch_one<T, OP, N, 4, CH, D, 1 | defer(4) | kBufLoad>(L);
+      // (U 4, 2 tiles) of LDS groups: a candidate from 8 MiB per leaf (engine_tune.c; round 6, the
+      // local fold forced at 47.6-47.9 us, profiles/r06/localab/, where the LDS groups with buffer
+      // loads ran 48.2-48.9 and 8 tiles 48.5-48.8: those are not built)
       if (unroll == sched(4, 1 | defer(2))) return launch_one<T, OP, N, 4, CH, D, 1 | defer(2)>(L);
-      if (unroll == sched(2, 1 | defer(8))) return launch_one<T, OP, N, 2, CH, D, 1 | defer(8)>(L);
     }
     return EMAC_ERR_UNSUPPORTED;
   }

@@ -407,6 +407,7 @@ def test_copy_reduce_headline_instance():
 DEFER_SHIFT = 11  # fold_kernel.hpp kDeferShift: deferred-store schedules (issue bits 11-12)
 LEAF_MAJOR = 1 << 13  # fold_kernel.hpp kLeafMajor: leaf-major deferred groups
 LM_OPEN_COPY = 1 << 16  # fold_kernel.hpp kLmOpenCopy: a chain's opening leaves copied into their accumulators
+BUF_LOAD = 1 << 15  # fold_kernel.hpp kBufLoad: leaf loads as buffer loads
 
 
 @pytest.mark.parametrize("copyin", ["6;1 -8 8", "6;1 -2 -2 -2 2 2 2"])
@@ -450,26 +451,33 @@ def test_every_tuned_schedule_bitwise(oracle, code, copyin):
         opencopy = (2, 1 | 2 << DEFER_SHIFT | LEAF_MAJOR | LM_OPEN_COPY)  # ... and for a chain its other form
         assert leaf in cands and (4, 1 | 1 << DEFER_SHIFT) in cands, cands
         assert (opencopy in cands) == (copyin != "6;1 -8 8"), cands
-    # the local fold: one destination, one bucket
-    n = 8 * 64000 + 40 if code == emac.FLOAT else 4 * 64000 + 20
-    srcs_np = xorshift_inputs(R, n, code, seed_base=0x10CA1)
-    lwant = srcs_np[0].copy()
-    for x in srcs_np[1:]:
-        lwant = lwant + x
-    srcs = [_dev(x) for x in srcs_np]
-    dst = torch.full((n,), -1, dtype=TORCH[code], device="cuda")
-    emac.tune_cache_clear()
-    h = emac.fold_init([t.data_ptr() for t in srcs], [dst.data_ptr()], n, code)
-    try:
-        for k in range(TUNE_STARTS):
-            dst.fill_(-1)
-            torch.cuda.synchronize()
-            emac.start(h)
-            emac.wait(h)
-            sc = emac.handle_schedule(h)
-            assert_bitwise([dst.cpu().numpy()], [lwant], f"local fold Start {k} {sc}")
-    finally:
-        emac.done(h)
+    # the local fold: one destination, one bucket -- under 8 MiB per leaf, and above it, where the
+    # candidates are (U 4, burst), (U 4, staggered) with buffer loads and the LDS groups of (U 2, 4
+    # tiles) and (U 4, 2 tiles) (engine_tune.c, round 6)
+    big = ((8 << 20) // 4 + 1000) if code == emac.FLOAT else ((8 << 20) // 8 + 500)
+    for n in ((8 * 64000 + 40 if code == emac.FLOAT else 4 * 64000 + 20), big):
+        srcs_np = xorshift_inputs(R, n, code, seed_base=0x10CA1 + n)
+        lwant = srcs_np[0].copy()
+        for x in srcs_np[1:]:
+            lwant = lwant + x
+        srcs = [_dev(x) for x in srcs_np]
+        dst = torch.full((n,), -1, dtype=TORCH[code], device="cuda")
+        emac.tune_cache_clear()
+        h = emac.fold_init([t.data_ptr() for t in srcs], [dst.data_ptr()], n, code)
+        try:
+            cands = emac.handle_candidates(h)
+            if n == big:
+                assert sorted(cands) == sorted([(4, 1), (4, 5 | BUF_LOAD), (2, 1 | 2 << DEFER_SHIFT),
+                                                (4, 1 | 1 << DEFER_SHIFT)]), cands
+            for k in range(TUNE_STARTS):
+                dst.fill_(-1)
+                torch.cuda.synchronize()
+                emac.start(h)
+                emac.wait(h)
+                sc = emac.handle_schedule(h)
+                assert_bitwise([dst.cpu().numpy()], [lwant], f"local fold {n} Start {k} {sc}")
+        finally:
+            emac.done(h)
 
 
 @pytest.mark.parametrize("copyin", ["6;1 -2 -2 -2 2 2 2", "6;1 -4 -2 2 4", "6;1 -2 -4 4 2", "6;1 -8 8", "6;1 -2 -2 2 2",
