@@ -1,13 +1,16 @@
 #!/bin/bash
 # Round 6: the local fold (8 x 32 MiB -> 1) under each one-destination schedule
-# forced (bench.py --shape local256 --schedules), two passes in opposite orders on one lease: the
-# kept candidates (LDS groups U 2 / U 4 x 4 tiles, U 4 staggered with buffer loads) against the LDS
-# groups with buffer loads, 2 and 8 tiles (fold_kernel.hpp, instantiated for this A/B).
+# forced (bench.py --shape local256 --schedules), two passes in opposite orders on one lease. W1 / W2
+# (comma-separated schedule words, env) pick the schedules; TAG names the output directory. The
+# first A/B also ran the LDS groups with buffer loads at 2 and 8 tiles: those kernels were slower
+# and are no longer instantiated, so the default lists name the kept schedules
+# (U 2, 4 tiles), (U 4, staggered, buffer loads), (U 4, 2 tiles), (U 4, burst)) plus (U 4, 4
+# tiles) and (U 2, burst), which the tuner now skips for this shape.
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r06/localab
+O=gpurun_out/r06/localab${TAG:+_$TAG}
 mkdir -p $O
-W1=65554,524372,65556,589842,589844,32788,98322
-W2=98322,32788,589844,589842,65556,524372,65554
+W1=${W1:-65554,524372,32788,20,65556,18}
+W2=${W2:-18,65556,20,32788,524372,65554}
 i=0
 for w in $W1 $W2; do
   i=$((i + 1))
