@@ -4,7 +4,7 @@
 # (comma-separated schedule words, env) pick the schedules; TAG names the output directory. The
 # first A/B also ran the LDS groups with buffer loads at 2 and 8 tiles: those kernels were slower
 # and are no longer instantiated, so the default lists name the kept schedules
-# (U 2, 4 tiles), (U 4, staggered, buffer loads), (U 4, 2 tiles), (U 4, burst)) plus (U 4, 4
+# (U 2, 4 tiles), (U 4, staggered, buffer loads), (U 4, 2 tiles), (U 4, burst) plus (U 4, 4
 # tiles) and (U 2, burst), which the tuner now skips for this shape.
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r06/localab${TAG:+_$TAG}
