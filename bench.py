@@ -1436,9 +1436,10 @@ def multi_gpu(args):
     # per process, 8 processes oversubscribe the GPU's queue slots and the scheduler time-slices them,
     # ~22.5 ms per Allreduce whatever its size; 2 queues each keep every queue resident
     # (profiles/r06/rehearsal/: 22.9 ms against 0.50 ms per Start). One process per GPU is untouched.
+    # (A value already in the environment is capped, not kept: the GPU boxes export HIP's default, 4.)
     shared_hwq = None
-    if torch.cuda.device_count() < world and "GPU_MAX_HW_QUEUES" not in os.environ:
-        shared_hwq = "2"
+    if torch.cuda.device_count() < world:
+        shared_hwq = str(max(1, min(2, int(os.environ.get("GPU_MAX_HW_QUEUES", "4")))))
 
     def run_child(i, transport, full, share):
         out = os.path.join("/tmp", f"emac_bench_{base_port}_{i}_{rank}.json")
