@@ -228,9 +228,12 @@ __device__ __forceinline__ bool join_gate(NodeSync &ns, int phase, unsigned long
 template <typename T, int R, int CH, bool SYS>
 __global__ __launch_bounds__(JB) void join_fused_kernel(JoinSegs segs, int nparts, int mode, emac_codes codes,
                                                                 emac_codes xcodes, NodeSync ns0, JoinCtl *ctl) {
-  // local leaves; the partial written through to memory, at system scope when a peer runs on another
-  // GPU, else at device scope (kDevStore: sc1 nt) -- enough for this GPU's other XCDs and processes
-  constexpr int CI_ISSUE = 1 | (SYS ? kSysStore : kDevStore);
+  // local leaves, read with nontemporal buffer loads (kBufLoad: the copy-in alone 35.5-36.4 us
+  // against 36.8-36.9 with global loads, Starts with 2 / 4 nodes on one GPU equal or 1-2 % faster;
+  // staggered issue and vector-major order were not better, profiles/r06/ciload/); the partial
+  // written through to memory, at system scope when a peer runs on another GPU, else at device
+  // scope (kDevStore: sc1 nt) -- enough for this GPU's other XCDs and processes
+  constexpr int CI_ISSUE = 1 | kBufLoad | (SYS ? kSysStore : kDevStore);
   unsigned long *const tr = segs.trace ? segs.trace + (size_t)blockIdx.x * kTraceSlots : nullptr;
   int ev = 0;
   auto mark = [&](unsigned tag, unsigned items) {  // (wave-uniform branch on tr)
