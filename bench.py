@@ -1436,10 +1436,7 @@ def multi_gpu(args):
     # per process, 8 processes oversubscribe the GPU's queue slots and the scheduler time-slices them,
     # ~22.5 ms per Allreduce whatever its size; 2 queues each keep every queue resident
     # (profiles/r06/rehearsal/: 22.9 ms against 0.50 ms per Start). One process per GPU is untouched.
-    # (A value already in the environment is capped, not kept: the GPU boxes export HIP's default, 4.)
-    shared_hwq = None
-    if torch.cuda.device_count() < world:
-        shared_hwq = str(max(1, min(2, int(os.environ.get("GPU_MAX_HW_QUEUES", "4")))))
+    shared_hwq = shared_hw_queues(torch.cuda.device_count(), world, os.environ.get("GPU_MAX_HW_QUEUES"))
 
     def run_child(i, transport, full, share):
         out = os.path.join("/tmp", f"emac_bench_{base_port}_{i}_{rank}.json")
@@ -1499,6 +1496,19 @@ def multi_gpu(args):
         emit(line)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def shared_hw_queues(devices, world, env_value):
+    """GPU_MAX_HW_QUEUES for the N > 1 children: None (left alone) with one rank per GPU, else at most
+    2 -- an exported value is capped, not kept, since the GPU boxes export HIP's default of 4, at which
+    8 processes sharing one GPU time-slice (profiles/r06/rehearsal/)."""
+    if devices >= world:
+        return None
+    try:
+        v = int(env_value) if env_value else 4
+    except ValueError:
+        v = 4
+    return str(max(1, min(2, v)))
 
 
 def node_result(node, steps):

@@ -193,3 +193,14 @@ def test_radix_crossover_and_vs_linear():
     # fixed cost == streaming time at 3 us * 3 TB/s / 8 ranks per rank
     assert abs(x["6;1 -8 8"]["crossover_bytes_per_rank"] - 3e-6 * 3e12 / 8) < 16
     assert abs(x["6;-64 -8 8"]["crossover_bytes_per_rank"] - 4e-6 * 2e12 / 8) < 16
+
+
+def test_shared_hw_queues():
+    """ranks sharing a GPU get at most 2 hardware queues each, whatever the environment exports
+    (the boxes export 4); one rank per GPU leaves the setting alone"""
+    assert bench.shared_hw_queues(8, 8, None) is None
+    assert bench.shared_hw_queues(8, 8, "4") is None
+    assert bench.shared_hw_queues(1, 8, None) == "2"
+    assert bench.shared_hw_queues(1, 8, "4") == "2"
+    assert bench.shared_hw_queues(1, 2, "1") == "1"
+    assert bench.shared_hw_queues(1, 4, "junk") == "2"
