@@ -198,6 +198,8 @@ def test_radix_crossover_and_vs_linear():
 def test_shared_hw_queues():
     """ranks sharing a GPU get at most 2 hardware queues each, whatever the environment exports
     (the boxes export 4); one rank per GPU leaves the setting alone"""
+    sys.path.insert(0, ROOT)
+    import bench
     assert bench.shared_hw_queues(8, 8, None) is None
     assert bench.shared_hw_queues(8, 8, "4") is None
     assert bench.shared_hw_queues(1, 8, None) == "2"
